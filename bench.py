@@ -1,0 +1,226 @@
+#!/usr/bin/env python3
+"""bench.py -- audio frames/s of csm_1b greedy generation (BASELINE.json metric).
+
+One *step* = one ``generate`` pass over this rank's batch of synthetic 10 s
+utterances: prompt prefill, 125 frames (backbone + 31 decoder passes each) and,
+unless --no-decode, the Mimi decode of every utterance to 24 kHz PCM.  Weights
+are synthetic (seed 0), the model is full csm_1b.
+
+N=1 runs configs[1] (batch 1).  With ``torchrun --nproc-per-node N`` each rank
+(one GPU, device = LOCAL_RANK) generates its own shard of utterances -- the path
+shards over independent utterances, so there is no data-path collective; RCCL
+(torch.distributed "nccl") is used only for the barrier, the max-over-ranks
+timer and the frame count.  ``value`` = frames of all ranks / max rank time.
+
+Extra JSON fields: ``roofline`` for the dominant kernel (decoder gate/up GEMV,
+timed live with HIP events on the engine stream) and ``cpu_baseline`` (the
+numpy oracle, i.e. a CPU restatement -- NOT the MLX reference -- on this host).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (os.path.join(ROOT, "csm-mlx_amd"), ROOT):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+
+METRIC = "audio frames/sec (24 kHz) csm_1b greedy, 10 s utterances, 1/2/4/8 GPU"
+FRAME_SAMPLES = 1920
+HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md chip table)
+
+
+def prompt_ids(g: int):
+    """configs[1]: BOS + 12 ids ~ U[0,128000) (seed 1) + EOS for utterance 0; seed 1000+g otherwise."""
+    rng = np.random.default_rng(1 if g == 0 else 1000 + g)
+    return [128000] + [int(x) for x in rng.integers(0, 128000, 12)] + [128001]
+
+
+def shard(global_batch: int, world: int, rank: int):
+    """Contiguous utterance partition: rank r owns [r*B/N, (r+1)*B/N)."""
+    per = global_batch // world
+    return list(range(rank * per, (rank + 1) * per))
+
+
+def dist_env():
+    return int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)), int(os.environ.get("LOCAL_RANK", 0))
+
+
+def aggregate(frames_local: float, dt_local: float, world: int, device=None):
+    """(sum of frames over ranks, max time over ranks)."""
+    if world == 1:
+        return frames_local, dt_local
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([frames_local, dt_local], dtype=torch.float64, device=device)
+    f = t[:1].clone()
+    m = t[1:].clone()
+    dist.all_reduce(f, op=dist.ReduceOp.SUM)
+    dist.all_reduce(m, op=dist.ReduceOp.MAX)
+    return float(f.item()), float(m.item())
+
+
+def build_codec(seed=0):
+    from csm_mlx.config import MIMI_CONFIGURATION
+    from csm_mlx.mimi import MimiCodec
+    from csm_mlx.tokenizers import set_audio_tokenizer
+    from csm_mlx.weights import synthetic_mimi_weights
+    m = MIMI_CONFIGURATION["mimi_202407"]
+    codec = MimiCodec(m, max_batch=64)
+    codec.load_weights(synthetic_mimi_weights(m, seed))
+    set_audio_tokenizer(codec, 32)
+    return codec
+
+
+def build_model(dtype: str, batch: int, seed=0):
+    from csm_mlx.models import CSM, csm_1b
+    from csm_mlx.weights import csm_param_specs, synthetic_csm_weights
+    args = csm_1b()
+    model = CSM(args, dtype=dtype, max_batch=batch)
+    names = list(csm_param_specs(args))
+    for i in range(0, len(names), 16):      # stream tensors in groups: bounded host memory
+        model.load_weights(list(synthetic_csm_weights(args, seed, names[i:i + 16]).items()), strict=False)
+    model.load_weights([], strict=True)
+    return model
+
+
+def cpu_baseline(frames: int = 2):
+    """The numpy oracle (CPU restatement of generation.py) on this host, csm_1b fp32, B=1."""
+    from threadpoolctl import threadpool_info, threadpool_limits
+    from csm_mlx.config import BACKBONE_CONFIGURATION as BB, DECODER_CONFIGURATION as DC
+    from csm_mlx.models import csm_1b
+    from csm_mlx.weights import synthetic_csm_weights
+    from oracle.csm_oracle import OracleCSM, text_frame
+    cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    with threadpool_limits(limits=cores):
+        args = csm_1b()
+        o = OracleCSM(args, synthetic_csm_weights(args, 0), BB["1b"], DC["100m"])
+        t, m = text_frame(prompt_ids(0), 32)
+        o.generate_codes(t, m, 1)                 # warm (page in weights)
+        t0 = time.perf_counter()
+        o.generate_codes(t, m, frames)
+        dt = time.perf_counter() - t0
+        threads = max((i.get("num_threads", 1) for i in threadpool_info()), default=1)
+    return {"value": frames / dt, "unit": "audio frames/s", "cores": int(threads), "kind": "port",
+            "sample": f"numpy fp32 oracle (CPU restatement, not MLX), csm_1b B=1 greedy, prompt prefill + "
+                      f"{frames} frames, codes only, {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=1, help="utterances per GPU")
+    ap.add_argument("--frames", type=int, default=125)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "float32"])
+    ap.add_argument("--no-decode", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-frames", type=int, default=2)
+    args = ap.parse_args()
+
+    rank, world, local = dist_env()
+    dev = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+        dist.init_process_group("nccl", device_id=dev)
+
+    def barrier_sync():
+        if world > 1:
+            import torch
+            import torch.distributed as dist
+            dist.barrier()
+            torch.cuda.synchronize()
+
+    from csm_mlx import _lib
+    from csm_mlx.generation import generate_batch
+    from csm_mlx.tokenizers import tokenize_text_segment
+
+    model = build_model(args.dtype, args.batch)
+    decode = not args.no_decode
+    if decode:
+        build_codec()
+    mine = shard(args.batch * world, world, rank)
+    prompts = [tokenize_text_segment(prompt_ids(g), 0, 32) for g in mine]
+    ms = args.frames * 80
+
+    def step():
+        out = generate_batch(model, prompts, ms, temperature=0.0, decode=decode)
+        if decode:
+            return sum(len(w) // FRAME_SAMPLES for w in out)
+        return sum(len(c) for c in out)
+
+    for _ in range(args.warmup):
+        step()
+    barrier_sync()
+    t0 = time.perf_counter()
+    frames = 0
+    for _ in range(args.steps):
+        frames += step()
+    barrier_sync()
+    dt = time.perf_counter() - t0
+    total_frames, max_dt = aggregate(float(frames), dt, world, dev)
+
+    # roofline of the dominant kernel: decoder gate/up (+RMSNorm, SiLU*up) GEMV, 124 launches/frame
+    import ctypes
+    L = _lib.lib()
+    roof = {}
+    for key, which in (("decoder_gate_up", 4), ("backbone_gate_up", 0)):
+        us, nb = ctypes.c_float(0), ctypes.c_double(0)
+        _lib.check(L.csm_bench_gemv(model.engine, which, args.batch, 400, ctypes.byref(us), ctypes.byref(nb)))
+        ach = nb.value / (us.value * 1e-6) / 1e9
+        roof[key] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "avg_us": round(us.value, 3),
+                     "bytes_per_launch": int(nb.value)}
+    traffic_file = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(traffic_file):
+        try:
+            tr = json.load(open(traffic_file))
+            for k in roof:
+                if k in tr:
+                    roof[k]["traffic"] = tr[k]
+        except Exception:  # noqa: BLE001
+            pass
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(total_frames / max_dt, 3),
+            "unit": "audio frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(max_dt / args.steps * 1000, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.dtype,
+            "data": "synthetic",
+            "config": {"workload": "csm_1b greedy generate(), 10 s utterances (125 frames) + Mimi decode"
+                                   if decode else "csm_1b greedy generate(), 10 s utterances (125 frames), codes only",
+                       "model": "csm_1b (synthetic seed-0 weights)", "global_batch": args.batch * world,
+                       "per_gpu_batch": args.batch, "frames": args.frames, "mimi_decode": decode,
+                       "parallelism": f"dp{world}", "rtf": round(total_frames / max_dt / 12.5, 2)},
+            "roofline": dict(roof["decoder_gate_up"], kernel="gemv_kernel<bf16,4,*,EPI_SILU_MUL,1,TAG=1> "
+                             "(decoder norm+gate/up+SiLU, 33.5 MB bf16 per launch)"),
+            "roofline_backbone": roof["backbone_gate_up"],
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(args.cpu_frames)
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,234 @@
+"""Frame generation -- drop-in for /root/reference/csm_mlx/generation.py.
+
+``generate_frame`` / ``generate`` / ``stream_generate`` keep the reference
+signatures (generation.py:21-31, 95-105, 181-191) plus the ``sampler=`` keyword
+the reference README/CLI pass (README.md:49; cli/generate.py:197-199).  The
+frame step itself runs as two captured HIP graphs inside libcsm_hip.so
+(csm-mlx_amd/csrc/csm_engine.hip); the host only assembles prompts, polls EOS
+flags every ``chunk`` frames and hands the code history to the Mimi decoder,
+which reads it straight from device memory.
+
+``generate_batch`` is the batched extension used by bench.py: B independent
+utterances share every weight read (the reference is batch-1 only,
+generation.py:156).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Any, Callable, Generator, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from .models import CSM
+from .sampling import Sampler
+from .segment import Segment
+from .tokenizers import decode_audio, get_audio_tokenizer, tokenize_segment, tokenize_text_segment
+
+default_stream = None  # MLX stream placeholder (generation.py:19); the engine owns its HIP stream
+
+
+def _resolve_sampler(temperature: float, sampler: Optional[Sampler], top_k: int = 0) -> Sampler:
+    if sampler is not None:
+        if callable(sampler) and not isinstance(sampler, Sampler):
+            raise NotImplementedError("arbitrary sampler callables cannot run inside the GPU frame graph; "
+                                      "use csm_mlx.sampling.make_sampler(temp, top_k=...)")
+        return sampler
+    return Sampler(float(temperature), int(top_k))
+
+
+def _seed_list(seed, B: int) -> np.ndarray:
+    if seed is None:
+        base = int.from_bytes(os.urandom(8), "little")
+        return np.array([(base + b) & ((1 << 64) - 1) for b in range(B)], np.uint64)
+    if np.ndim(seed) == 0:
+        return np.array([(int(seed) + b) & ((1 << 64) - 1) for b in range(B)], np.uint64)
+    s = np.asarray(seed, np.uint64).reshape(-1)
+    if len(s) != B:
+        raise ValueError("need one seed per utterance")
+    return s
+
+
+class FrameCache:
+    """Replaces the per-layer mlx_lm ``KVCache`` list: a batch slot in the engine
+    (KV caches, positions, code history live on the GPU)."""
+
+    def __init__(self, model: CSM, batch_size: int, sampler: Sampler, seeds=None):
+        self.model = model
+        self.B = batch_size
+        self.sampler = sampler
+        self.seeds = _seed_list(seeds, batch_size)
+        self.L = _lib.lib()
+        _lib.check(self.L.csm_begin(model.engine, batch_size, _lib.ptr(self.seeds), sampler.temp, sampler.top_k))
+        self.frames = 0
+
+    def prefill(self, b: int, tokens: np.ndarray, mask: np.ndarray):
+        t = np.ascontiguousarray(tokens, np.int32)
+        m = np.ascontiguousarray(mask, np.uint8)
+        _lib.check(self.L.csm_prefill(self.model.engine, b, t.shape[0], _lib.ptr(t), _lib.ptr(m)))
+
+    def run(self, nframes: int) -> bool:
+        done = ctypes.c_int(0)
+        _lib.check(self.L.csm_run_frames(self.model.engine, nframes, ctypes.byref(done)))
+        self.frames += nframes
+        return bool(done.value)
+
+    def codes(self) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+        """(history [F,B,K], n_frames [B], done [B])."""
+        F = ctypes.c_int(0)
+        _lib.check(self.L.csm_read_codes(self.model.engine, None, None, None, ctypes.byref(F)))
+        hist = np.zeros((F.value, self.B, self.model.n_audio_codebooks), np.int32)
+        n = np.zeros(self.B, np.int32)
+        d = np.zeros(self.B, np.uint8)
+        _lib.check(self.L.csm_read_codes(self.model.engine, _lib.ptr(hist), _lib.ptr(n), _lib.ptr(d), None))
+        return hist, n, d
+
+    def last_codes(self) -> np.ndarray:
+        out = np.zeros((self.B, self.model.n_audio_codebooks), np.int32)
+        _lib.check(self.L.csm_debug_read(self.model.engine, b"codes", _lib.ptr(out), out.nbytes, None))
+        return out
+
+    def debug(self, what: str, shape) -> np.ndarray:
+        out = np.zeros(shape, np.float32)
+        _lib.check(self.L.csm_debug_read(self.model.engine, what.encode(), _lib.ptr(out), out.nbytes, None))
+        return out
+
+
+def make_frame_cache(model: CSM, batch_size: int = 1, *, temperature: float = 0.8, sampler=None, seed=None):
+    return FrameCache(model, batch_size, _resolve_sampler(temperature, sampler), seed)
+
+
+def generate_frame(model: CSM, tokens, *, temperature: float = 0.8, token_mask=None,
+                   logits_processors: Optional[List[Callable]] = None, cache: Optional[FrameCache] = None,
+                   stream: Any = default_stream, c0_history: Optional[list] = None, sampler=None, seed=None):
+    """generation.py:21-92.  tokens (B, T, K+1); returns codes (B, K) int32.
+
+    The rows are appended to the backbone KV held by ``cache`` (a fresh one when None),
+    then one frame (c0 + 31 decoder steps) runs on the GPU."""
+    if logits_processors:
+        raise NotImplementedError("logits_processors run on host logits; not supported by the GPU frame graph")
+    tokens = np.asarray(tokens, np.int32)
+    mask = np.ones_like(tokens, dtype=bool) if token_mask is None else np.asarray(token_mask).astype(bool)
+    B = tokens.shape[0]
+    if cache is None:
+        cache = make_frame_cache(model, B, temperature=temperature, sampler=sampler, seed=seed)
+    for b in range(B):
+        cache.prefill(b, tokens[b], mask[b])
+    cache.run(1)
+    codes = cache.last_codes()
+    if c0_history is not None:
+        c0_history.append(codes[:, :1].copy())
+    return codes
+
+
+def build_prompt(model: CSM, text, speaker: int, context: Sequence[Segment]):
+    """generation.py:108-125 -> (L, K+1) tokens, mask."""
+    K = model.n_audio_codebooks
+    toks, masks = [], []
+    for seg in context:
+        t, m = tokenize_segment(seg, n_audio_codebooks=K)
+        toks.append(t)
+        masks.append(m)
+    t, m = tokenize_text_segment(text, speaker, K)
+    toks.append(t)
+    masks.append(m)
+    return np.concatenate(toks, 0).astype(np.int32), np.concatenate(masks, 0).astype(bool)
+
+
+def _check_window(model: CSM, L: int, max_audio_frames: int):
+    max_seq_len = model.max_seq_len - max_audio_frames                         # generation.py:131-137
+    if L >= max_seq_len:
+        raise ValueError(f"Inputs too long ({L}), must be below max_seq_len - max_audio_frames: {max_seq_len}")
+
+
+def generate_codes_batch(model: CSM, prompts: Sequence[Tuple[np.ndarray, np.ndarray]], max_audio_frames: int, *,
+                         sampler: Sampler, seeds=None, chunk: int = 16):
+    """Run the frame loop for B prompts.  Returns (hist [F,B,K], n_frames [B], cache)."""
+    B = len(prompts)
+    for t, _ in prompts:
+        _check_window(model, t.shape[0], max_audio_frames)
+    cache = FrameCache(model, B, sampler, seeds)
+    for b, (t, m) in enumerate(prompts):
+        cache.prefill(b, t, m)
+    left = max_audio_frames
+    while left > 0:
+        n = min(chunk, left)
+        all_done = cache.run(n)                                                  # EOS poll (generation.py:151)
+        left -= n
+        if all_done:
+            break
+    hist, n_frames, _ = cache.codes()
+    return hist, n_frames, cache
+
+
+def _decode_batch(model: CSM, hist: np.ndarray, n_frames: np.ndarray) -> List[np.ndarray]:
+    """Mimi decode per group of equal-length utterances (a shorter utterance must not see
+    frames generated after its EOS)."""
+    K = model.n_audio_codebooks
+    codec = get_audio_tokenizer(K)
+    out: List[Optional[np.ndarray]] = [None] * len(n_frames)
+    for F in sorted(set(int(f) for f in n_frames)):
+        idx = [b for b in range(len(n_frames)) if n_frames[b] == F]
+        if F == 0:
+            for b in idx:
+                out[b] = np.zeros((0,), np.float32)
+            continue
+        codes = np.ascontiguousarray(hist[:F, idx].transpose(1, 2, 0))          # (b, K, F)
+        pcm = codec.decode(codes)
+        for j, b in enumerate(idx):
+            out[b] = pcm[j, 0]
+    return out
+
+
+def generate(model: CSM, text, speaker: int, context: List[Segment], max_audio_length_ms: float = 90_000, *,
+             temperature: float = 0.8, logits_processors: Optional[List[Callable]] = None,
+             stream: Any = default_stream, sampler=None, seed=None) -> np.ndarray:
+    """generation.py:95-178: returns the (F*1920,) float32 waveform (or zeros((0,)) + warning)."""
+    if logits_processors:
+        raise NotImplementedError("logits_processors are not supported by the GPU frame graph")
+    max_audio_frames = int(max_audio_length_ms / 80)
+    prompt = build_prompt(model, text, speaker, context)
+    smp = _resolve_sampler(temperature, sampler)
+    hist, n_frames, _ = generate_codes_batch(model, [prompt], max_audio_frames, sampler=smp, seeds=seed)
+    if n_frames[0] == 0:
+        print("[WARN] No samples generated.")
+        return np.zeros((0,), dtype=np.float32)
+    return _decode_batch(model, hist, n_frames)[0]
+
+
+def generate_batch(model: CSM, prompts: Sequence[Tuple[np.ndarray, np.ndarray]], max_audio_length_ms: float = 10_000,
+                   *, temperature: float = 0.0, top_k: int = 0, sampler=None, seeds=None, decode: bool = True):
+    """Batched extension: B prompts (tokens, mask) -> list of waveforms (or codes if decode=False)."""
+    smp = _resolve_sampler(temperature, sampler, top_k)
+    hist, n_frames, _ = generate_codes_batch(model, prompts, int(max_audio_length_ms / 80), sampler=smp, seeds=seeds)
+    if not decode:
+        return [hist[: n_frames[b], b] for b in range(len(prompts))]
+    return _decode_batch(model, hist, n_frames)
+
+
+def stream_generate(model: CSM, text, speaker: int, context: List[Segment], max_audio_length_ms: float = 90_000,
+                    *, temperature: float = 0.8, logits_processors: Optional[List[Callable]] = None,
+                    stream: Any = default_stream, sampler=None, seed=None) -> Generator[np.ndarray, None, None]:
+    """generation.py:181-258: yields (1920,) float32 PCM per generated frame.
+
+    Codec streaming state is per call (the reference resets a process-global Mimi,
+    generation.py:224-225, :258)."""
+    if logits_processors:
+        raise NotImplementedError("logits_processors are not supported by the GPU frame graph")
+    max_audio_frames = int(max_audio_length_ms / 80)
+    t, m = build_prompt(model, text, speaker, context)
+    _check_window(model, t.shape[0], max_audio_frames)
+    smp = _resolve_sampler(temperature, sampler)
+    codec = get_audio_tokenizer(model.n_audio_codebooks)
+    cache = FrameCache(model, 1, smp, seed)
+    cache.prefill(0, t, m)
+    codec.reset_state(1)
+    try:
+        for _ in range(max_audio_frames):
+            if cache.run(1):
+                break                                                              # EOS (generation.py:239)
+            codes = cache.last_codes()
+            yield codec.decode_step(codes)[0]
+    finally:
+        codec.reset_state(1)

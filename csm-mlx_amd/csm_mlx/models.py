@@ -1,0 +1,157 @@
+"""``ModelArgs`` / ``csm_1b`` / ``CSM`` -- drop-in for /root/reference/csm_mlx/models.py.
+
+``CSM`` is a host-side handle: the parameters live on the GPU inside the C-ABI
+engine (libcsm_hip.so) once ``load_weights`` has run.  The attribute surface of
+the reference (``n_audio_codebooks``, ``backbone.layers``, ``decoder.layers``,
+``backbone.args`` ..., models.py:31-77) is kept so user code reads the same.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+from typing import Dict, Iterable, Optional, Tuple, Union
+
+import numpy as np
+
+from . import _lib
+from .config import BACKBONE_CONFIGURATION, DECODER_CONFIGURATION, LlamaArgs
+from .rope import llama3_rope_table
+
+
+@dataclass
+class ModelArgs:
+    """models.py:12-18."""
+    backbone_name: str
+    decoder_name: str
+    n_text_vocab: int
+    n_audio_vocab: int
+    n_audio_codebooks: int
+
+
+def csm_1b() -> ModelArgs:
+    """models.py:21-28."""
+    return ModelArgs(backbone_name="1b", decoder_name="100m", n_text_vocab=128256,
+                     n_audio_vocab=2051, n_audio_codebooks=32)
+
+
+def csm_tiny() -> ModelArgs:
+    """Test-only toy model with the reference's head geometry (4 codebooks, 64-entry Mimi codebooks)."""
+    return ModelArgs(backbone_name="tiny", decoder_name="tiny", n_text_vocab=1000,
+                     n_audio_vocab=67, n_audio_codebooks=4)
+
+
+class _Layer:
+    """Placeholder for one transformer block (weights live in the engine)."""
+
+
+class _StackView:
+    def __init__(self, args: LlamaArgs):
+        self.args = args
+        self.layers = [_Layer() for _ in range(args.num_hidden_layers)]
+
+
+def _llama_dims(a: LlamaArgs) -> _lib.CsmLlamaDims:
+    return _lib.CsmLlamaDims(a.num_hidden_layers, a.hidden_size, a.num_attention_heads, a.num_key_value_heads,
+                             a.head_dim, a.intermediate_size, a.rms_norm_eps)
+
+
+def default_device() -> int:
+    return int(os.environ.get("LOCAL_RANK", os.environ.get("CSM_DEVICE", "0")))
+
+
+class CSM:
+    """models.py:31-92.  ``dtype`` selects weight storage: "bf16" (perf) or "float32" (parity)."""
+
+    def __init__(self, args: ModelArgs, *, dtype: str = "bf16", device: Optional[int] = None, max_batch: int = 1):
+        self.args = args
+        self.n_text_vocab = args.n_text_vocab
+        self.n_audio_vocab = args.n_audio_vocab
+        self.n_audio_codebooks = args.n_audio_codebooks
+        bb = BACKBONE_CONFIGURATION[args.backbone_name]
+        dec = DECODER_CONFIGURATION[args.decoder_name]
+        self.n_backbone_embedding = bb.num_attention_heads * (bb.head_dim or 0)
+        self.n_decoder_embedding = dec.num_attention_heads * (dec.head_dim or 0)
+        self.backbone = _StackView(bb)
+        self.decoder = _StackView(dec)
+        if dtype not in ("bf16", "bfloat16", "float32", "f32"):
+            raise ValueError(f"unsupported dtype {dtype}")
+        self.dtype = "float32" if dtype in ("float32", "f32") else "bf16"
+        self.device = default_device() if device is None else device
+        self.max_seq_len = bb.max_position_embeddings or 2048      # generation.py:132
+        self._max_batch = max_batch
+        self._engine = None
+        self._loaded = set()
+
+    # ------------------------------------------------------------------ engine
+    def _dims(self) -> _lib.CsmDims:
+        return _lib.CsmDims(_llama_dims(self.backbone.args), _llama_dims(self.decoder.args), self.n_text_vocab,
+                            self.n_audio_vocab, self.n_audio_codebooks, self.max_seq_len)
+
+    @property
+    def engine(self):
+        if self._engine is None:
+            L = _lib.lib()
+            h = ctypes.c_void_p()
+            wdt = _lib.CSM_F32 if self.dtype == "float32" else _lib.CSM_BF16
+            _lib.check(L.csm_engine_create(ctypes.byref(self._dims()), self.device, wdt, self._max_batch,
+                                           self.max_seq_len, ctypes.byref(h)))
+            self._engine = h
+            for which, st in ((0, self.backbone.args), (1, self.decoder.args)):
+                t = llama3_rope_table(st, self.max_seq_len)
+                _lib.check(L.csm_set_rope_table(h, which, _lib.ptr(t), t.shape[0], st.head_dim))
+        return self._engine
+
+    def __del__(self):
+        try:
+            if self._engine is not None:
+                _lib.lib().csm_engine_destroy(self._engine)
+                self._engine = None
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ weights
+    def load_weights(self, file_or_weights: Union[str, Iterable[Tuple[str, np.ndarray]], Dict[str, np.ndarray]],
+                     strict: bool = True):
+        """MLX ``Module.load_weights``: a .safetensors/.npz path or (name, array) pairs."""
+        if isinstance(file_or_weights, (str, os.PathLike)):
+            items = _read_weight_file(str(file_or_weights))
+        elif isinstance(file_or_weights, dict):
+            items = file_or_weights.items()
+        else:
+            items = file_or_weights
+        L = _lib.lib()
+        eng = self.engine
+        for name, arr in items:
+            a, dt = _lib.host_tensor(arr)
+            rc = L.csm_load_tensor(eng, name.encode(), _lib.ptr(a), dt, _lib.shape_arr(a.shape), a.ndim)
+            if rc == _lib.CSM_ERR_ARG and not strict and "unknown tensor" in L.csm_last_error().decode():
+                continue
+            _lib.check(rc)
+            self._loaded.add(name)
+        if strict:
+            _lib.check(L.csm_weights_ready(eng))
+        return self
+
+    def embed_audio(self, codebook: int, tokens):
+        raise NotImplementedError("embeddings are gathered inside the HIP frame graph (models.py:79-80)")
+
+    def embed_tokens(self, tokens):
+        raise NotImplementedError("embeddings are gathered inside the HIP frame graph (models.py:82-92)")
+
+
+def _read_weight_file(path: str):
+    if path.endswith(".npz"):
+        with np.load(path, allow_pickle=False) as z:
+            for k in z.files:
+                yield k, z[k]
+        return
+    from safetensors import safe_open
+    with safe_open(path, framework="pt") as f:
+        import torch
+        for k in f.keys():
+            t = f.get_tensor(k)
+            if t.dtype == torch.bfloat16:
+                yield k, t.view(torch.uint16).numpy()
+            else:
+                yield k, t.float().numpy()

@@ -1,0 +1,83 @@
+// Shared device helpers for the CSM / Mimi HIP kernels (gfx950, wave64).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define CSM_WAVE 64
+
+typedef uint16_t bf16_t;  // raw bf16 bits; weights are stored as bf16 or f32
+
+__device__ __forceinline__ float bf16_lo(uint32_t u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float bf16_hi(uint32_t u) { return __uint_as_float(u & 0xffff0000u); }
+__device__ __forceinline__ float bf16_to_f32(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+
+// Load 8 consecutive weights starting at p (16-B aligned for bf16, 32-B for f32) as floats.
+template <typename WT> struct W8;
+template <> struct W8<bf16_t> {
+  __device__ __forceinline__ static void load(const bf16_t* p, float (&w)[8]) {
+    const uint4 u = *reinterpret_cast<const uint4*>(p);
+    w[0] = bf16_lo(u.x); w[1] = bf16_hi(u.x); w[2] = bf16_lo(u.y); w[3] = bf16_hi(u.y);
+    w[4] = bf16_lo(u.z); w[5] = bf16_hi(u.z); w[6] = bf16_lo(u.w); w[7] = bf16_hi(u.w);
+  }
+};
+template <> struct W8<float> {
+  __device__ __forceinline__ static void load(const float* p, float (&w)[8]) {
+    const float4 a = *reinterpret_cast<const float4*>(p);
+    const float4 b = *reinterpret_cast<const float4*>(p + 4);
+    w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w; w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+  }
+};
+
+template <typename WT> __device__ __forceinline__ float ld1(const WT* p);
+template <> __device__ __forceinline__ float ld1<float>(const float* p) { return *p; }
+template <> __device__ __forceinline__ float ld1<bf16_t>(const bf16_t* p) { return bf16_to_f32(*p); }
+
+template <typename T> __device__ __forceinline__ T st_cast(float v);
+template <> __device__ __forceinline__ float st_cast<float>(float v) { return v; }
+template <> __device__ __forceinline__ bf16_t st_cast<bf16_t>(float v) {
+  uint32_t u = __float_as_uint(v);
+  u = (u + 0x7FFFu + ((u >> 16) & 1u)) >> 16;  // RNE (inputs are finite)
+  return (bf16_t)u;
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, CSM_WAVE);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, CSM_WAVE));
+  return v;
+}
+
+__device__ __forceinline__ float silu_f(float x) { return x / (1.0f + expf(-x)); }
+__device__ __forceinline__ float gelu_tanh_f(float x) {
+  const float c = 0.7978845608028654f;  // sqrt(2/pi)
+  return 0.5f * x * (1.0f + tanhf(c * (x + 0.044715f * x * x * x)));
+}
+__device__ __forceinline__ float gelu_erf_f(float x) { return 0.5f * x * (1.0f + erff(x * 0.7071067811865476f)); }
+__device__ __forceinline__ float elu_f(float x) { return x > 0.f ? x : expm1f(x); }
+
+// Row -> (utterance, position) map shared by the projection epilogues and attention.
+//   b(m)   = b_off + m / T
+//   pos(m) = (pos_arr ? pos_arr[b(m)] : 0) + pos_const + m % T
+struct RowMap {
+  int T;
+  int b_off;
+  const int* pos_arr;
+  int pos_const;
+  __device__ __forceinline__ int b(int m) const { return b_off + m / T; }
+  __device__ __forceinline__ int pos(int m) const {
+    const int bb = b(m);
+    return (pos_arr ? pos_arr[bb] : 0) + pos_const + m % T;
+  }
+};
+
+// splitmix64 -- the sampler's counter-based RNG (restated in oracle/csm_oracle.py:gumbel_u)
+__host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}

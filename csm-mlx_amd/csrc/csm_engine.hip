@@ -1,0 +1,680 @@
+// CSM engine: device-resident weights, KV caches and the graph-captured frame loop behind
+// the C ABI of include/csm_hip.h.
+//
+// One frame (generation.py:21-92) is two captured HIP graphs replayed back to back:
+//   body : embed(previous codes) -> 16 backbone layers (M = B rows) -> final RMSNorm -> h_last
+//   head : c0 head -> sample c0 (+ gather decoder rows) -> 31 x [projection -> 4 decoder layers
+//          -> ci head -> sample ci (+ gather next row)] -> advance (history, EOS, frame counter)
+// All per-frame state (positions, codes, frame counter) lives in device memory so the same
+// graphs replay every frame without host involvement; the host only polls EOS flags.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <memory>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "../../include/csm_hip.h"
+#include "csm_kernels.h"
+#include "engine_util.h"
+
+namespace {
+
+struct LayerW {
+  void* wqkv = nullptr;  // [(Hq+2Hkv)*hd][D]
+  void* wo = nullptr;    // [D][Hq*hd]
+  void* wgu = nullptr;   // [2F][D] rows interleaved gate_j, up_j
+  void* wd = nullptr;    // [D][F]
+  float* n1 = nullptr;
+  float* n2 = nullptr;
+  float* kc = nullptr;   // [B][Hkv][S][hd]
+  float* vc = nullptr;
+};
+
+struct Stack {
+  csm_llama_dims d;
+  std::vector<LayerW> L;
+  float* norm = nullptr;
+  float* rope = nullptr;  // [S][hd/2][2]
+  int S_cap = 0;
+  int qkv_rows() const { return (d.n_heads + 2 * d.n_kv_heads) * d.head_dim; }
+  int q_dim() const { return d.n_heads * d.head_dim; }
+};
+
+}  // namespace
+
+struct csm_engine {
+  csm_dims dims;
+  int dev = 0;
+  int wdt = WDT_BF16;
+  size_t wsz = 2;
+  int B_max = 0, F_cap = 0, M_cap = 0;
+  hipStream_t st = nullptr;
+  Stack bb, dec;
+  int V = 0, Vpad = 0, K = 0, D = 0, Dd = 0;
+  void* text_emb = nullptr;
+  void* audio_emb = nullptr;
+  void* proj = nullptr;      // [Dd][D]
+  void* c0_head = nullptr;   // [Vpad][D]
+  void* audio_head = nullptr;  // [K-1][Vpad][Dd]
+  std::set<std::string> loaded;
+  std::vector<std::string> required;
+  // activations
+  float *x = nullptr, *q = nullptr, *att = nullptr, *mlp = nullptr;
+  float *h_last = nullptr, *c0_logits = nullptr, *ci_logits = nullptr;
+  float *dx = nullptr, *din = nullptr, *dq = nullptr, *datt = nullptr, *dmlp = nullptr;
+  int32_t* tok = nullptr;
+  uint8_t* msk = nullptr;
+  // per-batch state
+  int *codes = nullptr, *hist = nullptr, *pos = nullptr, *n_frames = nullptr, *frame_ctr = nullptr;
+  uint8_t* done = nullptr;
+  uint64_t* seeds = nullptr;
+  int B = 0;
+  float temperature = 0.f;
+  int top_k = 0;
+  int frames_run = 0;
+  bool need_body = false;
+  std::vector<int> prompt_len;
+  // graphs
+  hipGraphExec_t g_body = nullptr, g_head = nullptr;
+  int g_B = -1;
+  float g_temp = -1.f;
+  int g_topk = -1;
+  std::vector<void*> allocs;
+  std::vector<void*> batch_allocs;
+  std::vector<int> pos_host;
+
+  void* balloc(size_t bytes) {
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) throw CsmError(CSM_ERR_HIP, "hipMalloc(" + std::to_string(bytes) + ") failed");
+    (void)hipMemset(p, 0, bytes);
+    batch_allocs.push_back(p);
+    return p;
+  }
+  void* alloc(size_t bytes) {
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) throw CsmError(CSM_ERR_HIP, "hipMalloc(" + std::to_string(bytes) + ") failed");
+    (void)hipMemset(p, 0, bytes);
+    allocs.push_back(p);
+    return p;
+  }
+  ~csm_engine() {
+    if (g_body) (void)hipGraphExecDestroy(g_body);
+    if (g_head) (void)hipGraphExecDestroy(g_head);
+    for (void* p : allocs) (void)hipFree(p);
+    for (void* p : batch_allocs) (void)hipFree(p);
+    if (st) (void)hipStreamDestroy(st);
+  }
+};
+
+// ---------------------------------------------------------------------------------------------
+namespace {
+
+void alloc_stack(csm_engine* e, Stack& s, const csm_llama_dims& d, int S_cap, const char* prefix) {
+  s.d = d;
+  s.S_cap = S_cap;
+  s.L.resize(d.n_layers);
+  const size_t D = d.hidden, F = d.intermediate, hd = d.head_dim;
+  for (int i = 0; i < d.n_layers; ++i) {
+    LayerW& l = s.L[i];
+    l.wqkv = e->alloc((size_t)s.qkv_rows() * D * e->wsz);
+    l.wo = e->alloc(D * (size_t)s.q_dim() * e->wsz);
+    l.wgu = e->alloc(2 * F * D * e->wsz);
+    l.wd = e->alloc(D * F * e->wsz);
+    l.n1 = (float*)e->alloc(D * 4);
+    l.n2 = (float*)e->alloc(D * 4);
+    const std::string p = std::string(prefix) + ".layers." + std::to_string(i);
+    for (const char* n : {".self_attn.q_proj.weight", ".self_attn.k_proj.weight", ".self_attn.v_proj.weight",
+                          ".self_attn.o_proj.weight", ".mlp.gate_proj.weight", ".mlp.up_proj.weight",
+                          ".mlp.down_proj.weight", ".input_layernorm.weight", ".post_attention_layernorm.weight"})
+      e->required.push_back(p + n);
+  }
+  s.norm = (float*)e->alloc(D * 4);
+  s.rope = (float*)e->alloc((size_t)S_cap * hd * 4);
+  e->required.push_back(std::string(prefix) + ".norm.weight");
+}
+
+// One Llama block stack over M rows of the residual stream x (in place).
+void run_stack(csm_engine* e, Stack& s, float* x, int M, float* q, float* att, float* mlp, const RowMap& rm,
+               hipStream_t st) {
+  const csm_llama_dims& d = s.d;
+  const int tag = (&s == &e->dec) ? 1 : 0;
+  const int D = d.hidden, F = d.intermediate, hd = d.head_dim, Hq = d.n_heads, Hkv = d.n_kv_heads;
+  for (int i = 0; i < d.n_layers; ++i) {
+    LayerW& l = s.L[i];
+    GemvParams g{};
+    // norm1 + QKV + RoPE + KV append
+    g.W = l.wqkv; g.N = s.qkv_rows(); g.K = D; g.x = x; g.xs = D; g.M = M; g.nw = l.n1; g.eps = d.eps;
+    g.out = q; g.os = s.q_dim(); g.Hq = Hq; g.Hkv = Hkv; g.hd = hd; g.S_cap = s.S_cap; g.rope = s.rope;
+    g.kc = l.kc; g.vc = l.vc; g.rm = rm;
+    launch_gemv(g, e->wdt, EPI_QKV, 1, st, tag);
+    // attention
+    AttnParams a{};
+    a.q = q; a.qs = s.q_dim(); a.M = M; a.kc = l.kc; a.vc = l.vc; a.Hq = Hq; a.Hkv = Hkv; a.S_cap = s.S_cap;
+    a.scale = 1.0f / sqrtf((float)hd); a.mode = ATTN_CAUSAL; a.window = 0; a.rm = rm; a.out = att;
+    a.os = s.q_dim();
+    launch_attn(a, hd, st);
+    // o_proj + residual
+    g = GemvParams{};
+    g.W = l.wo; g.N = D; g.K = s.q_dim(); g.x = att; g.xs = s.q_dim(); g.M = M; g.out = x; g.os = D;
+    launch_gemv(g, e->wdt, EPI_ADD, 0, st, tag);
+    // norm2 + gate/up + SiLU*up
+    g = GemvParams{};
+    g.W = l.wgu; g.N = 2 * F; g.K = D; g.x = x; g.xs = D; g.M = M; g.nw = l.n2; g.eps = d.eps; g.out = mlp;
+    g.os = F;
+    launch_gemv(g, e->wdt, EPI_SILU_MUL, 1, st, tag);
+    // down + residual
+    g = GemvParams{};
+    g.W = l.wd; g.N = D; g.K = F; g.x = mlp; g.xs = F; g.M = M; g.out = x; g.os = D;
+    launch_gemv(g, e->wdt, EPI_ADD, 0, st, tag);
+  }
+}
+
+void enqueue_body(csm_engine* e, hipStream_t st) {
+  const int B = e->B;
+  EmbedParams ep{};
+  ep.codes = e->codes; ep.text_emb = e->text_emb; ep.audio_emb = e->audio_emb; ep.V = e->V; ep.K = e->K;
+  ep.D = e->D; ep.out = e->x; ep.pos_inc = e->pos;
+  launch_embed(ep, e->wdt, B, st);
+  RowMap rm{1, 0, e->pos, 0};
+  run_stack(e, e->bb, e->x, B, e->q, e->att, e->mlp, rm, st);
+  launch_rmsnorm_rows(e->x, e->D, e->bb.norm, e->bb.d.eps, e->D, e->h_last, e->D, B, st);
+}
+
+void enqueue_head(csm_engine* e, hipStream_t st) {
+  const int B = e->B, K = e->K, D = e->D, Dd = e->Dd, V = e->V, Vp = e->Vpad;
+  // c0 = codebook0_head(h_last)  (generation.py:42)
+  GemvParams g{};
+  g.W = e->c0_head; g.N = Vp; g.K = D; g.x = e->h_last; g.xs = D; g.M = B; g.out = e->c0_logits; g.os = Vp;
+  launch_gemv(g, e->wdt, EPI_STORE, 0, st);
+  SampleParams sp{};
+  sp.logits = e->c0_logits; sp.ls = Vp; sp.V = V; sp.temperature = e->temperature; sp.top_k = e->top_k;
+  sp.seeds = e->seeds; sp.frame_ctr = e->frame_ctr; sp.K = K; sp.cb = 0; sp.codes = e->codes;
+  sp.next_in = e->din; sp.h_last = e->h_last; sp.audio_emb = e->audio_emb; sp.V_emb = V; sp.D = D;
+  launch_sample(sp, e->wdt, B, st);
+  for (int i = 1; i < K; ++i) {
+    const int M = (i == 1) ? 2 * B : B;
+    // decoder(projection(decoder_inputs))  (generation.py:74-77); fresh KV each frame (:70)
+    g = GemvParams{};
+    g.W = e->proj; g.N = Dd; g.K = D; g.x = e->din; g.xs = D; g.M = M; g.out = e->dx; g.os = Dd;
+    launch_gemv(g, e->wdt, EPI_STORE, 0, st);
+    RowMap rm = (i == 1) ? RowMap{2, 0, nullptr, 0} : RowMap{1, 0, nullptr, i};
+    run_stack(e, e->dec, e->dx, M, e->dq, e->datt, e->dmlp, rm, st);
+    // ci_logits = norm(hidden[:, -1]) @ audio_head[i-1]  (generation.py:79)
+    g = GemvParams{};
+    g.W = (const char*)e->audio_head + (size_t)(i - 1) * Vp * Dd * e->wsz; g.N = Vp; g.K = Dd;
+    g.x = e->dx + (i == 1 ? Dd : 0); g.xs = (i == 1 ? 2 * Dd : Dd); g.M = B; g.nw = e->dec.norm;
+    g.eps = e->dec.d.eps; g.out = e->ci_logits + (size_t)(i - 1) * B * Vp; g.os = Vp;
+    launch_gemv(g, e->wdt, EPI_STORE, 1, st);
+    sp.logits = e->ci_logits + (size_t)(i - 1) * B * Vp;
+    sp.cb = i;
+    sp.next_in = (i + 1 < K) ? e->din : nullptr;
+    launch_sample(sp, e->wdt, B, st);
+  }
+  AdvanceParams ap{};
+  ap.codes = e->codes; ap.hist = e->hist; ap.F_cap = e->F_cap; ap.B = B; ap.K = K; ap.done = e->done;
+  ap.n_frames = e->n_frames; ap.frame_ctr = e->frame_ctr;
+  launch_advance(ap, st);
+}
+
+hipGraphExec_t capture(csm_engine* e, void (*fn)(csm_engine*, hipStream_t)) {
+  hipGraph_t graph;
+  HIPCHK(hipStreamBeginCapture(e->st, hipStreamCaptureModeThreadLocal));
+  fn(e, e->st);
+  HIPCHK(hipStreamEndCapture(e->st, &graph));
+  hipGraphExec_t exec;
+  HIPCHK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+  (void)hipGraphDestroy(graph);
+  return exec;
+}
+
+// (Re)allocate everything sized by the batch: KV caches, decoder activations, code history.
+void ensure_batch(csm_engine* e, int B) {
+  if (B <= e->B_max && !e->batch_allocs.empty()) return;
+  HIPCHK(hipDeviceSynchronize());
+  for (void* p : e->batch_allocs) (void)hipFree(p);
+  e->batch_allocs.clear();
+  if (e->g_body) { (void)hipGraphExecDestroy(e->g_body); e->g_body = nullptr; }
+  if (e->g_head) { (void)hipGraphExecDestroy(e->g_head); e->g_head = nullptr; }
+  e->g_B = -1;
+  e->B_max = std::max(B, e->B_max);
+  const size_t Bm = e->B_max, D = e->D, Dd = e->Dd, K = e->K, Vp = e->Vpad;
+  for (Stack* s : {&e->bb, &e->dec}) {
+    const size_t kv = Bm * s->d.n_kv_heads * (size_t)s->S_cap * s->d.head_dim * 4;
+    for (LayerW& l : s->L) {
+      l.kc = (float*)e->balloc(kv);
+      l.vc = (float*)e->balloc(kv);
+    }
+  }
+  e->h_last = (float*)e->balloc(Bm * D * 4);
+  e->c0_logits = (float*)e->balloc(Bm * Vp * 4);
+  e->ci_logits = (float*)e->balloc((K - 1) * Bm * Vp * 4);
+  e->dx = (float*)e->balloc(2 * Bm * Dd * 4);
+  e->din = (float*)e->balloc(2 * Bm * D * 4);
+  e->dq = (float*)e->balloc(2 * Bm * e->dec.q_dim() * 4);
+  e->datt = (float*)e->balloc(2 * Bm * e->dec.q_dim() * 4);
+  e->dmlp = (float*)e->balloc(2 * Bm * (size_t)e->dec.d.intermediate * 4);
+  e->codes = (int*)e->balloc(Bm * K * 4);
+  e->hist = (int*)e->balloc((size_t)e->F_cap * Bm * K * 4);
+  e->pos = (int*)e->balloc(Bm * 4);
+  e->n_frames = (int*)e->balloc(Bm * 4);
+  e->done = (uint8_t*)e->balloc(Bm);
+  e->seeds = (uint64_t*)e->balloc(Bm * 8);
+}
+
+}  // namespace
+
+// =============================================================================== C ABI
+extern "C" {
+
+int csm_device_count(int* n) {
+  CSM_TRY {
+    int c = 0;
+    HIPCHK(hipGetDeviceCount(&c));
+    if (n) *n = c;
+  }
+  CSM_CATCH
+}
+
+int csm_engine_create(const csm_dims* dims, int device, int weight_dtype, int max_batch, int max_frames,
+                      csm_engine** out) {
+  CSM_TRY {
+    if (!dims || !out || max_batch <= 0 || max_frames <= 0) throw CsmError(CSM_ERR_ARG, "bad engine arguments");
+    const csm_llama_dims& b = dims->backbone;
+    const csm_llama_dims& d = dims->decoder;
+    for (const csm_llama_dims* x : {&b, &d}) {
+      if (x->head_dim != 64 && x->head_dim != 128) throw CsmError(CSM_ERR_ARG, "head_dim must be 64 or 128");
+      if (x->hidden % 256 || x->intermediate % 256 || (x->n_heads * x->head_dim) % 256)
+        throw CsmError(CSM_ERR_ARG, "hidden/intermediate widths must be multiples of 256");
+      if (x->n_heads % x->n_kv_heads) throw CsmError(CSM_ERR_ARG, "n_heads % n_kv_heads != 0");
+    }
+    if (b.n_heads * b.head_dim != b.hidden) throw CsmError(CSM_ERR_ARG, "backbone hidden != heads*head_dim");
+    HIPCHK(hipSetDevice(device));
+    std::unique_ptr<csm_engine> e(new csm_engine());
+    e->dims = *dims;
+    e->dev = device;
+    e->wdt = weight_dtype == CSM_F32 ? WDT_F32 : WDT_BF16;
+    e->wsz = e->wdt == WDT_F32 ? 4 : 2;
+    e->B_max = max_batch;
+    e->F_cap = max_frames;
+    e->K = dims->n_audio_codebooks;
+    e->V = dims->n_audio_vocab;
+    e->Vpad = (e->V + 7) / 8 * 8;
+    e->D = b.hidden;
+    e->Dd = d.hidden;
+    const int S = dims->max_seq_len;
+    e->M_cap = std::max(S, 2 * max_batch);
+    HIPCHK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
+    alloc_stack(e.get(), e->bb, b, S, "backbone");
+    alloc_stack(e.get(), e->dec, d, e->K, "decoder");
+    const size_t D = e->D, Dd = e->Dd, K = e->K, Vp = e->Vpad, B = max_batch;
+    e->text_emb = e->alloc((size_t)dims->n_text_vocab * D * e->wsz);
+    e->audio_emb = e->alloc((size_t)e->V * K * D * e->wsz);
+    e->proj = e->alloc(Dd * D * e->wsz);
+    e->c0_head = e->alloc(Vp * D * e->wsz);
+    e->audio_head = e->alloc((K - 1) * Vp * Dd * e->wsz);
+    for (const char* n : {"text_embeddings.weight", "audio_embeddings.weight", "projection.weight",
+                          "codebook0_head.weight", "audio_head"})
+      e->required.push_back(n);
+    const size_t M = e->M_cap;
+    e->x = (float*)e->alloc(M * D * 4);
+    e->q = (float*)e->alloc(M * e->bb.q_dim() * 4);
+    e->att = (float*)e->alloc(M * e->bb.q_dim() * 4);
+    e->mlp = (float*)e->alloc(M * b.intermediate * 4);
+    e->tok = (int32_t*)e->alloc(M * (K + 1) * 4);
+    e->msk = (uint8_t*)e->alloc(M * (K + 1));
+    e->frame_ctr = (int*)e->alloc(16);
+    (void)Vp;
+    (void)B;
+    ensure_batch(e.get(), max_batch);
+    HIPCHK(hipDeviceSynchronize());
+    *out = e.release();
+  }
+  CSM_CATCH
+}
+
+int csm_engine_destroy(csm_engine* e) {
+  CSM_TRY { delete e; }
+  CSM_CATCH
+}
+
+int csm_set_rope_table(csm_engine* e, int which, const float* table, int n_pos, int head_dim) {
+  CSM_TRY {
+    Stack& s = which == 0 ? e->bb : e->dec;
+    if (head_dim != s.d.head_dim || n_pos < s.S_cap) throw CsmError(CSM_ERR_ARG, "rope table shape mismatch");
+    HIPCHK(hipSetDevice(e->dev));
+    HIPCHK(hipMemcpy(s.rope, table, (size_t)s.S_cap * head_dim * 4, hipMemcpyHostToDevice));
+  }
+  CSM_CATCH
+}
+
+int csm_load_tensor(csm_engine* e, const char* cname, const void* host, int src_dtype, const int64_t* shape,
+                    int ndim) {
+  CSM_TRY {
+    HIPCHK(hipSetDevice(e->dev));
+    const std::string name(cname);
+    std::vector<int64_t> shp(shape, shape + ndim);
+    auto numel = [&]() { int64_t n = 1; for (auto s : shp) n *= s; return (size_t)n; };
+    auto expect = [&](std::initializer_list<int64_t> want) {
+      if (shp != std::vector<int64_t>(want)) throw CsmError(CSM_ERR_ARG, "shape mismatch for " + name);
+    };
+    const size_t es = e->wsz;
+    auto conv = [&](size_t n) { return convert_to(host, src_dtype, n, e->wdt); };
+    auto conv_f32 = [&](size_t n) { return convert_to(host, src_dtype, n, WDT_F32); };
+
+    // --- stack parameters
+    for (int which = 0; which < 2; ++which) {
+      Stack& s = which == 0 ? e->bb : e->dec;
+      const std::string pre = which == 0 ? "backbone." : "decoder.";
+      if (name.rfind(pre, 0) != 0) continue;
+      const int D = s.d.hidden, F = s.d.intermediate, hd = s.d.head_dim;
+      const int qd = s.q_dim(), kvd = s.d.n_kv_heads * hd;
+      if (name == pre + "norm.weight") {
+        expect({D});
+        auto h = conv_f32(D);
+        HIPCHK(hipMemcpy(s.norm, h.data(), D * 4, hipMemcpyHostToDevice));
+        e->loaded.insert(name);
+        return CSM_OK;
+      }
+      int li = -1;
+      char tail[128] = {0};
+      if (sscanf(name.c_str() + pre.size(), "layers.%d.%127s", &li, tail) != 2 || li < 0 || li >= s.d.n_layers)
+        throw CsmError(CSM_ERR_ARG, "unknown tensor " + name);
+      LayerW& l = s.L[li];
+      const std::string t(tail);
+      if (t == "self_attn.q_proj.weight") {
+        expect({qd, D});
+        auto h = conv(numel());
+        HIPCHK(hipMemcpy(l.wqkv, h.data(), h.size(), hipMemcpyHostToDevice));
+      } else if (t == "self_attn.k_proj.weight" || t == "self_attn.v_proj.weight") {
+        expect({kvd, D});
+        auto h = conv(numel());
+        const size_t row0 = qd + (t[10] == 'k' ? 0 : kvd);
+        HIPCHK(hipMemcpy((char*)l.wqkv + row0 * D * es, h.data(), h.size(), hipMemcpyHostToDevice));
+      } else if (t == "self_attn.o_proj.weight") {
+        expect({D, qd});
+        auto h = conv(numel());
+        HIPCHK(hipMemcpy(l.wo, h.data(), h.size(), hipMemcpyHostToDevice));
+      } else if (t == "mlp.gate_proj.weight" || t == "mlp.up_proj.weight") {
+        expect({F, D});
+        auto h = conv(numel());
+        const size_t off = (t[4] == 'g') ? 0 : 1;  // interleave: row 2j gate, 2j+1 up
+        HIPCHK(hipMemcpy2D((char*)l.wgu + off * D * es, 2 * D * es, h.data(), D * es, D * es, F,
+                           hipMemcpyHostToDevice));
+      } else if (t == "mlp.down_proj.weight") {
+        expect({D, F});
+        auto h = conv(numel());
+        HIPCHK(hipMemcpy(l.wd, h.data(), h.size(), hipMemcpyHostToDevice));
+      } else if (t == "input_layernorm.weight" || t == "post_attention_layernorm.weight") {
+        expect({D});
+        auto h = conv_f32(D);
+        HIPCHK(hipMemcpy(t[0] == 'i' ? l.n1 : l.n2, h.data(), D * 4, hipMemcpyHostToDevice));
+      } else {
+        throw CsmError(CSM_ERR_ARG, "unknown tensor " + name);
+      }
+      e->loaded.insert(name);
+      return CSM_OK;
+    }
+    const int64_t D = e->D, Dd = e->Dd, V = e->V, K = e->K, Vp = e->Vpad;
+    if (name == "text_embeddings.weight") {
+      expect({e->dims.n_text_vocab, D});
+      auto h = conv(numel());
+      HIPCHK(hipMemcpy(e->text_emb, h.data(), h.size(), hipMemcpyHostToDevice));
+    } else if (name == "audio_embeddings.weight") {
+      expect({V * K, D});
+      auto h = conv(numel());
+      HIPCHK(hipMemcpy(e->audio_emb, h.data(), h.size(), hipMemcpyHostToDevice));
+    } else if (name == "projection.weight") {
+      expect({Dd, D});
+      auto h = conv(numel());
+      HIPCHK(hipMemcpy(e->proj, h.data(), h.size(), hipMemcpyHostToDevice));
+    } else if (name == "codebook0_head.weight") {
+      expect({V, D});
+      auto h = conv(numel());  // rows V..Vpad stay zero (padding)
+      HIPCHK(hipMemcpy(e->c0_head, h.data(), h.size(), hipMemcpyHostToDevice));
+    } else if (name == "audio_head") {
+      expect({K - 1, Dd, V});
+      // (in,out) layout -> per-codebook (out,in) GEMV rows: [K-1][Vpad][Dd]
+      auto f = conv_f32(numel());
+      const float* src = reinterpret_cast<const float*>(f.data());
+      std::vector<float> t((size_t)(K - 1) * Vp * Dd, 0.f);
+      for (int64_t c = 0; c < K - 1; ++c)
+        for (int64_t i = 0; i < Dd; ++i)
+          for (int64_t v = 0; v < V; ++v) t[((size_t)c * Vp + v) * Dd + i] = src[((size_t)c * Dd + i) * V + v];
+      auto h = convert_to(t.data(), CSM_F32, t.size(), e->wdt);
+      HIPCHK(hipMemcpy(e->audio_head, h.data(), h.size(), hipMemcpyHostToDevice));
+    } else {
+      throw CsmError(CSM_ERR_ARG, "unknown tensor " + name);
+    }
+    e->loaded.insert(name);
+  }
+  CSM_CATCH
+}
+
+int csm_weights_ready(csm_engine* e) {
+  CSM_TRY {
+    for (const auto& n : e->required)
+      if (!e->loaded.count(n)) throw CsmError(CSM_ERR_STATE, "missing weight " + n);
+  }
+  CSM_CATCH
+}
+
+int csm_begin(csm_engine* e, int B, const uint64_t* seeds, float temperature, int top_k) {
+  CSM_TRY {
+    if (B <= 0) throw CsmError(CSM_ERR_ARG, "batch size out of range");
+    if (temperature < 0.f) throw CsmError(CSM_ERR_ARG, "temperature must be >= 0");
+    HIPCHK(hipSetDevice(e->dev));
+    ensure_batch(e, B);
+    e->pos_host.assign(B, -1);
+    e->B = B;
+    e->temperature = temperature;
+    e->top_k = top_k;
+    e->frames_run = 0;
+    e->need_body = false;
+    e->prompt_len.assign(B, -1);
+    std::vector<uint64_t> s(B, 0);
+    if (seeds) memcpy(s.data(), seeds, B * 8);
+    HIPCHK(hipMemcpyAsync(e->seeds, s.data(), B * 8, hipMemcpyHostToDevice, e->st));
+    HIPCHK(hipMemsetAsync(e->done, 0, B, e->st));
+    HIPCHK(hipMemsetAsync(e->n_frames, 0, B * 4, e->st));
+    HIPCHK(hipMemsetAsync(e->frame_ctr, 0, 16, e->st));
+    HIPCHK(hipMemsetAsync(e->codes, 0, (size_t)B * e->K * 4, e->st));
+    HIPCHK(hipStreamSynchronize(e->st));
+  }
+  CSM_CATCH
+}
+
+int csm_prefill(csm_engine* e, int b, int T, const int32_t* tokens, const uint8_t* mask) {
+  CSM_TRY {
+    if (b < 0 || b >= e->B) throw CsmError(CSM_ERR_ARG, "utterance index out of range");
+    if (T <= 0 || T > e->M_cap) throw CsmError(CSM_ERR_ARG, "prompt length out of range");
+    const int start = e->pos_host[b] + 1;  // rows append after what the backbone already holds
+    if (start + T > e->dims.max_seq_len)
+      throw CsmError(CSM_ERR_TOO_LONG, "rows exceed the 2048-position window");
+    HIPCHK(hipSetDevice(e->dev));
+    const int K = e->K;
+    HIPCHK(hipMemcpyAsync(e->tok, tokens, (size_t)T * (K + 1) * 4, hipMemcpyHostToDevice, e->st));
+    HIPCHK(hipMemcpyAsync(e->msk, mask, (size_t)T * (K + 1), hipMemcpyHostToDevice, e->st));
+    EmbedParams ep{};
+    ep.tok = e->tok; ep.mask = e->msk; ep.text_emb = e->text_emb; ep.audio_emb = e->audio_emb; ep.V = e->V;
+    ep.K = K; ep.D = e->D; ep.out = e->x;
+    launch_embed(ep, e->wdt, T, e->st);
+    RowMap rm{T, b, nullptr, start};
+    run_stack(e, e->bb, e->x, T, e->q, e->att, e->mlp, rm, e->st);
+    launch_rmsnorm_rows(e->x + (size_t)(T - 1) * e->D, e->D, e->bb.norm, e->bb.d.eps, e->D,
+                        e->h_last + (size_t)b * e->D, e->D, 1, e->st);
+    e->pos_host[b] = start + T - 1;  // position of the last processed backbone row
+    HIPCHK(hipMemcpyAsync(e->pos + b, &e->pos_host[b], 4, hipMemcpyHostToDevice, e->st));
+    HIPCHK(hipStreamSynchronize(e->st));
+    HIPCHK(hipGetLastError());
+    e->prompt_len[b] = std::max(e->prompt_len[b], 0) + T;
+    e->need_body = false;
+  }
+  CSM_CATCH
+}
+
+int csm_run_frames(csm_engine* e, int nframes, int* all_done) {
+  CSM_TRY {
+    for (int b = 0; b < e->B; ++b)
+      if (e->prompt_len[b] < 0) throw CsmError(CSM_ERR_STATE, "csm_prefill not called for every utterance");
+    HIPCHK(hipSetDevice(e->dev));
+    if (e->frames_run + nframes > e->F_cap) nframes = e->F_cap - e->frames_run;
+    int maxpos = 0;
+    for (int b = 0; b < e->B; ++b) maxpos = std::max(maxpos, e->pos_host[b]);
+    if (maxpos + nframes + (e->need_body ? 1 : 0) > e->dims.max_seq_len)
+      throw CsmError(CSM_ERR_TOO_LONG, "frames exceed the 2048-position window");
+    if (nframes <= 0) { if (all_done) *all_done = 0; return CSM_OK; }
+    // CSM_GRAPH=0: eager launches of the same kernels (rocprofv3 kernel tracing of graph
+    // replays crashes on ROCm 7.2, so profiling runs use this mode).
+    static const bool use_graph = [] {
+      const char* v = getenv("CSM_GRAPH");
+      return !(v && v[0] == '0');
+    }();
+    if (!use_graph) {
+      for (int f = 0; f < nframes; ++f) {
+        if (e->need_body) {
+          enqueue_body(e, e->st);
+          for (int b = 0; b < e->B; ++b) e->pos_host[b] += 1;
+        }
+        enqueue_head(e, e->st);
+        e->need_body = true;
+        e->frames_run++;
+      }
+      HIPCHK(hipGetLastError());
+      nframes = 0;
+    }
+    if (use_graph && (e->g_B != e->B || e->g_temp != e->temperature || e->g_topk != e->top_k || !e->g_head)) {
+      if (e->g_body) (void)hipGraphExecDestroy(e->g_body);
+      if (e->g_head) (void)hipGraphExecDestroy(e->g_head);
+      e->g_body = capture(e, enqueue_body);
+      e->g_head = capture(e, enqueue_head);
+      e->g_B = e->B;
+      e->g_temp = e->temperature;
+      e->g_topk = e->top_k;
+    }
+    for (int f = 0; f < nframes; ++f) {
+      if (e->need_body) {
+        HIPCHK(hipGraphLaunch(e->g_body, e->st));
+        for (int b = 0; b < e->B; ++b) e->pos_host[b] += 1;
+      }
+      HIPCHK(hipGraphLaunch(e->g_head, e->st));
+      e->need_body = true;
+      e->frames_run++;
+    }
+    if (all_done) {
+      std::vector<uint8_t> d(e->B);
+      HIPCHK(hipMemcpyAsync(d.data(), e->done, e->B, hipMemcpyDeviceToHost, e->st));
+      HIPCHK(hipStreamSynchronize(e->st));
+      int all = 1;
+      for (auto v : d) all &= (v != 0);
+      *all_done = all;
+    }
+  }
+  CSM_CATCH
+}
+
+int csm_read_codes(csm_engine* e, int32_t* hist, int32_t* n_frames, uint8_t* done, int* frames_run) {
+  CSM_TRY {
+    HIPCHK(hipSetDevice(e->dev));
+    HIPCHK(hipStreamSynchronize(e->st));
+    if (hist)
+      HIPCHK(hipMemcpy(hist, e->hist, (size_t)e->frames_run * e->B * e->K * 4, hipMemcpyDeviceToHost));
+    if (n_frames) HIPCHK(hipMemcpy(n_frames, e->n_frames, e->B * 4, hipMemcpyDeviceToHost));
+    if (done) HIPCHK(hipMemcpy(done, e->done, e->B, hipMemcpyDeviceToHost));
+    if (frames_run) *frames_run = e->frames_run;
+  }
+  CSM_CATCH
+}
+
+int csm_debug_read(csm_engine* e, const char* what, void* host, int64_t nbytes, int64_t* needed) {
+  CSM_TRY {
+    HIPCHK(hipSetDevice(e->dev));
+    HIPCHK(hipStreamSynchronize(e->st));
+    const std::string w(what);
+    const void* src = nullptr;
+    size_t n = 0;
+    const size_t B = e->B, Vp = e->Vpad;
+    if (w == "h_last") { src = e->h_last; n = B * e->D * 4; }
+    else if (w == "c0_logits") { src = e->c0_logits; n = B * Vp * 4; }
+    else if (w == "ci_logits") { src = e->ci_logits; n = (e->K - 1) * B * Vp * 4; }
+    else if (w == "codes") { src = e->codes; n = B * e->K * 4; }
+    else if (w == "pos") { src = e->pos; n = B * 4; }
+    else throw CsmError(CSM_ERR_ARG, "unknown debug tap " + w);
+    if (needed) *needed = (int64_t)n;
+    if (host) {
+      if ((size_t)nbytes < n) throw CsmError(CSM_ERR_ARG, "debug buffer too small");
+      HIPCHK(hipMemcpy(host, src, n, hipMemcpyDeviceToHost));
+    }
+  }
+  CSM_CATCH
+}
+
+int csm_codes_device_ptr(csm_engine* e, void** p) {
+  CSM_TRY { *p = e->hist; }
+  CSM_CATCH
+}
+
+int csm_bench_gemv(csm_engine* e, int which, int M, int iters, float* avg_us, double* bytes) {
+  CSM_TRY {
+    if (M <= 0 || M > 2 * e->B_max || iters <= 0) throw CsmError(CSM_ERR_ARG, "bad bench arguments");
+    HIPCHK(hipSetDevice(e->dev));
+    Stack& s = (which / 4 == 0) ? e->bb : e->dec;
+    const int tag = (which / 4 == 0) ? 0 : 1;
+    float* x = (which / 4 == 0) ? e->x : e->dx;
+    float* mlp = (which / 4 == 0) ? e->mlp : e->dmlp;
+    const int D = s.d.hidden, F = s.d.intermediate;
+    const int kind = which % 4;
+    if (kind > 1) throw CsmError(CSM_ERR_ARG, "unknown bench kernel");
+    // one launch per layer in turn, as the frame does, so the weight working set (and hence
+    // L2 / Infinity-Cache residency) matches the real frame: backbone 16 x 67 MB streams from
+    // HBM, decoder 4 x 33.5 MB stays within the 256 MiB Infinity Cache.
+    auto params = [&](int layer, int& epi, int& norm) {
+      const LayerW& l = s.L[layer];
+      GemvParams g{};
+      if (kind == 0) {
+        g.W = l.wgu; g.N = 2 * F; g.K = D; g.x = x; g.xs = D; g.M = M; g.nw = l.n2; g.eps = s.d.eps;
+        g.out = mlp; g.os = F; epi = EPI_SILU_MUL; norm = 1;
+      } else {
+        g.W = l.wd; g.N = D; g.K = F; g.x = mlp; g.xs = F; g.M = M; g.out = x; g.os = D; epi = EPI_ADD; norm = 0;
+      }
+      return g;
+    };
+    int epi = 0, norm = 0;
+    GemvParams g = params(0, epi, norm);
+    size_t nbytes = (size_t)g.N * g.K * e->wsz;
+    nbytes += (size_t)M * g.K * 4 + (size_t)M * (epi == EPI_SILU_MUL ? F : D) * 4 * (epi == EPI_ADD ? 2 : 1);
+    const int nl = s.d.n_layers;
+    for (int i = 0; i < nl; ++i) { GemvParams gi = params(i, epi, norm); launch_gemv(gi, e->wdt, epi, norm, e->st, tag); }
+    hipEvent_t a, b;
+    HIPCHK(hipEventCreate(&a));
+    HIPCHK(hipEventCreate(&b));
+    HIPCHK(hipEventRecord(a, e->st));
+    for (int i = 0; i < iters; ++i) { GemvParams gi = params(i % nl, epi, norm); launch_gemv(gi, e->wdt, epi, norm, e->st, tag); }
+    HIPCHK(hipEventRecord(b, e->st));
+    HIPCHK(hipEventSynchronize(b));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, a, b));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    if (avg_us) *avg_us = ms * 1000.f / iters;
+    if (bytes) *bytes = (double)nbytes;
+  }
+  CSM_CATCH
+}
+
+int csm_synchronize(csm_engine* e) {
+  CSM_TRY {
+    HIPCHK(hipSetDevice(e->dev));
+    HIPCHK(hipStreamSynchronize(e->st));
+    HIPCHK(hipGetLastError());
+  }
+  CSM_CATCH
+}
+
+}  // extern "C"

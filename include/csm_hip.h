@@ -1,0 +1,124 @@
+/*
+ * csm_hip.h -- C ABI of libcsm_hip.so, the MI355X (gfx950) engine behind the
+ * csm_mlx drop-in API.  Plain pointers and sizes only; no torch types.
+ *
+ * Every entry point returns 0 on success or a negative csm_status; the message
+ * of the last failure on the calling thread is available from csm_last_error().
+ * The Python layer (csm-mlx_amd/csm_mlx/_lib.py) binds these with ctypes and
+ * maps failures to the reference's exceptions.
+ *
+ * Reference interfaces replaced (all /root/reference/csm_mlx/...):
+ *   csm_engine_create / csm_load_tensor    CSM(args) + Module.load_weights
+ *                                          (models.py:31-77; README.md:38-40)
+ *   csm_set_rope_table                     Llama3ScaledRoPE.rope_init cache (attention.py:57-92)
+ *   csm_begin / csm_prefill                generate(): prompt assembly + first generate_frame
+ *                                          backbone pass (generation.py:108-140)
+ *   csm_run_frames                         the frame loop: generate_frame (generation.py:21-92)
+ *                                          + EOS test (:151) + feedback row (:156-161)
+ *   csm_read_codes                         the stacked samples (generation.py:154, :167-170)
+ *   mimi_*                                 moshi_mlx Mimi encode / decode / decode_step /
+ *                                          reset_state (tokenizers.py:14-21, 61-85, 148-150;
+ *                                          generation.py:224-258)
+ */
+#ifndef CSM_HIP_H
+#define CSM_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum csm_status {
+  CSM_OK = 0,
+  CSM_ERR_ARG = -1,       /* bad argument / shape (ValueError) */
+  CSM_ERR_HIP = -2,       /* HIP runtime failure (RuntimeError) */
+  CSM_ERR_STATE = -3,     /* call out of order, e.g. weights missing */
+  CSM_ERR_TOO_LONG = -4   /* prompt + frames exceed the 2048-position window (generation.py:132-137) */
+};
+
+enum csm_dtype { CSM_F32 = 0, CSM_BF16 = 1 };
+
+typedef struct csm_llama_dims {
+  int n_layers, hidden, n_heads, n_kv_heads, head_dim, intermediate;
+  float eps;
+} csm_llama_dims;
+
+typedef struct csm_dims {
+  csm_llama_dims backbone, decoder;
+  int n_text_vocab, n_audio_vocab, n_audio_codebooks;
+  int max_seq_len; /* RoPE / KV window: 2048 (generation.py:132, attention.py:38) */
+} csm_dims;
+
+typedef struct csm_engine csm_engine;
+
+const char* csm_last_error(void);
+int csm_device_count(int* n);
+
+/* weight_dtype: storage of every Linear/Embedding weight (CSM_F32 parity mode, CSM_BF16 perf). */
+int csm_engine_create(const csm_dims* dims, int device, int weight_dtype, int max_batch, int max_frames,
+                      csm_engine** out);
+int csm_engine_destroy(csm_engine* e);
+/* name: MLX parameter key; host: src_dtype data, C-contiguous, shape as in the checkpoint */
+int csm_load_tensor(csm_engine* e, const char* name, const void* host, int src_dtype, const int64_t* shape,
+                    int ndim);
+/* which: 0 backbone, 1 decoder; table [max_seq_len][head_dim/2][2] = (cos, sin) float32 */
+int csm_set_rope_table(csm_engine* e, int which, const float* table, int n_pos, int head_dim);
+/* returns CSM_ERR_STATE and names the first missing tensor when weights are incomplete */
+int csm_weights_ready(csm_engine* e);
+
+/* Start a batch of B utterances.  temperature 0 = greedy (generation.py:51); top_k 0 = off.
+ * seeds[B]: per-utterance sampling seeds (build's counter-based Gumbel sampler). */
+int csm_begin(csm_engine* e, int B, const uint64_t* seeds, float temperature, int top_k);
+/* Prompt rows of utterance b: tokens/mask [T][K+1] (text id in the last column). */
+int csm_prefill(csm_engine* e, int b, int T, const int32_t* tokens, const uint8_t* mask);
+/* Generate up to nframes frames for the whole batch (one HIP graph replay per frame).
+ * *all_done (optional) = 1 when every utterance hit EOS. */
+int csm_run_frames(csm_engine* e, int nframes, int* all_done);
+/* hist [F][B][K] int32 of the frames generated so far, n_frames[B] emitted frames (EOS excluded),
+ * done[B].  Any pointer may be NULL. */
+int csm_read_codes(csm_engine* e, int32_t* hist, int32_t* n_frames, uint8_t* done, int* frames_run);
+/* Debug / parity taps: "h_last" [B][D], "c0_logits" [B][Vpad], "ci_logits" [K-1][B][Vpad], "codes" [B][K] */
+int csm_debug_read(csm_engine* e, const char* what, void* host, int64_t nbytes, int64_t* needed);
+/* Device pointer of the code history [F][B][K] (for on-device Mimi decode) */
+int csm_codes_device_ptr(csm_engine* e, void** dev_ptr);
+int csm_synchronize(csm_engine* e);
+/* Profiling hook: replay one GEMV of the frame (layer 0) `iters` times on the engine stream,
+ * timed with HIP events.  which = stack*4 + kind, stack 0 backbone / 1 decoder,
+ * kind 0 = norm+gate/up+SiLU, 1 = down+residual.  *bytes = algorithmic bytes per launch. */
+int csm_bench_gemv(csm_engine* e, int which, int M, int iters, float* avg_us, double* bytes);
+
+/* ------------------------------------------------------------------ Mimi codec */
+typedef struct mimi_dims {
+  int channels, dimension, n_filters, n_ratios, ratios[8];
+  int kernel_size, residual_kernel_size, last_kernel_size, compress;
+  int num_heads, num_layers, dim_feedforward, context;
+  int n_q, bins, codebook_dim, downsample_stride;
+  float norm_eps;
+  int gelu_erf;   /* 0: tanh approximation (mlx gelu_approx), 1: exact */
+  int attn_mode;  /* 0: moshi_mlx (no mask inside a call), 1: causal sliding window */
+} mimi_dims;
+
+typedef struct mimi_codec mimi_codec;
+
+int mimi_create(const mimi_dims* dims, int device, int max_batch, int max_frames, mimi_codec** out);
+int mimi_destroy(mimi_codec* m);
+int mimi_load_tensor(mimi_codec* m, const char* name, const void* host, int src_dtype, const int64_t* shape,
+                     int ndim);
+/* RoPE table for the codec transformer: [n_pos][head_dim/2][2] */
+int mimi_set_rope_table(mimi_codec* m, const float* table, int n_pos, int head_dim);
+int mimi_weights_ready(mimi_codec* m);
+/* pcm [B][N] float32 host -> codes [B][n_q][Tf] int32 host; *n_frames_out = Tf */
+int mimi_encode(mimi_codec* m, int B, int N, const float* pcm, int32_t* codes, int* n_frames_out);
+/* codes [B][n_q][F] -> pcm [B][F*frame_size].  codes_on_device / pcm_on_device select device pointers;
+ * codes_layout 0 = [B][n_q][F], 1 = engine history [F][B][n_q] */
+int mimi_decode(mimi_codec* m, int B, int F, const int32_t* codes, int codes_on_device, int codes_layout,
+                float* pcm, int pcm_on_device);
+/* streaming: reset per-utterance state, then one frame at a time: codes [B][n_q] -> pcm [B][frame_size] */
+int mimi_reset_state(mimi_codec* m, int B);
+int mimi_decode_step(mimi_codec* m, int B, const int32_t* codes, float* pcm);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CSM_HIP_H */

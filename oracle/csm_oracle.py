@@ -1,0 +1,307 @@
+"""CPU ORACLE -- numpy fp32 restatement of the reference CSM hot path.
+
+TEST INFRASTRUCTURE ONLY.  Only ``tests/``, ``__graft_entry__.smoke()`` and the
+``cpu_baseline`` leg of ``bench.py`` may import this module; the product path
+(csm-mlx_amd/) never does.
+
+Parity status: the reference (MLX, mlx-lm, moshi-mlx) cannot be imported or run
+in this container (ModuleNotFoundError, no network) and
+ships no tests, fixtures or golden vectors, so this restatement is
+**parity unpinned** against the reference itself.  It follows the reference
+sources line by line as a spec:
+
+  * frame step            /root/reference/csm_mlx/generation.py:21-92
+  * generate loop / EOS   /root/reference/csm_mlx/generation.py:95-178
+  * embeddings            /root/reference/csm_mlx/models.py:79-92
+  * Llama-3 scaled RoPE   /root/reference/csm_mlx/attention.py:10-177
+  * GQA attention         /root/reference/csm_mlx/attention.py:180-253
+  * Llama block / RMSNorm mlx_lm.models.llama (TransformerBlock, MLP) as wired
+                          by /root/reference/csm_mlx/models.py:50-77
+
+Sampling with temperature cannot reproduce MLX's RNG; it restates the build's
+own counter-based Gumbel-max sampler (``gumbel_u``) so GPU sampled codes can be
+checked bit-for-bit against this file.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional
+
+import numpy as np
+
+F32 = np.float32
+
+
+# ----------------------------------------------------------------------------- RoPE
+def llama3_rope_theta(dim: int, base: float, scale_factor: float, low_freq_factor: float = 1.0,
+                      high_freq_factor: float = 4.0, old_context_len: int = 8192) -> np.ndarray:
+    """attention.py:57-79 (rope_init) + :94-117 (apply_scaling), in float32 as MLX does."""
+    expo = (np.arange(0, dim, 2, dtype=F32)[: dim // 2] / F32(dim)).astype(F32)
+    freqs = (F32(1.0) / np.power(F32(base), expo, dtype=F32)).astype(F32)
+    low_freq_wavelen = old_context_len / low_freq_factor
+    high_freq_wavelen = old_context_len / high_freq_factor
+    out = []
+    for freq in freqs:
+        wavelen = F32(2 * math.pi) / freq                      # mx float32 scalar math
+        if wavelen < high_freq_wavelen:
+            out.append(freq)
+        elif wavelen > low_freq_wavelen:
+            out.append(freq / F32(scale_factor))
+        else:
+            smooth = (F32(old_context_len) / wavelen - F32(low_freq_factor)) / F32(high_freq_factor - low_freq_factor)
+            out.append((F32(1) - smooth) * freq / F32(scale_factor) + smooth * freq)
+    return np.array(out, dtype=F32)
+
+
+def rope_cache(theta: np.ndarray, max_seq_len: int = 2048) -> np.ndarray:
+    """attention.py:81-92 -> (max_seq_len, dim//2, 2) = [cos, sin]."""
+    seq = np.arange(max_seq_len, dtype=F32)
+    idx_theta = np.outer(seq, theta).astype(F32)
+    return np.stack([np.cos(idx_theta), np.sin(idx_theta)], axis=-1).astype(F32)
+
+
+def rope_apply(x: np.ndarray, cache: np.ndarray, offset: int) -> np.ndarray:
+    """attention.py:119-177: interleaved pairs (2i, 2i+1), fp32.  x: (B, T, H, hd)."""
+    b, t, h, hd = x.shape
+    if offset + t > cache.shape[0]:
+        raise ValueError("RoPE position beyond the cached 2048-position table (attention.py:152)")
+    c = cache[offset: offset + t].reshape(1, t, 1, hd // 2, 2)
+    xs = x.astype(F32).reshape(b, t, h, hd // 2, 2)
+    x0, x1 = xs[..., 0], xs[..., 1]
+    out = np.stack([x0 * c[..., 0] - x1 * c[..., 1], x1 * c[..., 0] + x0 * c[..., 1]], axis=-1)
+    return out.reshape(b, t, h, hd).astype(F32)
+
+
+# ----------------------------------------------------------------------------- blocks
+def rms_norm(x: np.ndarray, w: np.ndarray, eps: float) -> np.ndarray:
+    """mlx fast.rms_norm: x * rsqrt(mean(x^2) + eps) * w, fp32 internally."""
+    x = x.astype(F32)
+    ms = np.mean(x * x, axis=-1, keepdims=True, dtype=F32)
+    return (x * (F32(1) / np.sqrt(ms + F32(eps))) * w).astype(F32)
+
+
+def linear(x: np.ndarray, w: np.ndarray) -> np.ndarray:
+    """nn.Linear without bias: y = x @ W.T with W (out, in)."""
+    return np.matmul(x, w.T).astype(F32)
+
+
+def silu(x):
+    return (x / (F32(1) + np.exp(-x))).astype(F32)
+
+
+def sdpa(q, k, v, scale, causal_offset: Optional[int]):
+    """softmax(q k^T * scale + mask) v; q (B,H,T,hd), k/v (B,H,S,hd); causal iff T>1."""
+    s = np.matmul(q, np.swapaxes(k, -1, -2)).astype(F32) * F32(scale)
+    T, S = q.shape[2], k.shape[2]
+    if causal_offset is not None and T > 1:
+        qi = np.arange(T)[:, None] + causal_offset
+        kj = np.arange(S)[None, :]
+        s = np.where(kj <= qi, s, F32(-np.inf))
+    s = s - s.max(-1, keepdims=True)
+    p = np.exp(s)
+    p = p / p.sum(-1, keepdims=True)
+    return np.matmul(p.astype(F32), v).astype(F32)
+
+
+class KVCacheRef:
+    """mlx_lm KVCache semantics: append at offset, return the [:offset] view."""
+
+    def __init__(self):
+        self.k = None
+        self.v = None
+        self.offset = 0
+
+    def update_and_fetch(self, k, v):
+        self.k = k if self.k is None else np.concatenate([self.k, k], axis=2)
+        self.v = v if self.v is None else np.concatenate([self.v, v], axis=2)
+        self.offset = self.k.shape[2]
+        return self.k, self.v
+
+
+class LlamaRef:
+    """mlx_lm LlamaModel with embed_tokens=Identity and the reference Attention patched in."""
+
+    def __init__(self, w: Dict[str, np.ndarray], prefix: str, args):
+        self.w, self.p, self.a = w, prefix, args
+        rs = args.rope_scaling
+        theta = llama3_rope_theta(args.head_dim, args.rope_theta, rs.get("factor", 1.0),
+                                  1.0, 4.0, 8192)   # attention.py:201-205 passes only base/scale_factor
+        self.rope = rope_cache(theta, 2048)
+
+    def attention(self, i, x, cache: KVCacheRef):
+        a, w, p = self.a, self.w, f"{self.p}.layers.{i}.self_attn"
+        b, t, _ = x.shape
+        hd, H, Hkv = a.head_dim, a.num_attention_heads, a.num_key_value_heads
+        q = linear(x, w[f"{p}.q_proj.weight"]).reshape(b, t, H, hd)
+        k = linear(x, w[f"{p}.k_proj.weight"]).reshape(b, t, Hkv, hd)
+        v = linear(x, w[f"{p}.v_proj.weight"]).reshape(b, t, Hkv, hd)
+        off = cache.offset
+        q = rope_apply(q, self.rope, off)
+        k = rope_apply(k, self.rope, off)
+        q, k, v = (np.swapaxes(z, 1, 2) for z in (q, k, v))
+        k, v = cache.update_and_fetch(k, v)
+        rep = H // Hkv
+        k = np.repeat(k, rep, axis=1)
+        v = np.repeat(v, rep, axis=1)
+        o = sdpa(q, k, v, hd ** -0.5, off)
+        o = np.swapaxes(o, 1, 2).reshape(b, t, H * hd)
+        return linear(o, w[f"{p}.o_proj.weight"])
+
+    def __call__(self, x, caches: List[KVCacheRef]):
+        a, w = self.a, self.w
+        h = x.astype(F32)
+        for i in range(a.num_hidden_layers):
+            p = f"{self.p}.layers.{i}"
+            r = self.attention(i, rms_norm(h, w[f"{p}.input_layernorm.weight"], a.rms_norm_eps), caches[i])
+            h = (h + r).astype(F32)
+            n = rms_norm(h, w[f"{p}.post_attention_layernorm.weight"], a.rms_norm_eps)
+            g = linear(n, w[f"{p}.mlp.gate_proj.weight"])
+            u = linear(n, w[f"{p}.mlp.up_proj.weight"])
+            h = (h + linear((silu(g) * u).astype(F32), w[f"{p}.mlp.down_proj.weight"])).astype(F32)
+        return rms_norm(h, w[f"{self.p}.norm.weight"], a.rms_norm_eps)
+
+
+# ----------------------------------------------------------------------------- sampler (build's own RNG)
+MASK64 = (1 << 64) - 1
+
+
+def splitmix64(x: np.ndarray) -> np.ndarray:
+    x = (x + np.uint64(0x9E3779B97F4A7C15)) & np.uint64(MASK64)
+    x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return x ^ (x >> np.uint64(31))
+
+
+def gumbel_u(seed: int, step: int, n: int) -> np.ndarray:
+    """Uniform (0,1) doubles for vocab indices 0..n-1 of one sampling event.
+
+    key = splitmix64(splitmix64(seed) ^ step) ; u_v = ((splitmix64(key ^ v) >> 11) + 0.5) * 2^-53
+    (csm-mlx_amd/csrc/csm_kernels.hip ``sample_gumbel`` implements the same).
+    """
+    with np.errstate(over="ignore"):
+        k = splitmix64(np.array([seed & MASK64], dtype=np.uint64))
+        k = splitmix64(k ^ np.uint64(step & MASK64))
+        h = splitmix64(k ^ np.arange(n, dtype=np.uint64))
+    return ((h >> np.uint64(11)).astype(np.float64) + 0.5) * (2.0 ** -53)
+
+
+def topk_threshold(logits: np.ndarray, k: int) -> float:
+    """k-th largest value; every logit >= it is kept (ties at the boundary all kept)."""
+    if k <= 0 or k >= logits.shape[-1]:
+        return -np.inf
+    return float(np.sort(logits)[::-1][k - 1])
+
+
+def sample_one(logits: np.ndarray, temperature: float, top_k: int, seed: int, step: int) -> int:
+    """Greedy = first max (mx.argmax); else Gumbel-max of logits*(1/temp) over the top-k set."""
+    logits = logits.astype(F32)
+    if temperature == 0:
+        return int(np.argmax(logits))
+    thr = topk_threshold(logits, top_k)
+    scaled = (logits * F32(1.0 / temperature)).astype(F32).astype(np.float64)
+    u = gumbel_u(seed, step, logits.shape[-1])
+    g = -np.log(-np.log(u))
+    val = np.where(logits >= thr, scaled + g, -np.inf)
+    return int(np.argmax(val))
+
+
+# ----------------------------------------------------------------------------- CSM
+class OracleCSM:
+    """Restatement of ``CSM`` (models.py:31-92) + ``generate_frame`` (generation.py:21-92)."""
+
+    def __init__(self, args, weights: Dict[str, np.ndarray], bb_args, dec_args):
+        self.args = args
+        self.w = {k: np.asarray(v, dtype=F32) for k, v in weights.items()}
+        self.backbone = LlamaRef(self.w, "backbone", bb_args)
+        self.decoder = LlamaRef(self.w, "decoder", dec_args)
+        self.bb_args, self.dec_args = bb_args, dec_args
+        self.V, self.K = args.n_audio_vocab, args.n_audio_codebooks
+        self.debug = {}
+
+    def new_backbone_cache(self):
+        return [KVCacheRef() for _ in range(self.bb_args.num_hidden_layers)]
+
+    def embed_audio(self, codebook: int, tokens: np.ndarray) -> np.ndarray:
+        return self.w["audio_embeddings.weight"][tokens + codebook * self.V]     # models.py:79-80
+
+    def embed_tokens(self, tokens: np.ndarray) -> np.ndarray:                   # models.py:82-92
+        text = self.w["text_embeddings.weight"][tokens[:, :, -1]][:, :, None, :]
+        audio_tokens = tokens[:, :, :-1] + self.V * np.arange(self.K)
+        audio = self.w["audio_embeddings.weight"][audio_tokens.reshape(-1)].reshape(*tokens.shape[:2], self.K, -1)
+        return np.concatenate([audio, text], axis=-2)
+
+    def frame(self, tokens, mask, cache, temperature=0.0, top_k=0, seeds=None, frame_idx=0):
+        """generation.py:21-92.  tokens/mask (B,T,33).  Returns codes (B,K) int32."""
+        B = tokens.shape[0]
+        emb = self.embed_tokens(tokens) * mask[..., None].astype(F32)              # :34-35
+        x = np.zeros(emb.shape[:2] + emb.shape[3:], F32)
+        for j in range(emb.shape[2]):                                              # :36 sum over 33, in order
+            x = x + emb[:, :, j]
+        h = self.backbone(x, cache)                                                # :39
+        h_last = h[:, -1, :]                                                       # :40
+        c0_logits = linear(h_last, self.w["codebook0_head.weight"])                # :42
+        self.debug["c0_logits"] = c0_logits
+        self.debug["h_last"] = h_last
+        seeds = seeds if seeds is not None else [0] * B
+        c0 = np.array([sample_one(c0_logits[b], temperature, top_k, seeds[b], frame_idx * self.K)
+                       for b in range(B)], dtype=np.int64)                        # :51-54
+        out = np.zeros((B, self.K), np.int32)
+        out[:, 0] = c0
+        dec_in = np.stack([h_last, self.embed_audio(0, c0)], axis=1)               # :57-64
+        dcache = [KVCacheRef() for _ in range(self.dec_args.num_hidden_layers)]   # :70 fresh per frame
+        ci_logits_all = []
+        for i in range(1, self.K):                                                 # :72
+            z = self.decoder(linear(dec_in, self.w["projection.weight"]), dcache)  # :74-77
+            logits = np.matmul(z[:, -1, :], self.w["audio_head"][i - 1]).astype(F32)   # :79 (in,out) layout
+            ci_logits_all.append(logits)
+            ci = np.array([sample_one(logits[b], temperature, top_k, seeds[b], frame_idx * self.K + i)
+                           for b in range(B)], dtype=np.int64)
+            out[:, i] = ci
+            dec_in = self.embed_audio(i, ci)[:, None, :]                          # :87-89
+        self.debug["ci_logits"] = np.stack(ci_logits_all, axis=1)
+        return out
+
+    def generate_codes(self, prompt_tokens: np.ndarray, prompt_mask: np.ndarray, max_frames: int,
+                       temperature=0.0, top_k=0, seed=0, max_seq_len=2048, collect_logits=False):
+        """generation.py:95-178 up to (not including) decode_audio.  prompt (L,33).
+
+        Returns (codes (F,K) int32 up to EOS, logits list if requested)."""
+        L = prompt_tokens.shape[0]
+        if L >= max_seq_len - max_frames:                                          # :132-137
+            raise ValueError(f"Inputs too long ({L}), must be below max_seq_len - max_audio_frames: "
+                             f"{max_seq_len - max_frames}")
+        cache = self.new_backbone_cache()
+        inp, msk = prompt_tokens[None].astype(np.int64), prompt_mask[None].astype(bool)
+        samples, logs = [], []
+        for f in range(max_frames):                                                # :139
+            s = self.frame(inp, msk, cache, temperature, top_k, [seed], f)
+            if collect_logits:
+                logs.append((self.debug["c0_logits"][0].copy(), self.debug["ci_logits"][0].copy()))
+            if not s.any():                                                        # :151 EOS
+                break
+            samples.append(s[0])
+            inp = np.concatenate([s, np.zeros((1, 1), np.int32)], axis=1)[:, None, :].astype(np.int64)   # :156
+            msk = np.concatenate([np.ones_like(s, bool), np.zeros((1, 1), bool)], axis=1)[:, None, :]   # :159
+        codes = np.stack(samples) if samples else np.zeros((0, self.K), np.int32)
+        return (codes, logs) if collect_logits else codes
+
+
+def text_frame(ids, n_codebooks: int = 32) -> (np.ndarray, np.ndarray):
+    """tokenizers.py:43-58 given already-tokenized ids: (n,K+1) tokens with ids in the last col."""
+    ids = np.asarray(ids, dtype=np.int32)
+    t = np.zeros((len(ids), n_codebooks + 1), np.int32)
+    m = np.zeros((len(ids), n_codebooks + 1), bool)
+    t[:, -1] = ids
+    m[:, -1] = True
+    return t, m
+
+
+def audio_frame(codes_kt: np.ndarray) -> (np.ndarray, np.ndarray):
+    """tokenizers.py:69-85: (K,T) codes -> append EOS zero frame -> (T+1, 33) rows, mask cols 0..K-1."""
+    K, T = codes_kt.shape
+    c = np.concatenate([codes_kt, np.zeros((K, 1), codes_kt.dtype)], axis=1)
+    t = np.zeros((T + 1, K + 1), np.int32)
+    m = np.zeros((T + 1, K + 1), bool)
+    t[:, :-1] = c.T
+    m[:, :-1] = True
+    return t, m

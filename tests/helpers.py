@@ -1,0 +1,40 @@
+"""Shared builders for the parity tests (test infrastructure)."""
+import dataclasses
+import functools
+
+import numpy as np
+
+from csm_mlx.config import BACKBONE_CONFIGURATION as BB, DECODER_CONFIGURATION as DC
+from csm_mlx.weights import bf16_round, synthetic_csm_weights
+
+
+@functools.lru_cache(maxsize=4)
+def csm_weights(args_key, seed=0):
+    from csm_mlx.models import csm_1b, csm_tiny
+    args = {"tiny": csm_tiny, "1b": csm_1b}[args_key]()
+    return args, synthetic_csm_weights(args, seed)
+
+
+def oracle_for(args, weights, bf16=False):
+    from oracle.csm_oracle import OracleCSM
+    w = {k: bf16_round(v) for k, v in weights.items()} if bf16 else weights
+    return OracleCSM(args, w, BB[args.backbone_name], DC[args.decoder_name])
+
+
+def prompt_ids(seed: int, n_mid: int = 12, vocab: int = 128000, bos: int = 128000, eos: int = 128001):
+    """SURVEY 8(d) prompt recipe: BOS + n ids ~ U[0, vocab) + EOS."""
+    rng = np.random.default_rng(seed)
+    return [bos] + [int(x) for x in rng.integers(0, vocab, n_mid)] + [eos]
+
+
+def tiny_prompt_ids(seed: int, n_mid: int = 5):
+    rng = np.random.default_rng(seed)
+    return [998] + [int(x) for x in rng.integers(0, 990, n_mid)] + [999]
+
+
+def first_divergence(a: np.ndarray, b: np.ndarray):
+    n = min(len(a), len(b))
+    for i in range(n):
+        if not np.array_equal(a[i], b[i]):
+            return i
+    return None if len(a) == len(b) else n
