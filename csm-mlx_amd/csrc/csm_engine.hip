@@ -89,6 +89,7 @@ struct csm_engine {
   std::vector<void*> allocs;
   std::vector<void*> batch_allocs;
   std::vector<int> pos_host;
+  bool fuse_dec_attn = false;  // CSM_FUSE_DEC_ATTN=1: measured slower (14 us vs 8.5 us) on MI355X
 
   void* balloc(size_t bytes) {
     void* p = nullptr;
@@ -154,16 +155,19 @@ void run_stack(csm_engine* e, Stack& s, float* x, int M, float* q, float* att, f
     g.out = q; g.os = s.q_dim(); g.Hq = Hq; g.Hkv = Hkv; g.hd = hd; g.S_cap = s.S_cap; g.rope = s.rope;
     g.kc = l.kc; g.vc = l.vc; g.rm = rm;
     launch_gemv(g, e->wdt, EPI_QKV, 1, st, tag);
-    // attention
+    // attention (+ o_proj + residual fused for the short depth-decoder KV)
     AttnParams a{};
     a.q = q; a.qs = s.q_dim(); a.M = M; a.kc = l.kc; a.vc = l.vc; a.Hq = Hq; a.Hkv = Hkv; a.S_cap = s.S_cap;
     a.scale = 1.0f / sqrtf((float)hd); a.mode = ATTN_CAUSAL; a.window = 0; a.rm = rm; a.out = att;
     a.os = s.q_dim();
-    launch_attn(a, hd, st);
-    // o_proj + residual
     g = GemvParams{};
     g.W = l.wo; g.N = D; g.K = s.q_dim(); g.x = att; g.xs = s.q_dim(); g.M = M; g.out = x; g.os = D;
-    launch_gemv(g, e->wdt, EPI_ADD, 0, st, tag);
+    if (s.S_cap <= 64 && M <= 4 && rm.T * 1 >= M && e->fuse_dec_attn) {  // rows of ONE utterance
+      launch_attn_oproj(g, a, e->wdt, hd, st);
+    } else {
+      launch_attn(a, hd, st);
+      launch_gemv(g, e->wdt, EPI_ADD, 0, st, tag);
+    }
     // norm2 + gate/up + SiLU*up
     g = GemvParams{};
     g.W = l.wgu; g.N = 2 * F; g.K = D; g.x = x; g.xs = D; g.M = M; g.nw = l.n2; g.eps = d.eps; g.out = mlp;
@@ -295,8 +299,24 @@ int csm_engine_create(const csm_dims* dims, int device, int weight_dtype, int ma
       if (x->n_heads % x->n_kv_heads) throw CsmError(CSM_ERR_ARG, "n_heads % n_kv_heads != 0");
     }
     if (b.n_heads * b.head_dim != b.hidden) throw CsmError(CSM_ERR_ARG, "backbone hidden != heads*head_dim");
+    for (const csm_llama_dims* x : {&b, &d})
+      if (x->n_heads / x->n_kv_heads > 4) throw CsmError(CSM_ERR_ARG, "GQA group > 4 unsupported");
+    {  // every GEMV shape must tile into whole blocks
+      const int Vp = (dims->n_audio_vocab + 7) / 8 * 8;
+      std::vector<std::pair<int, int>> shapes = {{Vp, b.hidden}, {Vp, d.hidden}, {d.hidden, b.hidden}};
+      for (const csm_llama_dims* x : {&b, &d}) {
+        shapes.push_back({(x->n_heads + 2 * x->n_kv_heads) * x->head_dim, x->hidden});
+        shapes.push_back({x->hidden, x->n_heads * x->head_dim});
+        shapes.push_back({2 * x->intermediate, x->hidden});
+        shapes.push_back({x->hidden, x->intermediate});
+      }
+      for (auto [N, Kd] : shapes)
+        for (int M : {1, 4})
+          if (N % gemv_rows_per_block(N, Kd, M)) throw CsmError(CSM_ERR_ARG, "GEMV shape does not tile");
+    }
     HIPCHK(hipSetDevice(device));
     std::unique_ptr<csm_engine> e(new csm_engine());
+    if (const char* v = getenv("CSM_FUSE_DEC_ATTN")) e->fuse_dec_attn = v[0] != '0';
     e->dims = *dims;
     e->dev = device;
     e->wdt = weight_dtype == CSM_F32 ? WDT_F32 : WDT_BF16;
@@ -630,18 +650,25 @@ int csm_bench_gemv(csm_engine* e, int which, int M, int iters, float* avg_us, do
     float* mlp = (which / 4 == 0) ? e->mlp : e->dmlp;
     const int D = s.d.hidden, F = s.d.intermediate;
     const int kind = which % 4;
-    if (kind > 1) throw CsmError(CSM_ERR_ARG, "unknown bench kernel");
     // one launch per layer in turn, as the frame does, so the weight working set (and hence
     // L2 / Infinity-Cache residency) matches the real frame: backbone 16 x 67 MB streams from
     // HBM, decoder 4 x 33.5 MB stays within the 256 MiB Infinity Cache.
     auto params = [&](int layer, int& epi, int& norm) {
       const LayerW& l = s.L[layer];
       GemvParams g{};
-      if (kind == 0) {
+      if (kind == 0) {  // norm + gate/up + SiLU
         g.W = l.wgu; g.N = 2 * F; g.K = D; g.x = x; g.xs = D; g.M = M; g.nw = l.n2; g.eps = s.d.eps;
         g.out = mlp; g.os = F; epi = EPI_SILU_MUL; norm = 1;
-      } else {
+      } else if (kind == 1) {  // down + residual
         g.W = l.wd; g.N = D; g.K = F; g.x = mlp; g.xs = F; g.M = M; g.out = x; g.os = D; epi = EPI_ADD; norm = 0;
+      } else if (kind == 2) {  // norm + QKV + RoPE + KV append (position 0)
+        g.W = l.wqkv; g.N = s.qkv_rows(); g.K = D; g.x = x; g.xs = D; g.M = M; g.nw = l.n1; g.eps = s.d.eps;
+        g.out = (which / 4 == 0) ? e->q : e->dq; g.os = s.q_dim(); g.Hq = s.d.n_heads; g.Hkv = s.d.n_kv_heads;
+        g.hd = s.d.head_dim; g.S_cap = s.S_cap; g.rope = s.rope; g.kc = l.kc; g.vc = l.vc; g.rm = RowMap{1, 0, nullptr, 0};
+        epi = EPI_QKV; norm = 1;
+      } else {  // o_proj + residual
+        g.W = l.wo; g.N = D; g.K = s.q_dim(); g.x = (which / 4 == 0) ? e->att : e->datt; g.xs = s.q_dim(); g.M = M;
+        g.out = x; g.os = D; epi = EPI_ADD; norm = 0;
       }
       return g;
     };
@@ -664,6 +691,15 @@ int csm_bench_gemv(csm_engine* e, int which, int M, int iters, float* avg_us, do
     (void)hipEventDestroy(b);
     if (avg_us) *avg_us = ms * 1000.f / iters;
     if (bytes) *bytes = (double)nbytes;
+  }
+  CSM_CATCH
+}
+
+int csm_set_gemv_config(int G, int RPT) {
+  CSM_TRY {
+    if ((G && G != 64 && G != 128 && G != 256) || (RPT && RPT != 2 && RPT != 4))
+      throw CsmError(CSM_ERR_ARG, "G in {0,64,128,256}, RPT in {0,2,4}");
+    gemv_set_override(G, RPT);
   }
   CSM_CATCH
 }

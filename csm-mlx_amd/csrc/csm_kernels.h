@@ -23,6 +23,7 @@ struct GemvParams {
   float* kc;          // [B][Hkv][S_cap][hd]
   float* vc;
   RowMap rm;
+  int epi;            // set by launch_gemv
 };
 
 struct EmbedParams {
@@ -77,6 +78,11 @@ struct AdvanceParams {
 void launch_gemv(const GemvParams& p, int wdt, int epi, int norm, hipStream_t st, int tag = 2);
 void launch_embed(const EmbedParams& p, int wdt, int M, hipStream_t st);
 void launch_attn(const AttnParams& p, int hd, hipStream_t st);
+// rows per block of the GEMV launch for (N, K, M): N must be a multiple of it
+int gemv_rows_per_block(int N, int K, int M);
+void gemv_set_override(int G, int RPT);  // 0 = automatic
+// fused attention (<= 64 keys, M <= 4 rows) + o_proj + residual for the depth decoder
+void launch_attn_oproj(const GemvParams& p, const AttnParams& a, int wdt, int hd, hipStream_t st);
 void launch_rmsnorm_rows(const float* x, int xs, const float* w, float eps, int D, float* out, int os, int M,
                          hipStream_t st);
 void launch_sample(const SampleParams& p, int wdt, int B, hipStream_t st);

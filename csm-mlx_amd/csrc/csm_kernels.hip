@@ -15,172 +15,219 @@
 #include "csm_kernels.h"
 
 // ============================================================================ embed
+// x[m] = sum_j mask[m,j] * table_j[tok[m,j]]  over the K audio columns (row tok + V*j of the
+// audio table) then the text column -- the order of the reference's .sum(-2) over 33 rows
+// (generation.py:34-36).  Row pointers are resolved once into LDS; each thread then sums 8
+// consecutive dims with independent 16-B loads.
 template <typename WT>
 __global__ __launch_bounds__(256) void embed_rows_kernel(EmbedParams p) {
+  __shared__ const WT* rows[64];
   const int m = blockIdx.x;
   const int ncol = p.K + 1;
-  float* out = p.out + (size_t)m * p.D;
-  const int* tok = p.codes ? p.codes + (size_t)m * p.K : p.tok + (size_t)m * ncol;
-  if (p.pos_inc && threadIdx.x == 0) p.pos_inc[m] += 1;
-  for (int d = threadIdx.x; d < p.D; d += blockDim.x) {
-    float acc = 0.f;
-    for (int j = 0; j < ncol; ++j) {
-      bool on;
-      int t;
-      if (p.codes) {  // decode: row = [codes, 0], mask = [1]*K + [0]  (generation.py:156-161)
-        on = j < p.K;
-        t = on ? tok[j] : 0;
-      } else {
-        on = p.mask[(size_t)m * ncol + j] != 0;
-        t = tok[j];
-      }
-      if (!on) continue;  // masked rows contribute exact zeros
-      const WT* row = (j < p.K) ? (const WT*)p.audio_emb + ((size_t)t + (size_t)p.V * j) * p.D
-                                : (const WT*)p.text_emb + (size_t)t * p.D;
-      acc += ld1<WT>(row + d);
+  if (threadIdx.x < ncol) {
+    const int j = threadIdx.x;
+    const WT* r = nullptr;
+    if (p.codes) {  // decode: row = [codes, 0], mask = [1]*K + [0]  (generation.py:156-161)
+      if (j < p.K) r = (const WT*)p.audio_emb + ((size_t)p.codes[(size_t)m * p.K + j] + (size_t)p.V * j) * p.D;
+    } else if (p.mask[(size_t)m * ncol + j]) {
+      const int t = p.tok[(size_t)m * ncol + j];
+      r = (j < p.K) ? (const WT*)p.audio_emb + ((size_t)t + (size_t)p.V * j) * p.D
+                    : (const WT*)p.text_emb + (size_t)t * p.D;
     }
-    out[d] = acc;
+    rows[j] = r;
+  }
+  __syncthreads();
+  if (p.pos_inc && threadIdx.x == 0) p.pos_inc[m] += 1;
+  float* out = p.out + (size_t)m * p.D;
+  for (int d0 = threadIdx.x * 8; d0 < p.D; d0 += blockDim.x * 8) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll 4
+    for (int j = 0; j < ncol; ++j) {
+      const WT* r = rows[j];
+      if (!r) continue;  // masked columns contribute exact zeros
+      float w[8];
+      W8<WT>::load(r + d0, w);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += w[e];
+    }
+    *reinterpret_cast<float4*>(out + d0) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+    *reinterpret_cast<float4*>(out + d0 + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
   }
 }
 
 // ============================================================================ GEMV
 // y[m, n] = sum_k norm(x)[m, k] * W[n, k]   (W row-major [N][K], MLX (out,in) layout)
-// One wave owns RPW consecutive weight rows for MT x-rows at a time; lanes stride K by 8
-// elements (one 16-B bf16 load per row per step).  NORM=1 fuses RMSNorm of x (weight nw)
-// as a per-row scale applied after the reduction.
-template <int EPI, int RPW>
-__device__ __forceinline__ void gemv_epilogue(const GemvParams& p, int m, int row0, const float (&v)[RPW],
-                                              int lane) {
-  if constexpr (EPI == EPI_STORE || EPI == EPI_GELU || EPI == EPI_ADD) {
-#pragma unroll
-    for (int r = 0; r < RPW; ++r) {
-      if (lane == r) {
-        const int n = row0 + r;
-        float* o = p.out + (size_t)m * p.os + n;
-        float val = v[r];
-        if constexpr (EPI == EPI_GELU) val = p.gelu_erf ? gelu_erf_f(val) : gelu_tanh_f(val);
-        if constexpr (EPI == EPI_ADD) {
-          if (p.scale) val *= p.scale[n];
-          val += *o;
-        }
-        *o = val;
-      }
+//
+// A 256-thread block owns RPB = (256/G)*RPT consecutive weight rows.  The block is split into
+// 256/G row groups of G threads; a group walks K in strides of G*8 elements (one 16-B bf16 load
+// per row per step, straight to VGPRs -- the GEMV / M <= 16 regime: no LDS staging of the weight
+// stream), each thread carrying RPT rows x MT activation rows of fp32 accumulators.  Partials are
+// reduced with wave shuffles, then across the group's waves through LDS.  G is chosen so a group
+// covers K in 1-4 steps (G = 128 at K = 1024, 256 at K >= 2048): thousands of waves in flight for
+// the 16-67 MB projections.  NORM fuses RMSNorm of x (weight nw) as a per-row scale applied
+// after the reduction; the epilogue (store / residual add / SiLU*up / GELU / RoPE + KV append)
+// runs on row pairs so RoPE pairs and interleaved gate/up rows stay in one thread.
+__device__ void gemv_epilogue_pair(const GemvParams& p, int m, int n, float a, float b) {
+  switch (p.epi) {
+    case EPI_STORE: {
+      float* o = p.out + (size_t)m * p.os + n;
+      o[0] = a;
+      o[1] = b;
+      break;
     }
-  } else if constexpr (EPI == EPI_SILU_MUL) {
-#pragma unroll
-    for (int r = 0; r < RPW; r += 2) {
-      if (lane == r) {
-        const int j = (row0 + r) >> 1;
-        p.out[(size_t)m * p.os + j] = silu_f(v[r]) * v[r + 1];
-      }
+    case EPI_GELU: {
+      float* o = p.out + (size_t)m * p.os + n;
+      o[0] = p.gelu_erf ? gelu_erf_f(a) : gelu_tanh_f(a);
+      o[1] = p.gelu_erf ? gelu_erf_f(b) : gelu_tanh_f(b);
+      break;
     }
-  } else if constexpr (EPI == EPI_QKV) {
-    // rows: [q: Hq*hd | k: Hkv*hd | v: Hkv*hd]; RoPE on interleaved pairs (2i, 2i+1)
-    // (attention.py:157-177) with the cos/sin table; K/V appended at pos (KVCache.update_and_fetch)
-#pragma unroll
-    for (int r = 0; r < RPW; r += 2) {
-      if (lane == r) {
-        const int n = row0 + r;
-        const int qn = p.Hq * p.hd, kn = p.Hkv * p.hd;
-        float a = v[r], b = v[r + 1];
-        const int bb = p.rm.b(m), pos = p.rm.pos(m);
-        const int d = (n < qn ? n : (n < qn + kn ? n - qn : n - qn - kn)) % p.hd;
-        if (n < qn + kn) {
-          const float* cs = p.rope + ((size_t)pos * (p.hd >> 1) + (d >> 1)) * 2;
-          const float c = cs[0], s = cs[1];
-          const float y0 = a * c - b * s, y1 = b * c + a * s;
-          a = y0;
-          b = y1;
-        }
-        if (n < qn) {
-          float* o = p.out + (size_t)m * p.os + n;
-          o[0] = a;
-          o[1] = b;
-        } else {
-          const int nn = n < qn + kn ? n - qn : n - qn - kn;
-          const int kvh = nn / p.hd;
-          float* cache = n < qn + kn ? p.kc : p.vc;
-          float* o = cache + (((size_t)bb * p.Hkv + kvh) * p.S_cap + pos) * p.hd + d;
-          o[0] = a;
-          o[1] = b;
-        }
+    case EPI_ADD: {
+      float* o = p.out + (size_t)m * p.os + n;
+      if (p.scale) {
+        a *= p.scale[n];
+        b *= p.scale[n + 1];
       }
+      o[0] += a;
+      o[1] += b;
+      break;
+    }
+    case EPI_SILU_MUL:  // rows 2j (gate), 2j+1 (up) -> out[j]  (mlx_lm MLP: down(silu(gate)*up))
+      p.out[(size_t)m * p.os + (n >> 1)] = silu_f(a) * b;
+      break;
+    case EPI_QKV: {
+      // rows [q: Hq*hd | k: Hkv*hd | v: Hkv*hd]; RoPE on interleaved pairs (2i, 2i+1)
+      // (attention.py:157-177) from the cos/sin table; K/V appended at pos (KVCache.update_and_fetch)
+      const int qn = p.Hq * p.hd, kn = p.Hkv * p.hd;
+      const int bb = p.rm.b(m), pos = p.rm.pos(m);
+      const int nn = n < qn ? n : (n < qn + kn ? n - qn : n - qn - kn);
+      const int d = nn % p.hd;
+      if (n < qn + kn) {
+        const float2 cs = *reinterpret_cast<const float2*>(p.rope + ((size_t)pos * (p.hd >> 1) + (d >> 1)) * 2);
+        const float y0 = a * cs.x - b * cs.y, y1 = b * cs.x + a * cs.y;
+        a = y0;
+        b = y1;
+      }
+      float* o;
+      if (n < qn) {
+        o = p.out + (size_t)m * p.os + n;
+      } else {
+        float* cache = n < qn + kn ? p.kc : p.vc;
+        o = cache + (((size_t)bb * p.Hkv + nn / p.hd) * p.S_cap + pos) * p.hd + d;
+      }
+      *reinterpret_cast<float2*>(o) = make_float2(a, b);
+      break;
     }
   }
 }
 
-// TAG only separates kernel symbols per call site (0 backbone, 1 decoder, 2 heads/codec) so rocprof
-// reports the dominant decoder GEMV on its own row; it does not change the code.
-template <typename WT, int RPW, int MT, int EPI, int NORM, int TAG>
+template <typename WT, int G, int RPT, int MT, int TAG>
 __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int row0 = (blockIdx.x * 4 + wave) * RPW;
-  if (row0 >= p.N) return;
+  constexpr int NG = 256 / G;
+  constexpr int RPB = NG * RPT;
+  __shared__ float red[4][MT][RPT + 1];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int grp = tid / G, gt = tid % G;
+  const int row0 = blockIdx.x * RPB + grp * RPT;
+  const bool norm = p.nw != nullptr;
   const WT* W = (const WT*)p.W;
   for (int m0 = 0; m0 < p.M; m0 += MT) {
-    float acc[MT][RPW];
+    float acc[MT][RPT];
     float ss[MT];
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
       ss[i] = 0.f;
 #pragma unroll
-      for (int r = 0; r < RPW; ++r) acc[i][r] = 0.f;
+      for (int r = 0; r < RPT; ++r) acc[i][r] = 0.f;
     }
 #pragma unroll 2
-    for (int k = lane * 8; k < p.K; k += 512) {
-      float w[RPW][8];
+    for (int k = gt * 8; k < p.K; k += G * 8) {
+      float w[RPT][8];
 #pragma unroll
-      for (int r = 0; r < RPW; ++r) W8<WT>::load(W + (size_t)(row0 + r) * p.K + k, w[r]);
+      for (int r = 0; r < RPT; ++r) W8<WT>::load(W + (size_t)(row0 + r) * p.K + k, w[r]);
       float nw[8];
-      if constexpr (NORM) W8<float>::load(p.nw + k, nw);
+      if (norm) W8<float>::load(p.nw + k, nw);
 #pragma unroll
       for (int i = 0; i < MT; ++i) {
         if (m0 + i < p.M) {
           float xv[8];
           W8<float>::load(p.x + (size_t)(m0 + i) * p.xs + k, xv);
-          if constexpr (NORM) {
+          if (norm) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-              ss[i] += xv[j] * xv[j];
+              ss[i] = fmaf(xv[j], xv[j], ss[i]);
               xv[j] *= nw[j];
             }
           }
 #pragma unroll
-          for (int r = 0; r < RPW; ++r)
+          for (int r = 0; r < RPT; ++r)
 #pragma unroll
             for (int j = 0; j < 8; ++j) acc[i][r] = fmaf(w[r][j], xv[j], acc[i][r]);
         }
       }
     }
+    // reduce: wave shuffles, then the G/64 waves of the group through LDS
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
-      if (m0 + i >= p.M) break;
-      float scale = 1.f;
-      if constexpr (NORM) scale = rsqrtf(wave_sum(ss[i]) / (float)p.K + p.eps);
-      float v[RPW];
 #pragma unroll
-      for (int r = 0; r < RPW; ++r) v[r] = wave_sum(acc[i][r]) * scale;
-      gemv_epilogue<EPI, RPW>(p, m0 + i, row0, v, lane);
+      for (int r = 0; r < RPT; ++r) {
+        const float v = wave_sum(acc[i][r]);
+        if (lane == 0) red[wave][i][r] = v;
+      }
+      if (norm) {
+        const float v = wave_sum(ss[i]);
+        if (lane == 0) red[wave][i][RPT] = v;
+      }
     }
+    __syncthreads();
+    constexpr int WPG = G / 64;  // waves per group
+    constexpr int NPAIR = NG * MT * (RPT / 2);
+    if (tid < NPAIR) {
+      const int g = tid / (MT * (RPT / 2));
+      const int rem = tid % (MT * (RPT / 2));
+      const int i = rem / (RPT / 2), rp = (rem % (RPT / 2)) * 2;
+      const int m = m0 + i;
+      if (m < p.M) {
+        float a = 0.f, b = 0.f, sq = 0.f;
+#pragma unroll
+        for (int w = 0; w < WPG; ++w) {
+          a += red[g * WPG + w][i][rp];
+          b += red[g * WPG + w][i][rp + 1];
+          sq += red[g * WPG + w][i][RPT];
+        }
+        if (norm) {
+          const float sc = rsqrtf(sq / (float)p.K + p.eps);
+          a *= sc;
+          b *= sc;
+        }
+        gemv_epilogue_pair(p, m, blockIdx.x * RPB + g * RPT + rp, a, b);
+      }
+    }
+    __syncthreads();
   }
 }
 
 // ============================================================================ attention
-// One wave per (query row m, q head h).  Keys [k0, k1] of utterance b(m), online softmax
-// over 64-key chunks (lane = key for q.k, lane = head dim for p.V).  GQA: kv head h/(Hq/Hkv).
+// Decode-shaped GQA attention.  One block per (query row m, kv head); wave w serves q head
+// kvh*G + w (G = Hq/Hkv <= 4).  Keys [k0, k1] of utterance b(m) stream through LDS in chunks of
+// 64 rows (all 256 threads issue coalesced 16-B loads, so a chunk costs one memory latency), then
+// each wave scores its head (lane = key, K rows padded by 16 B: conflict-free ds_read_b128),
+// online softmax in fp32, and P.V with lane = head dim reading V rows from LDS.
 template <int HD>
 __global__ __launch_bounds__(256) void attn_kernel(AttnParams p) {
+  constexpr int KP = HD + 4;  // padded K row (floats)
+  __shared__ __attribute__((aligned(16))) float Ks[64 * KP];
+  __shared__ __attribute__((aligned(16))) float Vs[64 * HD];
   __shared__ __attribute__((aligned(16))) float qs[4][HD];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int gid = blockIdx.x * 4 + wave;
-  const int m = gid / p.Hq, h = gid % p.Hq;
-  const bool active = m < p.M;
-  const int mm = active ? m : 0;
-  const float* q = p.q + (size_t)mm * p.qs + h * HD;
-  for (int d = lane; d < HD; d += 64) qs[wave][d] = q[d];
-  __syncthreads();
-  if (!active) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int G = p.Hq / p.Hkv;
+  const int m = blockIdx.x / p.Hkv, kvh = blockIdx.x % p.Hkv;
+  const int h = kvh * G + wave;
+  const bool head_ok = wave < G;
+  if (head_ok) {
+    const float* q = p.q + (size_t)m * p.qs + h * HD;
+    for (int d = lane; d < HD; d += 64) qs[wave][d] = q[d] * p.scale;
+  }
   const int b = p.rm.b(m), pos = p.rm.pos(m);
   int k0, k1;
   if (p.mode == ATTN_CAUSAL) {
@@ -194,51 +241,235 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnParams p) {
     k0 = max(0, off - p.window);
     k1 = off + p.rm.T - 1;
   }
-  const int kvh = h / (p.Hq / p.Hkv);
   const float* K = p.kc + ((size_t)b * p.Hkv + kvh) * p.S_cap * HD;
   const float* V = p.vc + ((size_t)b * p.Hkv + kvh) * p.S_cap * HD;
   constexpr int NO = HD / 64;
+  constexpr int V4 = HD / 4;  // float4 per row
   float o[NO];
 #pragma unroll
   for (int i = 0; i < NO; ++i) o[i] = 0.f;
   float m_run = -INFINITY, l_run = 0.f;
   for (int c = k0; c <= k1; c += 64) {
-    const int j = c + lane;
+    const int n = min(64, k1 - c + 1);
+    __syncthreads();  // previous chunk consumed (and qs visible on the first pass)
+    {
+      constexpr int PER = 64 * V4 / 256;  // float4 per thread per tensor for a full chunk (4 or 8)
+      float4 kk[PER], vv[PER];
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int t = u * 256 + tid, j = t / V4, d4 = t % V4;
+        if (j < n) {
+          kk[u] = *reinterpret_cast<const float4*>(K + (size_t)(c + j) * HD + d4 * 4);
+          vv[u] = *reinterpret_cast<const float4*>(V + (size_t)(c + j) * HD + d4 * 4);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < PER; ++u) {
+        const int t = u * 256 + tid, j = t / V4, d4 = t % V4;
+        if (j < n) {
+          *reinterpret_cast<float4*>(&Ks[j * KP + d4 * 4]) = kk[u];
+          *reinterpret_cast<float4*>(&Vs[j * HD + d4 * 4]) = vv[u];
+        }
+      }
+    }
+    __syncthreads();
+    if (!head_ok) continue;
     float s = -INFINITY;
-    if (j <= k1) {
-      const float4* kr = reinterpret_cast<const float4*>(K + (size_t)j * HD);
+    if (lane < n) {
+      const float4* kr = reinterpret_cast<const float4*>(&Ks[lane * KP]);
       const float4* qr = reinterpret_cast<const float4*>(qs[wave]);
       float dot = 0.f;
 #pragma unroll
-      for (int d4 = 0; d4 < HD / 4; ++d4) {
+      for (int d4 = 0; d4 < V4; ++d4) {
         const float4 kk = kr[d4], qq = qr[d4];
         dot = fmaf(qq.x, kk.x, dot);
         dot = fmaf(qq.y, kk.y, dot);
         dot = fmaf(qq.z, kk.z, dot);
         dot = fmaf(qq.w, kk.w, dot);
       }
-      s = dot * p.scale;
+      s = dot;
     }
-    const float cmax = wave_max(s);
-    const float new_m = fmaxf(m_run, cmax);
+    const float new_m = fmaxf(m_run, wave_max(s));
     const float alpha = (m_run == -INFINITY) ? 0.f : expf(m_run - new_m);
-    const float pj = (j <= k1) ? expf(s - new_m) : 0.f;
+    const float pj = (lane < n) ? expf(s - new_m) : 0.f;
     l_run = l_run * alpha + wave_sum(pj);
 #pragma unroll
     for (int i = 0; i < NO; ++i) o[i] *= alpha;
-    const int n = min(64, k1 - c + 1);
-    for (int jj = 0; jj < n; ++jj) {
-      const float pb = __shfl(pj, jj, 64);
-      const float* vr = V + (size_t)(c + jj) * HD;
+    for (int j = 0; j < n; ++j) {
+      const float pb = __shfl(pj, j, 64);
 #pragma unroll
-      for (int i = 0; i < NO; ++i) o[i] = fmaf(pb, vr[lane + 64 * i], o[i]);
+      for (int i = 0; i < NO; ++i) o[i] = fmaf(pb, Vs[j * HD + lane + 64 * i], o[i]);
     }
     m_run = new_m;
   }
+  if (!head_ok) return;
   const float inv = 1.f / l_run;
   float* out = p.out + (size_t)m * p.os + h * HD;
 #pragma unroll
   for (int i = 0; i < NO; ++i) out[lane + 64 * i] = o[i] * inv;
+}
+
+// ============================================================================ fused decoder attention + o_proj
+// For the depth decoder (<= 32 cached positions per frame, generation.py:70-77) the attention of
+// all heads is ~65K FMAs over <= 64 KB of K/V, far cheaper than a kernel boundary.  Every o_proj
+// block: (1) issues its o_proj weight loads (independent of the attention), (2) stages q and the
+// live K/V rows of every kv head into LDS with all 256 threads (one memory latency), (3) computes
+// the attention of its M (<= 4) rows from LDS, (4) runs the o_proj GEMV (+ residual) from LDS.
+// One launch replaces attention + o_proj.
+template <typename WT, int HD, int G, int RPT, int MT>
+__global__ __launch_bounds__(256) void attn_oproj_kernel(GemvParams p, AttnParams a, int n_max) {
+  constexpr int NG = 256 / G;
+  constexpr int RPB = NG * RPT;
+  constexpr int KP = HD + 4;
+  constexpr int V4 = HD / 4;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  float* Ks = lds;                                   // [Hkv][n_max][KP]
+  float* Vs = Ks + (size_t)a.Hkv * n_max * KP;       // [Hkv][n_max][HD]
+  float* qa = Vs + (size_t)a.Hkv * n_max * HD;       // [M][Hq*HD]: q, overwritten by the attention output
+  __shared__ float red[4][MT][RPT];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int grp = tid / G, gt = tid % G;
+  const int row0 = blockIdx.x * RPB + grp * RPT;
+  const WT* W = (const WT*)p.W;
+  // (1) first K-step of weights in flight before anything else
+  float w[RPT][8];
+  const int k_first = gt * 8;
+  if (k_first < p.K) {
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) W8<WT>::load(W + (size_t)(row0 + r) * p.K + k_first, w[r]);
+  }
+  // (2) stage q rows and K/V rows [0, n_max) of the batch row b(0) (all rows share b in decoder steps
+  //     with T rows per utterance; rows of other utterances are staged per utterance below)
+  const int qd = a.Hq * HD;
+  const int b0 = a.rm.b(0);
+  {
+    float4 qv[4];
+    const int nq = p.M * (qd / 4);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int t = u * 256 + tid;
+      if (t < nq) qv[u] = *reinterpret_cast<const float4*>(a.q + (size_t)(t / (qd / 4)) * a.qs + (t % (qd / 4)) * 4);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int t = u * 256 + tid;
+      if (t < nq) *reinterpret_cast<float4*>(qa + (size_t)(t / (qd / 4)) * qd + (t % (qd / 4)) * 4) = qv[u];
+    }
+  }
+  // live rows only: the last row of the call has the largest position
+  const int n_live = a.rm.pos(p.M - 1) + 1;
+  const int total = a.Hkv * n_live * V4;
+  for (int t0 = 0; t0 < total; t0 += 256 * 8) {  // 8 loads per tensor in flight per thread
+    float4 kr[8], vr[8];
+    size_t dk[8], dv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int t = t0 + u * 256 + tid;
+      if (t < total) {
+        const int kv = t / (n_live * V4), rem = t % (n_live * V4);
+        const int j = rem / V4, d4 = rem % V4;
+        const size_t src = (((size_t)b0 * a.Hkv + kv) * a.S_cap + j) * HD + d4 * 4;
+        kr[u] = *reinterpret_cast<const float4*>(a.kc + src);
+        vr[u] = *reinterpret_cast<const float4*>(a.vc + src);
+        dk[u] = ((size_t)kv * n_max + j) * KP + d4 * 4;
+        dv[u] = ((size_t)kv * n_max + j) * HD + d4 * 4;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (t0 + u * 256 + tid < total) {
+        *reinterpret_cast<float4*>(Ks + dk[u]) = kr[u];
+        *reinterpret_cast<float4*>(Vs + dv[u]) = vr[u];
+      }
+    }
+  }
+  __syncthreads();
+  // (3) attention, one wave per (row, head)
+  for (int idx = wave; idx < p.M * a.Hq; idx += 4) {
+    const int m = idx / a.Hq, h = idx % a.Hq;
+    const int kv = h / (a.Hq / a.Hkv);
+    const int n = a.rm.pos(m) + 1;
+    float* qh = qa + (size_t)m * qd + h * HD;
+    float s = -INFINITY;
+    if (lane < n) {
+      const float4* kr = reinterpret_cast<const float4*>(Ks + ((size_t)kv * n_max + lane) * KP);
+      const float4* qr = reinterpret_cast<const float4*>(qh);
+      float dot = 0.f;
+#pragma unroll
+      for (int d4 = 0; d4 < V4; ++d4) {
+        const float4 kk = kr[d4], qq = qr[d4];
+        dot = fmaf(qq.x, kk.x, dot);
+        dot = fmaf(qq.y, kk.y, dot);
+        dot = fmaf(qq.z, kk.z, dot);
+        dot = fmaf(qq.w, kk.w, dot);
+      }
+      s = dot * a.scale;
+    }
+    const float mx = wave_max(s);
+    const float pj = (lane < n) ? expf(s - mx) : 0.f;
+    const float inv = 1.f / wave_sum(pj);
+    constexpr int NO = HD / 64;
+    float o[NO];
+#pragma unroll
+    for (int i = 0; i < NO; ++i) o[i] = 0.f;
+    const float* vb = Vs + (size_t)kv * n_max * HD;
+    for (int j = 0; j < n; ++j) {
+      const float pb = __shfl(pj, j, 64);
+#pragma unroll
+      for (int i = 0; i < NO; ++i) o[i] = fmaf(pb, vb[(size_t)j * HD + lane + 64 * i], o[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < NO; ++i) qh[lane + 64 * i] = o[i] * inv;  // q no longer needed by this wave
+  }
+  __syncthreads();
+  // (4) o_proj GEMV from LDS
+  float acc[MT][RPT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) acc[i][r] = 0.f;
+  for (int k = k_first; k < p.K; k += G * 8) {
+    if (k != k_first) {
+#pragma unroll
+      for (int r = 0; r < RPT; ++r) W8<WT>::load(W + (size_t)(row0 + r) * p.K + k, w[r]);
+    }
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      if (i < p.M) {
+        const float4 x0 = *reinterpret_cast<const float4*>(qa + (size_t)i * qd + k);
+        const float4 x1 = *reinterpret_cast<const float4*>(qa + (size_t)i * qd + k + 4);
+        const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+        for (int r = 0; r < RPT; ++r)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[i][r] = fmaf(w[r][j], xv[j], acc[i][r]);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) {
+      const float v = wave_sum(acc[i][r]);
+      if (lane == 0) red[wave][i][r] = v;
+    }
+  __syncthreads();
+  constexpr int WPG = G / 64;
+  constexpr int NPAIR = NG * MT * (RPT / 2);
+  if (tid < NPAIR) {
+    const int g = tid / (MT * (RPT / 2));
+    const int rem = tid % (MT * (RPT / 2));
+    const int i = rem / (RPT / 2), rp = (rem % (RPT / 2)) * 2;
+    if (i < p.M) {
+      float va = 0.f, vb2 = 0.f;
+#pragma unroll
+      for (int w2 = 0; w2 < WPG; ++w2) {
+        va += red[g * WPG + w2][i][rp];
+        vb2 += red[g * WPG + w2][i][rp + 1];
+      }
+      gemv_epilogue_pair(p, i, blockIdx.x * RPB + g * RPT + rp, va, vb2);
+    }
+  }
 }
 
 // ============================================================================ rmsnorm rows
@@ -267,107 +498,130 @@ __device__ __forceinline__ float key2f(uint32_t k) {
   return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
 }
 
-struct BestPair {
-  double v;
-  int i;
-};
-__device__ __forceinline__ BestPair best_of(BestPair a, BestPair b) {
-  if (b.v > a.v || (b.v == a.v && b.i < a.i)) return b;
-  return a;
+// (value, index) arg-max with the first-max tie rule of mx.argmax
+template <typename T>
+__device__ __forceinline__ void argmax_merge(T& v, int& i, T ov, int oi) {
+  if (ov > v || (ov == v && oi < i)) {
+    v = ov;
+    i = oi;
+  }
+}
+template <typename T>
+__device__ __forceinline__ int block_argmax(T v, int i, T* sv, int* si) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const T ov = __shfl_xor(v, o, 64);
+    const int oi = __shfl_xor(i, o, 64);
+    argmax_merge(v, i, ov, oi);
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) {
+    sv[wave] = v;
+    si[wave] = i;
+  }
+  __syncthreads();
+  T bv = sv[0];
+  int bi = si[0];
+  for (int w = 1; w < 4; ++w) argmax_merge(bv, bi, sv[w], si[w]);
+  return bi;
 }
 
-// One block per utterance.  Greedy: first max (mx.argmax).  Else Gumbel-max over
-// logits*(1/temp) restricted to values >= the top_k-th largest (radix select).
+// One block per utterance.  Greedy: first max (mx.argmax, generation.py:51-52).  Else Gumbel-max
+// over logits*(1/temp) restricted to values >= the top_k-th largest (radix select) -- mlx_lm
+// make_sampler(temp, top_k) semantics with the build's counter-based RNG.  The chosen code's
+// audio embedding (embed_audio, models.py:79-80) is gathered into the next decoder input row.
 template <typename WT>
 __global__ __launch_bounds__(256) void sample_kernel(SampleParams p) {
   __shared__ uint32_t hist[256];
   __shared__ uint32_t sh_prefix, sh_remain;
-  __shared__ double red_v[256];
-  __shared__ int red_i[256];
+  __shared__ double sdv[4];
+  __shared__ float sfv[4];
+  __shared__ int si[4];
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
   const float* lg = p.logits + (size_t)b * p.ls;
   const int V = p.V;
-  float thr = -INFINITY;
-  const bool greedy = p.temperature <= 0.f;
-  if (!greedy && p.top_k > 0 && p.top_k < V) {
-    uint32_t prefix = 0, maskbits = 0;
-    if (tid == 0) sh_remain = (uint32_t)p.top_k;
-    for (int shift = 24; shift >= 0; shift -= 8) {
-      hist[tid] = 0;
-      __syncthreads();
-      for (int v = tid; v < V; v += 256) {
-        const uint32_t key = f2key(lg[v]);
-        if ((key & maskbits) == prefix) atomicAdd(&hist[(key >> shift) & 255u], 1u);
+  int code;
+  if (p.temperature <= 0.f) {
+    float best = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int v = tid; v < V; v += 256) {
+      const float l = lg[v];
+      if (l > best) {  // increasing v per thread: first max kept
+        best = l;
+        bi = v;
       }
-      __syncthreads();
-      if (tid == 0) {
-        uint32_t cum = 0, rem = sh_remain;
-        int dsel = 0;
-        for (int dgt = 255; dgt >= 0; --dgt) {
-          if (cum + hist[dgt] >= rem) {
-            dsel = dgt;
-            rem -= cum;
-            break;
-          }
-          cum += hist[dgt];
-        }
-        sh_remain = rem;
-        sh_prefix = prefix | ((uint32_t)dsel << shift);
-      }
-      __syncthreads();
-      prefix = sh_prefix;
-      maskbits |= 255u << shift;
     }
-    thr = key2f(prefix);
-  }
-  const int step = p.frame_ctr[0] * p.K + p.cb;
-  uint64_t key = 0;
-  if (!greedy) key = splitmix64(splitmix64(p.seeds[b]) ^ (uint64_t)step);
-  const double inv_t = greedy ? 1.0 : (double)(1.0f / p.temperature);
-  BestPair best{-INFINITY, 0x7fffffff};
-  for (int v = tid; v < V; v += 256) {
-    const float l = lg[v];
-    double val;
-    if (greedy) {
-      val = (double)l;
-    } else {
+    code = block_argmax<float>(best, bi, sfv, si);
+  } else {
+    float thr = -INFINITY;
+    if (p.top_k > 0 && p.top_k < V) {
+      uint32_t prefix = 0, maskbits = 0;
+      if (tid == 0) sh_remain = (uint32_t)p.top_k;
+      for (int shift = 24; shift >= 0; shift -= 8) {
+        hist[tid] = 0;
+        __syncthreads();
+        for (int v = tid; v < V; v += 256) {
+          const uint32_t key = f2key(lg[v]);
+          if ((key & maskbits) == prefix) atomicAdd(&hist[(key >> shift) & 255u], 1u);
+        }
+        __syncthreads();
+        if (tid == 0) {
+          uint32_t cum = 0, rem = sh_remain;
+          int dsel = 0;
+          for (int dgt = 255; dgt >= 0; --dgt) {
+            if (cum + hist[dgt] >= rem) {
+              dsel = dgt;
+              rem -= cum;
+              break;
+            }
+            cum += hist[dgt];
+          }
+          sh_remain = rem;
+          sh_prefix = prefix | ((uint32_t)dsel << shift);
+        }
+        __syncthreads();
+        prefix = sh_prefix;
+        maskbits |= 255u << shift;
+      }
+      thr = key2f(prefix);
+    }
+    const int step = p.frame_ctr[0] * p.K + p.cb;
+    const uint64_t key = splitmix64(splitmix64(p.seeds[b]) ^ (uint64_t)step);
+    const float inv_t = 1.0f / p.temperature;
+    double best = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int v = tid; v < V; v += 256) {
+      const float l = lg[v];
       if (!(l >= thr)) continue;
       const uint64_t h = splitmix64(key ^ (uint64_t)v);
       const double u = ((double)(h >> 11) + 0.5) * 1.1102230246251565e-16;  // 2^-53
-      val = (double)(l * (float)inv_t) + (-log(-log(u)));
+      const double val = (double)(l * inv_t) + (-log(-log(u)));
+      if (val > best) {
+        best = val;
+        bi = v;
+      }
     }
-    best = best_of(best, BestPair{val, v});
-  }
-  red_v[tid] = best.v;
-  red_i[tid] = best.i;
-  __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if (tid < s) {
-      const BestPair o = best_of(BestPair{red_v[tid], red_i[tid]}, BestPair{red_v[tid + s], red_i[tid + s]});
-      red_v[tid] = o.v;
-      red_i[tid] = o.i;
-    }
-    __syncthreads();
+    code = block_argmax<double>(best, bi, sdv, si);
   }
   // NaN logits leave no winner; clamp so a bad row can never index outside the embedding table
-  const int code = min(max(red_i[0], 0), V - 1);
+  code = min(max(code, 0), V - 1);
   if (tid == 0) p.codes[(size_t)b * p.K + p.cb] = code;
-  // fused embed_audio for the next decoder input (generation.py:57-64, :87-89)
   if (p.next_in) {
     const int D = p.D;
     const WT* emb = (const WT*)p.audio_emb + ((size_t)code + (size_t)p.V_emb * p.cb) * D;
-    if (p.cb == 0) {
-      float* r0 = p.next_in + (size_t)(2 * b) * D;
-      float* r1 = r0 + D;
-      const float* hl = p.h_last + (size_t)b * D;
-      for (int d = tid; d < D; d += 256) {
-        r0[d] = hl[d];
-        r1[d] = ld1<WT>(emb + d);
+    float* dst = p.cb == 0 ? p.next_in + (size_t)(2 * b + 1) * D : p.next_in + (size_t)b * D;
+    for (int d0 = tid * 8; d0 < D; d0 += 256 * 8) {
+      float w[8];
+      W8<WT>::load(emb + d0, w);
+      *reinterpret_cast<float4*>(dst + d0) = make_float4(w[0], w[1], w[2], w[3]);
+      *reinterpret_cast<float4*>(dst + d0 + 4) = make_float4(w[4], w[5], w[6], w[7]);
+      if (p.cb == 0) {  // decoder step-1 rows are [h_last, E_a[c0]] (generation.py:62-64)
+        const float* hl = p.h_last + (size_t)b * D + d0;
+        float* r0 = p.next_in + (size_t)(2 * b) * D + d0;
+        *reinterpret_cast<float4*>(r0) = *reinterpret_cast<const float4*>(hl);
+        *reinterpret_cast<float4*>(r0 + 4) = *reinterpret_cast<const float4*>(hl + 4);
       }
-    } else {
-      float* r = p.next_in + (size_t)b * D;
-      for (int d = tid; d < D; d += 256) r[d] = ld1<WT>(emb + d);
     }
   }
 }
@@ -393,45 +647,63 @@ __global__ void advance_kernel(AdvanceParams p) {
 }
 
 // ============================================================================ launchers
-template <typename WT, int TAG>
-static void launch_gemv_t(const GemvParams& p, int epi, int norm, hipStream_t st) {
-  const int M = p.M;
-  // rows per wave: 4 for tall matrices, 2 otherwise (keeps >= ~1k waves in flight)
-  const int rpw = (p.N >= 8192) ? 4 : 2;
-  const int blocks = (p.N + 4 * rpw - 1) / (4 * rpw);
-#define GEMV_CASE(RPW, MT, E, NM) \
-  hipLaunchKernelGGL((gemv_kernel<WT, RPW, MT, E, NM, TAG>), dim3(blocks), dim3(256), 0, st, p)
-#define GEMV_NORM(RPW, MT, E) \
-  do { if (norm) GEMV_CASE(RPW, MT, E, 1); else GEMV_CASE(RPW, MT, E, 0); } while (0)
-#define GEMV_EPI(RPW, MT)                                   \
-  do {                                                      \
-    switch (epi) {                                          \
-      case EPI_STORE: GEMV_NORM(RPW, MT, EPI_STORE); break;   \
-      case EPI_ADD: GEMV_NORM(RPW, MT, EPI_ADD); break;       \
-      case EPI_SILU_MUL: GEMV_NORM(RPW, MT, EPI_SILU_MUL); break; \
-      case EPI_QKV: GEMV_NORM(RPW, MT, EPI_QKV); break;       \
-      case EPI_GELU: GEMV_NORM(RPW, MT, EPI_GELU); break;     \
-    }                                                       \
-  } while (0)
-  if (rpw == 4) {
-    if (M <= 1) GEMV_EPI(4, 1); else if (M <= 2) GEMV_EPI(4, 2); else GEMV_EPI(4, 4);
-  } else {
-    if (M <= 1) GEMV_EPI(2, 1); else if (M <= 2) GEMV_EPI(2, 2); else GEMV_EPI(2, 4);
-  }
-#undef GEMV_EPI
-#undef GEMV_NORM
-#undef GEMV_CASE
+// tiling choice (G threads per row group, RPT rows per thread); g_gemv_override lets the
+// profiling hook csm_set_gemv_config sweep alternatives.
+static int g_gemv_G = 0, g_gemv_RPT = 0;
+void gemv_set_override(int G, int RPT) {
+  g_gemv_G = G;
+  g_gemv_RPT = RPT;
 }
 
-void launch_gemv(const GemvParams& p, int wdt, int epi, int norm, hipStream_t st, int tag) {
+// Measured on MI355X (tools/gemv_sweep.py, bf16, M = 1): tall gate/up matrices want one wave per
+// row group (G = 64: no cross-wave reduction, 2-4 K-steps per thread); the K = 8192 down
+// projections want the whole block on a row pair (G = 256 at N = 1024, 128 at N = 2048); every
+// other shape is latency-bound and best at G = 128 (K >= 1024).  RPT = 2 wins everywhere at M = 1.
+static void gemv_tiling(int N, int K, int M, int& G, int& RPT) {
+  (void)M;
+  if (N >= 8192) G = 64;
+  else if (K >= 8192) G = N <= 1024 ? 256 : 128;
+  else G = K >= 1024 ? 128 : 64;
+  RPT = 2;
+  if (g_gemv_G) G = g_gemv_G;
+  if (g_gemv_RPT) RPT = g_gemv_RPT;
+}
+
+template <typename WT, int TAG>
+static void launch_gemv_t(const GemvParams& p, hipStream_t st) {
+  int G, RPT;
+  gemv_tiling(p.N, p.K, p.M, G, RPT);
+  const int blocks = p.N / ((256 / G) * RPT);
+  const bool mt1 = p.M == 1;
+#define GEMV_L(G_, R_, M_) hipLaunchKernelGGL((gemv_kernel<WT, G_, R_, M_, TAG>), dim3(blocks), dim3(256), 0, st, p)
+#define GEMV_M(G_, R_) do { if (mt1) GEMV_L(G_, R_, 1); else GEMV_L(G_, R_, 4); } while (0)
+#define GEMV_R(G_) do { if (RPT == 4) GEMV_M(G_, 4); else GEMV_M(G_, 2); } while (0)
+  if (G == 256) GEMV_R(256);
+  else if (G == 128) GEMV_R(128);
+  else GEMV_R(64);
+#undef GEMV_R
+#undef GEMV_M
+#undef GEMV_L
+}
+
+int gemv_rows_per_block(int N, int K, int M) {
+  int G, RPT;
+  gemv_tiling(N, K, M, G, RPT);
+  return (256 / G) * RPT;
+}
+
+void launch_gemv(const GemvParams& p0, int wdt, int epi, int norm, hipStream_t st, int tag) {
+  GemvParams p = p0;
+  p.epi = epi;
+  if (!norm) p.nw = nullptr;
   if (wdt == WDT_BF16) {
-    if (tag == 1) launch_gemv_t<bf16_t, 1>(p, epi, norm, st);
-    else if (tag == 2) launch_gemv_t<bf16_t, 2>(p, epi, norm, st);
-    else launch_gemv_t<bf16_t, 0>(p, epi, norm, st);
+    if (tag == 1) launch_gemv_t<bf16_t, 1>(p, st);
+    else if (tag == 2) launch_gemv_t<bf16_t, 2>(p, st);
+    else launch_gemv_t<bf16_t, 0>(p, st);
   } else {
-    if (tag == 1) launch_gemv_t<float, 1>(p, epi, norm, st);
-    else if (tag == 2) launch_gemv_t<float, 2>(p, epi, norm, st);
-    else launch_gemv_t<float, 0>(p, epi, norm, st);
+    if (tag == 1) launch_gemv_t<float, 1>(p, st);
+    else if (tag == 2) launch_gemv_t<float, 2>(p, st);
+    else launch_gemv_t<float, 0>(p, st);
   }
 }
 
@@ -441,8 +713,7 @@ void launch_embed(const EmbedParams& p, int wdt, int M, hipStream_t st) {
 }
 
 void launch_attn(const AttnParams& p, int hd, hipStream_t st) {
-  const int waves = p.M * p.Hq;
-  const int blocks = (waves + 3) / 4;
+  const int blocks = p.M * p.Hkv;
   if (hd == 64) hipLaunchKernelGGL(attn_kernel<64>, dim3(blocks), dim3(256), 0, st, p);
   else if (hd == 128) hipLaunchKernelGGL(attn_kernel<128>, dim3(blocks), dim3(256), 0, st, p);
 }
@@ -459,4 +730,37 @@ void launch_sample(const SampleParams& p, int wdt, int B, hipStream_t st) {
 
 void launch_advance(const AdvanceParams& p, hipStream_t st) {
   hipLaunchKernelGGL(advance_kernel, dim3(1), dim3(256), 0, st, p);
+}
+
+template <typename WT>
+static void launch_attn_oproj_t(const GemvParams& p, const AttnParams& a, int hd, hipStream_t st) {
+  const int G = p.K >= 2048 ? 256 : (p.K >= 1024 ? 128 : 64);
+  const int blocks = p.N / ((256 / G) * 2);
+  // live keys: every row's position + 1 (decoder step rows sit at positions < S_cap)
+  const int n_max = a.S_cap;
+  const size_t lds = ((size_t)a.Hkv * n_max * (hd + 4) + (size_t)a.Hkv * n_max * hd + (size_t)p.M * a.Hq * hd) * 4;
+#define AO_L(HD_, G_)                                                                                  \
+  do {                                                                                                 \
+    static bool attr_set = false;                                                                      \
+    if (!attr_set) {                                                                                   \
+      (void)hipFuncSetAttribute((const void*)attn_oproj_kernel<WT, HD_, G_, 2, 4>,                     \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);                \
+      (void)hipGetLastError();                                                                         \
+      attr_set = true;                                                                                 \
+    }                                                                                                  \
+    hipLaunchKernelGGL((attn_oproj_kernel<WT, HD_, G_, 2, 4>), dim3(blocks), dim3(256), lds, st, p, a, n_max); \
+  } while (0)
+#define AO_G(HD_) do { if (G == 256) AO_L(HD_, 256); else if (G == 128) AO_L(HD_, 128); else AO_L(HD_, 64); } while (0)
+  if (hd == 128) AO_G(128);
+  else AO_G(64);
+#undef AO_G
+#undef AO_L
+}
+
+void launch_attn_oproj(const GemvParams& p0, const AttnParams& a, int wdt, int hd, hipStream_t st) {
+  GemvParams p = p0;
+  p.epi = EPI_ADD;
+  p.nw = nullptr;
+  if (wdt == WDT_BF16) launch_attn_oproj_t<bf16_t>(p, a, hd, st);
+  else launch_attn_oproj_t<float>(p, a, hd, st);
 }

@@ -85,8 +85,11 @@ int csm_codes_device_ptr(csm_engine* e, void** dev_ptr);
 int csm_synchronize(csm_engine* e);
 /* Profiling hook: replay one GEMV of the frame (layer 0) `iters` times on the engine stream,
  * timed with HIP events.  which = stack*4 + kind, stack 0 backbone / 1 decoder,
- * kind 0 = norm+gate/up+SiLU, 1 = down+residual.  *bytes = algorithmic bytes per launch. */
+ * kind 0 = norm+gate/up+SiLU, 1 = down+residual, 2 = norm+QKV+RoPE, 3 = o_proj+residual.
+ * *bytes = algorithmic (weight) bytes per launch. */
 int csm_bench_gemv(csm_engine* e, int which, int M, int iters, float* avg_us, double* bytes);
+/* Profiling hook: force the GEMV tiling (threads per row group G, rows per thread RPT); 0 = auto. */
+int csm_set_gemv_config(int G, int RPT);
 
 /* ------------------------------------------------------------------ Mimi codec */
 typedef struct mimi_dims {

@@ -198,7 +198,7 @@ def sample_one(logits: np.ndarray, temperature: float, top_k: int, seed: int, st
     if temperature == 0:
         return int(np.argmax(logits))
     thr = topk_threshold(logits, top_k)
-    scaled = (logits * F32(1.0 / temperature)).astype(F32).astype(np.float64)
+    scaled = (logits * (F32(1.0) / F32(temperature))).astype(F32).astype(np.float64)
     u = gumbel_u(seed, step, logits.shape[-1])
     g = -np.log(-np.log(u))
     val = np.where(logits >= thr, scaled + g, -np.inf)
