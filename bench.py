@@ -210,8 +210,8 @@ def main():
                        "model": "csm_1b (synthetic seed-0 weights)", "global_batch": args.batch * world,
                        "per_gpu_batch": args.batch, "frames": args.frames, "mimi_decode": decode,
                        "parallelism": f"dp{world}", "rtf": round(total_frames / max_dt / 12.5, 2)},
-            "roofline": dict(roof["decoder_gate_up"], kernel="gemv_kernel<bf16,4,*,EPI_SILU_MUL,1,TAG=1> "
-                             "(decoder norm+gate/up+SiLU, 33.5 MB bf16 per launch)"),
+            "roofline": dict(roof["decoder_gate_up"], kernel="gemv_kernel<bf16_t,64,2,1,TAG=1> = decoder "
+                             "RMSNorm+gate/up+SiLU*up GEMV, 33.5 MB bf16 weights per launch, 124 launches/frame"),
             "roofline_backbone": roof["backbone_gate_up"],
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -129,6 +129,6 @@ class MimiArgs:
 MIMI_CONFIGURATION = {
     "mimi_202407": MimiArgs(),
     # test-only: same topology, narrow channels / short window
-    "tiny": MimiArgs(n_filters=8, dimension=64, num_heads=2, num_layers=2, dim_feedforward=128,
+    "tiny": MimiArgs(n_filters=8, dimension=128, num_heads=2, num_layers=2, dim_feedforward=256,
                      context=10, bins=64, codebook_dim=32, n_q=4),
 }

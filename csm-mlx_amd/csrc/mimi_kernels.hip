@@ -1,0 +1,371 @@
+// Mimi codec kernels for gfx950: SEANet causal convs / transposed convs as fp32 implicit GEMMs,
+// codec-transformer pieces (LayerNorm, RoPE + KV append, linear), split-RVQ gather / encode.
+//
+// Reference: moshi_mlx Mimi as called by /root/reference/csm_mlx/tokenizers.py:61-85 (encode),
+// :148-150 (decode) and generation.py:249-256 (decode_step); restated in oracle/mimi_oracle.py.
+// Everything stays fp32 (waveform parity target: 1e-4 RMS).
+#include "mimi_kernels.h"
+
+// ============================================================================ tiled GEMM core
+// out(i, j) = sum_kk A(i, kk) * B(kk, j); 64 x 64 tile, K-step 16, 4x4 outputs per thread.
+// Problems supply a(), b(), store(); B_KCONTIG selects the B-tile load mapping (consecutive kk
+// per thread when B's memory is contiguous along kk, else consecutive j).
+template <class P>
+__global__ __launch_bounds__(256) void gemm64_kernel(P p) {
+  __shared__ __attribute__((aligned(16))) float As[16][68];
+  __shared__ __attribute__((aligned(16))) float Bs[16][68];
+  const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
+  const int i0 = blockIdx.y * 64, j0 = blockIdx.x * 64, z = blockIdx.z;
+  const int KD = p.kdim();
+  float acc[4][4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[r][c] = 0.f;
+  for (int k0 = 0; k0 < KD; k0 += 16) {
+    {
+      const int i = tid >> 2, kb = (tid & 3) * 4;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        v[e] = (i0 + i < p.M && k0 + kb + e < KD) ? p.a(z, i0 + i, k0 + kb + e) : 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) As[kb + e][i] = v[e];
+    }
+    if constexpr (P::B_KCONTIG) {
+      const int j = tid >> 2, kb = (tid & 3) * 4;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        v[e] = (j0 + j < p.N && k0 + kb + e < KD) ? p.b(z, k0 + kb + e, j0 + j) : 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) Bs[kb + e][j] = v[e];
+    } else {
+      const int kk = tid >> 4, jb = (tid & 15) * 4;
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        v[e] = (k0 + kk < KD && j0 + jb + e < p.N) ? p.b(z, k0 + kk, j0 + jb + e) : 0.f;
+      *reinterpret_cast<float4*>(&Bs[kk][jb]) = make_float4(v[0], v[1], v[2], v[3]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < 16; ++kk) {
+      const float4 a = *reinterpret_cast<const float4*>(&As[kk][ty * 4]);
+      const float4 b = *reinterpret_cast<const float4*>(&Bs[kk][tx * 4]);
+      const float av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[r][c] = fmaf(av[r], bv[c], acc[r][c]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int i = i0 + ty * 4 + r, j = j0 + tx * 4 + c;
+      if (i < p.M && j < p.N) p.store(z, i, j, acc[r][c]);
+    }
+}
+
+// ---------------------------------------------------------------------------- causal conv1d
+struct ConvProblem {
+  ConvParams c;
+  int M, N;
+  static constexpr bool B_KCONTIG = false;
+  __device__ int kdim() const { return c.Cin * c.k; }
+  __device__ float a(int, int co, int kk) const { return c.w[(size_t)co * c.Cin * c.k + kk]; }
+  __device__ float b(int z, int kk, int t) const {
+    const int ci = kk / c.k, j = kk - ci * c.k;
+    int u = t * c.stride + j * c.dil - c.pad_l;
+    if (u < 0 || u >= c.Tin) {
+      if (!c.replicate) return 0.f;
+      u = u < 0 ? 0 : c.Tin - 1;
+    }
+    const float v = c.x[(size_t)z * c.x_bstride + (size_t)ci * c.x_cstride + c.x_off + u];
+    return c.elu_in ? elu_f(v) : v;
+  }
+  __device__ void store(int z, int co, int t, float v) const {
+    if (c.bias) v += c.bias[co];
+    if (c.resid) v += c.resid[(size_t)z * c.r_bstride + (size_t)co * c.r_cstride + c.r_off + t];
+    c.y[(size_t)z * c.y_bstride + (size_t)co * c.y_cstride + c.y_off + t] = v;
+  }
+};
+
+void launch_conv1d(const ConvParams& p, hipStream_t st) {
+  ConvProblem pr{p, p.Cout, p.Tout};
+  dim3 grid((p.Tout + 63) / 64, (p.Cout + 63) / 64, p.B);
+  hipLaunchKernelGGL(gemm64_kernel<ConvProblem>, grid, dim3(256), 0, st, pr);
+}
+
+// ---------------------------------------------------------------------------- transposed conv (k = 2s)
+struct ConvTrProblem {
+  ConvTrParams c;
+  int M, N;
+  static constexpr bool B_KCONTIG = false;
+  __device__ int kdim() const { return c.Cin * 2; }
+  __device__ float a(int z, int co, int kk) const {
+    const int r = z % c.s;
+    return c.wt[((size_t)r * c.Cout + co) * c.Cin * 2 + kk];
+  }
+  __device__ float b(int z, int kk, int i) const {
+    const int bb = z / c.s;
+    const int ci = kk >> 1, e = kk & 1;
+    const int ti = c.t_in0 + i - e;
+    if (ti < 0) return 0.f;
+    const float v = c.x[(size_t)bb * c.x_bstride + (size_t)ci * c.x_cstride + c.x_off + ti];
+    return c.elu_in ? elu_f(v) : v;
+  }
+  __device__ void store(int z, int co, int i, float v) const {
+    const int bb = z / c.s, r = z % c.s;
+    if (c.bias) v += c.bias[co];
+    c.y[(size_t)bb * c.y_bstride + (size_t)co * c.y_cstride + c.y_off + (size_t)i * c.s + r] = v;
+  }
+};
+
+void launch_convtr(const ConvTrParams& p, hipStream_t st) {
+  ConvTrProblem pr{p, p.Cout, p.n_in};
+  dim3 grid((p.n_in + 63) / 64, (p.Cout + 63) / 64, p.B * p.s);
+  hipLaunchKernelGGL(gemm64_kernel<ConvTrProblem>, grid, dim3(256), 0, st, pr);
+}
+
+// ---------------------------------------------------------------------------- linear (rows x W^T)
+struct LinProblem {
+  LinParams c;
+  int M, N;  // M = output features (weight rows), N = activation rows
+  static constexpr bool B_KCONTIG = true;
+  __device__ int kdim() const { return c.K; }
+  __device__ float a(int, int n, int kk) const { return c.W[(size_t)n * c.K + kk]; }
+  __device__ float b(int, int kk, int m) const { return c.x[(size_t)m * c.xs + kk]; }
+  __device__ void store(int, int n, int m, float v) const {
+    if (c.conv_T) {  // conv layout out[b][n][t], m = b*T + t
+      const int bb = m / c.conv_T, t = m % c.conv_T;
+      float* o = c.out + (size_t)bb * c.conv_bstride + (size_t)n * c.conv_T + t;
+      *o = c.accumulate ? *o + v : v;
+      return;
+    }
+    float* o = c.out + (size_t)m * c.os + n;
+    switch (c.epi) {
+      case EPI_GELU:
+        *o = c.gelu_erf ? gelu_erf_f(v) : gelu_tanh_f(v);
+        break;
+      case EPI_ADD:
+        *o += c.scale ? c.scale[n] * v : v;
+        break;
+      default:
+        *o = v;
+    }
+  }
+};
+
+void launch_linear(const LinParams& p, hipStream_t st) {
+  LinProblem pr{p, p.N, p.M};
+  dim3 grid((p.M + 63) / 64, (p.N + 63) / 64, 1);
+  hipLaunchKernelGGL(gemm64_kernel<LinProblem>, grid, dim3(256), 0, st, pr);
+}
+
+// ============================================================================ LayerNorm rows
+// mlx fast.layer_norm: (x - mean) / sqrt(var + eps) * w + b, two-pass in fp32.
+__global__ __launch_bounds__(256) void layernorm_rows_kernel(const float* x, int D, const float* w, const float* b,
+                                                              float eps, float* out) {
+  __shared__ float red[4];
+  const int m = blockIdx.x, tid = threadIdx.x;
+  const float* xr = x + (size_t)m * D;
+  float s = 0.f;
+  for (int d = tid; d < D; d += 256) s += xr[d];
+  s = wave_sum(s);
+  if ((tid & 63) == 0) red[tid >> 6] = s;
+  __syncthreads();
+  const float mean = (red[0] + red[1] + red[2] + red[3]) / (float)D;
+  __syncthreads();
+  float v = 0.f;
+  for (int d = tid; d < D; d += 256) {
+    const float t = xr[d] - mean;
+    v += t * t;
+  }
+  v = wave_sum(v);
+  if ((tid & 63) == 0) red[tid >> 6] = v;
+  __syncthreads();
+  const float rstd = 1.f / sqrtf((red[0] + red[1] + red[2] + red[3]) / (float)D + eps);
+  for (int d = tid; d < D; d += 256) out[(size_t)m * D + d] = (xr[d] - mean) * rstd * w[d] + b[d];
+}
+
+void launch_layernorm_rows(const float* x, int D, const float* w, const float* b, float eps, float* out, int M,
+                           hipStream_t st) {
+  hipLaunchKernelGGL(layernorm_rows_kernel, dim3(M), dim3(256), 0, st, x, D, w, b, eps, out);
+}
+
+// ============================================================================ layout transposes
+__global__ void conv_to_rows_kernel(const float* x, int C, int T, int x_bstride, int x_cstride, int x_off,
+                                    float* rows) {
+  const int b = blockIdx.z, t = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int c = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (t < T && c < C) rows[((size_t)b * T + t) * C + c] = x[(size_t)b * x_bstride + (size_t)c * x_cstride + x_off + t];
+}
+void launch_conv_to_rows(const float* x, int B, int C, int T, int x_bstride, int x_cstride, int x_off, float* rows,
+                         hipStream_t st) {
+  hipLaunchKernelGGL(conv_to_rows_kernel, dim3((T + 63) / 64, (C + 3) / 4, B), dim3(256), 0, st, x, C, T, x_bstride,
+                     x_cstride, x_off, rows);
+}
+__global__ void rows_to_conv_kernel(const float* rows, int C, int T, float* y, int y_bstride, int y_cstride,
+                                    int y_off) {
+  const int b = blockIdx.z, t = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int c = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (t < T && c < C) y[(size_t)b * y_bstride + (size_t)c * y_cstride + y_off + t] = rows[((size_t)b * T + t) * C + c];
+}
+void launch_rows_to_conv(const float* rows, int B, int C, int T, float* y, int y_bstride, int y_cstride, int y_off,
+                         hipStream_t st) {
+  hipLaunchKernelGGL(rows_to_conv_kernel, dim3((T + 63) / 64, (C + 3) / 4, B), dim3(256), 0, st, rows, C, T, y,
+                     y_bstride, y_cstride, y_off);
+}
+
+// ============================================================================ RoPE + KV append
+// moshi_mlx nn.RoPE(traditional=True): rotate (x[2i], x[2i+1]) of q and k per head.
+__global__ void rope_append_kernel(const float* qkv, int M, int D, int H, int hd, const float* rope, RowMap rm,
+                                   float* qout, float* kc, float* vc, int S_cap) {
+  const int m = blockIdx.x;
+  const int b = rm.b(m), pos = rm.pos(m);
+  const float* row = qkv + (size_t)m * 3 * D;
+  for (int pi = threadIdx.x; pi < D / 2; pi += blockDim.x) {
+    const int n = pi * 2, h = n / hd, d = n % hd;
+    const float2 cs = *reinterpret_cast<const float2*>(rope + ((size_t)pos * (hd / 2) + d / 2) * 2);
+    const float q0 = row[n], q1 = row[n + 1];
+    const float k0 = row[D + n], k1 = row[D + n + 1];
+    qout[(size_t)m * D + n] = q0 * cs.x - q1 * cs.y;
+    qout[(size_t)m * D + n + 1] = q0 * cs.y + q1 * cs.x;
+    const size_t ci = (((size_t)b * H + h) * S_cap + pos) * hd + d;
+    kc[ci] = k0 * cs.x - k1 * cs.y;
+    kc[ci + 1] = k0 * cs.y + k1 * cs.x;
+    vc[ci] = row[2 * D + n];
+    vc[ci + 1] = row[2 * D + n + 1];
+  }
+}
+void launch_rope_append(const float* qkv, int M, int D, int H, int hd, const float* rope, RowMap rm, float* qout,
+                        float* kc, float* vc, int S_cap, hipStream_t st) {
+  hipLaunchKernelGGL(rope_append_kernel, dim3(M), dim3(256), 0, st, qkv, M, D, H, hd, rope, rm, qout, kc, vc, S_cap);
+}
+
+// ============================================================================ depthwise upsample
+__global__ void upsample_dw_kernel(const float* x, int C, int x_bstride, int x_cstride, int x_off, const float* w,
+                                   int s, int t_in0, int n_in, float* y, int y_bstride, int y_cstride, int y_off) {
+  const int b = blockIdx.z, c = blockIdx.y;
+  const int o = blockIdx.x * blockDim.x + threadIdx.x;  // output index within the produced range
+  if (o >= n_in * s) return;
+  const int i = o / s, r = o % s, ti = t_in0 + i;
+  const float* xr = x + (size_t)b * x_bstride + (size_t)c * x_cstride + x_off;
+  float v = xr[ti] * w[(size_t)c * 2 * s + r];
+  if (ti - 1 >= 0) v += xr[ti - 1] * w[(size_t)c * 2 * s + r + s];
+  y[(size_t)b * y_bstride + (size_t)c * y_cstride + y_off + o] = v;
+}
+void launch_upsample_dw(const float* x, int B, int C, int x_bstride, int x_cstride, int x_off, const float* w, int s,
+                        int t_in0, int n_in, float* y, int y_bstride, int y_cstride, int y_off, hipStream_t st) {
+  hipLaunchKernelGGL(upsample_dw_kernel, dim3((n_in * s + 255) / 256, C, B), dim3(256), 0, st, x, C, x_bstride,
+                     x_cstride, x_off, w, s, t_in0, n_in, y, y_bstride, y_cstride, y_off);
+}
+
+// ============================================================================ RVQ
+// decode gather: the codebook rows are summed in codebook order with plain fp32 adds, exactly as
+// the restated ResidualVectorQuantizer.decode accumulates them.  Ids >= bins (2048..2050, valid
+// CSM outputs but outside the Mimi codebook) are clamped to bins-1.
+__global__ void rvq_gather_kernel(const int* codes, int layout, int B, int F, int n_q, int k0, int k1,
+                                  const float* cb, int bins, int cd, float* q) {
+  const int m = blockIdx.x;  // b*F + f
+  const int b = m / F, f = m % F;
+  for (int d = threadIdx.x; d < cd; d += blockDim.x) {
+    float acc = 0.f;
+    for (int k = k0; k < k1; ++k) {
+      int c = layout == 0 ? codes[((size_t)b * n_q + k) * F + f] : codes[((size_t)f * B + b) * n_q + k];
+      c = min(max(c, 0), bins - 1);
+      acc = acc + cb[((size_t)k * bins + c) * cd + d];
+    }
+    q[(size_t)m * cd + d] = acc;
+  }
+}
+void launch_rvq_gather(const int* codes, int layout, int B, int F, int n_q, int k0, int k1, const float* cb, int bins,
+                       int cd, float* q, hipStream_t st) {
+  hipLaunchKernelGGL(rvq_gather_kernel, dim3(B * F), dim3(256), 0, st, codes, layout, B, F, n_q, k0, k1, cb, bins, cd,
+                     q);
+}
+
+// encode: one block per latent row; residual in LDS; per codebook every thread scores bins/256
+// codes as c2half - r.c (moshi_mlx EuclideanCodebook.encode), first-minimum arg-min.
+__global__ __launch_bounds__(256) void rvq_encode_kernel(float* r, int T, int cd, const float* cb,
+                                                         const float* c2half, int bins, int k0, int k1, int n_q,
+                                                         int* codes) {
+  __shared__ __attribute__((aligned(16))) float rs[1024];
+  __shared__ float sv[4];
+  __shared__ int si[4];
+  const int m = blockIdx.x, tid = threadIdx.x;
+  const int b = m / T, t = m % T;
+  for (int d = tid; d < cd; d += 256) rs[d] = r[(size_t)m * cd + d];
+  __syncthreads();
+  for (int k = k0; k < k1; ++k) {
+    const float* cbk = cb + (size_t)k * bins * cd;
+    float best = INFINITY;
+    int bi = 0x7fffffff;
+    for (int c = tid; c < bins; c += 256) {
+      const float4* cr = reinterpret_cast<const float4*>(cbk + (size_t)c * cd);
+      const float4* rr = reinterpret_cast<const float4*>(rs);
+      float dot = 0.f;
+      for (int d4 = 0; d4 < cd / 4; ++d4) {
+        const float4 a = cr[d4], x = rr[d4];
+        dot = fmaf(a.x, x.x, dot);
+        dot = fmaf(a.y, x.y, dot);
+        dot = fmaf(a.z, x.z, dot);
+        dot = fmaf(a.w, x.w, dot);
+      }
+      const float dist = c2half[(size_t)k * bins + c] - dot;
+      if (dist < best) {
+        best = dist;
+        bi = c;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ov < best || (ov == best && oi < bi)) {
+        best = ov;
+        bi = oi;
+      }
+    }
+    if ((tid & 63) == 0) {
+      sv[tid >> 6] = best;
+      si[tid >> 6] = bi;
+    }
+    __syncthreads();
+    float bv = sv[0];
+    int bidx = si[0];
+    for (int w = 1; w < 4; ++w)
+      if (sv[w] < bv || (sv[w] == bv && si[w] < bidx)) {
+        bv = sv[w];
+        bidx = si[w];
+      }
+    bidx = min(max(bidx, 0), bins - 1);
+    if (tid == 0) codes[((size_t)b * n_q + k) * T + t] = bidx;
+    for (int d = tid; d < cd; d += 256) rs[d] = rs[d] - cbk[(size_t)bidx * cd + d];
+    __syncthreads();
+  }
+  for (int d = tid; d < cd; d += 256) r[(size_t)m * cd + d] = rs[d];
+}
+void launch_rvq_encode(float* r, int M, int T, int cd, const float* cb, const float* c2half, int bins, int k0, int k1,
+                       int n_q, int* codes, hipStream_t st) {
+  hipLaunchKernelGGL(rvq_encode_kernel, dim3(M), dim3(256), 0, st, r, T, cd, cb, c2half, bins, k0, k1, n_q, codes);
+}
+
+// ============================================================================ window copy
+__global__ void copy_window_kernel(const float* src, int src_bstride, int src_cstride, int src_off, float* dst,
+                                   int dst_bstride, int dst_cstride, int dst_off, int len) {
+  const int b = blockIdx.z, c = blockIdx.y, i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < len)
+    dst[(size_t)b * dst_bstride + (size_t)c * dst_cstride + dst_off + i] =
+        src[(size_t)b * src_bstride + (size_t)c * src_cstride + src_off + i];
+}
+void launch_copy_window(const float* src, int B, int C, int src_bstride, int src_cstride, int src_off, float* dst,
+                        int dst_bstride, int dst_cstride, int dst_off, int len, hipStream_t st) {
+  if (len <= 0) return;
+  hipLaunchKernelGGL(copy_window_kernel, dim3((len + 255) / 256, C, B), dim3(256), 0, st, src, src_bstride,
+                     src_cstride, src_off, dst, dst_bstride, dst_cstride, dst_off, len);
+}

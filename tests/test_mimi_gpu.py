@@ -1,0 +1,86 @@
+"""GPU parity: the HIP Mimi codec (mimi_* C ABI) against the numpy oracle.
+
+Codes from encode must be bit-exact; decoded waveforms must agree within 1e-4 RMS
+(the north-star tolerance) -- observed errors are ~1e-6.  Both transformer attention
+modes are covered ("mlx": moshi_mlx no-mask-in-call semantics, the default; "causal").
+"""
+import dataclasses
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _pcm(n, seed=0, amp=0.1):
+    t = np.arange(n) / 24000.0
+    rng = np.random.default_rng(seed)
+    f = rng.uniform(100, 400, 3)
+    x = amp * sum(np.sin(2 * np.pi * fi * t + rng.uniform(0, 6.28)) for fi in f) + rng.normal(0, 0.01, n)
+    return x.astype(np.float32)
+
+
+def _pair(name, mode, max_batch=2):
+    from csm_mlx.config import MIMI_CONFIGURATION
+    from csm_mlx.mimi import MimiCodec
+    from csm_mlx.weights import synthetic_mimi_weights
+    from oracle.mimi_oracle import OracleMimi
+    m = dataclasses.replace(MIMI_CONFIGURATION[name], attn_mode=mode)
+    w = synthetic_mimi_weights(m)
+    codec = MimiCodec(m, max_batch=max_batch, max_frames=200)
+    codec.load_weights(w)
+    return m, codec, OracleMimi(m, w)
+
+
+def _rms(a, b):
+    return float(np.sqrt(np.mean((np.asarray(a, np.float64) - b) ** 2)))
+
+
+@pytest.mark.parametrize("name", ["tiny", "mimi_202407"])
+@pytest.mark.parametrize("mode", ["mlx", "causal"])
+def test_decode_parity(name, mode):
+    m, codec, o = _pair(name, mode)
+    rng = np.random.default_rng(5)
+    codes = rng.integers(0, m.bins, (2, m.n_q, 12)).astype(np.int32)
+    y = codec.decode(codes)
+    ref = o.decode(codes)
+    assert y.shape == ref.shape == (2, 1, 12 * m.frame_size)
+    assert _rms(y, ref) <= 1e-4, _rms(y, ref)
+
+
+@pytest.mark.parametrize("name", ["tiny", "mimi_202407"])
+@pytest.mark.parametrize("mode", ["mlx", "causal"])
+def test_encode_codes_bit_exact(name, mode):
+    m, codec, o = _pair(name, mode)
+    pcm = np.stack([_pcm(24000 * 2 + 480, 1), _pcm(24000 * 2 + 480, 2)])
+    codes = codec.encode(pcm[:, None, :])
+    ref = o.encode(pcm[:, None, :])
+    assert codes.shape == ref.shape
+    mism = int((codes != ref).sum())
+    assert mism == 0, f"{mism} of {codes.size} codes differ; first at {np.argwhere(codes != ref)[:3].tolist()}"
+
+
+@pytest.mark.parametrize("name", ["tiny", "mimi_202407"])
+@pytest.mark.parametrize("mode", ["mlx", "causal"])
+def test_decode_step_stream_parity(name, mode):
+    m, codec, o = _pair(name, mode, max_batch=1)
+    rng = np.random.default_rng(9)
+    codes = rng.integers(0, m.bins, (1, m.n_q, 6)).astype(np.int32)
+    codec.reset_state(1)
+    o.reset_state()
+    got = np.concatenate([codec.decode_step(codes[:, :, f: f + 1]) for f in range(6)], axis=2)
+    ref = np.concatenate([o.decode_step(codes[:, :, f: f + 1]) for f in range(6)], axis=2)
+    assert _rms(got, ref) <= 1e-4, _rms(got, ref)
+    if mode == "causal":  # causal codec: streaming == one-shot (SURVEY 4.4 invariant)
+        assert _rms(got, codec.decode(codes)) <= 1e-4
+
+
+def test_encode_decode_batch_equals_single():
+    m, codec, _ = _pair("tiny", "mlx")
+    pcm = np.stack([_pcm(9600, 3), _pcm(9600, 4)])
+    both = codec.encode(pcm)
+    one = codec.encode(pcm[1:2])
+    assert np.array_equal(both[1:2], one)
+    y2 = codec.decode(both)
+    y1 = codec.decode(both[1:2])
+    assert _rms(y2[1:2], y1) <= 1e-6
