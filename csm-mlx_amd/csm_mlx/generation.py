@@ -229,6 +229,6 @@ def stream_generate(model: CSM, text, speaker: int, context: List[Segment], max_
             if cache.run(1):
                 break                                                              # EOS (generation.py:239)
             codes = cache.last_codes()
-            yield codec.decode_step(codes)[0]
+            yield codec.decode_step(codes)[0, 0]
     finally:
         codec.reset_state(1)

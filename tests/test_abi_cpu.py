@@ -1,0 +1,77 @@
+"""CPU tests of the drop-in surface and the C ABI library (no compute calls without a GPU)."""
+import numpy as np
+import pytest
+
+
+def test_library_exports_every_declared_symbol():
+    from csm_mlx import _lib
+    names = _lib.declared_symbols()
+    assert "csm_engine_create" in names and "mimi_decode_step" in names
+    L = _lib.lib()
+    missing = [n for n in names if not hasattr(L, n)]
+    assert not missing, missing
+
+
+def test_reference_import_surface():
+    from csm_mlx import CSM, Segment, csm_1b, generate, stream_generate  # noqa: F401
+    import csm_mlx
+    from csm_mlx.generation import generate_frame  # noqa: F401
+    a = csm_1b()
+    assert (a.n_text_vocab, a.n_audio_vocab, a.n_audio_codebooks) == (128256, 2051, 32)
+    for n in ("CSMDataset", "CSMTrainer", "TrainArgs", "load_adapters"):
+        with pytest.raises(NotImplementedError):
+            getattr(csm_mlx, n)
+
+
+def test_csm_handle_attributes_without_gpu():
+    from csm_mlx import CSM, csm_1b
+    m = CSM(csm_1b())
+    assert m.n_audio_codebooks == 32 and len(m.backbone.layers) == 16 and len(m.decoder.layers) == 4
+    assert m.n_backbone_embedding == 2048 and m.n_decoder_embedding == 1024
+    assert m.backbone.args.rope_scaling["factor"] == 32.0
+    assert m.max_seq_len == 2048
+
+
+def test_segment_semantics():
+    from csm_mlx import Segment
+    s = Segment(1, "hi")                     # no validation at construction (segment.py:36-46)
+    with pytest.raises(ValueError):
+        _ = s.audio
+    s2 = Segment(0, "x", audio=np.zeros(10, np.float32))
+    assert s2.audio.shape == (10,)
+
+
+def test_sampler_descriptor():
+    from csm_mlx import make_sampler
+    s = make_sampler(0.8, top_k=50)
+    assert s.temp == 0.8 and s.top_k == 50 and not s.greedy
+    assert make_sampler(0.0).greedy
+    with pytest.raises(NotImplementedError):
+        make_sampler(0.8, top_p=0.9)
+
+
+def test_param_inventory_counts():
+    """~1.553 B parameters; 8(d): 4,553,371,648 params streamed per frame."""
+    from csm_mlx.models import csm_1b
+    from csm_mlx.weights import csm_param_specs
+    specs = csm_param_specs(csm_1b())
+    n = {k: int(np.prod(s)) for k, (s, _) in specs.items()}
+    total = sum(n.values())
+    assert 1.55e9 < total < 1.56e9
+    bb = sum(v for k, v in n.items() if k.startswith("backbone.")) + n["codebook0_head.weight"]
+    dec = sum(v for k, v in n.items() if k.startswith("decoder."))
+    per_frame = bb + 31 * (dec + n["projection.weight"] + n["audio_head"] // 31)
+    assert per_frame == 4_553_371_648
+
+
+def test_weights_loading_rejects_bad_shapes_without_gpu():
+    """Shape validation is host-side; without a GPU the engine cannot be created, which must
+    raise loudly (no CPU fallback)."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from csm_mlx import CSM
+    from csm_mlx.models import csm_tiny
+    m = CSM(csm_tiny(), dtype="float32")
+    with pytest.raises(Exception):
+        m.load_weights({"projection.weight": np.zeros((3, 3), np.float32)})

@@ -1,0 +1,163 @@
+"""CPU tests of the oracle: restated rules, external cross-checks, golden fixtures."""
+import dataclasses
+import math
+import os
+
+import numpy as np
+import pytest
+
+from helpers import csm_weights, oracle_for, tiny_prompt_ids
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+# ----------------------------------------------------------------------------- RoPE (attention.py:57-117)
+def test_llama3_rope_scaling_rule():
+    from oracle.csm_oracle import llama3_rope_theta
+    hd, base = 64, 500000.0
+    theta = llama3_rope_theta(hd, base, 32.0)
+    freqs = 1.0 / base ** (np.arange(0, hd, 2) / hd)
+    for f, t in zip(freqs, theta):
+        wl = 2 * math.pi / f
+        if wl < 2048:
+            assert t == pytest.approx(f, rel=1e-6)
+        elif wl > 8192:
+            assert t == pytest.approx(f / 32, rel=1e-6)
+        else:
+            s = (8192 / wl - 1) / 3
+            assert t == pytest.approx((1 - s) * f / 32 + s * f, rel=1e-5)
+
+
+def test_package_rope_table_equals_oracle():
+    from csm_mlx.config import BACKBONE_CONFIGURATION as BB, DECODER_CONFIGURATION as DC
+    from csm_mlx.rope import llama3_rope_table
+    from oracle.csm_oracle import llama3_rope_theta, rope_cache
+    for a in (BB["1b"], DC["100m"]):
+        ref = rope_cache(llama3_rope_theta(a.head_dim, a.rope_theta, 32.0), 2048)
+        assert np.array_equal(llama3_rope_table(a, 2048), ref)
+
+
+# ----------------------------------------------------------------------------- frame layout (tokenizers.py)
+def test_frame_layout_matches_oracle():
+    from csm_mlx.tokenizers import audio_codes_to_frames, tokenize_text_segment
+    from oracle.csm_oracle import audio_frame, text_frame
+    t, m = tokenize_text_segment([5, 6, 7], 0, 32)
+    ot, om = text_frame([5, 6, 7], 32)
+    assert np.array_equal(t, ot) and np.array_equal(m, om)
+    assert m[:, -1].all() and not m[:, :-1].any()
+    codes = np.random.default_rng(0).integers(0, 2048, (32, 5))
+    a, am = audio_codes_to_frames(codes)
+    oa, oam = audio_frame(codes)
+    assert np.array_equal(a, oa) and np.array_equal(am, oam)
+    assert a.shape == (6, 33) and (a[-1] == 0).all()          # EOS zero frame appended
+    assert am[:, :-1].all() and not am[:, -1].any()
+
+
+# ----------------------------------------------------------------------------- sampler
+def test_gumbel_stream_deterministic_and_uniform():
+    from oracle.csm_oracle import gumbel_u
+    u = gumbel_u(1234, 7, 200000)
+    assert np.array_equal(u, gumbel_u(1234, 7, 200000))
+    assert not np.array_equal(u, gumbel_u(1234, 8, 200000))
+    assert 0.0 < u.min() and u.max() < 1.0 and abs(u.mean() - 0.5) < 0.01
+
+
+def test_topk_keeps_k_and_greedy_first_max():
+    from oracle.csm_oracle import sample_one, topk_threshold
+    lg = np.array([1.0, 3.0, 3.0, 2.0, -1.0], np.float32)
+    assert sample_one(lg, 0.0, 0, 0, 0) == 1                    # first max (mx.argmax)
+    assert topk_threshold(lg, 2) == 3.0
+    picks = {sample_one(lg, 1.0, 2, s, 0) for s in range(200)}
+    assert picks <= {1, 2}                                      # only the top-2 values survive
+
+
+# ----------------------------------------------------------------------------- CSM oracle consistency
+def test_kv_cache_decode_equals_teacher_forced_prefill():
+    """Step-by-step decode through the KV cache == one prefill over the same rows."""
+    from oracle.csm_oracle import text_frame
+    args, w = csm_weights("tiny")
+    o = oracle_for(args, w)
+    t, m = text_frame(tiny_prompt_ids(4), args.n_audio_codebooks)
+    rows = np.random.default_rng(1).integers(0, 64, (3, args.n_audio_codebooks + 1)).astype(np.int32)
+    rows[:, -1] = 0
+    full_t = np.concatenate([t, rows])
+    full_m = np.concatenate([m, np.tile(np.r_[np.ones(args.n_audio_codebooks, bool), False], (3, 1))])
+    x_full = (o.embed_tokens(full_t[None]) * full_m[None, ..., None]).sum(-2)
+    h_full = o.backbone(x_full, o.new_backbone_cache())
+    cache = o.new_backbone_cache()
+    o.backbone((o.embed_tokens(t[None]) * m[None, ..., None]).sum(-2), cache)
+    for i in range(3):
+        r, rm = full_t[len(t) + i][None, None], full_m[len(t) + i][None, None]
+        h = o.backbone((o.embed_tokens(r) * rm[..., None]).sum(-2), cache)
+        np.testing.assert_allclose(h[0, -1], h_full[0, len(t) + i], rtol=2e-4, atol=2e-5)
+
+
+def test_csm_oracle_golden():
+    from oracle.csm_oracle import text_frame
+    g = np.load(os.path.join(GOLD, "csm_tiny_oracle.npz"))
+    args, w = csm_weights("tiny")
+    o = oracle_for(args, w)
+    t, m = text_frame(g["ids"], args.n_audio_codebooks)
+    codes, logs = o.generate_codes(t, m, 8, collect_logits=True)
+    assert np.array_equal(codes, g["codes"])
+    np.testing.assert_allclose(np.stack([l[0] for l in logs]), g["c0_logits"], rtol=1e-5, atol=1e-6)
+    assert np.array_equal(o.generate_codes(t, m, 8, temperature=0.8, top_k=5, seed=1234), g["sampled_codes"])
+
+
+# ----------------------------------------------------------------------------- Mimi oracle
+@pytest.mark.parametrize("name", ["tiny", "mimi_202407"])
+def test_mimi_oracle_matches_transformers(name):
+    """Causal mode == the independent transformers MimiModel with mapped weights."""
+    from csm_mlx.config import MIMI_CONFIGURATION
+    from csm_mlx.weights import synthetic_mimi_weights
+    from hf_mimi_map import build_hf_mimi
+    from oracle.mimi_oracle import OracleMimi
+    import torch
+    m = dataclasses.replace(MIMI_CONFIGURATION[name], attn_mode="causal")
+    w = synthetic_mimi_weights(m)
+    o = OracleMimi(m, w)
+    hf = build_hf_mimi(m, w)
+    from golden.make_golden import pcm_fixture
+    pcm = pcm_fixture(24000)
+    codes = o.encode(pcm[None, None])
+    with torch.no_grad():
+        hc = hf.encode(torch.from_numpy(pcm[None, None]), return_dict=False)[0].numpy()
+        hy = hf.decode(torch.from_numpy(codes.astype(np.int64)), return_dict=False)[0].numpy()
+    assert np.array_equal(hc, codes)
+    y = o.decode(codes)
+    assert float(np.sqrt(np.mean((hy - y) ** 2))) < 1e-5
+
+
+def test_mimi_oracle_streaming():
+    """Causal: concatenated decode_step == one-shot decode.  mlx mode: they differ (the
+    reference's moshi_mlx applies no mask inside a call, so one-shot decode is bidirectional)."""
+    from csm_mlx.config import MIMI_CONFIGURATION
+    from csm_mlx.weights import synthetic_mimi_weights
+    from oracle.mimi_oracle import OracleMimi
+    codes = np.random.default_rng(2).integers(0, 64, (1, 4, 5)).astype(np.int32)
+    for mode in ("causal", "mlx"):
+        m = dataclasses.replace(MIMI_CONFIGURATION["tiny"], attn_mode=mode)
+        o = OracleMimi(m, synthetic_mimi_weights(m))
+        one = o.decode(codes)
+        o.reset_state()
+        st = np.concatenate([o.decode_step(codes[:, :, f: f + 1]) for f in range(5)], axis=2)
+        err = float(np.abs(one - st).max())
+        if mode == "causal":
+            assert err < 1e-5
+        else:
+            assert err > 1e-4
+
+
+def test_mimi_oracle_golden():
+    from csm_mlx.config import MIMI_CONFIGURATION
+    from csm_mlx.weights import synthetic_mimi_weights
+    from golden.make_golden import pcm_fixture
+    from oracle.mimi_oracle import OracleMimi
+    g = np.load(os.path.join(GOLD, "mimi_tiny_oracle.npz"))
+    for mode in ("mlx", "causal"):
+        m = dataclasses.replace(MIMI_CONFIGURATION["tiny"], attn_mode=mode)
+        o = OracleMimi(m, synthetic_mimi_weights(m, 0))
+        codes = o.encode(pcm_fixture()[None, None])
+        assert np.array_equal(codes, g[f"{mode}_codes"])
+        y = o.decode(codes)
+        np.testing.assert_allclose(y[0, 0, :512], g[f"{mode}_pcm_head"], rtol=1e-5, atol=1e-6)
