@@ -73,6 +73,8 @@ struct csm_engine {
   uint8_t* msk = nullptr;
   // per-batch state
   int *codes = nullptr, *hist = nullptr, *pos = nullptr, *n_frames = nullptr, *frame_ctr = nullptr;
+  unsigned long long* part = nullptr;  // [K][B_max][part_stride] arg-max partials of the heads
+  int part_stride = 0;
   uint8_t* done = nullptr;
   uint64_t* seeds = nullptr;
   int B = 0;
@@ -193,20 +195,30 @@ void enqueue_body(csm_engine* e, hipStream_t st) {
 
 void enqueue_head(csm_engine* e, hipStream_t st) {
   const int B = e->B, K = e->K, D = e->D, Dd = e->Dd, V = e->V, Vp = e->Vpad;
-  // c0 = codebook0_head(h_last)  (generation.py:42)
+  const bool greedy = e->temperature <= 0.f;
+  const int n0 = Vp / gemv_rows_per_block(Vp, D, B);   // c0-head blocks (partials per row)
+  const int ni = Vp / gemv_rows_per_block(Vp, Dd, B);  // ci-head blocks
+  auto part = [&](int cb) { return e->part + (size_t)cb * e->B_max * e->part_stride; };
+  SampleParams sp{};
+  sp.ls = Vp; sp.V = V; sp.temperature = e->temperature; sp.top_k = e->top_k; sp.seeds = e->seeds;
+  sp.frame_ctr = e->frame_ctr; sp.K = K; sp.codes = e->codes; sp.part_stride = e->part_stride;
+  // c0 = codebook0_head(h_last) (generation.py:42); greedy arg-max fused into the GEMV epilogue
   GemvParams g{};
   g.W = e->c0_head; g.N = Vp; g.K = D; g.x = e->h_last; g.xs = D; g.M = B; g.out = e->c0_logits; g.os = Vp;
-  launch_gemv(g, e->wdt, EPI_STORE, 0, st);
-  SampleParams sp{};
-  sp.logits = e->c0_logits; sp.ls = Vp; sp.V = V; sp.temperature = e->temperature; sp.top_k = e->top_k;
-  sp.seeds = e->seeds; sp.frame_ctr = e->frame_ctr; sp.K = K; sp.cb = 0; sp.codes = e->codes;
-  sp.next_in = e->din; sp.h_last = e->h_last; sp.audio_emb = e->audio_emb; sp.V_emb = V; sp.D = D;
-  launch_sample(sp, e->wdt, B, st);
+  g.part = part(0); g.part_stride = e->part_stride; g.n_valid = V;
+  launch_gemv(g, e->wdt, greedy ? EPI_ARGMAX : EPI_STORE, 0, st);
+  if (!greedy) {
+    sp.logits = e->c0_logits; sp.cb = 0; sp.part = part(0);
+    launch_sample(sp, e->wdt, B, st);
+  }
   for (int i = 1; i < K; ++i) {
     const int M = (i == 1) ? 2 * B : B;
-    // decoder(projection(decoder_inputs))  (generation.py:74-77); fresh KV each frame (:70)
+    // decoder(projection(decoder_inputs)) (generation.py:74-77): the projection gathers its input
+    // rows itself -- [h_last, E_a[c0]] at step 1 (:62-64), E_a[c_{i-1} + V*(i-1)] after (:87-89)
     g = GemvParams{};
-    g.W = e->proj; g.N = Dd; g.K = D; g.x = e->din; g.xs = D; g.M = M; g.out = e->dx; g.os = Dd;
+    g.W = e->proj; g.N = Dd; g.K = D; g.x = e->h_last; g.xs = D; g.M = M; g.out = e->dx; g.os = Dd;
+    g.xpart = part(i - 1); g.xpart_stride = e->part_stride; g.xpart_n = greedy ? (i == 1 ? n0 : ni) : 1;
+    g.xtab = e->audio_emb; g.xV = V; g.xcb = i - 1; g.x_step1 = (i == 1); g.x_codes = e->codes; g.x_codes_K = K;
     launch_gemv(g, e->wdt, EPI_STORE, 0, st);
     RowMap rm = (i == 1) ? RowMap{2, 0, nullptr, 0} : RowMap{1, 0, nullptr, i};
     run_stack(e, e->dec, e->dx, M, e->dq, e->datt, e->dmlp, rm, st);
@@ -215,15 +227,19 @@ void enqueue_head(csm_engine* e, hipStream_t st) {
     g.W = (const char*)e->audio_head + (size_t)(i - 1) * Vp * Dd * e->wsz; g.N = Vp; g.K = Dd;
     g.x = e->dx + (i == 1 ? Dd : 0); g.xs = (i == 1 ? 2 * Dd : Dd); g.M = B; g.nw = e->dec.norm;
     g.eps = e->dec.d.eps; g.out = e->ci_logits + (size_t)(i - 1) * B * Vp; g.os = Vp;
-    launch_gemv(g, e->wdt, EPI_STORE, 1, st);
-    sp.logits = e->ci_logits + (size_t)(i - 1) * B * Vp;
-    sp.cb = i;
-    sp.next_in = (i + 1 < K) ? e->din : nullptr;
-    launch_sample(sp, e->wdt, B, st);
+    g.part = part(i); g.part_stride = e->part_stride; g.n_valid = V;
+    launch_gemv(g, e->wdt, greedy ? EPI_ARGMAX : EPI_STORE, 1, st);
+    if (!greedy) {
+      sp.logits = e->ci_logits + (size_t)(i - 1) * B * Vp; sp.cb = i; sp.part = part(i);
+      launch_sample(sp, e->wdt, B, st);
+    }
   }
   AdvanceParams ap{};
-  ap.codes = e->codes; ap.hist = e->hist; ap.F_cap = e->F_cap; ap.B = B; ap.K = K; ap.done = e->done;
+  ap.codes = e->codes; ap.hist = e->hist; ap.F_cap = e->F_cap; ap.B = B; ap.K = K; ap.V = V; ap.done = e->done;
   ap.n_frames = e->n_frames; ap.frame_ctr = e->frame_ctr;
+  if (greedy) {
+    ap.last_part = part(K - 1); ap.last_stride = e->part_stride; ap.last_n = ni;
+  }
   launch_advance(ap, st);
 }
 
@@ -270,6 +286,9 @@ void ensure_batch(csm_engine* e, int B) {
   e->n_frames = (int*)e->balloc(Bm * 4);
   e->done = (uint8_t*)e->balloc(Bm);
   e->seeds = (uint64_t*)e->balloc(Bm * 8);
+  e->part_stride = std::max(Vp / gemv_rows_per_block((int)Vp, (int)D, 1), Vp / gemv_rows_per_block((int)Vp, (int)Dd, 1));
+  e->part_stride = std::max(e->part_stride, (int)(Vp / 2));
+  e->part = (unsigned long long*)e->balloc(K * Bm * (size_t)e->part_stride * 8);
 }
 
 }  // namespace
@@ -691,6 +710,44 @@ int csm_bench_gemv(csm_engine* e, int which, int M, int iters, float* avg_us, do
     (void)hipEventDestroy(b);
     if (avg_us) *avg_us = ms * 1000.f / iters;
     if (bytes) *bytes = (double)nbytes;
+  }
+  CSM_CATCH
+}
+
+int csm_bench_floor(csm_engine* e, int n_kernels, int blocks, int graph, float* us_per_kernel) {
+  CSM_TRY {
+    if (n_kernels <= 0 || blocks <= 0) throw CsmError(CSM_ERR_ARG, "bad floor arguments");
+    HIPCHK(hipSetDevice(e->dev));
+    int* ctr = e->frame_ctr + 2;  // scratch word (frame_ctr[2] is unused)
+    hipGraphExec_t exec = nullptr;
+    if (graph) {
+      hipGraph_t gr;
+      HIPCHK(hipStreamBeginCapture(e->st, hipStreamCaptureModeThreadLocal));
+      for (int i = 0; i < n_kernels; ++i) launch_empty(blocks, ctr, e->st);
+      HIPCHK(hipStreamEndCapture(e->st, &gr));
+      HIPCHK(hipGraphInstantiate(&exec, gr, nullptr, nullptr, 0));
+      (void)hipGraphDestroy(gr);
+      HIPCHK(hipGraphLaunch(exec, e->st));
+    }
+    HIPCHK(hipStreamSynchronize(e->st));
+    hipEvent_t a, b;
+    HIPCHK(hipEventCreate(&a));
+    HIPCHK(hipEventCreate(&b));
+    HIPCHK(hipEventRecord(a, e->st));
+    for (int r = 0; r < 5; ++r) {
+      if (graph) HIPCHK(hipGraphLaunch(exec, e->st));
+      else for (int i = 0; i < n_kernels; ++i) launch_empty(blocks, ctr, e->st);
+    }
+    HIPCHK(hipEventRecord(b, e->st));
+    HIPCHK(hipEventSynchronize(b));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, a, b));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    if (exec) (void)hipGraphExecDestroy(exec);
+    HIPCHK(hipMemsetAsync(ctr, 0, 4, e->st));
+    HIPCHK(hipStreamSynchronize(e->st));
+    if (us_per_kernel) *us_per_kernel = ms * 1000.f / (5.f * n_kernels);
   }
   CSM_CATCH
 }

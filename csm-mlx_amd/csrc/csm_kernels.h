@@ -3,7 +3,7 @@
 #include "common.h"
 
 enum { WDT_F32 = 0, WDT_BF16 = 1 };
-enum { EPI_STORE = 0, EPI_ADD = 1, EPI_SILU_MUL = 2, EPI_QKV = 3, EPI_GELU = 4 };
+enum { EPI_STORE = 0, EPI_ADD = 1, EPI_SILU_MUL = 2, EPI_QKV = 3, EPI_GELU = 4, EPI_ARGMAX = 5 };
 enum { ATTN_CAUSAL = 0, ATTN_WINDOW = 1, ATTN_BLOCK = 2 };
 
 struct GemvParams {
@@ -24,7 +24,26 @@ struct GemvParams {
   float* vc;
   RowMap rm;
   int epi;            // set by launch_gemv
+  // EPI_ARGMAX: logits stored to out AND the block's best (value, first index) for each row
+  // packed as (orderable float << 32 | ~index) into part[m * part_stride + blockIdx.x]
+  unsigned long long* part;
+  int part_stride, n_valid;
+  // x gather mode (x_codes != null): row m of x is table[(code(m) + V*cb) * K] where code(m) is
+  // the arg-max of xpart[b(m) * xpart_stride + 0..xpart_n); with x_step1 rows alternate
+  // [x_dense row b (h_last), table row] (decoder step 1).  Block 0 writes codes[b*K_cb + cb].
+  const unsigned long long* xpart;
+  int xpart_stride, xpart_n;
+  const void* xtab;
+  int xV, xcb, x_step1, x_codes_K;
+  int* x_codes;
 };
+
+__device__ __forceinline__ unsigned long long pack_argmax(float v, int idx) {
+  const uint32_t u = __float_as_uint(v);
+  const uint32_t key = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  return ((unsigned long long)key << 32) | (unsigned long long)(0xFFFFFFFFu - (uint32_t)idx);
+}
+__device__ __forceinline__ int unpack_argmax(unsigned long long p) { return (int)(0xFFFFFFFFu - (uint32_t)p); }
 
 struct EmbedParams {
   const int* tok;        // [M][K+1] prompt tokens (or null)
@@ -59,20 +78,19 @@ struct SampleParams {
   const int* frame_ctr;
   int K, cb;
   int* codes;           // [B][K]
-  // fused next-input gather (null next_in = skip)
-  float* next_in;
-  const float* h_last;  // [B][D] (cb == 0: decoder step-1 rows are [h_last, E_a[c0]])
-  const void* audio_emb;
-  int V_emb, D;
+  unsigned long long* part;  // optional: publish the code as partial [b * part_stride]
+  int part_stride;
 };
 
 struct AdvanceParams {
-  const int* codes;
+  int* codes;
   int* hist;      // [F_cap][B][K]
-  int F_cap, B, K;
+  int F_cap, B, K, V;
   uint8_t* done;
   int* n_frames;
   int* frame_ctr;
+  const unsigned long long* last_part;  // greedy: partials of the last head (null: codes already final)
+  int last_stride, last_n;
 };
 
 void launch_gemv(const GemvParams& p, int wdt, int epi, int norm, hipStream_t st, int tag = 2);
@@ -87,3 +105,5 @@ void launch_rmsnorm_rows(const float* x, int xs, const float* w, float eps, int 
                          hipStream_t st);
 void launch_sample(const SampleParams& p, int wdt, int B, hipStream_t st);
 void launch_advance(const AdvanceParams& p, hipStream_t st);
+
+void launch_empty(int blocks, int* p, hipStream_t st);

@@ -91,6 +91,12 @@ __device__ void gemv_epilogue_pair(const GemvParams& p, int m, int n, float a, f
       o[1] += b;
       break;
     }
+    case EPI_ARGMAX: {  // logits (c0 / ci heads); the packed block arg-max is reduced by the caller
+      float* o = p.out + (size_t)m * p.os + n;
+      o[0] = a;
+      o[1] = b;
+      break;
+    }
     case EPI_SILU_MUL:  // rows 2j (gate), 2j+1 (up) -> out[j]  (mlx_lm MLP: down(silu(gate)*up))
       p.out[(size_t)m * p.os + (n >> 1)] = silu_f(a) * b;
       break;
@@ -131,9 +137,46 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
   const int row0 = blockIdx.x * RPB + grp * RPT;
   const bool norm = p.nw != nullptr;
   const WT* W = (const WT*)p.W;
+  // x gather mode: resolve each needed row's code from the producer's block partials once
+  __shared__ int gcode[512];  // codes of the gathered rows (M <= 512)
+  if (p.xpart) {
+    for (int m = wave; m < p.M; m += 4) {
+      const int bb = p.x_step1 ? (m >> 1) : m;
+      if (p.x_step1 && !(m & 1)) continue;
+      unsigned long long best = 0;
+      for (int i = lane; i < p.xpart_n; i += 64) {
+        const unsigned long long v = p.xpart[(size_t)bb * p.xpart_stride + i];
+        best = v > best ? v : best;
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long v = __shfl_xor(best, o, 64);
+        best = v > best ? v : best;
+      }
+      if (lane == 0) {
+        const int c = min(max(unpack_argmax(best), 0), p.xV - 1);
+        gcode[m] = c;
+        if (blockIdx.x == 0) p.x_codes[(size_t)bb * p.x_codes_K + p.xcb] = c;
+      }
+    }
+    __syncthreads();
+  }
   for (int m0 = 0; m0 < p.M; m0 += MT) {
     float acc[MT][RPT];
     float ss[MT];
+    const float* xf[MT];
+    const WT* xw[MT];
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      const int m = m0 + i;
+      xf[i] = p.x + (size_t)m * p.xs;
+      xw[i] = nullptr;
+      if (p.xpart && m < p.M && !(p.x_step1 && !(m & 1))) {
+        xw[i] = (const WT*)p.xtab + ((size_t)gcode[m] + (size_t)p.xV * p.xcb) * p.K;
+      } else if (p.x_step1) {
+        xf[i] = p.x + (size_t)(m >> 1) * p.xs;
+      }
+    }
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
       ss[i] = 0.f;
@@ -151,7 +194,8 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
       for (int i = 0; i < MT; ++i) {
         if (m0 + i < p.M) {
           float xv[8];
-          W8<float>::load(p.x + (size_t)(m0 + i) * p.xs + k, xv);
+          if (xw[i]) W8<WT>::load(xw[i] + k, xv);
+          else W8<float>::load(xf[i] + k, xv);
           if (norm) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
@@ -182,6 +226,8 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
     __syncthreads();
     constexpr int WPG = G / 64;  // waves per group
     constexpr int NPAIR = NG * MT * (RPT / 2);
+    unsigned long long akey = 0;
+    int arow = -1;
     if (tid < NPAIR) {
       const int g = tid / (MT * (RPT / 2));
       const int rem = tid % (MT * (RPT / 2));
@@ -201,6 +247,29 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
           b *= sc;
         }
         gemv_epilogue_pair(p, m, blockIdx.x * RPB + g * RPT + rp, a, b);
+        if (p.epi == EPI_ARGMAX) {
+          const int n = blockIdx.x * RPB + g * RPT + rp;
+          unsigned long long key = 0;
+          if (n < p.n_valid) key = pack_argmax(a, n);
+          if (n + 1 < p.n_valid) {
+            const unsigned long long kb = pack_argmax(b, n + 1);
+            key = kb > key ? kb : key;
+          }
+          akey = key;
+          arow = i;
+        }
+      }
+    }
+    if (p.epi == EPI_ARGMAX && wave == 0) {  // block arg-max per row -> partial slot
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        unsigned long long v = (tid < NPAIR && arow == i) ? akey : 0ull;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          const unsigned long long w = __shfl_xor(v, o, 64);
+          v = w > v ? w : v;
+        }
+        if (lane == 0 && m0 + i < p.M) p.part[(size_t)(m0 + i) * p.part_stride + blockIdx.x] = v;
       }
     }
     __syncthreads();
@@ -210,12 +279,15 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
 // ============================================================================ attention
 // Decode-shaped GQA attention.  One block per (query row m, kv head); wave w serves q head
 // kvh*G + w (G = Hq/Hkv <= 4).  Keys [k0, k1] of utterance b(m) stream through LDS in chunks of
-// 64 rows (all 256 threads issue coalesced 16-B loads, so a chunk costs one memory latency), then
-// each wave scores its head (lane = key, K rows padded by 16 B: conflict-free ds_read_b128),
-// online softmax in fp32, and P.V with lane = head dim reading V rows from LDS.
+// 64 rows; the chunk loads are software-pipelined through registers (chunk c+1 is in flight while
+// chunk c is scored), all 256 threads issuing coalesced 16-B loads.  Each wave scores its head
+// (lane = key, K rows padded by 16 B: conflict-free ds_read_b128), online softmax in fp32, and
+// P.V with lane = head dim reading V rows from LDS.
 template <int HD>
 __global__ __launch_bounds__(256) void attn_kernel(AttnParams p) {
   constexpr int KP = HD + 4;  // padded K row (floats)
+  constexpr int V4 = HD / 4;  // float4 per row
+  constexpr int PER = 64 * V4 / 256;  // float4 per thread per tensor for a full chunk (4 or 8)
   __shared__ __attribute__((aligned(16))) float Ks[64 * KP];
   __shared__ __attribute__((aligned(16))) float Vs[64 * HD];
   __shared__ __attribute__((aligned(16))) float qs[4][HD];
@@ -224,10 +296,6 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnParams p) {
   const int m = blockIdx.x / p.Hkv, kvh = blockIdx.x % p.Hkv;
   const int h = kvh * G + wave;
   const bool head_ok = wave < G;
-  if (head_ok) {
-    const float* q = p.q + (size_t)m * p.qs + h * HD;
-    for (int d = lane; d < HD; d += 64) qs[wave][d] = q[d] * p.scale;
-  }
   const int b = p.rm.b(m), pos = p.rm.pos(m);
   int k0, k1;
   if (p.mode == ATTN_CAUSAL) {
@@ -243,8 +311,26 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnParams p) {
   }
   const float* K = p.kc + ((size_t)b * p.Hkv + kvh) * p.S_cap * HD;
   const float* V = p.vc + ((size_t)b * p.Hkv + kvh) * p.S_cap * HD;
+  // chunk loads through registers; rows past the live range re-read the last live row (always a
+  // valid address), so the register array is written unconditionally and stays in VGPRs
+  // native ext-vector (not HIP's float4 struct, whose copies lower to memcpy and defeat SROA)
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  f32x4 kk[PER], vv[PER];
+  auto fetch = [&](const int c_) {
+    const int n_ = min(64, k1 - c_ + 1);
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int t = u * 256 + tid, j = min(t / V4, n_ - 1), d4 = t % V4;
+      kk[u] = *reinterpret_cast<const f32x4*>(K + (size_t)(c_ + j) * HD + d4 * 4);
+      vv[u] = *reinterpret_cast<const f32x4*>(V + (size_t)(c_ + j) * HD + d4 * 4);
+    }
+  };
+  fetch(k0);  // first chunk in flight together with q
+  if (head_ok) {
+    const float* q = p.q + (size_t)m * p.qs + h * HD;
+    for (int d = lane; d < HD; d += 64) qs[wave][d] = q[d] * p.scale;
+  }
   constexpr int NO = HD / 64;
-  constexpr int V4 = HD / 4;  // float4 per row
   float o[NO];
 #pragma unroll
   for (int i = 0; i < NO; ++i) o[i] = 0.f;
@@ -252,27 +338,16 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnParams p) {
   for (int c = k0; c <= k1; c += 64) {
     const int n = min(64, k1 - c + 1);
     __syncthreads();  // previous chunk consumed (and qs visible on the first pass)
-    {
-      constexpr int PER = 64 * V4 / 256;  // float4 per thread per tensor for a full chunk (4 or 8)
-      float4 kk[PER], vv[PER];
 #pragma unroll
-      for (int u = 0; u < PER; ++u) {
-        const int t = u * 256 + tid, j = t / V4, d4 = t % V4;
-        if (j < n) {
-          kk[u] = *reinterpret_cast<const float4*>(K + (size_t)(c + j) * HD + d4 * 4);
-          vv[u] = *reinterpret_cast<const float4*>(V + (size_t)(c + j) * HD + d4 * 4);
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < PER; ++u) {
-        const int t = u * 256 + tid, j = t / V4, d4 = t % V4;
-        if (j < n) {
-          *reinterpret_cast<float4*>(&Ks[j * KP + d4 * 4]) = kk[u];
-          *reinterpret_cast<float4*>(&Vs[j * HD + d4 * 4]) = vv[u];
-        }
+    for (int u = 0; u < PER; ++u) {
+      const int t = u * 256 + tid, j = t / V4, d4 = t % V4;
+      if (j < n) {
+        *reinterpret_cast<f32x4*>(&Ks[j * KP + d4 * 4]) = kk[u];
+        *reinterpret_cast<f32x4*>(&Vs[j * HD + d4 * 4]) = vv[u];
       }
     }
     __syncthreads();
+    fetch(min(c + 64, k1));  // next chunk streams while this one is scored (clamped: unconditional)
     if (!head_ok) continue;
     float s = -INFINITY;
     if (lane < n) {
@@ -281,11 +356,11 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnParams p) {
       float dot = 0.f;
 #pragma unroll
       for (int d4 = 0; d4 < V4; ++d4) {
-        const float4 kk = kr[d4], qq = qr[d4];
-        dot = fmaf(qq.x, kk.x, dot);
-        dot = fmaf(qq.y, kk.y, dot);
-        dot = fmaf(qq.z, kk.z, dot);
-        dot = fmaf(qq.w, kk.w, dot);
+        const float4 a = kr[d4], q4 = qr[d4];
+        dot = fmaf(q4.x, a.x, dot);
+        dot = fmaf(q4.y, a.y, dot);
+        dot = fmaf(q4.z, a.z, dot);
+        dot = fmaf(q4.w, a.w, dot);
       }
       s = dot;
     }
@@ -347,8 +422,8 @@ __global__ __launch_bounds__(256) void attn_oproj_kernel(GemvParams p, AttnParam
     const int nq = p.M * (qd / 4);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      const int t = u * 256 + tid;
-      if (t < nq) qv[u] = *reinterpret_cast<const float4*>(a.q + (size_t)(t / (qd / 4)) * a.qs + (t % (qd / 4)) * 4);
+      const int t = min(u * 256 + tid, nq - 1);
+      qv[u] = *reinterpret_cast<const float4*>(a.q + (size_t)(t / (qd / 4)) * a.qs + (t % (qd / 4)) * 4);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -361,25 +436,23 @@ __global__ __launch_bounds__(256) void attn_oproj_kernel(GemvParams p, AttnParam
   const int total = a.Hkv * n_live * V4;
   for (int t0 = 0; t0 < total; t0 += 256 * 8) {  // 8 loads per tensor in flight per thread
     float4 kr[8], vr[8];
-    size_t dk[8], dv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int t = min(t0 + u * 256 + tid, total - 1);  // clamped: always a valid row
+      const int kv = t / (n_live * V4), rem = t % (n_live * V4);
+      const int j = rem / V4, d4 = rem % V4;
+      const size_t src = (((size_t)b0 * a.Hkv + kv) * a.S_cap + j) * HD + d4 * 4;
+      kr[u] = *reinterpret_cast<const float4*>(a.kc + src);
+      vr[u] = *reinterpret_cast<const float4*>(a.vc + src);
+    }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int t = t0 + u * 256 + tid;
       if (t < total) {
         const int kv = t / (n_live * V4), rem = t % (n_live * V4);
         const int j = rem / V4, d4 = rem % V4;
-        const size_t src = (((size_t)b0 * a.Hkv + kv) * a.S_cap + j) * HD + d4 * 4;
-        kr[u] = *reinterpret_cast<const float4*>(a.kc + src);
-        vr[u] = *reinterpret_cast<const float4*>(a.vc + src);
-        dk[u] = ((size_t)kv * n_max + j) * KP + d4 * 4;
-        dv[u] = ((size_t)kv * n_max + j) * HD + d4 * 4;
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      if (t0 + u * 256 + tid < total) {
-        *reinterpret_cast<float4*>(Ks + dk[u]) = kr[u];
-        *reinterpret_cast<float4*>(Vs + dv[u]) = vr[u];
+        *reinterpret_cast<float4*>(Ks + ((size_t)kv * n_max + j) * KP + d4 * 4) = kr[u];
+        *reinterpret_cast<float4*>(Vs + ((size_t)kv * n_max + j) * HD + d4 * 4) = vr[u];
       }
     }
   }
@@ -606,29 +679,32 @@ __global__ __launch_bounds__(256) void sample_kernel(SampleParams p) {
   }
   // NaN logits leave no winner; clamp so a bad row can never index outside the embedding table
   code = min(max(code, 0), V - 1);
-  if (tid == 0) p.codes[(size_t)b * p.K + p.cb] = code;
-  if (p.next_in) {
-    const int D = p.D;
-    const WT* emb = (const WT*)p.audio_emb + ((size_t)code + (size_t)p.V_emb * p.cb) * D;
-    float* dst = p.cb == 0 ? p.next_in + (size_t)(2 * b + 1) * D : p.next_in + (size_t)b * D;
-    for (int d0 = tid * 8; d0 < D; d0 += 256 * 8) {
-      float w[8];
-      W8<WT>::load(emb + d0, w);
-      *reinterpret_cast<float4*>(dst + d0) = make_float4(w[0], w[1], w[2], w[3]);
-      *reinterpret_cast<float4*>(dst + d0 + 4) = make_float4(w[4], w[5], w[6], w[7]);
-      if (p.cb == 0) {  // decoder step-1 rows are [h_last, E_a[c0]] (generation.py:62-64)
-        const float* hl = p.h_last + (size_t)b * D + d0;
-        float* r0 = p.next_in + (size_t)(2 * b) * D + d0;
-        *reinterpret_cast<float4*>(r0) = *reinterpret_cast<const float4*>(hl);
-        *reinterpret_cast<float4*>(r0 + 4) = *reinterpret_cast<const float4*>(hl + 4);
-      }
-    }
+  if (tid == 0) {
+    p.codes[(size_t)b * p.K + p.cb] = code;
+    if (p.part) p.part[(size_t)b * p.part_stride] = pack_argmax(0.f, code);  // consumed as a 1-entry partial
   }
 }
 
 // ============================================================================ advance
 __global__ void advance_kernel(AdvanceParams p) {
   const int f = p.frame_ctr[0];
+  if (p.last_part) {  // greedy: arg-max of the last head's block partials -> codes[b][K-1]
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int b = wave; b < p.B; b += blockDim.x / 64) {
+      unsigned long long best = 0;
+      for (int i = lane; i < p.last_n; i += 64) {
+        const unsigned long long v = p.last_part[(size_t)b * p.last_stride + i];
+        best = v > best ? v : best;
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long v = __shfl_xor(best, o, 64);
+        best = v > best ? v : best;
+      }
+      if (lane == 0) p.codes[(size_t)b * p.K + p.K - 1] = min(max(unpack_argmax(best), 0), p.V - 1);
+    }
+    __syncthreads();
+  }
   for (int b = threadIdx.x; b < p.B; b += blockDim.x) {
     bool any = false;
     for (int k = 0; k < p.K; ++k) {
@@ -763,4 +839,12 @@ void launch_attn_oproj(const GemvParams& p0, const AttnParams& a, int wdt, int h
   p.nw = nullptr;
   if (wdt == WDT_BF16) launch_attn_oproj_t<bf16_t>(p, a, hd, st);
   else launch_attn_oproj_t<float>(p, a, hd, st);
+}
+
+// ============================================================================ launch-floor probe
+__global__ void empty_kernel(int* p) {
+  if (p && threadIdx.x == 0 && blockIdx.x == 0) p[0] += 1;
+}
+void launch_empty(int blocks, int* p, hipStream_t st) {
+  hipLaunchKernelGGL(empty_kernel, dim3(blocks), dim3(256), 0, st, p);
 }

@@ -90,6 +90,9 @@ int csm_synchronize(csm_engine* e);
 int csm_bench_gemv(csm_engine* e, int which, int M, int iters, float* avg_us, double* bytes);
 /* Profiling hook: force the GEMV tiling (threads per row group G, rows per thread RPT); 0 = auto. */
 int csm_set_gemv_config(int G, int RPT);
+/* Profiling hook: per-kernel time of n dependent near-empty kernels (blocks x 256 threads),
+ * replayed as one HIP graph (graph=1) or launched eagerly (graph=0). */
+int csm_bench_floor(csm_engine* e, int n_kernels, int blocks, int graph, float* us_per_kernel);
 
 /* ------------------------------------------------------------------ Mimi codec */
 typedef struct mimi_dims {
