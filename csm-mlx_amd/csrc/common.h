@@ -19,11 +19,24 @@ template <> struct W8<bf16_t> {
     w[0] = bf16_lo(u.x); w[1] = bf16_hi(u.x); w[2] = bf16_lo(u.y); w[3] = bf16_hi(u.y);
     w[4] = bf16_lo(u.z); w[5] = bf16_hi(u.z); w[6] = bf16_lo(u.w); w[7] = bf16_hi(u.w);
   }
+  // streamed-once weights: non-temporal 16-B load (does not displace re-read lines in L2/MALL)
+  __device__ __forceinline__ static void load_nt(const bf16_t* p, float (&w)[8]) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 u = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    w[0] = bf16_lo(u.x); w[1] = bf16_hi(u.x); w[2] = bf16_lo(u.y); w[3] = bf16_hi(u.y);
+    w[4] = bf16_lo(u.z); w[5] = bf16_hi(u.z); w[6] = bf16_lo(u.w); w[7] = bf16_hi(u.w);
+  }
 };
 template <> struct W8<float> {
   __device__ __forceinline__ static void load(const float* p, float (&w)[8]) {
     const float4 a = *reinterpret_cast<const float4*>(p);
     const float4 b = *reinterpret_cast<const float4*>(p + 4);
+    w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w; w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+  }
+  __device__ __forceinline__ static void load_nt(const float* p, float (&w)[8]) {
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    const f32x4 a = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+    const f32x4 b = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p + 4));
     w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w; w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
   }
 };

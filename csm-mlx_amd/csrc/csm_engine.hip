@@ -91,7 +91,15 @@ struct csm_engine {
   std::vector<void*> allocs;
   std::vector<void*> batch_allocs;
   std::vector<int> pos_host;
-  bool fuse_dec_attn = false;  // CSM_FUSE_DEC_ATTN=1: measured slower (14 us vs 8.5 us) on MI355X
+  // attention -> o_proj in one launch (attn_oproj_kernel, CSM_FUSE_ATTN=1 / csm_set_option).
+  // Off by default: bit-exact and stable, but on MI355X at B=1 it measured 208.3 vs 209.2 frames/s
+  // for two launches -- the in-launch hand-off (drain + counter + poll + sc1 reload) costs what
+  // the removed kernel boundary saved.
+  bool fuse_attn = false;
+  unsigned* hs_body = nullptr;  // per-call monotonic hand-off counters, then the graph's epoch word
+  unsigned* hs_head = nullptr;
+  size_t hs_body_bytes = 0, hs_head_bytes = 0;
+  int* hs_err = nullptr;  // set by a hand-off that timed out
 
   void* balloc(size_t bytes) {
     void* p = nullptr;
@@ -143,12 +151,25 @@ void alloc_stack(csm_engine* e, Stack& s, const csm_llama_dims& d, int S_cap, co
   e->required.push_back(std::string(prefix) + ".norm.weight");
 }
 
+// Debug-only timing ablation (CSM_ABLATE bit mask, read at graph capture): skips kernels so their
+// in-graph cost can be measured as a frame-time delta.  Results are garbage when set.
+int ablate() {
+  static int m = -1;
+  if (m < 0) {
+    const char* v = getenv("CSM_ABLATE");
+    m = v ? atoi(v) : 0;
+  }
+  return m;
+}
+
 // One Llama block stack over M rows of the residual stream x (in place).
+// hs: per-layer hand-off counters for the fused attention -> o_proj launch (nullptr: two launches).
 void run_stack(csm_engine* e, Stack& s, float* x, int M, float* q, float* att, float* mlp, const RowMap& rm,
-               hipStream_t st) {
+               hipStream_t st, unsigned* hs = nullptr, const unsigned* epoch = nullptr) {
   const csm_llama_dims& d = s.d;
   const int tag = (&s == &e->dec) ? 1 : 0;
   const int D = d.hidden, F = d.intermediate, hd = d.head_dim, Hq = d.n_heads, Hkv = d.n_kv_heads;
+  const int ab = tag ? ablate() : (ablate() >> 8) & 31;  // bits 0-4 decoder, 8-12 backbone
   for (int i = 0; i < d.n_layers; ++i) {
     LayerW& l = s.L[i];
     GemvParams g{};
@@ -156,29 +177,30 @@ void run_stack(csm_engine* e, Stack& s, float* x, int M, float* q, float* att, f
     g.W = l.wqkv; g.N = s.qkv_rows(); g.K = D; g.x = x; g.xs = D; g.M = M; g.nw = l.n1; g.eps = d.eps;
     g.out = q; g.os = s.q_dim(); g.Hq = Hq; g.Hkv = Hkv; g.hd = hd; g.S_cap = s.S_cap; g.rope = s.rope;
     g.kc = l.kc; g.vc = l.vc; g.rm = rm;
-    launch_gemv(g, e->wdt, EPI_QKV, 1, st, tag);
+    if (!(ab & 2)) launch_gemv(g, e->wdt, EPI_QKV, 1, st, tag);
     // attention (+ o_proj + residual fused for the short depth-decoder KV)
     AttnParams a{};
     a.q = q; a.qs = s.q_dim(); a.M = M; a.kc = l.kc; a.vc = l.vc; a.Hq = Hq; a.Hkv = Hkv; a.S_cap = s.S_cap;
     a.scale = 1.0f / sqrtf((float)hd); a.mode = ATTN_CAUSAL; a.window = 0; a.rm = rm; a.out = att;
+    a.epoch = epoch;
     a.os = s.q_dim();
     g = GemvParams{};
     g.W = l.wo; g.N = D; g.K = s.q_dim(); g.x = att; g.xs = s.q_dim(); g.M = M; g.out = x; g.os = D;
-    if (s.S_cap <= 64 && M <= 4 && rm.T * 1 >= M && e->fuse_dec_attn) {  // rows of ONE utterance
-      launch_attn_oproj(g, a, e->wdt, hd, st);
+    if (hs && epoch && e->fuse_attn && !(ab & 5) && attn_oproj_supported(g, a)) {
+      launch_attn_oproj(g, a, e->wdt, hd, hs + i, e->hs_err, st, tag);
     } else {
-      launch_attn(a, hd, st);
-      launch_gemv(g, e->wdt, EPI_ADD, 0, st, tag);
+      if (!(ab & 1)) launch_attn(a, hd, st);
+      if (!(ab & 4)) launch_gemv(g, e->wdt, EPI_ADD, 0, st, tag);
     }
     // norm2 + gate/up + SiLU*up
     g = GemvParams{};
     g.W = l.wgu; g.N = 2 * F; g.K = D; g.x = x; g.xs = D; g.M = M; g.nw = l.n2; g.eps = d.eps; g.out = mlp;
     g.os = F;
-    launch_gemv(g, e->wdt, EPI_SILU_MUL, 1, st, tag);
+    if (!(ab & 8)) launch_gemv(g, e->wdt, EPI_SILU_MUL, 1, st, tag);
     // down + residual
     g = GemvParams{};
     g.W = l.wd; g.N = D; g.K = F; g.x = mlp; g.xs = F; g.M = M; g.out = x; g.os = D;
-    launch_gemv(g, e->wdt, EPI_ADD, 0, st, tag);
+    if (!(ab & 16)) launch_gemv(g, e->wdt, EPI_ADD, 0, st, tag);
   }
 }
 
@@ -187,9 +209,10 @@ void enqueue_body(csm_engine* e, hipStream_t st) {
   EmbedParams ep{};
   ep.codes = e->codes; ep.text_emb = e->text_emb; ep.audio_emb = e->audio_emb; ep.V = e->V; ep.K = e->K;
   ep.D = e->D; ep.out = e->x; ep.pos_inc = e->pos;
+  ep.epoch_inc = e->hs_body + e->bb.d.n_layers;  // one hand-off epoch per body replay
   launch_embed(ep, e->wdt, B, st);
   RowMap rm{1, 0, e->pos, 0};
-  run_stack(e, e->bb, e->x, B, e->q, e->att, e->mlp, rm, st);
+  run_stack(e, e->bb, e->x, B, e->q, e->att, e->mlp, rm, st, e->hs_body, e->hs_body + e->bb.d.n_layers);
   launch_rmsnorm_rows(e->x, e->D, e->bb.norm, e->bb.d.eps, e->D, e->h_last, e->D, B, st);
 }
 
@@ -206,6 +229,8 @@ void enqueue_head(csm_engine* e, hipStream_t st) {
   GemvParams g{};
   g.W = e->c0_head; g.N = Vp; g.K = D; g.x = e->h_last; g.xs = D; g.M = B; g.out = e->c0_logits; g.os = Vp;
   g.part = part(0); g.part_stride = e->part_stride; g.n_valid = V;
+  const int n_hs = e->dec.d.n_layers * (K - 1);
+  g.epoch_inc = e->hs_head + n_hs;  // one hand-off epoch per head replay
   launch_gemv(g, e->wdt, greedy ? EPI_ARGMAX : EPI_STORE, 0, st);
   if (!greedy) {
     sp.logits = e->c0_logits; sp.cb = 0; sp.part = part(0);
@@ -219,16 +244,17 @@ void enqueue_head(csm_engine* e, hipStream_t st) {
     g.W = e->proj; g.N = Dd; g.K = D; g.x = e->h_last; g.xs = D; g.M = M; g.out = e->dx; g.os = Dd;
     g.xpart = part(i - 1); g.xpart_stride = e->part_stride; g.xpart_n = greedy ? (i == 1 ? n0 : ni) : 1;
     g.xtab = e->audio_emb; g.xV = V; g.xcb = i - 1; g.x_step1 = (i == 1); g.x_codes = e->codes; g.x_codes_K = K;
-    launch_gemv(g, e->wdt, EPI_STORE, 0, st);
+    if (!(i >= 2 && (ablate() & 32))) launch_gemv(g, e->wdt, EPI_STORE, 0, st);
     RowMap rm = (i == 1) ? RowMap{2, 0, nullptr, 0} : RowMap{1, 0, nullptr, i};
-    run_stack(e, e->dec, e->dx, M, e->dq, e->datt, e->dmlp, rm, st);
+    run_stack(e, e->dec, e->dx, M, e->dq, e->datt, e->dmlp, rm, st,
+              e->hs_head + (size_t)(i - 1) * e->dec.d.n_layers, e->hs_head + n_hs);
     // ci_logits = norm(hidden[:, -1]) @ audio_head[i-1]  (generation.py:79)
     g = GemvParams{};
     g.W = (const char*)e->audio_head + (size_t)(i - 1) * Vp * Dd * e->wsz; g.N = Vp; g.K = Dd;
     g.x = e->dx + (i == 1 ? Dd : 0); g.xs = (i == 1 ? 2 * Dd : Dd); g.M = B; g.nw = e->dec.norm;
     g.eps = e->dec.d.eps; g.out = e->ci_logits + (size_t)(i - 1) * B * Vp; g.os = Vp;
     g.part = part(i); g.part_stride = e->part_stride; g.n_valid = V;
-    launch_gemv(g, e->wdt, greedy ? EPI_ARGMAX : EPI_STORE, 1, st);
+    if (!(ablate() & 64)) launch_gemv(g, e->wdt, greedy ? EPI_ARGMAX : EPI_STORE, 1, st);
     if (!greedy) {
       sp.logits = e->ci_logits + (size_t)(i - 1) * B * Vp; sp.cb = i; sp.part = part(i);
       launch_sample(sp, e->wdt, B, st);
@@ -291,6 +317,13 @@ void ensure_batch(csm_engine* e, int B) {
   e->part = (unsigned long long*)e->balloc(K * Bm * (size_t)e->part_stride * 8);
 }
 
+// A bounded in-launch wait that gave up leaves results undefined: fail loudly.
+void check_handoff(csm_engine* e) {
+  int err = 0;
+  HIPCHK(hipMemcpy(&err, e->hs_err, 4, hipMemcpyDeviceToHost));
+  if (err) throw CsmError(CSM_ERR_HIP, "in-launch attention hand-off timed out (results invalid)");
+}
+
 }  // namespace
 
 // =============================================================================== C ABI
@@ -335,7 +368,7 @@ int csm_engine_create(const csm_dims* dims, int device, int weight_dtype, int ma
     }
     HIPCHK(hipSetDevice(device));
     std::unique_ptr<csm_engine> e(new csm_engine());
-    if (const char* v = getenv("CSM_FUSE_DEC_ATTN")) e->fuse_dec_attn = v[0] != '0';
+    if (const char* v = getenv("CSM_FUSE_ATTN")) e->fuse_attn = v[0] != '0';
     e->dims = *dims;
     e->dev = device;
     e->wdt = weight_dtype == CSM_F32 ? WDT_F32 : WDT_BF16;
@@ -369,6 +402,12 @@ int csm_engine_create(const csm_dims* dims, int device, int weight_dtype, int ma
     e->tok = (int32_t*)e->alloc(M * (K + 1) * 4);
     e->msk = (uint8_t*)e->alloc(M * (K + 1));
     e->frame_ctr = (int*)e->alloc(16);
+    // per-call counters, then the graph's epoch word
+    e->hs_body_bytes = ((size_t)(b.n_layers + 1) * 4 + 15) / 16 * 16;
+    e->hs_head_bytes = ((size_t)(d.n_layers * (e->K - 1) + 1) * 4 + 15) / 16 * 16;
+    e->hs_body = (unsigned*)e->alloc(e->hs_body_bytes);
+    e->hs_head = (unsigned*)e->alloc(e->hs_head_bytes);
+    e->hs_err = (int*)e->alloc(16);
     (void)Vp;
     (void)B;
     ensure_batch(e.get(), max_batch);
@@ -523,6 +562,9 @@ int csm_begin(csm_engine* e, int B, const uint64_t* seeds, float temperature, in
     HIPCHK(hipMemsetAsync(e->done, 0, B, e->st));
     HIPCHK(hipMemsetAsync(e->n_frames, 0, B * 4, e->st));
     HIPCHK(hipMemsetAsync(e->frame_ctr, 0, 16, e->st));
+    HIPCHK(hipMemsetAsync(e->hs_err, 0, 16, e->st));
+    HIPCHK(hipMemsetAsync(e->hs_body, 0, e->hs_body_bytes, e->st));  // (a timed-out call leaves them set)
+    HIPCHK(hipMemsetAsync(e->hs_head, 0, e->hs_head_bytes, e->st));
     HIPCHK(hipMemsetAsync(e->codes, 0, (size_t)B * e->K * 4, e->st));
     HIPCHK(hipStreamSynchronize(e->st));
   }
@@ -610,6 +652,7 @@ int csm_run_frames(csm_engine* e, int nframes, int* all_done) {
       std::vector<uint8_t> d(e->B);
       HIPCHK(hipMemcpyAsync(d.data(), e->done, e->B, hipMemcpyDeviceToHost, e->st));
       HIPCHK(hipStreamSynchronize(e->st));
+      check_handoff(e);
       int all = 1;
       for (auto v : d) all &= (v != 0);
       *all_done = all;
@@ -622,6 +665,7 @@ int csm_read_codes(csm_engine* e, int32_t* hist, int32_t* n_frames, uint8_t* don
   CSM_TRY {
     HIPCHK(hipSetDevice(e->dev));
     HIPCHK(hipStreamSynchronize(e->st));
+    check_handoff(e);
     if (hist)
       HIPCHK(hipMemcpy(hist, e->hist, (size_t)e->frames_run * e->B * e->K * 4, hipMemcpyDeviceToHost));
     if (n_frames) HIPCHK(hipMemcpy(n_frames, e->n_frames, e->B * 4, hipMemcpyDeviceToHost));
@@ -748,6 +792,18 @@ int csm_bench_floor(csm_engine* e, int n_kernels, int blocks, int graph, float* 
     HIPCHK(hipMemsetAsync(ctr, 0, 4, e->st));
     HIPCHK(hipStreamSynchronize(e->st));
     if (us_per_kernel) *us_per_kernel = ms * 1000.f / (5.f * n_kernels);
+  }
+  CSM_CATCH
+}
+
+int csm_set_option(csm_engine* e, const char* key, int value) {
+  CSM_TRY {
+    const std::string k(key ? key : "");
+    if (k == "fuse_attn") e->fuse_attn = value != 0;
+    else if (k == "nt_mask") gemv_set_nt_mask(value);
+    else if (k == "handoff_acquire") attn_oproj_set_acquire(value);
+    else throw CsmError(CSM_ERR_ARG, "unknown option " + k);
+    e->g_B = -1;  // re-capture the frame graphs with the new setting
   }
   CSM_CATCH
 }

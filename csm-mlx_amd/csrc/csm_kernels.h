@@ -36,6 +36,7 @@ struct GemvParams {
   const void* xtab;
   int xV, xcb, x_step1, x_codes_K;
   int* x_codes;
+  unsigned* epoch_inc;  // if set: block 0 does *epoch_inc += 1 (one graph replay = one hand-off epoch)
 };
 
 __device__ __forceinline__ unsigned long long pack_argmax(float v, int idx) {
@@ -54,6 +55,7 @@ struct EmbedParams {
   int V, K, D;
   float* out;            // [M][D]
   int* pos_inc;          // decode mode: pos[m] += 1 (position of the new backbone row)
+  unsigned* epoch_inc;   // if set: *epoch_inc += 1 (one graph replay = one hand-off epoch)
 };
 
 struct AttnParams {
@@ -67,6 +69,7 @@ struct AttnParams {
   RowMap rm;
   float* out;
   int os;
+  const unsigned* epoch;  // attn_oproj: hand-off epoch of this call (counter target = epoch * M*Hkv)
 };
 
 struct SampleParams {
@@ -100,7 +103,12 @@ void launch_attn(const AttnParams& p, int hd, hipStream_t st);
 int gemv_rows_per_block(int N, int K, int M);
 void gemv_set_override(int G, int RPT);  // 0 = automatic
 // fused attention (<= 64 keys, M <= 4 rows) + o_proj + residual for the depth decoder
-void launch_attn_oproj(const GemvParams& p, const AttnParams& a, int wdt, int hd, hipStream_t st);
+// attention published in-launch to the o_proj GEMV (+ residual); ctr: a zeroed per-call word
+bool attn_oproj_supported(const GemvParams& p, const AttnParams& a);
+void attn_oproj_set_acquire(int on);
+void gemv_set_nt_mask(int mask);
+void launch_attn_oproj(const GemvParams& p, const AttnParams& a, int wdt, int hd, unsigned* ctr, int* err,
+                       hipStream_t st, int tag);
 void launch_rmsnorm_rows(const float* x, int xs, const float* w, float eps, int D, float* out, int os, int M,
                          hipStream_t st);
 void launch_sample(const SampleParams& p, int wdt, int B, hipStream_t st);

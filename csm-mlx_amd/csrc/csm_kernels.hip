@@ -14,6 +14,8 @@
 // round trip); x rows are tiny and served from L1/L2.
 #include "csm_kernels.h"
 
+#include <cstdlib>
+
 // ============================================================================ embed
 // x[m] = sum_j mask[m,j] * table_j[tok[m,j]]  over the K audio columns (row tok + V*j of the
 // audio table) then the text column -- the order of the reference's .sum(-2) over 33 rows
@@ -38,6 +40,7 @@ __global__ __launch_bounds__(256) void embed_rows_kernel(EmbedParams p) {
   }
   __syncthreads();
   if (p.pos_inc && threadIdx.x == 0) p.pos_inc[m] += 1;
+  if (p.epoch_inc && threadIdx.x == 0 && m == 0) *p.epoch_inc += 1;
   float* out = p.out + (size_t)m * p.D;
   for (int d0 = threadIdx.x * 8; d0 < p.D; d0 += blockDim.x * 8) {
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -137,6 +140,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
   const int row0 = blockIdx.x * RPB + grp * RPT;
   const bool norm = p.nw != nullptr;
   const WT* W = (const WT*)p.W;
+  if (p.epoch_inc && blockIdx.x == 0 && tid == 0) *p.epoch_inc += 1;
   // x gather mode: resolve each needed row's code from the producer's block partials once
   __shared__ int gcode[512];  // codes of the gathered rows (M <= 512)
   if (p.xpart) {
@@ -187,7 +191,10 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
     for (int k = gt * 8; k < p.K; k += G * 8) {
       float w[RPT][8];
 #pragma unroll
-      for (int r = 0; r < RPT; ++r) W8<WT>::load(W + (size_t)(row0 + r) * p.K + k, w[r]);
+      for (int r = 0; r < RPT; ++r) {
+        if constexpr ((TAG & 4) != 0) W8<WT>::load_nt(W + (size_t)(row0 + r) * p.K + k, w[r]);
+        else W8<WT>::load(W + (size_t)(row0 + r) * p.K + k, w[r]);
+      }
       float nw[8];
       if (norm) W8<float>::load(p.nw + k, nw);
 #pragma unroll
@@ -277,23 +284,27 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
 }
 
 // ============================================================================ attention
-// Decode-shaped GQA attention.  One block per (query row m, kv head); wave w serves q head
-// kvh*G + w (G = Hq/Hkv <= 4).  Keys [k0, k1] of utterance b(m) stream through LDS in chunks of
-// 64 rows; the chunk loads are software-pipelined through registers (chunk c+1 is in flight while
+// Decode-shaped GQA attention for one (query row m, kv head) per 256-thread block; wave w serves
+// q head kvh*G + w (G = Hq/Hkv <= 4).  Keys [k0, k1] of utterance b(m) stream through LDS in chunks
+// of 64 rows; the chunk loads are software-pipelined through registers (chunk c+1 is in flight while
 // chunk c is scored), all 256 threads issuing coalesced 16-B loads.  Each wave scores its head
 // (lane = key, K rows padded by 16 B: conflict-free ds_read_b128), online softmax in fp32, and
-// P.V with lane = head dim reading V rows from LDS.
+// P.V with lane = head dim reading V rows from LDS.  SC1 = write the output with write-through
+// (sc1) stores, for a consumer in the same launch (attn_oproj_kernel).
 template <int HD>
-__global__ __launch_bounds__(256) void attn_kernel(AttnParams p) {
+struct AttnLds {
+  float Ks[64 * (HD + 4)];
+  float Vs[64 * HD];
+  float qs[4][HD];
+};
+
+template <int HD, bool SC1>
+__device__ __forceinline__ void attn_block(const AttnParams& p, int m, int kvh, AttnLds<HD>& L) {
   constexpr int KP = HD + 4;  // padded K row (floats)
   constexpr int V4 = HD / 4;  // float4 per row
   constexpr int PER = 64 * V4 / 256;  // float4 per thread per tensor for a full chunk (4 or 8)
-  __shared__ __attribute__((aligned(16))) float Ks[64 * KP];
-  __shared__ __attribute__((aligned(16))) float Vs[64 * HD];
-  __shared__ __attribute__((aligned(16))) float qs[4][HD];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int G = p.Hq / p.Hkv;
-  const int m = blockIdx.x / p.Hkv, kvh = blockIdx.x % p.Hkv;
   const int h = kvh * G + wave;
   const bool head_ok = wave < G;
   const int b = p.rm.b(m), pos = p.rm.pos(m);
@@ -312,8 +323,8 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnParams p) {
   const float* K = p.kc + ((size_t)b * p.Hkv + kvh) * p.S_cap * HD;
   const float* V = p.vc + ((size_t)b * p.Hkv + kvh) * p.S_cap * HD;
   // chunk loads through registers; rows past the live range re-read the last live row (always a
-  // valid address), so the register array is written unconditionally and stays in VGPRs
-  // native ext-vector (not HIP's float4 struct, whose copies lower to memcpy and defeat SROA)
+  // valid address), so the register array is written unconditionally and stays in VGPRs.
+  // Native ext-vector (not HIP's float4 struct, whose copies lower to memcpy and defeat SROA).
   typedef float f32x4 __attribute__((ext_vector_type(4)));
   f32x4 kk[PER], vv[PER];
   auto fetch = [&](const int c_) {
@@ -328,7 +339,7 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnParams p) {
   fetch(k0);  // first chunk in flight together with q
   if (head_ok) {
     const float* q = p.q + (size_t)m * p.qs + h * HD;
-    for (int d = lane; d < HD; d += 64) qs[wave][d] = q[d] * p.scale;
+    for (int d = lane; d < HD; d += 64) L.qs[wave][d] = q[d] * p.scale;
   }
   constexpr int NO = HD / 64;
   float o[NO];
@@ -342,8 +353,8 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnParams p) {
     for (int u = 0; u < PER; ++u) {
       const int t = u * 256 + tid, j = t / V4, d4 = t % V4;
       if (j < n) {
-        *reinterpret_cast<f32x4*>(&Ks[j * KP + d4 * 4]) = kk[u];
-        *reinterpret_cast<f32x4*>(&Vs[j * HD + d4 * 4]) = vv[u];
+        *reinterpret_cast<f32x4*>(&L.Ks[j * KP + d4 * 4]) = kk[u];
+        *reinterpret_cast<f32x4*>(&L.Vs[j * HD + d4 * 4]) = vv[u];
       }
     }
     __syncthreads();
@@ -351,8 +362,8 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnParams p) {
     if (!head_ok) continue;
     float s = -INFINITY;
     if (lane < n) {
-      const float4* kr = reinterpret_cast<const float4*>(&Ks[lane * KP]);
-      const float4* qr = reinterpret_cast<const float4*>(qs[wave]);
+      const float4* kr = reinterpret_cast<const float4*>(&L.Ks[lane * KP]);
+      const float4* qr = reinterpret_cast<const float4*>(L.qs[wave]);
       float dot = 0.f;
 #pragma unroll
       for (int d4 = 0; d4 < V4; ++d4) {
@@ -373,7 +384,7 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnParams p) {
     for (int j = 0; j < n; ++j) {
       const float pb = __shfl(pj, j, 64);
 #pragma unroll
-      for (int i = 0; i < NO; ++i) o[i] = fmaf(pb, Vs[j * HD + lane + 64 * i], o[i]);
+      for (int i = 0; i < NO; ++i) o[i] = fmaf(pb, L.Vs[j * HD + lane + 64 * i], o[i]);
     }
     m_run = new_m;
   }
@@ -381,167 +392,150 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnParams p) {
   const float inv = 1.f / l_run;
   float* out = p.out + (size_t)m * p.os + h * HD;
 #pragma unroll
-  for (int i = 0; i < NO; ++i) out[lane + 64 * i] = o[i] * inv;
+  for (int i = 0; i < NO; ++i) {
+    if constexpr (SC1) __hip_atomic_store(out + lane + 64 * i, o[i] * inv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else out[lane + 64 * i] = o[i] * inv;
+  }
 }
 
-// ============================================================================ fused decoder attention + o_proj
-// For the depth decoder (<= 32 cached positions per frame, generation.py:70-77) the attention of
-// all heads is ~65K FMAs over <= 64 KB of K/V, far cheaper than a kernel boundary.  Every o_proj
-// block: (1) issues its o_proj weight loads (independent of the attention), (2) stages q and the
-// live K/V rows of every kv head into LDS with all 256 threads (one memory latency), (3) computes
-// the attention of its M (<= 4) rows from LDS, (4) runs the o_proj GEMV (+ residual) from LDS.
-// One launch replaces attention + o_proj.
-template <typename WT, int HD, int G, int RPT, int MT>
-__global__ __launch_bounds__(256) void attn_oproj_kernel(GemvParams p, AttnParams a, int n_max) {
+template <int HD>
+__global__ __launch_bounds__(256) void attn_kernel(AttnParams p) {
+  __shared__ __attribute__((aligned(16))) AttnLds<HD> L;
+  attn_block<HD, false>(p, blockIdx.x / p.Hkv, blockIdx.x % p.Hkv, L);
+}
+
+// ============================================================================ attention -> o_proj in one launch
+// Blocks [0, P) (P = M*Hkv) first compute the attention of one (row, kv head) each and publish it
+// write-through (sc1 stores, drained, then one relaxed agent-scope add to the call's counter).
+// Every block issues its o_proj weight loads BEFORE that (weights do not depend on the
+// attention), then waits for the counter and runs the GEMV (+ residual) reading the attention
+// output with sc1 loads -- MI355X_MICROARCH.md "Valid forms" hand-off: no fences.  Counters are
+// monotonic (zeroed by csm_begin only): the graph's first kernel bumps an epoch word once per
+// replay and the call waits for counter >= epoch * P, so replays need no memset node (a captured
+// hipMemsetAsync node raced the kernel under ROCm 7.0's runtime) and no contended reset atomic.
+// Producers are the lowest block ids (dispatched first) and every spin is bounded: on timeout
+// the block sets *err and exits (the host raises).
+// One launch replaces attention + o_proj: the kernel boundary and the o_proj weight latency
+// disappear behind the attention.
+template <typename WT, int HD, int G, int RPT, int MT, int TAG>
+__global__ __launch_bounds__(256) void attn_oproj_kernel(GemvParams p, AttnParams a, unsigned* ctr, int* err, int acq) {
   constexpr int NG = 256 / G;
   constexpr int RPB = NG * RPT;
-  constexpr int KP = HD + 4;
-  constexpr int V4 = HD / 4;
-  extern __shared__ __attribute__((aligned(16))) float lds[];
-  float* Ks = lds;                                   // [Hkv][n_max][KP]
-  float* Vs = Ks + (size_t)a.Hkv * n_max * KP;       // [Hkv][n_max][HD]
-  float* qa = Vs + (size_t)a.Hkv * n_max * HD;       // [M][Hq*HD]: q, overwritten by the attention output
+  constexpr int KS = 2;  // K-steps of weights prefetched before the wait (K <= 2*G*8)
+  __shared__ __attribute__((aligned(16))) AttnLds<HD> L;
   __shared__ float red[4][MT][RPT];
+  __shared__ int go;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int grp = tid / G, gt = tid % G;
   const int row0 = blockIdx.x * RPB + grp * RPT;
   const WT* W = (const WT*)p.W;
-  // (1) first K-step of weights in flight before anything else
-  float w[RPT][8];
-  const int k_first = gt * 8;
-  if (k_first < p.K) {
+  const unsigned P = (unsigned)(a.M * a.Hkv);
+  const unsigned target = P * *a.epoch;  // written by an earlier kernel of this replay
+  // (1) weights of the first KS K-steps in flight
+  float w[KS][RPT][8];
 #pragma unroll
-    for (int r = 0; r < RPT; ++r) W8<WT>::load(W + (size_t)(row0 + r) * p.K + k_first, w[r]);
-  }
-  // (2) stage q rows and K/V rows [0, n_max) of the batch row b(0) (all rows share b in decoder steps
-  //     with T rows per utterance; rows of other utterances are staged per utterance below)
-  const int qd = a.Hq * HD;
-  const int b0 = a.rm.b(0);
-  {
-    float4 qv[4];
-    const int nq = p.M * (qd / 4);
+  for (int s = 0; s < KS; ++s) {
+    const int k = gt * 8 + s * G * 8;
+    if (k < p.K) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int t = min(u * 256 + tid, nq - 1);
-      qv[u] = *reinterpret_cast<const float4*>(a.q + (size_t)(t / (qd / 4)) * a.qs + (t % (qd / 4)) * 4);
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int t = u * 256 + tid;
-      if (t < nq) *reinterpret_cast<float4*>(qa + (size_t)(t / (qd / 4)) * qd + (t % (qd / 4)) * 4) = qv[u];
-    }
-  }
-  // live rows only: the last row of the call has the largest position
-  const int n_live = a.rm.pos(p.M - 1) + 1;
-  const int total = a.Hkv * n_live * V4;
-  for (int t0 = 0; t0 < total; t0 += 256 * 8) {  // 8 loads per tensor in flight per thread
-    float4 kr[8], vr[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int t = min(t0 + u * 256 + tid, total - 1);  // clamped: always a valid row
-      const int kv = t / (n_live * V4), rem = t % (n_live * V4);
-      const int j = rem / V4, d4 = rem % V4;
-      const size_t src = (((size_t)b0 * a.Hkv + kv) * a.S_cap + j) * HD + d4 * 4;
-      kr[u] = *reinterpret_cast<const float4*>(a.kc + src);
-      vr[u] = *reinterpret_cast<const float4*>(a.vc + src);
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int t = t0 + u * 256 + tid;
-      if (t < total) {
-        const int kv = t / (n_live * V4), rem = t % (n_live * V4);
-        const int j = rem / V4, d4 = rem % V4;
-        *reinterpret_cast<float4*>(Ks + ((size_t)kv * n_max + j) * KP + d4 * 4) = kr[u];
-        *reinterpret_cast<float4*>(Vs + ((size_t)kv * n_max + j) * HD + d4 * 4) = vr[u];
+      for (int r = 0; r < RPT; ++r) {
+        if constexpr ((TAG & 4) != 0) W8<WT>::load_nt(W + (size_t)(row0 + r) * p.K + k, w[s][r]);
+        else W8<WT>::load(W + (size_t)(row0 + r) * p.K + k, w[s][r]);
       }
     }
   }
-  __syncthreads();
-  // (3) attention, one wave per (row, head)
-  for (int idx = wave; idx < p.M * a.Hq; idx += 4) {
-    const int m = idx / a.Hq, h = idx % a.Hq;
-    const int kv = h / (a.Hq / a.Hkv);
-    const int n = a.rm.pos(m) + 1;
-    float* qh = qa + (size_t)m * qd + h * HD;
-    float s = -INFINITY;
-    if (lane < n) {
-      const float4* kr = reinterpret_cast<const float4*>(Ks + ((size_t)kv * n_max + lane) * KP);
-      const float4* qr = reinterpret_cast<const float4*>(qh);
-      float dot = 0.f;
-#pragma unroll
-      for (int d4 = 0; d4 < V4; ++d4) {
-        const float4 kk = kr[d4], qq = qr[d4];
-        dot = fmaf(qq.x, kk.x, dot);
-        dot = fmaf(qq.y, kk.y, dot);
-        dot = fmaf(qq.z, kk.z, dot);
-        dot = fmaf(qq.w, kk.w, dot);
+  // (2) producers: attention of (m, kvh), published write-through
+  if (blockIdx.x < P) {
+    attn_block<HD, true>(a, blockIdx.x / a.Hkv, blockIdx.x % a.Hkv, L);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // (3) wait for all P producers: one lane polls one word, relaxed, with s_sleep; bounded
+  if (tid == 0) {
+    int ok = 1;
+    unsigned spins = 0;
+    const unsigned long long t0 = wall_clock64();  // 100 MHz constant clock
+    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(2);
+      if ((++spins & 255) == 0 && (wall_clock64() - t0 > 20000000ull ||  // 200 ms: give up
+                                   __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+        break;
       }
-      s = dot * a.scale;
     }
-    const float mx = wave_max(s);
-    const float pj = (lane < n) ? expf(s - mx) : 0.f;
-    const float inv = 1.f / wave_sum(pj);
-    constexpr int NO = HD / 64;
-    float o[NO];
-#pragma unroll
-    for (int i = 0; i < NO; ++i) o[i] = 0.f;
-    const float* vb = Vs + (size_t)kv * n_max * HD;
-    for (int j = 0; j < n; ++j) {
-      const float pb = __shfl(pj, j, 64);
-#pragma unroll
-      for (int i = 0; i < NO; ++i) o[i] = fmaf(pb, vb[(size_t)j * HD + lane + 64 * i], o[i]);
+    if (acq) {  // optional agent-scope acquire (debug: the sc1-load form needs none)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-#pragma unroll
-    for (int i = 0; i < NO; ++i) qh[lane + 64 * i] = o[i] * inv;  // q no longer needed by this wave
+    go = ok;
   }
   __syncthreads();
-  // (4) o_proj GEMV from LDS
-  float acc[MT][RPT];
+  if (!go) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the sc1 loads below the poll
+
+  // (4) o_proj GEMV over the attention output (sc1 loads: bytes written in this launch)
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)p.x, 0, (int)min((size_t)0x7fffffff, (size_t)p.M * p.xs * 4), 0x00020000);
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  for (int m0 = 0; m0 < p.M; m0 += MT) {
+    float acc[MT][RPT];
 #pragma unroll
-  for (int i = 0; i < MT; ++i)
+    for (int i = 0; i < MT; ++i)
 #pragma unroll
-    for (int r = 0; r < RPT; ++r) acc[i][r] = 0.f;
-  for (int k = k_first; k < p.K; k += G * 8) {
-    if (k != k_first) {
+      for (int r = 0; r < RPT; ++r) acc[i][r] = 0.f;
+    int s = 0;
+    for (int k = gt * 8; k < p.K; k += G * 8, ++s) {
+      float wl[RPT][8];
+      if (s >= KS || m0 > 0) {
 #pragma unroll
-      for (int r = 0; r < RPT; ++r) W8<WT>::load(W + (size_t)(row0 + r) * p.K + k, w[r]);
-    }
-#pragma unroll
-    for (int i = 0; i < MT; ++i) {
-      if (i < p.M) {
-        const float4 x0 = *reinterpret_cast<const float4*>(qa + (size_t)i * qd + k);
-        const float4 x1 = *reinterpret_cast<const float4*>(qa + (size_t)i * qd + k + 4);
-        const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+        for (int r = 0; r < RPT; ++r) W8<WT>::load(W + (size_t)(row0 + r) * p.K + k, wl[r]);
+      } else {
 #pragma unroll
         for (int r = 0; r < RPT; ++r)
 #pragma unroll
-          for (int j = 0; j < 8; ++j) acc[i][r] = fmaf(w[r][j], xv[j], acc[i][r]);
+          for (int j = 0; j < 8; ++j) wl[r][j] = (s == 0) ? w[0][r][j] : w[KS - 1][r][j];
+      }
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        if (m0 + i < p.M) {
+          const int off = ((m0 + i) * p.xs + k) * 4;
+          const f32x4 x0 = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 16);
+          const f32x4 x1 = __builtin_amdgcn_raw_buffer_load_b128(xr, off + 16, 0, 16);
+          const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+          for (int r = 0; r < RPT; ++r)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[i][r] = fmaf(wl[r][j], xv[j], acc[i][r]);
+        }
       }
     }
-  }
 #pragma unroll
-  for (int i = 0; i < MT; ++i)
+    for (int i = 0; i < MT; ++i)
 #pragma unroll
-    for (int r = 0; r < RPT; ++r) {
-      const float v = wave_sum(acc[i][r]);
-      if (lane == 0) red[wave][i][r] = v;
-    }
-  __syncthreads();
-  constexpr int WPG = G / 64;
-  constexpr int NPAIR = NG * MT * (RPT / 2);
-  if (tid < NPAIR) {
-    const int g = tid / (MT * (RPT / 2));
-    const int rem = tid % (MT * (RPT / 2));
-    const int i = rem / (RPT / 2), rp = (rem % (RPT / 2)) * 2;
-    if (i < p.M) {
-      float va = 0.f, vb2 = 0.f;
-#pragma unroll
-      for (int w2 = 0; w2 < WPG; ++w2) {
-        va += red[g * WPG + w2][i][rp];
-        vb2 += red[g * WPG + w2][i][rp + 1];
+      for (int r = 0; r < RPT; ++r) {
+        const float v = wave_sum(acc[i][r]);
+        if (lane == 0) red[wave][i][r] = v;
       }
-      gemv_epilogue_pair(p, i, blockIdx.x * RPB + g * RPT + rp, va, vb2);
+    __syncthreads();
+    constexpr int WPG = G / 64;
+    constexpr int NPAIR = NG * MT * (RPT / 2);
+    if (tid < NPAIR) {
+      const int g = tid / (MT * (RPT / 2));
+      const int rem = tid % (MT * (RPT / 2));
+      const int i = rem / (RPT / 2), rp = (rem % (RPT / 2)) * 2;
+      if (m0 + i < p.M) {
+        float va = 0.f, vb = 0.f;
+#pragma unroll
+        for (int w2 = 0; w2 < WPG; ++w2) {
+          va += red[g * WPG + w2][i][rp];
+          vb += red[g * WPG + w2][i][rp + 1];
+        }
+        gemv_epilogue_pair(p, m0 + i, blockIdx.x * RPB + g * RPT + rp, va, vb);
+      }
     }
+    __syncthreads();
   }
 }
 
@@ -768,14 +762,28 @@ int gemv_rows_per_block(int N, int K, int M) {
   return (256 / G) * RPT;
 }
 
+// Weight-load cache policy per stack tag (bit t set -> non-temporal loads for tag t).  The
+// backbone streams 1.95 GB per frame once; the decoder's 221 MB are re-read 31x per frame and
+// can stay resident in the 256 MiB Infinity Cache if the backbone stream does not evict them.
+static int g_nt_mask = -1;
+void gemv_set_nt_mask(int mask) { g_nt_mask = mask; }
+static int gemv_nt_mask() {
+  if (g_nt_mask < 0) {
+    const char* e = getenv("CSM_NT_MASK");
+    g_nt_mask = e ? atoi(e) : 5;  // backbone + heads (measured: 209.9 vs 202.0 fps all-default)
+  }
+  return g_nt_mask;
+}
+
 void launch_gemv(const GemvParams& p0, int wdt, int epi, int norm, hipStream_t st, int tag) {
   GemvParams p = p0;
   p.epi = epi;
   if (!norm) p.nw = nullptr;
+  const bool nt = (gemv_nt_mask() >> tag) & 1;
   if (wdt == WDT_BF16) {
-    if (tag == 1) launch_gemv_t<bf16_t, 1>(p, st);
-    else if (tag == 2) launch_gemv_t<bf16_t, 2>(p, st);
-    else launch_gemv_t<bf16_t, 0>(p, st);
+    if (tag == 1) nt ? launch_gemv_t<bf16_t, 5>(p, st) : launch_gemv_t<bf16_t, 1>(p, st);
+    else if (tag == 2) nt ? launch_gemv_t<bf16_t, 6>(p, st) : launch_gemv_t<bf16_t, 2>(p, st);
+    else nt ? launch_gemv_t<bf16_t, 4>(p, st) : launch_gemv_t<bf16_t, 0>(p, st);
   } else {
     if (tag == 1) launch_gemv_t<float, 1>(p, st);
     else if (tag == 2) launch_gemv_t<float, 2>(p, st);
@@ -808,37 +816,49 @@ void launch_advance(const AdvanceParams& p, hipStream_t st) {
   hipLaunchKernelGGL(advance_kernel, dim3(1), dim3(256), 0, st, p);
 }
 
-template <typename WT>
-static void launch_attn_oproj_t(const GemvParams& p, const AttnParams& a, int hd, hipStream_t st) {
-  const int G = p.K >= 2048 ? 256 : (p.K >= 1024 ? 128 : 64);
-  const int blocks = p.N / ((256 / G) * 2);
-  // live keys: every row's position + 1 (decoder step rows sit at positions < S_cap)
-  const int n_max = a.S_cap;
-  const size_t lds = ((size_t)a.Hkv * n_max * (hd + 4) + (size_t)a.Hkv * n_max * hd + (size_t)p.M * a.Hq * hd) * 4;
-#define AO_L(HD_, G_)                                                                                  \
-  do {                                                                                                 \
-    static bool attr_set = false;                                                                      \
-    if (!attr_set) {                                                                                   \
-      (void)hipFuncSetAttribute((const void*)attn_oproj_kernel<WT, HD_, G_, 2, 4>,                     \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);                \
-      (void)hipGetLastError();                                                                         \
-      attr_set = true;                                                                                 \
-    }                                                                                                  \
-    hipLaunchKernelGGL((attn_oproj_kernel<WT, HD_, G_, 2, 4>), dim3(blocks), dim3(256), lds, st, p, a, n_max); \
-  } while (0)
-#define AO_G(HD_) do { if (G == 256) AO_L(HD_, 256); else if (G == 128) AO_L(HD_, 128); else AO_L(HD_, 64); } while (0)
+static int g_handoff_acq = 0;
+void attn_oproj_set_acquire(int on) { g_handoff_acq = on; }
+
+template <typename WT, int TAG>
+static void launch_attn_oproj_t(const GemvParams& p, const AttnParams& a, int hd, unsigned* ctr, int* err,
+                                hipStream_t st) {
+  int G, RPT;
+  gemv_tiling(p.N, p.K, p.M, G, RPT);
+  const int blocks = p.N / ((256 / G) * RPT);
+  const bool mt1 = p.M == 1;
+#define AO_L(HD_, G_, M_) \
+  hipLaunchKernelGGL((attn_oproj_kernel<WT, HD_, G_, 2, M_, TAG>), dim3(blocks), dim3(256), 0, st, p, a, ctr, err, g_handoff_acq)
+#define AO_M(HD_, G_) do { if (mt1) AO_L(HD_, G_, 1); else AO_L(HD_, G_, 4); } while (0)
+#define AO_G(HD_) do { if (G == 128) AO_M(HD_, 128); else AO_M(HD_, 64); } while (0)
   if (hd == 128) AO_G(128);
   else AO_G(64);
 #undef AO_G
+#undef AO_M
 #undef AO_L
 }
 
-void launch_attn_oproj(const GemvParams& p0, const AttnParams& a, int wdt, int hd, hipStream_t st) {
+bool attn_oproj_supported(const GemvParams& p, const AttnParams& a) {
+  int G, RPT;
+  gemv_tiling(p.N, p.K, p.M, G, RPT);
+  const int blocks = p.N / ((256 / G) * RPT);
+  // producers must fit in the grid, all weights of a row group in <= 2 K-steps, RPT = 2
+  return RPT == 2 && (G == 128 || G == 64) && a.M * a.Hkv <= blocks && p.K <= 2 * G * 8 && a.M <= 64 &&
+         (a.Hq / a.Hkv) <= 4;
+}
+
+void launch_attn_oproj(const GemvParams& p0, const AttnParams& a, int wdt, int hd, unsigned* ctr, int* err,
+                       hipStream_t st, int tag) {
   GemvParams p = p0;
   p.epi = EPI_ADD;
   p.nw = nullptr;
-  if (wdt == WDT_BF16) launch_attn_oproj_t<bf16_t>(p, a, hd, st);
-  else launch_attn_oproj_t<float>(p, a, hd, st);
+  const bool nt = (gemv_nt_mask() >> tag) & 1;
+  if (wdt == WDT_BF16) {
+    if (tag == 1) nt ? launch_attn_oproj_t<bf16_t, 5>(p, a, hd, ctr, err, st) : launch_attn_oproj_t<bf16_t, 1>(p, a, hd, ctr, err, st);
+    else nt ? launch_attn_oproj_t<bf16_t, 4>(p, a, hd, ctr, err, st) : launch_attn_oproj_t<bf16_t, 0>(p, a, hd, ctr, err, st);
+  } else {
+    if (tag == 1) launch_attn_oproj_t<float, 1>(p, a, hd, ctr, err, st);
+    else launch_attn_oproj_t<float, 0>(p, a, hd, ctr, err, st);
+  }
 }
 
 // ============================================================================ launch-floor probe

@@ -88,6 +88,10 @@ int csm_synchronize(csm_engine* e);
  * kind 0 = norm+gate/up+SiLU, 1 = down+residual, 2 = norm+QKV+RoPE, 3 = o_proj+residual.
  * *bytes = algorithmic (weight) bytes per launch. */
 int csm_bench_gemv(csm_engine* e, int which, int M, int iters, float* avg_us, double* bytes);
+/* Tuning / debug switches (re-capture the frame graphs): "fuse_attn" (attention -> o_proj in one
+ * launch, default 0), "nt_mask" (bit t: non-temporal weight loads for stack tag t, default 5),
+ * "handoff_acquire" (agent acquire after the in-launch hand-off poll, default 0). */
+int csm_set_option(csm_engine* e, const char* key, int value);
 /* Profiling hook: force the GEMV tiling (threads per row group G, rows per thread RPT); 0 = auto. */
 int csm_set_gemv_config(int G, int RPT);
 /* Profiling hook: per-kernel time of n dependent near-empty kernels (blocks x 256 threads),

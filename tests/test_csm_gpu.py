@@ -158,3 +158,33 @@ def test_csm_1b_first_frames(dtype):
     orc = _oracle_frames(o, ids, 3, args.n_audio_codebooks)
     _compare(eng, orc, 3, 2e-4 if dtype == "float32" else 2e-3)
     del model
+
+
+@pytest.mark.parametrize("which,dtype,batch,frames", [("tiny", "float32", 3, 16), ("1b", "bf16", 2, 20)])
+def test_fused_attention_handoff_matches_two_launches(tiny, which, dtype, batch, frames):
+    """attn_oproj_kernel (attention published in-launch to the o_proj GEMV) must reproduce the
+    two-launch path bit for bit: same attention code, same GEMV tiling and reduction order.
+    Repeated runs exercise the self-resetting hand-off counters across graph replays."""
+    from csm_mlx import _lib
+    from csm_mlx.generation import generate_codes_batch
+    from csm_mlx.sampling import Sampler
+    from csm_mlx.tokenizers import tokenize_text_segment
+    args, w = tiny if which == "tiny" else csm_weights("1b")
+    model = _model(args, w, dtype, max_batch=batch)
+    K = args.n_audio_codebooks
+    ids = [tiny_prompt_ids(20 + b, 3 + 2 * b) if which == "tiny" else prompt_ids(20 + b) for b in range(batch)]
+    prompts = [tokenize_text_segment(i, 0, K) for i in ids]
+    L = _lib.lib()
+
+    def run():
+        hist, n, _ = generate_codes_batch(model, prompts, frames, sampler=Sampler(0.0, 0))
+        return hist, n
+
+    _lib.check(L.csm_set_option(model.engine, b"fuse_attn", 0))
+    ref, n_ref = run()
+    _lib.check(L.csm_set_option(model.engine, b"fuse_attn", 1))
+    for _ in range(3):
+        got, n_got = run()
+        assert np.array_equal(n_got, n_ref)
+        assert np.array_equal(got, ref), f"first diff at {np.argwhere(got != ref)[0]}"
+    del model
