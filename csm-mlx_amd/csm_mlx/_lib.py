@@ -80,6 +80,8 @@ def lib():
             "csm_synchronize": ([P], I),
             "csm_set_gemv_config": ([I, I], I),
             "csm_set_option": ([P, ctypes.c_char_p, I], I),
+            "csm_lab_stream": ([I, ctypes.c_double, ctypes.c_double, I, I, I, ctypes.POINTER(F)], I),
+            "csm_lab_gemv": ([I, I, I, I, ctypes.c_double, I, I, I, ctypes.POINTER(F)], I),
             "csm_bench_floor": ([P, I, I, I, ctypes.POINTER(F)], I),
             "csm_bench_gemv": ([P, I, I, I, ctypes.POINTER(F), ctypes.POINTER(ctypes.c_double)], I),
             "mimi_create": ([ctypes.POINTER(MimiDims), I, I, I, ctypes.POINTER(P)], I),

@@ -41,6 +41,37 @@ template <> struct W8<float> {
   }
 };
 
+// 8 consecutive weights held raw in VGPRs (loaded early, converted at use): 16 B bf16 / 32 B f32.
+template <typename WT> struct Raw8;
+template <> struct Raw8<bf16_t> {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 u;
+  template <bool NT> __device__ __forceinline__ void load(const bf16_t* p) {
+    if constexpr (NT) u = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    else u = *reinterpret_cast<const u32x4*>(p);
+  }
+  __device__ __forceinline__ void get(float (&w)[8]) const {
+    w[0] = bf16_lo(u.x); w[1] = bf16_hi(u.x); w[2] = bf16_lo(u.y); w[3] = bf16_hi(u.y);
+    w[4] = bf16_lo(u.z); w[5] = bf16_hi(u.z); w[6] = bf16_lo(u.w); w[7] = bf16_hi(u.w);
+  }
+};
+template <> struct Raw8<float> {
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  f32x4 a, b;
+  template <bool NT> __device__ __forceinline__ void load(const float* p) {
+    if constexpr (NT) {
+      a = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+      b = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p + 4));
+    } else {
+      a = *reinterpret_cast<const f32x4*>(p);
+      b = *reinterpret_cast<const f32x4*>(p + 4);
+    }
+  }
+  __device__ __forceinline__ void get(float (&w)[8]) const {
+    w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w; w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+  }
+};
+
 template <typename WT> __device__ __forceinline__ float ld1(const WT* p);
 template <> __device__ __forceinline__ float ld1<float>(const float* p) { return *p; }
 template <> __device__ __forceinline__ float ld1<bf16_t>(const bf16_t* p) { return bf16_to_f32(*p); }

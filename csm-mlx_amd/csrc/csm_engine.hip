@@ -799,11 +799,15 @@ int csm_bench_floor(csm_engine* e, int n_kernels, int blocks, int graph, float* 
 int csm_set_option(csm_engine* e, const char* key, int value) {
   CSM_TRY {
     const std::string k(key ? key : "");
-    if (k == "fuse_attn") e->fuse_attn = value != 0;
+    if (k == "fuse_attn") {
+      if (!e) throw CsmError(CSM_ERR_ARG, "fuse_attn needs an engine");
+      e->fuse_attn = value != 0;
+    }
     else if (k == "nt_mask") gemv_set_nt_mask(value);
     else if (k == "handoff_acquire") attn_oproj_set_acquire(value);
+    else if (k == "gemv_xl") gemv_set_xl(value);
     else throw CsmError(CSM_ERR_ARG, "unknown option " + k);
-    e->g_B = -1;  // re-capture the frame graphs with the new setting
+    if (e) e->g_B = -1;  // re-capture the frame graphs with the new setting
   }
   CSM_CATCH
 }

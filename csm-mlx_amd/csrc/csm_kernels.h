@@ -107,6 +107,7 @@ void gemv_set_override(int G, int RPT);  // 0 = automatic
 bool attn_oproj_supported(const GemvParams& p, const AttnParams& a);
 void attn_oproj_set_acquire(int on);
 void gemv_set_nt_mask(int mask);
+void gemv_set_xl(int on);
 void launch_attn_oproj(const GemvParams& p, const AttnParams& a, int wdt, int hd, unsigned* ctr, int* err,
                        hipStream_t st, int tag);
 void launch_rmsnorm_rows(const float* x, int xs, const float* w, float eps, int D, float* out, int os, int M,

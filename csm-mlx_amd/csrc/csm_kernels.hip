@@ -283,6 +283,183 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
   }
 }
 
+// ============================================================================ GEMV, activations in LDS
+// Decode-regime variant (M <= MT, K <= XL_KMAX) of gemv_kernel.  Profiling (tools/lab.py) showed
+// the register-direct kernel at ~half the streaming rate on the K = 1024/2048 matrices: every
+// wave re-read the fp32 activation row AND the RMSNorm weight for its K slice through the vector
+// memory path -- 2x the weight bytes per CU.  Here the block (1) puts ALL of its weight K-steps in
+// flight into VGPRs first, (2) stages x (dense or gathered table rows) times the norm weight into
+// LDS once, reducing sum(x^2) per row once per block, (3) runs the dot products from LDS.  Per
+// thread the weight K-slices, accumulation order and pair epilogues are those of gemv_kernel.
+constexpr int XL_KMAX = 2048;
+
+template <typename WT, int G, int RPT, int MT, int TAG>
+__global__ __launch_bounds__(256) void gemv_xl_kernel(GemvParams p) {
+  constexpr int NG = 256 / G;
+  constexpr int RPB = NG * RPT;
+  constexpr int NKM = XL_KMAX / (G * 8);  // K-steps per thread at most
+  constexpr bool NT = (TAG & 4) != 0;
+  __shared__ __attribute__((aligned(16))) float xl[MT][XL_KMAX];
+  __shared__ float red[4][MT][RPT];
+  __shared__ float rss[4][MT];
+  __shared__ int gcode[MT];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int grp = tid / G, gt = tid % G;
+  const int row0 = blockIdx.x * RPB + grp * RPT;
+  const bool norm = p.nw != nullptr;
+  const WT* W = (const WT*)p.W;
+  if (p.epoch_inc && blockIdx.x == 0 && tid == 0) *p.epoch_inc += 1;
+  // (1) every weight K-step of this thread in flight before anything else
+  Raw8<WT> wr[NKM][RPT];
+#pragma unroll
+  for (int s = 0; s < NKM; ++s) {
+    const int k = gt * 8 + s * G * 8;
+    if (k < p.K) {
+#pragma unroll
+      for (int r = 0; r < RPT; ++r) wr[s][r].template load<NT>(W + (size_t)(row0 + r) * p.K + k);
+    }
+  }
+  // (2a) gather mode: resolve the rows' codes from the producer's arg-max partials
+  if (p.xpart) {
+    for (int m = wave; m < p.M; m += 4) {
+      const int bb = p.x_step1 ? (m >> 1) : m;
+      if (p.x_step1 && !(m & 1)) continue;
+      unsigned long long best = 0;
+      for (int i = lane; i < p.xpart_n; i += 64) {
+        const unsigned long long v = p.xpart[(size_t)bb * p.xpart_stride + i];
+        best = v > best ? v : best;
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long v = __shfl_xor(best, o, 64);
+        best = v > best ? v : best;
+      }
+      if (lane == 0) {
+        const int c = min(max(unpack_argmax(best), 0), p.xV - 1);
+        gcode[m] = c;
+        if (blockIdx.x == 0) p.x_codes[(size_t)bb * p.x_codes_K + p.xcb] = c;
+      }
+    }
+    __syncthreads();
+  }
+  // (2b) stage x (* norm weight) into LDS; sum(x^2) per row once per block
+  float ssp[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    ssp[i] = 0.f;
+    if (i < p.M) {
+      const bool gathered = p.xpart && !(p.x_step1 && !(i & 1));
+      const WT* xw = gathered ? (const WT*)p.xtab + ((size_t)gcode[i] + (size_t)p.xV * p.xcb) * p.K : nullptr;
+      const float* xf = p.x + (size_t)(p.x_step1 ? (i >> 1) : i) * p.xs;
+      for (int k = tid * 8; k < p.K; k += 256 * 8) {
+        float xv[8];
+        if (gathered) W8<WT>::load(xw + k, xv);
+        else W8<float>::load(xf + k, xv);
+        if (norm) {
+          float nw[8];
+          W8<float>::load(p.nw + k, nw);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            ssp[i] = fmaf(xv[j], xv[j], ssp[i]);
+            xv[j] *= nw[j];
+          }
+        }
+        *reinterpret_cast<float4*>(&xl[i][k]) = make_float4(xv[0], xv[1], xv[2], xv[3]);
+        *reinterpret_cast<float4*>(&xl[i][k + 4]) = make_float4(xv[4], xv[5], xv[6], xv[7]);
+      }
+    }
+    if (norm) {
+      const float v = wave_sum(ssp[i]);
+      if (lane == 0) rss[wave][i] = v;
+    }
+  }
+  __syncthreads();
+  // (3) dot products from LDS
+  float acc[MT][RPT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) acc[i][r] = 0.f;
+#pragma unroll
+  for (int s = 0; s < NKM; ++s) {
+    const int k = gt * 8 + s * G * 8;
+    if (k < p.K) {
+      float w[RPT][8];
+#pragma unroll
+      for (int r = 0; r < RPT; ++r) wr[s][r].get(w[r]);
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        if (i < p.M) {
+          const float4 x0 = *reinterpret_cast<const float4*>(&xl[i][k]);
+          const float4 x1 = *reinterpret_cast<const float4*>(&xl[i][k + 4]);
+          const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+          for (int r = 0; r < RPT; ++r)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) acc[i][r] = fmaf(w[r][j], xv[j], acc[i][r]);
+        }
+      }
+    }
+  }
+  // (4) reduce: wave shuffles, then the G/64 waves of each group through LDS; pair epilogues
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) {
+      const float v = wave_sum(acc[i][r]);
+      if (lane == 0) red[wave][i][r] = v;
+    }
+  __syncthreads();
+  constexpr int WPG = G / 64;
+  constexpr int NPAIR = NG * MT * (RPT / 2);
+  unsigned long long akey = 0;
+  int arow = -1;
+  if (tid < NPAIR) {
+    const int g = tid / (MT * (RPT / 2));
+    const int rem = tid % (MT * (RPT / 2));
+    const int i = rem / (RPT / 2), rp = (rem % (RPT / 2)) * 2;
+    if (i < p.M) {
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int w = 0; w < WPG; ++w) {
+        a += red[g * WPG + w][i][rp];
+        b += red[g * WPG + w][i][rp + 1];
+      }
+      if (norm) {
+        const float sq = (rss[0][i] + rss[1][i]) + (rss[2][i] + rss[3][i]);
+        const float sc = rsqrtf(sq / (float)p.K + p.eps);
+        a *= sc;
+        b *= sc;
+      }
+      const int n = blockIdx.x * RPB + g * RPT + rp;
+      gemv_epilogue_pair(p, i, n, a, b);
+      if (p.epi == EPI_ARGMAX) {
+        unsigned long long key = 0;
+        if (n < p.n_valid) key = pack_argmax(a, n);
+        if (n + 1 < p.n_valid) {
+          const unsigned long long kb = pack_argmax(b, n + 1);
+          key = kb > key ? kb : key;
+        }
+        akey = key;
+        arow = i;
+      }
+    }
+  }
+  if (p.epi == EPI_ARGMAX && wave == 0) {  // block arg-max per row -> partial slot
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      unsigned long long v = (tid < NPAIR && arow == i) ? akey : 0ull;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long w = __shfl_xor(v, o, 64);
+        v = w > v ? w : v;
+      }
+      if (lane == 0 && i < p.M) p.part[(size_t)i * p.part_stride + blockIdx.x] = v;
+    }
+  }
+}
+
 // ============================================================================ attention
 // Decode-shaped GQA attention for one (query row m, kv head) per 256-thread block; wave w serves
 // q head kvh*G + w (G = Hq/Hkv <= 4).  Keys [k0, k1] of utterance b(m) stream through LDS in chunks
@@ -729,6 +906,9 @@ void gemv_set_override(int G, int RPT) {
 // row group (G = 64: no cross-wave reduction, 2-4 K-steps per thread); the K = 8192 down
 // projections want the whole block on a row pair (G = 256 at N = 1024, 128 at N = 2048); every
 // other shape is latency-bound and best at G = 128 (K >= 1024).  RPT = 2 wins everywhere at M = 1.
+static int g_gemv_xl = 1;  // LDS-staged activations for the decode regime (gemv_xl_kernel)
+void gemv_set_xl(int on) { g_gemv_xl = on; }
+
 static void gemv_tiling(int N, int K, int M, int& G, int& RPT) {
   (void)M;
   if (N >= 8192) G = 64;
@@ -745,7 +925,12 @@ static void launch_gemv_t(const GemvParams& p, hipStream_t st) {
   gemv_tiling(p.N, p.K, p.M, G, RPT);
   const int blocks = p.N / ((256 / G) * RPT);
   const bool mt1 = p.M == 1;
-#define GEMV_L(G_, R_, M_) hipLaunchKernelGGL((gemv_kernel<WT, G_, R_, M_, TAG>), dim3(blocks), dim3(256), 0, st, p)
+  const bool xl = g_gemv_xl && p.M <= 4 && p.K <= XL_KMAX && p.K % 8 == 0;
+#define GEMV_L(G_, R_, M_)                                                                            \
+  do {                                                                                                \
+    if (xl) hipLaunchKernelGGL((gemv_xl_kernel<WT, G_, R_, M_, TAG>), dim3(blocks), dim3(256), 0, st, p); \
+    else hipLaunchKernelGGL((gemv_kernel<WT, G_, R_, M_, TAG>), dim3(blocks), dim3(256), 0, st, p);  \
+  } while (0)
 #define GEMV_M(G_, R_) do { if (mt1) GEMV_L(G_, R_, 1); else GEMV_L(G_, R_, 4); } while (0)
 #define GEMV_R(G_) do { if (RPT == 4) GEMV_M(G_, 4); else GEMV_M(G_, 2); } while (0)
   if (G == 256) GEMV_R(256);

@@ -90,10 +90,17 @@ int csm_synchronize(csm_engine* e);
 int csm_bench_gemv(csm_engine* e, int which, int M, int iters, float* avg_us, double* bytes);
 /* Tuning / debug switches (re-capture the frame graphs): "fuse_attn" (attention -> o_proj in one
  * launch, default 0), "nt_mask" (bit t: non-temporal weight loads for stack tag t, default 5),
- * "handoff_acquire" (agent acquire after the in-launch hand-off poll, default 0). */
+ * "handoff_acquire" (agent acquire after the in-launch hand-off poll, default 0), "gemv_xl"
+ * (decode GEMVs with LDS-staged activations, default 1). */
 int csm_set_option(csm_engine* e, const char* key, int value);
 /* Profiling hook: force the GEMV tiling (threads per row group G, rows per thread RPT); 0 = auto. */
 int csm_set_gemv_config(int G, int RPT);
+/* Measurement lab (profiling only): a pure streaming read of `bytes` (blocks x 256 threads x
+ * `loads` 16-B loads; nt = non-temporal) and the production GEMV on a synthetic bf16 N x K matrix
+ * (kind 0 = norm + SiLU*up, 1 = store; tag = stack tag, bit 2 = nt loads), each rotating over
+ * `span` bytes of distinct copies (one copy: cache-hot; >> 256 MiB: HBM-cold). */
+int csm_lab_stream(int device, double bytes, double span, int loads, int nt, int iters, float* avg_us);
+int csm_lab_gemv(int device, int N, int K, int M, double span, int kind, int tag, int iters, float* avg_us);
 /* Profiling hook: per-kernel time of n dependent near-empty kernels (blocks x 256 threads),
  * replayed as one HIP graph (graph=1) or launched eagerly (graph=0). */
 int csm_bench_floor(csm_engine* e, int n_kernels, int blocks, int graph, float* us_per_kernel);
