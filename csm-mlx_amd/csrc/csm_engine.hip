@@ -63,6 +63,11 @@ struct csm_engine {
   void* proj = nullptr;      // [Dd][D]
   void* c0_head = nullptr;   // [Vpad][D]
   void* audio_head = nullptr;  // [K-1][Vpad][Dd]
+  // projection folded into the decoder-input table: proj_tab[cb][code] = projection(E_a[code + V*cb])
+  // (fp32, the exact output of the projection GEMV), cb < K-1.  Decoder steps >= 2 gather their
+  // input row from it instead of running the projection GEMV.
+  float* proj_tab = nullptr;
+  bool proj_tab_dirty = true;
   std::set<std::string> loaded;
   std::vector<std::string> required;
   // activations
@@ -96,6 +101,7 @@ struct csm_engine {
   // for two launches -- the in-launch hand-off (drain + counter + poll + sc1 reload) costs what
   // the removed kernel boundary saved.
   bool fuse_attn = false;
+  bool fold_proj = true;  // csm_set_option "fold_proj": decoder steps >= 2 read the folded table
   unsigned* hs_body = nullptr;  // per-call monotonic hand-off counters, then the graph's epoch word
   unsigned* hs_head = nullptr;
   size_t hs_body_bytes = 0, hs_head_bytes = 0;
@@ -164,8 +170,11 @@ int ablate() {
 
 // One Llama block stack over M rows of the residual stream x (in place).
 // hs: per-layer hand-off counters for the fused attention -> o_proj launch (nullptr: two launches).
+// gather0: x-gather fields for layer 0's QKV GEMV (its input rows come from a table; the GEMV also
+// writes them to x as the residual stream).
 void run_stack(csm_engine* e, Stack& s, float* x, int M, float* q, float* att, float* mlp, const RowMap& rm,
-               hipStream_t st, unsigned* hs = nullptr, const unsigned* epoch = nullptr) {
+               hipStream_t st, unsigned* hs = nullptr, const unsigned* epoch = nullptr,
+               const GemvParams* gather0 = nullptr) {
   const csm_llama_dims& d = s.d;
   const int tag = (&s == &e->dec) ? 1 : 0;
   const int D = d.hidden, F = d.intermediate, hd = d.head_dim, Hq = d.n_heads, Hkv = d.n_kv_heads;
@@ -177,6 +186,11 @@ void run_stack(csm_engine* e, Stack& s, float* x, int M, float* q, float* att, f
     g.W = l.wqkv; g.N = s.qkv_rows(); g.K = D; g.x = x; g.xs = D; g.M = M; g.nw = l.n1; g.eps = d.eps;
     g.out = q; g.os = s.q_dim(); g.Hq = Hq; g.Hkv = Hkv; g.hd = hd; g.S_cap = s.S_cap; g.rope = s.rope;
     g.kc = l.kc; g.vc = l.vc; g.rm = rm;
+    if (i == 0 && gather0) {
+      g.xpart = gather0->xpart; g.xpart_stride = gather0->xpart_stride; g.xpart_n = gather0->xpart_n;
+      g.xtab = gather0->xtab; g.xtab_f32 = gather0->xtab_f32; g.xV = gather0->xV; g.xcb = gather0->xcb;
+      g.x_codes = gather0->x_codes; g.x_codes_K = gather0->x_codes_K; g.x_copy = x;
+    }
     if (!(ab & 2)) launch_gemv(g, e->wdt, EPI_QKV, 1, st, tag);
     // attention (+ o_proj + residual fused for the short depth-decoder KV)
     AttnParams a{};
@@ -244,10 +258,13 @@ void enqueue_head(csm_engine* e, hipStream_t st) {
     g.W = e->proj; g.N = Dd; g.K = D; g.x = e->h_last; g.xs = D; g.M = M; g.out = e->dx; g.os = Dd;
     g.xpart = part(i - 1); g.xpart_stride = e->part_stride; g.xpart_n = greedy ? (i == 1 ? n0 : ni) : 1;
     g.xtab = e->audio_emb; g.xV = V; g.xcb = i - 1; g.x_step1 = (i == 1); g.x_codes = e->codes; g.x_codes_K = K;
-    if (!(i >= 2 && (ablate() & 32))) launch_gemv(g, e->wdt, EPI_STORE, 0, st);
+    const bool folded = i >= 2 && e->proj_tab && e->fold_proj;
+    if (!folded) launch_gemv(g, e->wdt, EPI_STORE, 0, st);
+    GemvParams g0 = g;  // steps >= 2: layer 0 gathers projection(E_a[c]) from the folded table
+    g0.xtab = e->proj_tab; g0.xtab_f32 = 1;
     RowMap rm = (i == 1) ? RowMap{2, 0, nullptr, 0} : RowMap{1, 0, nullptr, i};
     run_stack(e, e->dec, e->dx, M, e->dq, e->datt, e->dmlp, rm, st,
-              e->hs_head + (size_t)(i - 1) * e->dec.d.n_layers, e->hs_head + n_hs);
+              e->hs_head + (size_t)(i - 1) * e->dec.d.n_layers, e->hs_head + n_hs, folded ? &g0 : nullptr);
     // ci_logits = norm(hidden[:, -1]) @ audio_head[i-1]  (generation.py:79)
     g = GemvParams{};
     g.W = (const char*)e->audio_head + (size_t)(i - 1) * Vp * Dd * e->wsz; g.N = Vp; g.K = Dd;
@@ -315,6 +332,23 @@ void ensure_batch(csm_engine* e, int B) {
   e->part_stride = std::max(Vp / gemv_rows_per_block((int)Vp, (int)D, 1), Vp / gemv_rows_per_block((int)Vp, (int)Dd, 1));
   e->part_stride = std::max(e->part_stride, (int)(Vp / 2));
   e->part = (unsigned long long*)e->balloc(K * Bm * (size_t)e->part_stride * 8);
+}
+
+// proj_tab[cb] = projection(E_a rows of codebook cb), computed by the projection GEMV itself
+// (per-row arithmetic identical to the per-step launch it replaces).
+void build_proj_table(csm_engine* e) {
+  const int V = e->V, D = e->D, Dd = e->Dd;
+  float* scratch = e->mlp;  // [M_cap][F] fp32: >= V*D floats (checked at create)
+  for (int cb = 0; cb < e->K - 1; ++cb) {
+    launch_to_f32((const char*)e->audio_emb + (size_t)cb * V * D * e->wsz, e->wdt, scratch, (size_t)V * D, e->st);
+    GemvParams g{};
+    g.W = e->proj; g.N = Dd; g.K = D; g.x = scratch; g.xs = D; g.M = V;
+    g.out = e->proj_tab + (size_t)cb * V * Dd; g.os = Dd;
+    launch_gemv(g, e->wdt, EPI_STORE, 0, e->st);
+  }
+  HIPCHK(hipStreamSynchronize(e->st));
+  HIPCHK(hipGetLastError());
+  e->proj_tab_dirty = false;
 }
 
 // A bounded in-launch wait that gave up leaves results undefined: fail loudly.
@@ -391,6 +425,7 @@ int csm_engine_create(const csm_dims* dims, int device, int weight_dtype, int ma
     e->proj = e->alloc(Dd * D * e->wsz);
     e->c0_head = e->alloc(Vp * D * e->wsz);
     e->audio_head = e->alloc((K - 1) * Vp * Dd * e->wsz);
+    e->proj_tab = (float*)e->alloc((K - 1) * (size_t)e->V * Dd * 4);
     for (const char* n : {"text_embeddings.weight", "audio_embeddings.weight", "projection.weight",
                           "codebook0_head.weight", "audio_head"})
       e->required.push_back(n);
@@ -399,6 +434,8 @@ int csm_engine_create(const csm_dims* dims, int device, int weight_dtype, int ma
     e->q = (float*)e->alloc(M * e->bb.q_dim() * 4);
     e->att = (float*)e->alloc(M * e->bb.q_dim() * 4);
     e->mlp = (float*)e->alloc(M * b.intermediate * 4);
+    if (M * (size_t)b.intermediate < (size_t)e->V * e->D)
+      throw CsmError(CSM_ERR_ARG, "activation scratch too small for the projection table build");
     e->tok = (int32_t*)e->alloc(M * (K + 1) * 4);
     e->msk = (uint8_t*)e->alloc(M * (K + 1));
     e->frame_ctr = (int*)e->alloc(16);
@@ -505,10 +542,12 @@ int csm_load_tensor(csm_engine* e, const char* cname, const void* host, int src_
       auto h = conv(numel());
       HIPCHK(hipMemcpy(e->text_emb, h.data(), h.size(), hipMemcpyHostToDevice));
     } else if (name == "audio_embeddings.weight") {
+      e->proj_tab_dirty = true;
       expect({V * K, D});
       auto h = conv(numel());
       HIPCHK(hipMemcpy(e->audio_emb, h.data(), h.size(), hipMemcpyHostToDevice));
     } else if (name == "projection.weight") {
+      e->proj_tab_dirty = true;
       expect({Dd, D});
       auto h = conv(numel());
       HIPCHK(hipMemcpy(e->proj, h.data(), h.size(), hipMemcpyHostToDevice));
@@ -549,6 +588,7 @@ int csm_begin(csm_engine* e, int B, const uint64_t* seeds, float temperature, in
     if (temperature < 0.f) throw CsmError(CSM_ERR_ARG, "temperature must be >= 0");
     HIPCHK(hipSetDevice(e->dev));
     ensure_batch(e, B);
+    if (e->proj_tab_dirty) build_proj_table(e);
     e->pos_host.assign(B, -1);
     e->B = B;
     e->temperature = temperature;
@@ -806,6 +846,10 @@ int csm_set_option(csm_engine* e, const char* key, int value) {
     else if (k == "nt_mask") gemv_set_nt_mask(value);
     else if (k == "handoff_acquire") attn_oproj_set_acquire(value);
     else if (k == "gemv_xl") gemv_set_xl(value);
+    else if (k == "fold_proj") {
+      if (!e) throw CsmError(CSM_ERR_ARG, "fold_proj needs an engine");
+      e->fold_proj = value != 0;
+    }
     else throw CsmError(CSM_ERR_ARG, "unknown option " + k);
     if (e) e->g_B = -1;  // re-capture the frame graphs with the new setting
   }

@@ -36,6 +36,8 @@ struct GemvParams {
   const void* xtab;
   int xV, xcb, x_step1, x_codes_K;
   int* x_codes;
+  int xtab_f32;         // gathered table rows are fp32 (else the weight type)
+  float* x_copy;        // if set: block 0 also stores the raw (un-normed) x rows here [M][K]
   unsigned* epoch_inc;  // if set: block 0 does *epoch_inc += 1 (one graph replay = one hand-off epoch)
 };
 
@@ -98,6 +100,8 @@ struct AdvanceParams {
 
 void launch_gemv(const GemvParams& p, int wdt, int epi, int norm, hipStream_t st, int tag = 2);
 void launch_embed(const EmbedParams& p, int wdt, int M, hipStream_t st);
+// dst[i] = float(src[i]) for n elements (n % 8 == 0)
+void launch_to_f32(const void* src, int wdt, float* dst, size_t n, hipStream_t st);
 void launch_attn(const AttnParams& p, int hd, hipStream_t st);
 // rows per block of the GEMV launch for (N, K, M): N must be a multiple of it
 int gemv_rows_per_block(int N, int K, int M);

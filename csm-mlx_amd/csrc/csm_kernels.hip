@@ -176,7 +176,9 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
       xf[i] = p.x + (size_t)m * p.xs;
       xw[i] = nullptr;
       if (p.xpart && m < p.M && !(p.x_step1 && !(m & 1))) {
-        xw[i] = (const WT*)p.xtab + ((size_t)gcode[m] + (size_t)p.xV * p.xcb) * p.K;
+        const size_t trow = ((size_t)gcode[m] + (size_t)p.xV * p.xcb) * p.K;
+        if (p.xtab_f32) xf[i] = (const float*)p.xtab + trow;
+        else xw[i] = (const WT*)p.xtab + trow;
       } else if (p.x_step1) {
         xf[i] = p.x + (size_t)(m >> 1) * p.xs;
       }
@@ -203,6 +205,11 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
           float xv[8];
           if (xw[i]) W8<WT>::load(xw[i] + k, xv);
           else W8<float>::load(xf[i] + k, xv);
+          if (p.x_copy && blockIdx.x == 0 && grp == 0) {  // group 0 of block 0 walks all of K
+            float* xc = p.x_copy + (size_t)(m0 + i) * p.K + k;
+            *reinterpret_cast<float4*>(xc) = make_float4(xv[0], xv[1], xv[2], xv[3]);
+            *reinterpret_cast<float4*>(xc + 4) = make_float4(xv[4], xv[5], xv[6], xv[7]);
+          }
           if (norm) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
@@ -350,12 +357,19 @@ __global__ __launch_bounds__(256) void gemv_xl_kernel(GemvParams p) {
     ssp[i] = 0.f;
     if (i < p.M) {
       const bool gathered = p.xpart && !(p.x_step1 && !(i & 1));
-      const WT* xw = gathered ? (const WT*)p.xtab + ((size_t)gcode[i] + (size_t)p.xV * p.xcb) * p.K : nullptr;
-      const float* xf = p.x + (size_t)(p.x_step1 ? (i >> 1) : i) * p.xs;
+      const size_t trow = gathered ? ((size_t)gcode[i] + (size_t)p.xV * p.xcb) * p.K : 0;
+      const bool g16 = gathered && !p.xtab_f32;
+      const WT* xw = g16 ? (const WT*)p.xtab + trow : nullptr;
+      const float* xf = gathered ? (const float*)p.xtab + trow : p.x + (size_t)(p.x_step1 ? (i >> 1) : i) * p.xs;
+      float* xc = (p.x_copy && blockIdx.x == 0) ? p.x_copy + (size_t)i * p.K : nullptr;
       for (int k = tid * 8; k < p.K; k += 256 * 8) {
         float xv[8];
-        if (gathered) W8<WT>::load(xw + k, xv);
+        if (g16) W8<WT>::load(xw + k, xv);
         else W8<float>::load(xf + k, xv);
+        if (xc) {
+          *reinterpret_cast<float4*>(xc + k) = make_float4(xv[0], xv[1], xv[2], xv[3]);
+          *reinterpret_cast<float4*>(xc + k + 4) = make_float4(xv[4], xv[5], xv[6], xv[7]);
+        }
         if (norm) {
           float nw[8];
           W8<float>::load(p.nw + k, nw);
@@ -974,6 +988,22 @@ void launch_gemv(const GemvParams& p0, int wdt, int epi, int norm, hipStream_t s
     else if (tag == 2) launch_gemv_t<float, 2>(p, st);
     else launch_gemv_t<float, 0>(p, st);
   }
+}
+
+template <typename WT>
+__global__ __launch_bounds__(256) void to_f32_kernel(const WT* src, float* dst, size_t n) {
+  const size_t i = ((size_t)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (i >= n) return;
+  float v[8];
+  W8<WT>::load(src + i, v);
+  *reinterpret_cast<float4*>(dst + i) = make_float4(v[0], v[1], v[2], v[3]);
+  *reinterpret_cast<float4*>(dst + i + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+
+void launch_to_f32(const void* src, int wdt, float* dst, size_t n, hipStream_t st) {
+  const int blocks = (int)((n / 8 + 255) / 256);
+  if (wdt == WDT_BF16) hipLaunchKernelGGL(to_f32_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, (const bf16_t*)src, dst, n);
+  else hipLaunchKernelGGL(to_f32_kernel<float>, dim3(blocks), dim3(256), 0, st, (const float*)src, dst, n);
 }
 
 void launch_embed(const EmbedParams& p, int wdt, int M, hipStream_t st) {

@@ -91,7 +91,8 @@ int csm_bench_gemv(csm_engine* e, int which, int M, int iters, float* avg_us, do
 /* Tuning / debug switches (re-capture the frame graphs): "fuse_attn" (attention -> o_proj in one
  * launch, default 0), "nt_mask" (bit t: non-temporal weight loads for stack tag t, default 5),
  * "handoff_acquire" (agent acquire after the in-launch hand-off poll, default 0), "gemv_xl"
- * (decode GEMVs with LDS-staged activations, default 1). */
+ * (decode GEMVs with LDS-staged activations, default 1), "fold_proj" (decoder steps >= 2 gather
+ * projection(E_a[c]) from a table built at csm_begin instead of running the projection, default 1). */
 int csm_set_option(csm_engine* e, const char* key, int value);
 /* Profiling hook: force the GEMV tiling (threads per row group G, rows per thread RPT); 0 = auto. */
 int csm_set_gemv_config(int G, int RPT);
