@@ -12,7 +12,8 @@ import re
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcsm_hip.so")
+# CSM_HIP_LIB: A/B-test another in-tree build of the same ABI (profiling only)
+LIB_PATH = os.environ.get("CSM_HIP_LIB") or os.path.join(_HERE, "libcsm_hip.so")
 HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "csm_hip.h")
 
 CSM_OK, CSM_ERR_ARG, CSM_ERR_HIP, CSM_ERR_STATE, CSM_ERR_TOO_LONG = 0, -1, -2, -3, -4

@@ -96,16 +96,12 @@ struct csm_engine {
   std::vector<void*> allocs;
   std::vector<void*> batch_allocs;
   std::vector<int> pos_host;
-  // attention -> o_proj in one launch (attn_oproj_kernel, CSM_FUSE_ATTN=1 / csm_set_option).
-  // Off by default: bit-exact and stable, but on MI355X at B=1 it measured 208.3 vs 209.2 frames/s
-  // for two launches -- the in-launch hand-off (drain + counter + poll + sc1 reload) costs what
-  // the removed kernel boundary saved.
+  // depth-decoder attention recomputed inside the o_proj launch (dec_attn_oproj_kernel, CSM_FUSE_ATTN=1
+  // or csm_set_option("fuse_attn", 1); bit-identical results).  Off: on MI355X the redundant
+  // per-block attention (12.4 us eager) costs more than attention + o_proj launched separately
+  // (6.1 + 5.3 us) plus the boundary it removes -- 205 vs 227 frames/s.
   bool fuse_attn = false;
   bool fold_proj = true;  // csm_set_option "fold_proj": decoder steps >= 2 read the folded table
-  unsigned* hs_body = nullptr;  // per-call monotonic hand-off counters, then the graph's epoch word
-  unsigned* hs_head = nullptr;
-  size_t hs_body_bytes = 0, hs_head_bytes = 0;
-  int* hs_err = nullptr;  // set by a hand-off that timed out
 
   void* balloc(size_t bytes) {
     void* p = nullptr;
@@ -169,12 +165,10 @@ int ablate() {
 }
 
 // One Llama block stack over M rows of the residual stream x (in place).
-// hs: per-layer hand-off counters for the fused attention -> o_proj launch (nullptr: two launches).
 // gather0: x-gather fields for layer 0's QKV GEMV (its input rows come from a table; the GEMV also
 // writes them to x as the residual stream).
 void run_stack(csm_engine* e, Stack& s, float* x, int M, float* q, float* att, float* mlp, const RowMap& rm,
-               hipStream_t st, unsigned* hs = nullptr, const unsigned* epoch = nullptr,
-               const GemvParams* gather0 = nullptr) {
+               hipStream_t st, const GemvParams* gather0 = nullptr) {
   const csm_llama_dims& d = s.d;
   const int tag = (&s == &e->dec) ? 1 : 0;
   const int D = d.hidden, F = d.intermediate, hd = d.head_dim, Hq = d.n_heads, Hkv = d.n_kv_heads;
@@ -196,12 +190,11 @@ void run_stack(csm_engine* e, Stack& s, float* x, int M, float* q, float* att, f
     AttnParams a{};
     a.q = q; a.qs = s.q_dim(); a.M = M; a.kc = l.kc; a.vc = l.vc; a.Hq = Hq; a.Hkv = Hkv; a.S_cap = s.S_cap;
     a.scale = 1.0f / sqrtf((float)hd); a.mode = ATTN_CAUSAL; a.window = 0; a.rm = rm; a.out = att;
-    a.epoch = epoch;
     a.os = s.q_dim();
     g = GemvParams{};
     g.W = l.wo; g.N = D; g.K = s.q_dim(); g.x = att; g.xs = s.q_dim(); g.M = M; g.out = x; g.os = D;
-    if (hs && epoch && e->fuse_attn && !(ab & 5) && attn_oproj_supported(g, a)) {
-      launch_attn_oproj(g, a, e->wdt, hd, hs + i, e->hs_err, st, tag);
+    if (tag == 1 && e->fuse_attn && !(ab & 5) && dec_attn_oproj_supported(g, a, hd)) {
+      launch_dec_attn_oproj(g, a, e->wdt, st, tag);
     } else {
       if (!(ab & 1)) launch_attn(a, hd, st);
       if (!(ab & 4)) launch_gemv(g, e->wdt, EPI_ADD, 0, st, tag);
@@ -223,10 +216,9 @@ void enqueue_body(csm_engine* e, hipStream_t st) {
   EmbedParams ep{};
   ep.codes = e->codes; ep.text_emb = e->text_emb; ep.audio_emb = e->audio_emb; ep.V = e->V; ep.K = e->K;
   ep.D = e->D; ep.out = e->x; ep.pos_inc = e->pos;
-  ep.epoch_inc = e->hs_body + e->bb.d.n_layers;  // one hand-off epoch per body replay
   launch_embed(ep, e->wdt, B, st);
   RowMap rm{1, 0, e->pos, 0};
-  run_stack(e, e->bb, e->x, B, e->q, e->att, e->mlp, rm, st, e->hs_body, e->hs_body + e->bb.d.n_layers);
+  run_stack(e, e->bb, e->x, B, e->q, e->att, e->mlp, rm, st);
   launch_rmsnorm_rows(e->x, e->D, e->bb.norm, e->bb.d.eps, e->D, e->h_last, e->D, B, st);
 }
 
@@ -243,8 +235,6 @@ void enqueue_head(csm_engine* e, hipStream_t st) {
   GemvParams g{};
   g.W = e->c0_head; g.N = Vp; g.K = D; g.x = e->h_last; g.xs = D; g.M = B; g.out = e->c0_logits; g.os = Vp;
   g.part = part(0); g.part_stride = e->part_stride; g.n_valid = V;
-  const int n_hs = e->dec.d.n_layers * (K - 1);
-  g.epoch_inc = e->hs_head + n_hs;  // one hand-off epoch per head replay
   launch_gemv(g, e->wdt, greedy ? EPI_ARGMAX : EPI_STORE, 0, st);
   if (!greedy) {
     sp.logits = e->c0_logits; sp.cb = 0; sp.part = part(0);
@@ -263,8 +253,7 @@ void enqueue_head(csm_engine* e, hipStream_t st) {
     GemvParams g0 = g;  // steps >= 2: layer 0 gathers projection(E_a[c]) from the folded table
     g0.xtab = e->proj_tab; g0.xtab_f32 = 1;
     RowMap rm = (i == 1) ? RowMap{2, 0, nullptr, 0} : RowMap{1, 0, nullptr, i};
-    run_stack(e, e->dec, e->dx, M, e->dq, e->datt, e->dmlp, rm, st,
-              e->hs_head + (size_t)(i - 1) * e->dec.d.n_layers, e->hs_head + n_hs, folded ? &g0 : nullptr);
+    run_stack(e, e->dec, e->dx, M, e->dq, e->datt, e->dmlp, rm, st, folded ? &g0 : nullptr);
     // ci_logits = norm(hidden[:, -1]) @ audio_head[i-1]  (generation.py:79)
     g = GemvParams{};
     g.W = (const char*)e->audio_head + (size_t)(i - 1) * Vp * Dd * e->wsz; g.N = Vp; g.K = Dd;
@@ -351,12 +340,6 @@ void build_proj_table(csm_engine* e) {
   e->proj_tab_dirty = false;
 }
 
-// A bounded in-launch wait that gave up leaves results undefined: fail loudly.
-void check_handoff(csm_engine* e) {
-  int err = 0;
-  HIPCHK(hipMemcpy(&err, e->hs_err, 4, hipMemcpyDeviceToHost));
-  if (err) throw CsmError(CSM_ERR_HIP, "in-launch attention hand-off timed out (results invalid)");
-}
 
 }  // namespace
 
@@ -439,12 +422,6 @@ int csm_engine_create(const csm_dims* dims, int device, int weight_dtype, int ma
     e->tok = (int32_t*)e->alloc(M * (K + 1) * 4);
     e->msk = (uint8_t*)e->alloc(M * (K + 1));
     e->frame_ctr = (int*)e->alloc(16);
-    // per-call counters, then the graph's epoch word
-    e->hs_body_bytes = ((size_t)(b.n_layers + 1) * 4 + 15) / 16 * 16;
-    e->hs_head_bytes = ((size_t)(d.n_layers * (e->K - 1) + 1) * 4 + 15) / 16 * 16;
-    e->hs_body = (unsigned*)e->alloc(e->hs_body_bytes);
-    e->hs_head = (unsigned*)e->alloc(e->hs_head_bytes);
-    e->hs_err = (int*)e->alloc(16);
     (void)Vp;
     (void)B;
     ensure_batch(e.get(), max_batch);
@@ -602,9 +579,6 @@ int csm_begin(csm_engine* e, int B, const uint64_t* seeds, float temperature, in
     HIPCHK(hipMemsetAsync(e->done, 0, B, e->st));
     HIPCHK(hipMemsetAsync(e->n_frames, 0, B * 4, e->st));
     HIPCHK(hipMemsetAsync(e->frame_ctr, 0, 16, e->st));
-    HIPCHK(hipMemsetAsync(e->hs_err, 0, 16, e->st));
-    HIPCHK(hipMemsetAsync(e->hs_body, 0, e->hs_body_bytes, e->st));  // (a timed-out call leaves them set)
-    HIPCHK(hipMemsetAsync(e->hs_head, 0, e->hs_head_bytes, e->st));
     HIPCHK(hipMemsetAsync(e->codes, 0, (size_t)B * e->K * 4, e->st));
     HIPCHK(hipStreamSynchronize(e->st));
   }
@@ -692,7 +666,6 @@ int csm_run_frames(csm_engine* e, int nframes, int* all_done) {
       std::vector<uint8_t> d(e->B);
       HIPCHK(hipMemcpyAsync(d.data(), e->done, e->B, hipMemcpyDeviceToHost, e->st));
       HIPCHK(hipStreamSynchronize(e->st));
-      check_handoff(e);
       int all = 1;
       for (auto v : d) all &= (v != 0);
       *all_done = all;
@@ -705,7 +678,6 @@ int csm_read_codes(csm_engine* e, int32_t* hist, int32_t* n_frames, uint8_t* don
   CSM_TRY {
     HIPCHK(hipSetDevice(e->dev));
     HIPCHK(hipStreamSynchronize(e->st));
-    check_handoff(e);
     if (hist)
       HIPCHK(hipMemcpy(hist, e->hist, (size_t)e->frames_run * e->B * e->K * 4, hipMemcpyDeviceToHost));
     if (n_frames) HIPCHK(hipMemcpy(n_frames, e->n_frames, e->B * 4, hipMemcpyDeviceToHost));
@@ -844,7 +816,6 @@ int csm_set_option(csm_engine* e, const char* key, int value) {
       e->fuse_attn = value != 0;
     }
     else if (k == "nt_mask") gemv_set_nt_mask(value);
-    else if (k == "handoff_acquire") attn_oproj_set_acquire(value);
     else if (k == "gemv_xl") gemv_set_xl(value);
     else if (k == "fold_proj") {
       if (!e) throw CsmError(CSM_ERR_ARG, "fold_proj needs an engine");

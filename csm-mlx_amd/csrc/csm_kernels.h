@@ -38,7 +38,6 @@ struct GemvParams {
   int* x_codes;
   int xtab_f32;         // gathered table rows are fp32 (else the weight type)
   float* x_copy;        // if set: block 0 also stores the raw (un-normed) x rows here [M][K]
-  unsigned* epoch_inc;  // if set: block 0 does *epoch_inc += 1 (one graph replay = one hand-off epoch)
 };
 
 __device__ __forceinline__ unsigned long long pack_argmax(float v, int idx) {
@@ -57,7 +56,6 @@ struct EmbedParams {
   int V, K, D;
   float* out;            // [M][D]
   int* pos_inc;          // decode mode: pos[m] += 1 (position of the new backbone row)
-  unsigned* epoch_inc;   // if set: *epoch_inc += 1 (one graph replay = one hand-off epoch)
 };
 
 struct AttnParams {
@@ -71,7 +69,6 @@ struct AttnParams {
   RowMap rm;
   float* out;
   int os;
-  const unsigned* epoch;  // attn_oproj: hand-off epoch of this call (counter target = epoch * M*Hkv)
 };
 
 struct SampleParams {
@@ -106,14 +103,11 @@ void launch_attn(const AttnParams& p, int hd, hipStream_t st);
 // rows per block of the GEMV launch for (N, K, M): N must be a multiple of it
 int gemv_rows_per_block(int N, int K, int M);
 void gemv_set_override(int G, int RPT);  // 0 = automatic
-// fused attention (<= 64 keys, M <= 4 rows) + o_proj + residual for the depth decoder
-// attention published in-launch to the o_proj GEMV (+ residual); ctr: a zeroed per-call word
-bool attn_oproj_supported(const GemvParams& p, const AttnParams& a);
-void attn_oproj_set_acquire(int on);
+// depth-decoder attention recomputed inside every o_proj block (+ residual): one launch
+bool dec_attn_oproj_supported(const GemvParams& p, const AttnParams& a, int hd);
+void launch_dec_attn_oproj(const GemvParams& p, const AttnParams& a, int wdt, hipStream_t st, int tag);
 void gemv_set_nt_mask(int mask);
 void gemv_set_xl(int on);
-void launch_attn_oproj(const GemvParams& p, const AttnParams& a, int wdt, int hd, unsigned* ctr, int* err,
-                       hipStream_t st, int tag);
 void launch_rmsnorm_rows(const float* x, int xs, const float* w, float eps, int D, float* out, int os, int M,
                          hipStream_t st);
 void launch_sample(const SampleParams& p, int wdt, int B, hipStream_t st);

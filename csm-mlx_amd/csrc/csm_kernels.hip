@@ -40,7 +40,6 @@ __global__ __launch_bounds__(256) void embed_rows_kernel(EmbedParams p) {
   }
   __syncthreads();
   if (p.pos_inc && threadIdx.x == 0) p.pos_inc[m] += 1;
-  if (p.epoch_inc && threadIdx.x == 0 && m == 0) *p.epoch_inc += 1;
   float* out = p.out + (size_t)m * p.D;
   for (int d0 = threadIdx.x * 8; d0 < p.D; d0 += blockDim.x * 8) {
     float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -140,7 +139,6 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
   const int row0 = blockIdx.x * RPB + grp * RPT;
   const bool norm = p.nw != nullptr;
   const WT* W = (const WT*)p.W;
-  if (p.epoch_inc && blockIdx.x == 0 && tid == 0) *p.epoch_inc += 1;
   // x gather mode: resolve each needed row's code from the producer's block partials once
   __shared__ int gcode[512];  // codes of the gathered rows (M <= 512)
   if (p.xpart) {
@@ -316,7 +314,6 @@ __global__ __launch_bounds__(256) void gemv_xl_kernel(GemvParams p) {
   const int row0 = blockIdx.x * RPB + grp * RPT;
   const bool norm = p.nw != nullptr;
   const WT* W = (const WT*)p.W;
-  if (p.epoch_inc && blockIdx.x == 0 && tid == 0) *p.epoch_inc += 1;
   // (1) every weight K-step of this thread in flight before anything else
   Raw8<WT> wr[NKM][RPT];
 #pragma unroll
@@ -480,8 +477,61 @@ __global__ __launch_bounds__(256) void gemv_xl_kernel(GemvParams p) {
 // of 64 rows; the chunk loads are software-pipelined through registers (chunk c+1 is in flight while
 // chunk c is scored), all 256 threads issuing coalesced 16-B loads.  Each wave scores its head
 // (lane = key, K rows padded by 16 B: conflict-free ds_read_b128), online softmax in fp32, and
-// P.V with lane = head dim reading V rows from LDS.  SC1 = write the output with write-through
-// (sc1) stores, for a consumer in the same launch (attn_oproj_kernel).
+// P.V with lane = head dim reading V rows from LDS.
+// One wave scores one head against a chunk of n <= 64 keys held in LDS (K rows padded to KP floats,
+// V rows HD floats) with online-softmax state (m_run, l_run, o).  The q.k dot runs as four
+// independent FMA chains (one per float4 lane) and P.V broadcasts p_j with v_readlane (scalar, no
+// LDS round trip) four keys at a time so the V reads are in flight together: the single-chain /
+// ds_bpermute form spent ~3 us of dependent latency per head at 32 keys.  Shared by attn_block and
+// dec_attn_oproj_kernel, so both produce bit-identical outputs.
+template <int HD>
+__device__ __forceinline__ void attn_chunk(const float* qr_, const float* Kc, const float* Vc, int n, int lane,
+                                           float& m_run, float& l_run, float (&o)[HD / 64]) {
+  constexpr int KP = HD + 4, V4 = HD / 4, NO = HD / 64;
+  float s = -INFINITY;
+  if (lane < n) {
+    const float4* kr = reinterpret_cast<const float4*>(Kc + lane * KP);
+    const float4* qr = reinterpret_cast<const float4*>(qr_);
+    float d0 = 0.f, d1 = 0.f, d2 = 0.f, d3 = 0.f;
+#pragma unroll
+    for (int d4 = 0; d4 < V4; ++d4) {
+      const float4 a = kr[d4], q4 = qr[d4];
+      d0 = fmaf(q4.x, a.x, d0);
+      d1 = fmaf(q4.y, a.y, d1);
+      d2 = fmaf(q4.z, a.z, d2);
+      d3 = fmaf(q4.w, a.w, d3);
+    }
+    s = (d0 + d1) + (d2 + d3);
+  }
+  const float new_m = fmaxf(m_run, wave_max(s));
+  const float alpha = (m_run == -INFINITY) ? 0.f : expf(m_run - new_m);
+  const float pj = (lane < n) ? expf(s - new_m) : 0.f;
+  l_run = l_run * alpha + wave_sum(pj);
+#pragma unroll
+  for (int i = 0; i < NO; ++i) o[i] *= alpha;
+  const int pji = __float_as_int(pj);
+  int j = 0;
+  for (; j + 4 <= n; j += 4) {
+    float v[4][NO];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int i = 0; i < NO; ++i) v[u][i] = Vc[(j + u) * HD + lane + 64 * i];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float pb = __int_as_float(__builtin_amdgcn_readlane(pji, j + u));
+#pragma unroll
+      for (int i = 0; i < NO; ++i) o[i] = fmaf(pb, v[u][i], o[i]);
+    }
+  }
+  for (; j < n; ++j) {
+    const float pb = __int_as_float(__builtin_amdgcn_readlane(pji, j));
+#pragma unroll
+    for (int i = 0; i < NO; ++i) o[i] = fmaf(pb, Vc[j * HD + lane + 64 * i], o[i]);
+  }
+  m_run = new_m;
+}
+
 template <int HD>
 struct AttnLds {
   float Ks[64 * (HD + 4)];
@@ -489,7 +539,7 @@ struct AttnLds {
   float qs[4][HD];
 };
 
-template <int HD, bool SC1>
+template <int HD>
 __device__ __forceinline__ void attn_block(const AttnParams& p, int m, int kvh, AttnLds<HD>& L) {
   constexpr int KP = HD + 4;  // padded K row (floats)
   constexpr int V4 = HD / 4;  // float4 per row
@@ -551,182 +601,164 @@ __device__ __forceinline__ void attn_block(const AttnParams& p, int m, int kvh, 
     __syncthreads();
     fetch(min(c + 64, k1));  // next chunk streams while this one is scored (clamped: unconditional)
     if (!head_ok) continue;
-    float s = -INFINITY;
-    if (lane < n) {
-      const float4* kr = reinterpret_cast<const float4*>(&L.Ks[lane * KP]);
-      const float4* qr = reinterpret_cast<const float4*>(L.qs[wave]);
-      float dot = 0.f;
-#pragma unroll
-      for (int d4 = 0; d4 < V4; ++d4) {
-        const float4 a = kr[d4], q4 = qr[d4];
-        dot = fmaf(q4.x, a.x, dot);
-        dot = fmaf(q4.y, a.y, dot);
-        dot = fmaf(q4.z, a.z, dot);
-        dot = fmaf(q4.w, a.w, dot);
-      }
-      s = dot;
-    }
-    const float new_m = fmaxf(m_run, wave_max(s));
-    const float alpha = (m_run == -INFINITY) ? 0.f : expf(m_run - new_m);
-    const float pj = (lane < n) ? expf(s - new_m) : 0.f;
-    l_run = l_run * alpha + wave_sum(pj);
-#pragma unroll
-    for (int i = 0; i < NO; ++i) o[i] *= alpha;
-    for (int j = 0; j < n; ++j) {
-      const float pb = __shfl(pj, j, 64);
-#pragma unroll
-      for (int i = 0; i < NO; ++i) o[i] = fmaf(pb, L.Vs[j * HD + lane + 64 * i], o[i]);
-    }
-    m_run = new_m;
+    attn_chunk<HD>(L.qs[wave], L.Ks, L.Vs, n, lane, m_run, l_run, o);
   }
   if (!head_ok) return;
   const float inv = 1.f / l_run;
   float* out = p.out + (size_t)m * p.os + h * HD;
 #pragma unroll
   for (int i = 0; i < NO; ++i) {
-    if constexpr (SC1) __hip_atomic_store(out + lane + 64 * i, o[i] * inv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else out[lane + 64 * i] = o[i] * inv;
+    out[lane + 64 * i] = o[i] * inv;
   }
 }
 
 template <int HD>
 __global__ __launch_bounds__(256) void attn_kernel(AttnParams p) {
   __shared__ __attribute__((aligned(16))) AttnLds<HD> L;
-  attn_block<HD, false>(p, blockIdx.x / p.Hkv, blockIdx.x % p.Hkv, L);
+  attn_block<HD>(p, blockIdx.x / p.Hkv, blockIdx.x % p.Hkv, L);
 }
 
-// ============================================================================ attention -> o_proj in one launch
-// Blocks [0, P) (P = M*Hkv) first compute the attention of one (row, kv head) each and publish it
-// write-through (sc1 stores, drained, then one relaxed agent-scope add to the call's counter).
-// Every block issues its o_proj weight loads BEFORE that (weights do not depend on the
-// attention), then waits for the counter and runs the GEMV (+ residual) reading the attention
-// output with sc1 loads -- MI355X_MICROARCH.md "Valid forms" hand-off: no fences.  Counters are
-// monotonic (zeroed by csm_begin only): the graph's first kernel bumps an epoch word once per
-// replay and the call waits for counter >= epoch * P, so replays need no memset node (a captured
-// hipMemsetAsync node raced the kernel under ROCm 7.0's runtime) and no contended reset atomic.
-// Producers are the lowest block ids (dispatched first) and every spin is bounded: on timeout
-// the block sets *err and exits (the host raises).
-// One launch replaces attention + o_proj: the kernel boundary and the o_proj weight latency
-// disappear behind the attention.
-template <typename WT, int HD, int G, int RPT, int MT, int TAG>
-__global__ __launch_bounds__(256) void attn_oproj_kernel(GemvParams p, AttnParams a, unsigned* ctr, int* err, int acq) {
+// ============================================================================ decoder attention + o_proj
+// The depth decoder attends over <= 32 cached positions (generation.py:70-77: one position per
+// codebook step), ~66K FMAs over <= 64 KB of K/V -- far less than the cost of a kernel boundary
+// plus a latency-bound attention launch.  Every o_proj block therefore recomputes the attention
+// of all heads itself: (1) it puts its o_proj weights in flight, (2) stages q (pre-scaled) and the
+// live K/V rows of every kv head into LDS, (3) runs each (row, head) exactly as attn_block does for
+// a single 64-key chunk (same operation order: bit-identical outputs), writing the attention
+// output into LDS, (4) runs the o_proj GEMV (+ residual) from LDS with gemv_kernel's K-slicing and
+// reduction order (G = 128: bit-identical to the two-launch path for any RPT).  RPT = 8 keeps the
+// grid at N/16 blocks, bounding the redundant attention work.
+constexpr int DA_NMAX = 32;   // cached positions
+constexpr int DA_HKV = 2;     // kv heads
+constexpr int DA_QD = 1024;   // Hq * head_dim
+constexpr int DA_M = 2;       // rows (decoder step 1: [h_last, c0] rows)
+
+template <typename WT, int HD, int RPT, int TAG>
+__global__ __launch_bounds__(256) void dec_attn_oproj_kernel(GemvParams p, AttnParams a) {
+  constexpr int G = 128;
   constexpr int NG = 256 / G;
   constexpr int RPB = NG * RPT;
-  constexpr int KS = 2;  // K-steps of weights prefetched before the wait (K <= 2*G*8)
-  __shared__ __attribute__((aligned(16))) AttnLds<HD> L;
-  __shared__ float red[4][MT][RPT];
-  __shared__ int go;
+  constexpr int KP = HD + 4;
+  constexpr int V4 = HD / 4;
+  constexpr int NKM = DA_QD / (G * 8);
+  constexpr bool NT = (TAG & 4) != 0;
+  __shared__ __attribute__((aligned(16))) float Ks[DA_HKV * DA_NMAX * KP];
+  __shared__ __attribute__((aligned(16))) float Vs[DA_HKV * DA_NMAX * HD];
+  __shared__ __attribute__((aligned(16))) float qs[DA_M][DA_QD];  // q * scale
+  __shared__ __attribute__((aligned(16))) float xo[DA_M][DA_QD];  // attention output = o_proj input
+  __shared__ float red[4][DA_M][RPT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int grp = tid / G, gt = tid % G;
   const int row0 = blockIdx.x * RPB + grp * RPT;
   const WT* W = (const WT*)p.W;
-  const unsigned P = (unsigned)(a.M * a.Hkv);
-  const unsigned target = P * *a.epoch;  // written by an earlier kernel of this replay
-  // (1) weights of the first KS K-steps in flight
-  float w[KS][RPT][8];
+  // (1) o_proj weights in flight
+  Raw8<WT> wr[NKM][RPT];
 #pragma unroll
-  for (int s = 0; s < KS; ++s) {
+  for (int s = 0; s < NKM; ++s) {
     const int k = gt * 8 + s * G * 8;
     if (k < p.K) {
 #pragma unroll
-      for (int r = 0; r < RPT; ++r) {
-        if constexpr ((TAG & 4) != 0) W8<WT>::load_nt(W + (size_t)(row0 + r) * p.K + k, w[s][r]);
-        else W8<WT>::load(W + (size_t)(row0 + r) * p.K + k, w[s][r]);
-      }
+      for (int r = 0; r < RPT; ++r) wr[s][r].template load<NT>(W + (size_t)(row0 + r) * p.K + k);
     }
   }
-  // (2) producers: attention of (m, kvh), published write-through
-  if (blockIdx.x < P) {
-    attn_block<HD, true>(a, blockIdx.x / a.Hkv, blockIdx.x % a.Hkv, L);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
-    __syncthreads();
-    if (tid == 0) __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // (2) stage q rows (scaled, as attn_block) and K/V rows [0, n_live) of utterance b(0)
+  const int qd = a.Hq * HD;
+  for (int t = tid; t < p.M * (qd / 4); t += 256) {
+    const int m = t / (qd / 4), c = (t % (qd / 4)) * 4;
+    const float4 v = *reinterpret_cast<const float4*>(a.q + (size_t)m * a.qs + c);
+    *reinterpret_cast<float4*>(&qs[m][c]) = make_float4(v.x * a.scale, v.y * a.scale, v.z * a.scale, v.w * a.scale);
   }
-  // (3) wait for all P producers: one lane polls one word, relaxed, with s_sleep; bounded
-  if (tid == 0) {
-    int ok = 1;
-    unsigned spins = 0;
-    const unsigned long long t0 = wall_clock64();  // 100 MHz constant clock
-    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(2);
-      if ((++spins & 255) == 0 && (wall_clock64() - t0 > 20000000ull ||  // 200 ms: give up
-                                   __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-        __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ok = 0;
-        break;
+  const int b0 = a.rm.b(0);
+  const int n_live = a.rm.pos(p.M - 1) + 1;  // the last row has the largest position
+  const int total = a.Hkv * n_live * V4;
+  for (int t0 = 0; t0 < total; t0 += 256 * 8) {
+    float4 kr[8], vr[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int t = min(t0 + u * 256 + tid, total - 1);  // clamped: always a valid row
+      const int kv = t / (n_live * V4), rem = t % (n_live * V4);
+      const size_t src = (((size_t)b0 * a.Hkv + kv) * a.S_cap + rem / V4) * HD + (rem % V4) * 4;
+      kr[u] = *reinterpret_cast<const float4*>(a.kc + src);
+      vr[u] = *reinterpret_cast<const float4*>(a.vc + src);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int t = t0 + u * 256 + tid;
+      if (t < total) {
+        const int kv = t / (n_live * V4), rem = t % (n_live * V4);
+        const int j = rem / V4, d4 = rem % V4;
+        *reinterpret_cast<float4*>(&Ks[(kv * DA_NMAX + j) * KP + d4 * 4]) = kr[u];
+        *reinterpret_cast<float4*>(&Vs[(kv * DA_NMAX + j) * HD + d4 * 4]) = vr[u];
       }
     }
-    if (acq) {  // optional agent-scope acquire (debug: the sc1-load form needs none)
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    go = ok;
   }
   __syncthreads();
-  if (!go) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the sc1 loads below the poll
-
-  // (4) o_proj GEMV over the attention output (sc1 loads: bytes written in this launch)
-  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)p.x, 0, (int)min((size_t)0x7fffffff, (size_t)p.M * p.xs * 4), 0x00020000);
-  typedef float f32x4 __attribute__((ext_vector_type(4)));
-  for (int m0 = 0; m0 < p.M; m0 += MT) {
-    float acc[MT][RPT];
+  // (3) attention, one wave per (row, head): attn_block's single-chunk arithmetic
+  constexpr int NO = HD / 64;
+  for (int idx = wave; idx < p.M * a.Hq; idx += 4) {
+    const int m = idx / a.Hq, h = idx % a.Hq;
+    const int kv = h / (a.Hq / a.Hkv);
+    const int n = a.rm.pos(m) + 1;
+    float m_run = -INFINITY, l_run = 0.f;
+    float o[NO];
 #pragma unroll
-    for (int i = 0; i < MT; ++i)
+    for (int q = 0; q < NO; ++q) o[q] = 0.f;
+    attn_chunk<HD>(&qs[m][h * HD], &Ks[kv * DA_NMAX * KP], &Vs[kv * DA_NMAX * HD], n, lane, m_run, l_run, o);
+    const float inv = 1.f / l_run;
 #pragma unroll
-      for (int r = 0; r < RPT; ++r) acc[i][r] = 0.f;
-    int s = 0;
-    for (int k = gt * 8; k < p.K; k += G * 8, ++s) {
-      float wl[RPT][8];
-      if (s >= KS || m0 > 0) {
+    for (int i = 0; i < NO; ++i) xo[m][h * HD + lane + 64 * i] = o[i] * inv;
+  }
+  __syncthreads();
+  // (4) o_proj GEMV from LDS (+ residual)
+  float acc[DA_M][RPT];
 #pragma unroll
-        for (int r = 0; r < RPT; ++r) W8<WT>::load(W + (size_t)(row0 + r) * p.K + k, wl[r]);
-      } else {
+  for (int i = 0; i < DA_M; ++i)
 #pragma unroll
-        for (int r = 0; r < RPT; ++r)
+    for (int r = 0; r < RPT; ++r) acc[i][r] = 0.f;
 #pragma unroll
-          for (int j = 0; j < 8; ++j) wl[r][j] = (s == 0) ? w[0][r][j] : w[KS - 1][r][j];
-      }
+  for (int s = 0; s < NKM; ++s) {
+    const int k = gt * 8 + s * G * 8;
+    if (k < p.K) {
+      float w[RPT][8];
 #pragma unroll
-      for (int i = 0; i < MT; ++i) {
-        if (m0 + i < p.M) {
-          const int off = ((m0 + i) * p.xs + k) * 4;
-          const f32x4 x0 = __builtin_amdgcn_raw_buffer_load_b128(xr, off, 0, 16);
-          const f32x4 x1 = __builtin_amdgcn_raw_buffer_load_b128(xr, off + 16, 0, 16);
+      for (int r = 0; r < RPT; ++r) wr[s][r].get(w[r]);
+#pragma unroll
+      for (int i = 0; i < DA_M; ++i) {
+        if (i < p.M) {
+          const float4 x0 = *reinterpret_cast<const float4*>(&xo[i][k]);
+          const float4 x1 = *reinterpret_cast<const float4*>(&xo[i][k + 4]);
           const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
 #pragma unroll
           for (int r = 0; r < RPT; ++r)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) acc[i][r] = fmaf(wl[r][j], xv[j], acc[i][r]);
+            for (int j = 0; j < 8; ++j) acc[i][r] = fmaf(w[r][j], xv[j], acc[i][r]);
         }
       }
     }
+  }
 #pragma unroll
-    for (int i = 0; i < MT; ++i)
+  for (int i = 0; i < DA_M; ++i)
 #pragma unroll
-      for (int r = 0; r < RPT; ++r) {
-        const float v = wave_sum(acc[i][r]);
-        if (lane == 0) red[wave][i][r] = v;
-      }
-    __syncthreads();
-    constexpr int WPG = G / 64;
-    constexpr int NPAIR = NG * MT * (RPT / 2);
-    if (tid < NPAIR) {
-      const int g = tid / (MT * (RPT / 2));
-      const int rem = tid % (MT * (RPT / 2));
-      const int i = rem / (RPT / 2), rp = (rem % (RPT / 2)) * 2;
-      if (m0 + i < p.M) {
-        float va = 0.f, vb = 0.f;
-#pragma unroll
-        for (int w2 = 0; w2 < WPG; ++w2) {
-          va += red[g * WPG + w2][i][rp];
-          vb += red[g * WPG + w2][i][rp + 1];
-        }
-        gemv_epilogue_pair(p, m0 + i, blockIdx.x * RPB + g * RPT + rp, va, vb);
-      }
+    for (int r = 0; r < RPT; ++r) {
+      const float v = wave_sum(acc[i][r]);
+      if (lane == 0) red[wave][i][r] = v;
     }
-    __syncthreads();
+  __syncthreads();
+  constexpr int WPG = G / 64;
+  constexpr int NPAIR = NG * DA_M * (RPT / 2);
+  if (tid < NPAIR) {
+    const int g = tid / (DA_M * (RPT / 2));
+    const int rem = tid % (DA_M * (RPT / 2));
+    const int i = rem / (RPT / 2), rp = (rem % (RPT / 2)) * 2;
+    if (i < p.M) {
+      float va = 0.f, vb2 = 0.f;
+#pragma unroll
+      for (int w2 = 0; w2 < WPG; ++w2) {
+        va += red[g * WPG + w2][i][rp];
+        vb2 += red[g * WPG + w2][i][rp + 1];
+      }
+      gemv_epilogue_pair(p, i, blockIdx.x * RPB + g * RPT + rp, va, vb2);
+    }
   }
 }
 
@@ -1031,48 +1063,25 @@ void launch_advance(const AdvanceParams& p, hipStream_t st) {
   hipLaunchKernelGGL(advance_kernel, dim3(1), dim3(256), 0, st, p);
 }
 
-static int g_handoff_acq = 0;
-void attn_oproj_set_acquire(int on) { g_handoff_acq = on; }
-
-template <typename WT, int TAG>
-static void launch_attn_oproj_t(const GemvParams& p, const AttnParams& a, int hd, unsigned* ctr, int* err,
-                                hipStream_t st) {
+bool dec_attn_oproj_supported(const GemvParams& p, const AttnParams& a, int hd) {
+  // one utterance's rows, <= 32 positions, <= 2 kv heads, q_dim <= 1024, o_proj at G = 128
   int G, RPT;
   gemv_tiling(p.N, p.K, p.M, G, RPT);
-  const int blocks = p.N / ((256 / G) * RPT);
-  const bool mt1 = p.M == 1;
-#define AO_L(HD_, G_, M_) \
-  hipLaunchKernelGGL((attn_oproj_kernel<WT, HD_, G_, 2, M_, TAG>), dim3(blocks), dim3(256), 0, st, p, a, ctr, err, g_handoff_acq)
-#define AO_M(HD_, G_) do { if (mt1) AO_L(HD_, G_, 1); else AO_L(HD_, G_, 4); } while (0)
-#define AO_G(HD_) do { if (G == 128) AO_M(HD_, 128); else AO_M(HD_, 64); } while (0)
-  if (hd == 128) AO_G(128);
-  else AO_G(64);
-#undef AO_G
-#undef AO_M
-#undef AO_L
+  return G == 128 && hd == 128 && p.M <= DA_M && a.rm.T >= p.M && a.S_cap <= DA_NMAX && a.Hkv <= DA_HKV &&
+         a.Hq * hd <= DA_QD && p.K == a.Hq * hd && p.N % 16 == 0 && a.mode == ATTN_CAUSAL;
 }
 
-bool attn_oproj_supported(const GemvParams& p, const AttnParams& a) {
-  int G, RPT;
-  gemv_tiling(p.N, p.K, p.M, G, RPT);
-  const int blocks = p.N / ((256 / G) * RPT);
-  // producers must fit in the grid, all weights of a row group in <= 2 K-steps, RPT = 2
-  return RPT == 2 && (G == 128 || G == 64) && a.M * a.Hkv <= blocks && p.K <= 2 * G * 8 && a.M <= 64 &&
-         (a.Hq / a.Hkv) <= 4;
-}
-
-void launch_attn_oproj(const GemvParams& p0, const AttnParams& a, int wdt, int hd, unsigned* ctr, int* err,
-                       hipStream_t st, int tag) {
+void launch_dec_attn_oproj(const GemvParams& p0, const AttnParams& a, int wdt, hipStream_t st, int tag) {
   GemvParams p = p0;
   p.epi = EPI_ADD;
   p.nw = nullptr;
+  const int blocks = p.N / 16;  // G = 128, RPT = 8
   const bool nt = (gemv_nt_mask() >> tag) & 1;
   if (wdt == WDT_BF16) {
-    if (tag == 1) nt ? launch_attn_oproj_t<bf16_t, 5>(p, a, hd, ctr, err, st) : launch_attn_oproj_t<bf16_t, 1>(p, a, hd, ctr, err, st);
-    else nt ? launch_attn_oproj_t<bf16_t, 4>(p, a, hd, ctr, err, st) : launch_attn_oproj_t<bf16_t, 0>(p, a, hd, ctr, err, st);
+    if (nt) hipLaunchKernelGGL((dec_attn_oproj_kernel<bf16_t, 128, 8, 5>), dim3(blocks), dim3(256), 0, st, p, a);
+    else hipLaunchKernelGGL((dec_attn_oproj_kernel<bf16_t, 128, 8, 1>), dim3(blocks), dim3(256), 0, st, p, a);
   } else {
-    if (tag == 1) launch_attn_oproj_t<float, 1>(p, a, hd, ctr, err, st);
-    else launch_attn_oproj_t<float, 0>(p, a, hd, ctr, err, st);
+    hipLaunchKernelGGL((dec_attn_oproj_kernel<float, 128, 8, 1>), dim3(blocks), dim3(256), 0, st, p, a);
   }
 }
 

@@ -88,9 +88,9 @@ int csm_synchronize(csm_engine* e);
  * kind 0 = norm+gate/up+SiLU, 1 = down+residual, 2 = norm+QKV+RoPE, 3 = o_proj+residual.
  * *bytes = algorithmic (weight) bytes per launch. */
 int csm_bench_gemv(csm_engine* e, int which, int M, int iters, float* avg_us, double* bytes);
-/* Tuning / debug switches (re-capture the frame graphs): "fuse_attn" (attention -> o_proj in one
- * launch, default 0), "nt_mask" (bit t: non-temporal weight loads for stack tag t, default 5),
- * "handoff_acquire" (agent acquire after the in-launch hand-off poll, default 0), "gemv_xl"
+/* Tuning / debug switches (re-capture the frame graphs): "fuse_attn" (decoder attention recomputed
+ * inside the o_proj launch, default 0), "nt_mask" (bit t: non-temporal weight loads for stack tag
+ * t, default 5), "gemv_xl"
  * (decode GEMVs with LDS-staged activations, default 1), "fold_proj" (decoder steps >= 2 gather
  * projection(E_a[c]) from a table built at csm_begin instead of running the projection, default 1). */
 int csm_set_option(csm_engine* e, const char* key, int value);

@@ -160,11 +160,11 @@ def test_csm_1b_first_frames(dtype):
     del model
 
 
-@pytest.mark.parametrize("which,dtype,batch,frames", [("tiny", "float32", 3, 16), ("1b", "bf16", 2, 20)])
-def test_fused_attention_handoff_matches_two_launches(tiny, which, dtype, batch, frames):
-    """attn_oproj_kernel (attention published in-launch to the o_proj GEMV) must reproduce the
-    two-launch path bit for bit: same attention code, same GEMV tiling and reduction order.
-    Repeated runs exercise the self-resetting hand-off counters across graph replays."""
+@pytest.mark.parametrize("which,dtype,batch,frames", [("tiny", "float32", 1, 16), ("tiny", "float32", 3, 8), ("1b", "bf16", 1, 20)])
+def test_fused_decoder_attention_matches_two_launches(tiny, which, dtype, batch, frames):
+    """dec_attn_oproj_kernel (decoder attention recomputed inside the o_proj launch) must reproduce
+    the two-launch path bit for bit: same attention arithmetic, same GEMV K-slicing and reduction
+    order.  B > 1 exercises the two-launch fallback inside the same run."""
     from csm_mlx import _lib
     from csm_mlx.generation import generate_codes_batch
     from csm_mlx.sampling import Sampler

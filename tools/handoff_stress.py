@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
-"""Stress the in-launch attention -> o_proj hand-off (attn_oproj_kernel).
+"""Stress the fused decoder attention + o_proj launch (dec_attn_oproj_kernel).
 
-The fused launch must give codes bitwise equal to the two-launch path (same attention code,
-same GEMV tiling and reduction order).  Runs csm_1b greedy generation R times per mode and
+The fused launch must give codes bitwise equal to the two-launch path (same attention arithmetic,
+same GEMV K-slicing and reduction order).  Runs csm_1b greedy generation R times per mode and
 reports runs whose codes differ from the two-launch reference.
 
 usage: python tools/handoff_stress.py [--reps 5] [--frames 125] [--dtype bf16]
@@ -59,9 +59,8 @@ def main():
     opt("fuse_attn", 0)
     ref = run()
     print(f"reference (two launches): codes {ref.shape}", flush=True)
-    for name, acq in (("fused", 0), ("fused+acquire", 1)):
+    for name in ("fused",):
         opt("fuse_attn", 1)
-        opt("handoff_acquire", acq)
         bad = 0
         t0 = time.time()
         for r in range(a.reps):
@@ -74,7 +73,6 @@ def main():
                 else:
                     print(f"  {name} rep {r}: shape {got.shape}", flush=True)
         print(f"{name}: {bad}/{a.reps} runs differ ({time.time() - t0:.1f} s)", flush=True)
-    opt("handoff_acquire", 0)
 
 
 if __name__ == "__main__":
