@@ -19,6 +19,7 @@ numpy oracle, i.e. a CPU restatement -- NOT the MLX reference -- on this host).
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -53,7 +54,7 @@ def dist_env():
 
 
 def aggregate(frames_local: float, dt_local: float, world: int, device=None):
-    """(sum of frames over ranks, max time over ranks)."""
+    """(sum of frames over ranks, max time over ranks); device None = CPU tensors (gloo)."""
     if world == 1:
         return frames_local, dt_local
     import torch
@@ -66,23 +67,23 @@ def aggregate(frames_local: float, dt_local: float, world: int, device=None):
     return float(f.item()), float(m.item())
 
 
-def build_codec(seed=0):
+def build_codec(seed=0, device=None):
     from csm_mlx.config import MIMI_CONFIGURATION
     from csm_mlx.mimi import MimiCodec
     from csm_mlx.tokenizers import set_audio_tokenizer
     from csm_mlx.weights import synthetic_mimi_weights
     m = MIMI_CONFIGURATION["mimi_202407"]
-    codec = MimiCodec(m, max_batch=64)
+    codec = MimiCodec(m, max_batch=64, device=device)
     codec.load_weights(synthetic_mimi_weights(m, seed))
     set_audio_tokenizer(codec, 32)
     return codec
 
 
-def build_model(dtype: str, batch: int, seed=0):
+def build_model(dtype: str, batch: int, seed=0, device=None):
     from csm_mlx.models import CSM, csm_1b
     from csm_mlx.weights import csm_param_specs, synthetic_csm_weights
     args = csm_1b()
-    model = CSM(args, dtype=dtype, max_batch=batch)
+    model = CSM(args, dtype=dtype, max_batch=batch, device=device)
     names = list(csm_param_specs(args))
     for i in range(0, len(names), 16):      # stream tensors in groups: bounded host memory
         model.load_weights(list(synthetic_csm_weights(args, seed, names[i:i + 16]).items()), strict=False)
@@ -122,33 +123,45 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "float32"])
     ap.add_argument("--no-decode", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-frames", type=int, default=2)
+    ap.add_argument("--cpu-frames", type=int, default=96, help="oracle frames timed for cpu_baseline (~10 s on 16 cores)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (RCCL over xGMI) for real runs; gloo rehearses N ranks on fewer GPUs")
     args = ap.parse_args()
 
     rank, world, local = dist_env()
     dev = None
     if world > 1:
+        # torch (and its HIP runtime) first, so RCCL and the engine share one runtime
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dev = torch.device("cuda", local)
-        dist.init_process_group("nccl", device_id=dev)
+        device = local % max(1, torch.cuda.device_count())  # wraps only when rehearsing on fewer GPUs
+        if args.dist_backend == "nccl":
+            torch.cuda.set_device(device)
+            dev = torch.device("cuda", device)
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    from csm_mlx import _lib
+    if world == 1:
+        n_dev = ctypes.c_int(0)
+        _lib.check(_lib.lib().csm_device_count(ctypes.byref(n_dev)))
+        device = local % max(1, n_dev.value)
 
     def barrier_sync():
         if world > 1:
             import torch
             import torch.distributed as dist
             dist.barrier()
-            torch.cuda.synchronize()
+            if dev is not None:
+                torch.cuda.synchronize()
 
-    from csm_mlx import _lib
     from csm_mlx.generation import generate_batch
     from csm_mlx.tokenizers import tokenize_text_segment
 
-    model = build_model(args.dtype, args.batch)
+    model = build_model(args.dtype, args.batch, device=device)
     decode = not args.no_decode
     if decode:
-        build_codec()
+        build_codec(device=device)
     mine = shard(args.batch * world, world, rank)
     prompts = [tokenize_text_segment(prompt_ids(g), 0, 32) for g in mine]
     ms = args.frames * 80
@@ -171,7 +184,6 @@ def main():
     total_frames, max_dt = aggregate(float(frames), dt, world, dev)
 
     # roofline of the dominant kernel: decoder gate/up (+RMSNorm, SiLU*up) GEMV, 124 launches/frame
-    import ctypes
     L = _lib.lib()
     roof = {}
     for key, which in (("decoder_gate_up", 4), ("backbone_gate_up", 0)):
@@ -210,7 +222,7 @@ def main():
                        "model": "csm_1b (synthetic seed-0 weights)", "global_batch": args.batch * world,
                        "per_gpu_batch": args.batch, "frames": args.frames, "mimi_decode": decode,
                        "parallelism": f"dp{world}", "rtf": round(total_frames / max_dt / 12.5, 2)},
-            "roofline": dict(roof["decoder_gate_up"], kernel="gemv_kernel<bf16_t,64,2,1,TAG=1> = decoder "
+            "roofline": dict(roof["decoder_gate_up"], kernel="gemv_xl_kernel<bf16,G=64,RPT=2,MT=1,TAG=1> = decoder "
                              "RMSNorm+gate/up+SiLU*up GEMV, 33.5 MB bf16 weights per launch, 124 launches/frame"),
             "roofline_backbone": roof["backbone_gate_up"],
         }
