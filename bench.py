@@ -120,7 +120,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=1, help="utterances per GPU")
     ap.add_argument("--frames", type=int, default=125)
-    ap.add_argument("--dtype", default="bf16", choices=["bf16", "float32"])
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "float32", "q4"],
+                    help="weight storage; q4 = nn.quantize(model, 64, 4) int4 (configs[4])")
     ap.add_argument("--no-decode", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=96, help="oracle frames timed for cpu_baseline (~10 s on 16 cores)")

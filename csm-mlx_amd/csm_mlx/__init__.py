@@ -6,13 +6,14 @@ library libcsm_hip.so built from csm-mlx_amd/csrc.  The fine-tuning names the
 reference also exports (CSMDataset, CSMTrainer, TrainArgs, load_adapters) are out
 of scope for this engine and raise on access.
 """
+from . import nn
 from .generation import generate, generate_batch, generate_frame, stream_generate
 from .models import CSM, ModelArgs, csm_1b
 from .sampling import make_sampler
 from .segment import Segment
 
 __all__ = ["generate", "stream_generate", "CSM", "csm_1b", "Segment", "generate_frame", "generate_batch",
-           "make_sampler", "ModelArgs"]
+           "make_sampler", "ModelArgs", "nn"]
 
 _OUT_OF_SCOPE = {"CSMDataset", "CSMTrainer", "TrainArgs", "load_adapters"}
 

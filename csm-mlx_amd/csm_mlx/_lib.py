@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("CSM_HIP_LIB") or os.path.join(_HERE, "libcsm_hip.so")
 HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "csm_hip.h")
 
 CSM_OK, CSM_ERR_ARG, CSM_ERR_HIP, CSM_ERR_STATE, CSM_ERR_TOO_LONG = 0, -1, -2, -3, -4
-CSM_F32, CSM_BF16 = 0, 1
+CSM_F32, CSM_BF16, CSM_Q4, CSM_U32 = 0, 1, 2, 3
 
 
 class CsmLlamaDims(ctypes.Structure):
@@ -72,6 +72,7 @@ def lib():
             "csm_load_tensor": ([P, ctypes.c_char_p, P, I, ctypes.POINTER(I64), I], I),
             "csm_set_rope_table": ([P, I, P, I, I], I),
             "csm_weights_ready": ([P], I),
+            "csm_quantize": ([P, I, I], I),
             "csm_begin": ([P, I, P, F, I], I),
             "csm_prefill": ([P, I, I, P, P], I),
             "csm_run_frames": ([P, I, ctypes.POINTER(I)], I),
@@ -131,8 +132,10 @@ def shape_arr(shape):
 
 
 def host_tensor(a):
-    """(contiguous array, csm dtype) for float32 / bf16-bits (uint16) host data."""
+    """(contiguous array, csm dtype) for float32 / bf16-bits (uint16) / packed-int4 (uint32) host data."""
     a = np.asarray(a)
+    if a.dtype == np.uint32:  # MLX-packed int4 (QuantizedLinear / QuantizedEmbedding .weight)
+        return np.ascontiguousarray(a), CSM_U32
     if a.dtype == np.uint16:
         return np.ascontiguousarray(a), CSM_BF16
     if str(a.dtype) == "bfloat16":  # ml_dtypes-style arrays

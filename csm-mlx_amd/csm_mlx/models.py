@@ -61,7 +61,8 @@ def default_device() -> int:
 
 
 class CSM:
-    """models.py:31-92.  ``dtype`` selects weight storage: "bf16" (perf) or "float32" (parity)."""
+    """models.py:31-92.  ``dtype`` selects weight storage: "bf16" (perf), "float32" (parity) or "q4"
+    (int4 g64, as after ``nn.quantize(model, 64, 4)``; see ``quantize``)."""
 
     def __init__(self, args: ModelArgs, *, dtype: str = "bf16", device: Optional[int] = None, max_batch: int = 1):
         self.args = args
@@ -74,9 +75,10 @@ class CSM:
         self.n_decoder_embedding = dec.num_attention_heads * (dec.head_dim or 0)
         self.backbone = _StackView(bb)
         self.decoder = _StackView(dec)
-        if dtype not in ("bf16", "bfloat16", "float32", "f32"):
+        if dtype not in ("bf16", "bfloat16", "float32", "f32", "q4", "int4"):
             raise ValueError(f"unsupported dtype {dtype}")
-        self.dtype = "float32" if dtype in ("float32", "f32") else "bf16"
+        self.dtype = "float32" if dtype in ("float32", "f32") else ("q4" if dtype in ("q4", "int4") else "bf16")
+        self.quantization = {"group_size": 64, "bits": 4} if self.dtype == "q4" else None
         self.device = default_device() if device is None else device
         self.max_seq_len = bb.max_position_embeddings or 2048      # generation.py:132
         self._max_batch = max_batch
@@ -93,7 +95,7 @@ class CSM:
         if self._engine is None:
             L = _lib.lib()
             h = ctypes.c_void_p()
-            wdt = _lib.CSM_F32 if self.dtype == "float32" else _lib.CSM_BF16
+            wdt = {"float32": _lib.CSM_F32, "bf16": _lib.CSM_BF16, "q4": _lib.CSM_Q4}[self.dtype]
             _lib.check(L.csm_engine_create(ctypes.byref(self._dims()), self.device, wdt, self._max_batch,
                                            self.max_seq_len, ctypes.byref(h)))
             self._engine = h
@@ -133,6 +135,22 @@ class CSM:
             _lib.check(L.csm_weights_ready(eng))
         return self
 
+    def quantize(self, group_size: int = 64, bits: int = 4):
+        """``nn.quantize(model, group_size, bits)`` (run_streaming_csm_mlx.py:811-818, README.md:108-111).
+
+        Every Linear / Embedding weight becomes MLX affine int4 (audio_head and norms stay as they
+        are).  Before any weights are loaded this switches the engine to int4 storage (later float
+        loads are quantized on the device, MLX-quantized checkpoints load directly); after loading
+        it converts the resident weights in place on the GPU."""
+        if (group_size, bits) != (64, 4):
+            raise ValueError("only group_size=64, bits=4 is supported")
+        if self._engine is None:
+            self.dtype = "q4"
+        else:
+            _lib.check(_lib.lib().csm_quantize(self._engine, group_size, bits))
+        self.quantization = {"group_size": group_size, "bits": bits}
+        return self
+
     def embed_audio(self, codebook: int, tokens):
         raise NotImplementedError("embeddings are gathered inside the HIP frame graph (models.py:79-80)")
 
@@ -153,5 +171,7 @@ def _read_weight_file(path: str):
             t = f.get_tensor(k)
             if t.dtype == torch.bfloat16:
                 yield k, t.view(torch.uint16).numpy()
+            elif t.dtype in (torch.uint32, torch.int32) and k.endswith(".weight"):  # MLX-packed int4
+                yield k, t.view(torch.int32).numpy().view(np.uint32)
             else:
                 yield k, t.float().numpy()

@@ -125,3 +125,20 @@ __host__ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
   return x ^ (x >> 31);
 }
+
+// ---------------------------------------------------------------------------- int4 (MLX affine, g64)
+// Device layout of a quantized [N][K] matrix (one allocation): nibbles [N][K/2] (element k of a row in
+// byte k/2, low nibble for even k -- MLX's uint32 packing read as bytes), then per group of 64 a
+// uint32 {lo16 = scale bf16, hi16 = bias bf16} [N][K/64].  w_hat = scale * q + bias.
+constexpr int Q4_GROUP = 64;
+__host__ __device__ __forceinline__ size_t q4_bytes(size_t N, size_t K) { return N * K / 2 + N * (K / Q4_GROUP) * 4; }
+__host__ __device__ __forceinline__ size_t q4_sb_offset(size_t N, size_t K) { return N * K / 2; }
+
+// 8 dequantized weights of row r starting at k (k % 8 == 0) of a quantized matrix with N rows
+__device__ __forceinline__ void q4_load8(const uint8_t* base, size_t N, int K, size_t r, int k, float (&w)[8]) {
+  const uint32_t q = *reinterpret_cast<const uint32_t*>(base + r * (K / 2) + k / 2);
+  const uint32_t sb = reinterpret_cast<const uint32_t*>(base + q4_sb_offset(N, K))[r * (K / Q4_GROUP) + k / Q4_GROUP];
+  const float s = bf16_lo(sb), b = bf16_hi(sb);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) w[j] = fmaf(s, (float)((q >> (4 * j)) & 15u), b);
+}

@@ -18,6 +18,7 @@
 #include <map>
 #include <set>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "../../include/csm_hip.h"
@@ -52,8 +53,18 @@ struct Stack {
 struct csm_engine {
   csm_dims dims;
   int dev = 0;
-  int wdt = WDT_BF16;
-  size_t wsz = 2;
+  int wdt = WDT_BF16;       // Linear / Embedding weights: WDT_F32, WDT_BF16 or WDT_Q4 (nn.quantize'd)
+  int head_wdt = WDT_BF16;  // audio_head: never quantized (a raw array, models.py:65-67)
+  size_t wsz = 2;           // bytes per element of the dense (non-q4) weight dtype
+  // bytes of one [N][K] Linear/Embedding weight in the engine's storage dtype
+  size_t wbytes(size_t N, size_t K) const { return wdt == WDT_Q4 ? q4_bytes(N, K) : N * K * wsz; }
+  // pre-quantized MLX tensors wait here until .weight, .scales and .biases have all arrived
+  struct PendingQ4 {
+    std::vector<uint8_t> packed, scales, biases;
+    int sdt = 0;
+    int64_t n = 0, k = 0;
+  };
+  std::map<std::string, PendingQ4> pending_q4;
   int B_max = 0, F_cap = 0, M_cap = 0;
   hipStream_t st = nullptr;
   Stack bb, dec;
@@ -117,6 +128,15 @@ struct csm_engine {
     allocs.push_back(p);
     return p;
   }
+  void release(void* p) {
+    for (auto& a : allocs)
+      if (a == p) {
+        (void)hipFree(p);
+        a = allocs.back();
+        allocs.pop_back();
+        return;
+      }
+  }
   ~csm_engine() {
     if (g_body) (void)hipGraphExecDestroy(g_body);
     if (g_head) (void)hipGraphExecDestroy(g_head);
@@ -136,10 +156,10 @@ void alloc_stack(csm_engine* e, Stack& s, const csm_llama_dims& d, int S_cap, co
   const size_t D = d.hidden, F = d.intermediate, hd = d.head_dim;
   for (int i = 0; i < d.n_layers; ++i) {
     LayerW& l = s.L[i];
-    l.wqkv = e->alloc((size_t)s.qkv_rows() * D * e->wsz);
-    l.wo = e->alloc(D * (size_t)s.q_dim() * e->wsz);
-    l.wgu = e->alloc(2 * F * D * e->wsz);
-    l.wd = e->alloc(D * F * e->wsz);
+    l.wqkv = e->alloc(e->wbytes(s.qkv_rows(), D));
+    l.wo = e->alloc(e->wbytes(D, s.q_dim()));
+    l.wgu = e->alloc(e->wbytes(2 * F, D));
+    l.wd = e->alloc(e->wbytes(D, F));
     l.n1 = (float*)e->alloc(D * 4);
     l.n2 = (float*)e->alloc(D * 4);
     const std::string p = std::string(prefix) + ".layers." + std::to_string(i);
@@ -211,12 +231,23 @@ void run_stack(csm_engine* e, Stack& s, float* x, int M, float* q, float* att, f
   }
 }
 
+void embed(csm_engine* e, const EmbedParams& ep, int M, hipStream_t st) {
+  if (e->wdt == WDT_Q4) launch_embed_q4(ep, e->dims.n_text_vocab, M, st);
+  else launch_embed(ep, e->wdt, M, st);
+}
+
+// GEMV rows per block for an (N, K) matrix of the given storage dtype (arg-max partial counts)
+int head_blocks(int N, int K, int M, int wdt) {
+  const int rpb = wdt == WDT_Q4 ? gemv_q4_rows_per_block(N, K, M) : gemv_rows_per_block(N, K, M);
+  return (N + rpb - 1) / rpb;
+}
+
 void enqueue_body(csm_engine* e, hipStream_t st) {
   const int B = e->B;
   EmbedParams ep{};
   ep.codes = e->codes; ep.text_emb = e->text_emb; ep.audio_emb = e->audio_emb; ep.V = e->V; ep.K = e->K;
   ep.D = e->D; ep.out = e->x; ep.pos_inc = e->pos;
-  launch_embed(ep, e->wdt, B, st);
+  embed(e, ep, B, st);
   RowMap rm{1, 0, e->pos, 0};
   run_stack(e, e->bb, e->x, B, e->q, e->att, e->mlp, rm, st);
   launch_rmsnorm_rows(e->x, e->D, e->bb.norm, e->bb.d.eps, e->D, e->h_last, e->D, B, st);
@@ -225,8 +256,8 @@ void enqueue_body(csm_engine* e, hipStream_t st) {
 void enqueue_head(csm_engine* e, hipStream_t st) {
   const int B = e->B, K = e->K, D = e->D, Dd = e->Dd, V = e->V, Vp = e->Vpad;
   const bool greedy = e->temperature <= 0.f;
-  const int n0 = Vp / gemv_rows_per_block(Vp, D, B);   // c0-head blocks (partials per row)
-  const int ni = Vp / gemv_rows_per_block(Vp, Dd, B);  // ci-head blocks
+  const int n0 = head_blocks(Vp, D, B, e->wdt);        // c0-head blocks (partials per row)
+  const int ni = head_blocks(Vp, Dd, B, e->head_wdt);  // ci-head blocks
   auto part = [&](int cb) { return e->part + (size_t)cb * e->B_max * e->part_stride; };
   SampleParams sp{};
   sp.ls = Vp; sp.V = V; sp.temperature = e->temperature; sp.top_k = e->top_k; sp.seeds = e->seeds;
@@ -248,6 +279,7 @@ void enqueue_head(csm_engine* e, hipStream_t st) {
     g.W = e->proj; g.N = Dd; g.K = D; g.x = e->h_last; g.xs = D; g.M = M; g.out = e->dx; g.os = Dd;
     g.xpart = part(i - 1); g.xpart_stride = e->part_stride; g.xpart_n = greedy ? (i == 1 ? n0 : ni) : 1;
     g.xtab = e->audio_emb; g.xV = V; g.xcb = i - 1; g.x_step1 = (i == 1); g.x_codes = e->codes; g.x_codes_K = K;
+    g.xtab_q4_rows = V * K;
     const bool folded = i >= 2 && e->proj_tab && e->fold_proj;
     if (!folded) launch_gemv(g, e->wdt, EPI_STORE, 0, st);
     GemvParams g0 = g;  // steps >= 2: layer 0 gathers projection(E_a[c]) from the folded table
@@ -256,11 +288,11 @@ void enqueue_head(csm_engine* e, hipStream_t st) {
     run_stack(e, e->dec, e->dx, M, e->dq, e->datt, e->dmlp, rm, st, folded ? &g0 : nullptr);
     // ci_logits = norm(hidden[:, -1]) @ audio_head[i-1]  (generation.py:79)
     g = GemvParams{};
-    g.W = (const char*)e->audio_head + (size_t)(i - 1) * Vp * Dd * e->wsz; g.N = Vp; g.K = Dd;
+    g.W = (const char*)e->audio_head + (size_t)(i - 1) * Vp * Dd * (e->head_wdt == WDT_F32 ? 4 : 2); g.N = Vp; g.K = Dd;
     g.x = e->dx + (i == 1 ? Dd : 0); g.xs = (i == 1 ? 2 * Dd : Dd); g.M = B; g.nw = e->dec.norm;
     g.eps = e->dec.d.eps; g.out = e->ci_logits + (size_t)(i - 1) * B * Vp; g.os = Vp;
     g.part = part(i); g.part_stride = e->part_stride; g.n_valid = V;
-    if (!(ablate() & 64)) launch_gemv(g, e->wdt, greedy ? EPI_ARGMAX : EPI_STORE, 1, st);
+    if (!(ablate() & 64)) launch_gemv(g, e->head_wdt, greedy ? EPI_ARGMAX : EPI_STORE, 1, st);
     if (!greedy) {
       sp.logits = e->ci_logits + (size_t)(i - 1) * B * Vp; sp.cb = i; sp.part = part(i);
       launch_sample(sp, e->wdt, B, st);
@@ -318,8 +350,8 @@ void ensure_batch(csm_engine* e, int B) {
   e->n_frames = (int*)e->balloc(Bm * 4);
   e->done = (uint8_t*)e->balloc(Bm);
   e->seeds = (uint64_t*)e->balloc(Bm * 8);
-  e->part_stride = std::max(Vp / gemv_rows_per_block((int)Vp, (int)D, 1), Vp / gemv_rows_per_block((int)Vp, (int)Dd, 1));
-  e->part_stride = std::max(e->part_stride, (int)(Vp / 2));
+  // partial slots per row: enough for any head tiling (c0 / ci heads, dense or q4; >= Vp/2 blocks never occur)
+  e->part_stride = (int)(Vp / 2);
   e->part = (unsigned long long*)e->balloc(K * Bm * (size_t)e->part_stride * 8);
 }
 
@@ -329,7 +361,8 @@ void build_proj_table(csm_engine* e) {
   const int V = e->V, D = e->D, Dd = e->Dd;
   float* scratch = e->mlp;  // [M_cap][F] fp32: >= V*D floats (checked at create)
   for (int cb = 0; cb < e->K - 1; ++cb) {
-    launch_to_f32((const char*)e->audio_emb + (size_t)cb * V * D * e->wsz, e->wdt, scratch, (size_t)V * D, e->st);
+    if (e->wdt == WDT_Q4) launch_q4_to_f32(e->audio_emb, V * e->K, D, cb * V, V, scratch, e->st);
+    else launch_to_f32((const char*)e->audio_emb + (size_t)cb * V * D * e->wsz, e->wdt, scratch, (size_t)V * D, e->st);
     GemvParams g{};
     g.W = e->proj; g.N = Dd; g.K = D; g.x = scratch; g.xs = D; g.M = V;
     g.out = e->proj_tab + (size_t)cb * V * Dd; g.os = Dd;
@@ -340,6 +373,108 @@ void build_proj_table(csm_engine* e) {
   e->proj_tab_dirty = false;
 }
 
+
+// Where an MLX Linear/Embedding weight lives in the engine: rows row0 + r*rstep (r < n) of a
+// [Ntot][K] matrix at base.  False for parameters nn.quantize leaves alone (norms, audio_head).
+struct Place {
+  void* base = nullptr;
+  int Ntot = 0, K = 0, row0 = 0, rstep = 1, n = 0;
+};
+
+bool weight_place(csm_engine* e, const std::string& name, Place& pl) {
+  for (int which = 0; which < 2; ++which) {
+    Stack& s = which == 0 ? e->bb : e->dec;
+    const std::string pre = which == 0 ? "backbone.layers." : "decoder.layers.";
+    if (name.rfind(pre, 0) != 0) continue;
+    int li = -1;
+    char tail[128] = {0};
+    if (sscanf(name.c_str() + pre.size(), "%d.%127s", &li, tail) != 2 || li < 0 || li >= s.d.n_layers) return false;
+    LayerW& l = s.L[li];
+    const std::string t(tail);
+    const int D = s.d.hidden, F = s.d.intermediate, qd = s.q_dim(), kvd = s.d.n_kv_heads * s.d.head_dim;
+    const int qkv = s.qkv_rows();
+    if (t == "self_attn.q_proj.weight") pl = Place{l.wqkv, qkv, D, 0, 1, qd};
+    else if (t == "self_attn.k_proj.weight") pl = Place{l.wqkv, qkv, D, qd, 1, kvd};
+    else if (t == "self_attn.v_proj.weight") pl = Place{l.wqkv, qkv, D, qd + kvd, 1, kvd};
+    else if (t == "self_attn.o_proj.weight") pl = Place{l.wo, D, qd, 0, 1, D};
+    else if (t == "mlp.gate_proj.weight") pl = Place{l.wgu, 2 * F, D, 0, 2, F};
+    else if (t == "mlp.up_proj.weight") pl = Place{l.wgu, 2 * F, D, 1, 2, F};
+    else if (t == "mlp.down_proj.weight") pl = Place{l.wd, D, F, 0, 1, D};
+    else return false;
+    return true;
+  }
+  const int D = e->D, Dd = e->Dd, V = e->V, K = e->K, Vp = e->Vpad;
+  if (name == "text_embeddings.weight") pl = Place{e->text_emb, e->dims.n_text_vocab, D, 0, 1, e->dims.n_text_vocab};
+  else if (name == "audio_embeddings.weight") pl = Place{e->audio_emb, V * K, D, 0, 1, V * K};
+  else if (name == "projection.weight") pl = Place{e->proj, Dd, D, 0, 1, Dd};
+  else if (name == "codebook0_head.weight") pl = Place{e->c0_head, Vp, D, 0, 1, V};
+  else return false;
+  return true;
+}
+
+// Device scratch for load-time conversions (grown on demand, freed after each load)
+struct DevBuf {
+  void* p = nullptr;
+  explicit DevBuf(size_t n) { HIPCHK(hipMalloc(&p, n)); }
+  ~DevBuf() { if (p) (void)hipFree(p); }
+};
+
+// int4 engine: an MLX float weight is quantized on the device; a pre-quantized one (uint32
+// .weight + .scales + .biases, MLX QuantizedLinear / QuantizedEmbedding keys) is placed once all
+// three parts have arrived.  Returns false for names that are not quantized parameters.
+bool load_q4(csm_engine* e, const std::string& name, const void* host, int src_dtype, const std::vector<int64_t>& shp) {
+  std::string base = name, part = "weight";
+  for (const char* suf : {".scales", ".biases"})
+    if (name.size() > strlen(suf) && name.compare(name.size() - strlen(suf), strlen(suf), suf) == 0) {
+      base = name.substr(0, name.size() - strlen(suf)) + ".weight";
+      part = suf + 1;
+    }
+  Place pl;
+  if (!weight_place(e, base, pl)) return false;
+  size_t numel = 1;
+  for (auto v : shp) numel *= (size_t)v;
+  if (part == "weight" && src_dtype != CSM_U32) {  // float weight -> quantize (nn.quantize)
+    if (shp != std::vector<int64_t>{pl.n, pl.K}) throw CsmError(CSM_ERR_ARG, "shape mismatch for " + name);
+    auto h = convert_to(host, src_dtype, numel, WDT_F32);
+    DevBuf tmp(h.size());
+    HIPCHK(hipMemcpy(tmp.p, h.data(), h.size(), hipMemcpyHostToDevice));
+    launch_q4_quantize(tmp.p, WDT_F32, pl.n, pl.K, pl.base, pl.Ntot, pl.row0, pl.rstep, e->st);
+    HIPCHK(hipStreamSynchronize(e->st));
+    HIPCHK(hipGetLastError());
+    e->loaded.insert(base);
+    if (base == "audio_embeddings.weight" || base == "projection.weight") e->proj_tab_dirty = true;
+    return true;
+  }
+  auto& pq = e->pending_q4[base];
+  const size_t es = src_dtype == CSM_F32 || src_dtype == CSM_U32 ? 4 : 2;
+  if (part == "weight") {
+    if (shp != std::vector<int64_t>{pl.n, pl.K / 8}) throw CsmError(CSM_ERR_ARG, "packed shape mismatch for " + name);
+    pq.packed.assign((const uint8_t*)host, (const uint8_t*)host + numel * 4);
+  } else {
+    if (src_dtype != CSM_F32 && src_dtype != CSM_BF16) throw CsmError(CSM_ERR_ARG, name + " must be f32 or bf16");
+    if (shp != std::vector<int64_t>{pl.n, pl.K / Q4_GROUP}) throw CsmError(CSM_ERR_ARG, "shape mismatch for " + name);
+    if (!pq.scales.empty() || !pq.biases.empty())
+      if (pq.sdt != src_dtype) throw CsmError(CSM_ERR_ARG, "scales / biases dtypes differ for " + base);
+    pq.sdt = src_dtype;
+    (part == "scales" ? pq.scales : pq.biases).assign((const uint8_t*)host, (const uint8_t*)host + numel * es);
+  }
+  if (pq.packed.empty() || pq.scales.empty() || pq.biases.empty()) return true;
+  // all three parts present: nibble rows (strided for interleaved gate/up) + sb words
+  const size_t rowb = (size_t)pl.K / 2;
+  HIPCHK(hipMemcpy2D((uint8_t*)pl.base + (size_t)pl.row0 * rowb, rowb * pl.rstep, pq.packed.data(), rowb, rowb, pl.n,
+                     hipMemcpyHostToDevice));
+  DevBuf sc(pq.scales.size()), bi(pq.biases.size());
+  HIPCHK(hipMemcpy(sc.p, pq.scales.data(), pq.scales.size(), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(bi.p, pq.biases.data(), pq.biases.size(), hipMemcpyHostToDevice));
+  launch_q4_set_sb(sc.p, bi.p, pq.sdt == CSM_BF16 ? WDT_BF16 : WDT_F32, pl.n, pl.K, pl.base, pl.Ntot, pl.row0,
+                   pl.rstep, e->st);
+  HIPCHK(hipStreamSynchronize(e->st));
+  HIPCHK(hipGetLastError());
+  e->pending_q4.erase(base);
+  e->loaded.insert(base);
+  if (base == "audio_embeddings.weight" || base == "projection.weight") e->proj_tab_dirty = true;
+  return true;
+}
 
 }  // namespace
 
@@ -370,7 +505,9 @@ int csm_engine_create(const csm_dims* dims, int device, int weight_dtype, int ma
     if (b.n_heads * b.head_dim != b.hidden) throw CsmError(CSM_ERR_ARG, "backbone hidden != heads*head_dim");
     for (const csm_llama_dims* x : {&b, &d})
       if (x->n_heads / x->n_kv_heads > 4) throw CsmError(CSM_ERR_ARG, "GQA group > 4 unsupported");
-    {  // every GEMV shape must tile into whole blocks
+    if (weight_dtype != CSM_F32 && weight_dtype != CSM_BF16 && weight_dtype != CSM_Q4)
+      throw CsmError(CSM_ERR_ARG, "weight_dtype must be CSM_F32, CSM_BF16 or CSM_Q4");
+    {  // every GEMV shape must tile into whole blocks (q4: any even N whose K the q4 tiling covers)
       const int Vp = (dims->n_audio_vocab + 7) / 8 * 8;
       std::vector<std::pair<int, int>> shapes = {{Vp, b.hidden}, {Vp, d.hidden}, {d.hidden, b.hidden}};
       for (const csm_llama_dims* x : {&b, &d}) {
@@ -379,16 +516,20 @@ int csm_engine_create(const csm_dims* dims, int device, int weight_dtype, int ma
         shapes.push_back({2 * x->intermediate, x->hidden});
         shapes.push_back({x->hidden, x->intermediate});
       }
-      for (auto [N, Kd] : shapes)
+      for (auto [N, Kd] : shapes) {
         for (int M : {1, 4})
           if (N % gemv_rows_per_block(N, Kd, M)) throw CsmError(CSM_ERR_ARG, "GEMV shape does not tile");
+        if (!gemv_q4_supported(N, Kd) && weight_dtype == CSM_Q4)
+          throw CsmError(CSM_ERR_ARG, "int4 GEMV does not support this shape");
+      }
     }
     HIPCHK(hipSetDevice(device));
     std::unique_ptr<csm_engine> e(new csm_engine());
     if (const char* v = getenv("CSM_FUSE_ATTN")) e->fuse_attn = v[0] != '0';
     e->dims = *dims;
     e->dev = device;
-    e->wdt = weight_dtype == CSM_F32 ? WDT_F32 : WDT_BF16;
+    e->wdt = weight_dtype == CSM_F32 ? WDT_F32 : (weight_dtype == CSM_Q4 ? WDT_Q4 : WDT_BF16);
+    e->head_wdt = e->wdt == WDT_F32 ? WDT_F32 : WDT_BF16;
     e->wsz = e->wdt == WDT_F32 ? 4 : 2;
     e->B_max = max_batch;
     e->F_cap = max_frames;
@@ -403,11 +544,11 @@ int csm_engine_create(const csm_dims* dims, int device, int weight_dtype, int ma
     alloc_stack(e.get(), e->bb, b, S, "backbone");
     alloc_stack(e.get(), e->dec, d, e->K, "decoder");
     const size_t D = e->D, Dd = e->Dd, K = e->K, Vp = e->Vpad, B = max_batch;
-    e->text_emb = e->alloc((size_t)dims->n_text_vocab * D * e->wsz);
-    e->audio_emb = e->alloc((size_t)e->V * K * D * e->wsz);
-    e->proj = e->alloc(Dd * D * e->wsz);
-    e->c0_head = e->alloc(Vp * D * e->wsz);
-    e->audio_head = e->alloc((K - 1) * Vp * Dd * e->wsz);
+    e->text_emb = e->alloc(e->wbytes(dims->n_text_vocab, D));
+    e->audio_emb = e->alloc(e->wbytes((size_t)e->V * K, D));
+    e->proj = e->alloc(e->wbytes(Dd, D));
+    e->c0_head = e->alloc(e->wbytes(Vp, D));
+    e->audio_head = e->alloc((K - 1) * Vp * Dd * (e->head_wdt == WDT_F32 ? 4 : 2));
     e->proj_tab = (float*)e->alloc((K - 1) * (size_t)e->V * Dd * 4);
     for (const char* n : {"text_embeddings.weight", "audio_embeddings.weight", "projection.weight",
                           "codebook0_head.weight", "audio_head"})
@@ -456,6 +597,8 @@ int csm_load_tensor(csm_engine* e, const char* cname, const void* host, int src_
     auto expect = [&](std::initializer_list<int64_t> want) {
       if (shp != std::vector<int64_t>(want)) throw CsmError(CSM_ERR_ARG, "shape mismatch for " + name);
     };
+    if (e->wdt == WDT_Q4 && load_q4(e, name, host, src_dtype, shp)) return CSM_OK;
+    if (src_dtype == CSM_U32) throw CsmError(CSM_ERR_ARG, "packed int4 tensor " + name + " needs a CSM_Q4 engine");
     const size_t es = e->wsz;
     auto conv = [&](size_t n) { return convert_to(host, src_dtype, n, e->wdt); };
     auto conv_f32 = [&](size_t n) { return convert_to(host, src_dtype, n, WDT_F32); };
@@ -541,7 +684,7 @@ int csm_load_tensor(csm_engine* e, const char* cname, const void* host, int src_
       for (int64_t c = 0; c < K - 1; ++c)
         for (int64_t i = 0; i < Dd; ++i)
           for (int64_t v = 0; v < V; ++v) t[((size_t)c * Vp + v) * Dd + i] = src[((size_t)c * Dd + i) * V + v];
-      auto h = convert_to(t.data(), CSM_F32, t.size(), e->wdt);
+      auto h = convert_to(t.data(), CSM_F32, t.size(), e->head_wdt);
       HIPCHK(hipMemcpy(e->audio_head, h.data(), h.size(), hipMemcpyHostToDevice));
     } else {
       throw CsmError(CSM_ERR_ARG, "unknown tensor " + name);
@@ -555,6 +698,47 @@ int csm_weights_ready(csm_engine* e) {
   CSM_TRY {
     for (const auto& n : e->required)
       if (!e->loaded.count(n)) throw CsmError(CSM_ERR_STATE, "missing weight " + n);
+  }
+  CSM_CATCH
+}
+
+int csm_quantize(csm_engine* e, int group_size, int bits) {
+  CSM_TRY {
+    if (group_size != Q4_GROUP || bits != 4) throw CsmError(CSM_ERR_ARG, "only group_size=64, bits=4 is supported");
+    if (e->wdt == WDT_Q4) return CSM_OK;  // already quantized (nn.quantize on a quantized model is a no-op here)
+    HIPCHK(hipSetDevice(e->dev));
+    HIPCHK(hipDeviceSynchronize());
+    const int old = e->wdt;
+    const size_t old_es = e->wsz;
+    // every Linear / Embedding matrix, whole (all rows of fused / interleaved layouts): row order kept
+    std::vector<std::tuple<void**, int, int>> mats;
+    for (Stack* s : {&e->bb, &e->dec})
+      for (LayerW& l : s->L) {
+        const int D = s->d.hidden, F = s->d.intermediate;
+        mats.emplace_back(&l.wqkv, s->qkv_rows(), D);
+        mats.emplace_back(&l.wo, D, s->q_dim());
+        mats.emplace_back(&l.wgu, 2 * F, D);
+        mats.emplace_back(&l.wd, D, F);
+      }
+    mats.emplace_back(&e->text_emb, e->dims.n_text_vocab, e->D);
+    mats.emplace_back(&e->audio_emb, e->V * e->K, e->D);
+    mats.emplace_back(&e->proj, e->Dd, e->D);
+    mats.emplace_back(&e->c0_head, e->Vpad, e->D);
+    for (auto& [pp, N, Kd] : mats)
+      if (!gemv_q4_supported(N, Kd)) throw CsmError(CSM_ERR_ARG, "int4 GEMV does not support this shape");
+    for (auto& [pp, N, Kd] : mats) {
+      void* q = e->alloc(q4_bytes(N, Kd));
+      launch_q4_quantize(*pp, old, N, Kd, q, N, 0, 1, e->st);
+      HIPCHK(hipStreamSynchronize(e->st));
+      HIPCHK(hipGetLastError());
+      e->release(*pp);
+      *pp = q;
+    }
+    (void)old_es;
+    e->head_wdt = old;
+    e->wdt = WDT_Q4;
+    e->proj_tab_dirty = true;
+    e->g_B = -1;
   }
   CSM_CATCH
 }
@@ -599,7 +783,7 @@ int csm_prefill(csm_engine* e, int b, int T, const int32_t* tokens, const uint8_
     EmbedParams ep{};
     ep.tok = e->tok; ep.mask = e->msk; ep.text_emb = e->text_emb; ep.audio_emb = e->audio_emb; ep.V = e->V;
     ep.K = K; ep.D = e->D; ep.out = e->x;
-    launch_embed(ep, e->wdt, T, e->st);
+    embed(e, ep, T, e->st);
     RowMap rm{T, b, nullptr, start};
     run_stack(e, e->bb, e->x, T, e->q, e->att, e->mlp, rm, e->st);
     launch_rmsnorm_rows(e->x + (size_t)(T - 1) * e->D, e->D, e->bb.norm, e->bb.d.eps, e->D,
@@ -700,6 +884,12 @@ int csm_debug_read(csm_engine* e, const char* what, void* host, int64_t nbytes, 
     else if (w == "ci_logits") { src = e->ci_logits; n = (e->K - 1) * B * Vp * 4; }
     else if (w == "codes") { src = e->codes; n = B * e->K * 4; }
     else if (w == "pos") { src = e->pos; n = B * 4; }
+    else if (w.rfind("weight:", 0) == 0) {  // a whole stored matrix in its device layout (not fused ones)
+      Place pl;
+      if (!weight_place(e, w.substr(7), pl) || pl.n != pl.Ntot) throw CsmError(CSM_ERR_ARG, "no whole matrix " + w);
+      src = pl.base;
+      n = e->wbytes(pl.Ntot, pl.K);
+    }
     else throw CsmError(CSM_ERR_ARG, "unknown debug tap " + w);
     if (needed) *needed = (int64_t)n;
     if (host) {
@@ -749,7 +939,7 @@ int csm_bench_gemv(csm_engine* e, int which, int M, int iters, float* avg_us, do
     };
     int epi = 0, norm = 0;
     GemvParams g = params(0, epi, norm);
-    size_t nbytes = (size_t)g.N * g.K * e->wsz;
+    size_t nbytes = e->wbytes(g.N, g.K);
     nbytes += (size_t)M * g.K * 4 + (size_t)M * (epi == EPI_SILU_MUL ? F : D) * 4 * (epi == EPI_ADD ? 2 : 1);
     const int nl = s.d.n_layers;
     for (int i = 0; i < nl; ++i) { GemvParams gi = params(i, epi, norm); launch_gemv(gi, e->wdt, epi, norm, e->st, tag); }

@@ -2,7 +2,7 @@
 #pragma once
 #include "common.h"
 
-enum { WDT_F32 = 0, WDT_BF16 = 1 };
+enum { WDT_F32 = 0, WDT_BF16 = 1, WDT_Q4 = 2 };  // WDT_Q4: MLX affine int4, group 64 (common.h layout)
 enum { EPI_STORE = 0, EPI_ADD = 1, EPI_SILU_MUL = 2, EPI_QKV = 3, EPI_GELU = 4, EPI_ARGMAX = 5 };
 enum { ATTN_CAUSAL = 0, ATTN_WINDOW = 1, ATTN_BLOCK = 2 };
 
@@ -37,6 +37,7 @@ struct GemvParams {
   int xV, xcb, x_step1, x_codes_K;
   int* x_codes;
   int xtab_f32;         // gathered table rows are fp32 (else the weight type)
+  int xtab_q4_rows;     // int4 weights: total rows of the (quantized) gathered table
   float* x_copy;        // if set: block 0 also stores the raw (un-normed) x rows here [M][K]
 };
 
@@ -46,6 +47,66 @@ __device__ __forceinline__ unsigned long long pack_argmax(float v, int idx) {
   return ((unsigned long long)key << 32) | (unsigned long long)(0xFFFFFFFFu - (uint32_t)idx);
 }
 __device__ __forceinline__ int unpack_argmax(unsigned long long p) { return (int)(0xFFFFFFFFu - (uint32_t)p); }
+
+// Pair epilogue shared by every GEMV kernel (rows n, n+1 of output row m).
+__device__ __forceinline__ void gemv_epilogue_pair(const GemvParams& p, int m, int n, float a, float b) {
+  switch (p.epi) {
+    case EPI_STORE: {
+      float* o = p.out + (size_t)m * p.os + n;
+      o[0] = a;
+      o[1] = b;
+      break;
+    }
+    case EPI_GELU: {
+      float* o = p.out + (size_t)m * p.os + n;
+      o[0] = p.gelu_erf ? gelu_erf_f(a) : gelu_tanh_f(a);
+      o[1] = p.gelu_erf ? gelu_erf_f(b) : gelu_tanh_f(b);
+      break;
+    }
+    case EPI_ADD: {
+      float* o = p.out + (size_t)m * p.os + n;
+      if (p.scale) {
+        a *= p.scale[n];
+        b *= p.scale[n + 1];
+      }
+      o[0] += a;
+      o[1] += b;
+      break;
+    }
+    case EPI_ARGMAX: {  // logits (c0 / ci heads); the packed block arg-max is reduced by the caller
+      float* o = p.out + (size_t)m * p.os + n;
+      o[0] = a;
+      o[1] = b;
+      break;
+    }
+    case EPI_SILU_MUL:  // rows 2j (gate), 2j+1 (up) -> out[j]  (mlx_lm MLP: down(silu(gate)*up))
+      p.out[(size_t)m * p.os + (n >> 1)] = silu_f(a) * b;
+      break;
+    case EPI_QKV: {
+      // rows [q: Hq*hd | k: Hkv*hd | v: Hkv*hd]; RoPE on interleaved pairs (2i, 2i+1)
+      // (attention.py:157-177) from the cos/sin table; K/V appended at pos (KVCache.update_and_fetch)
+      const int qn = p.Hq * p.hd, kn = p.Hkv * p.hd;
+      const int bb = p.rm.b(m), pos = p.rm.pos(m);
+      const int nn = n < qn ? n : (n < qn + kn ? n - qn : n - qn - kn);
+      const int d = nn % p.hd;
+      if (n < qn + kn) {
+        const float2 cs = *reinterpret_cast<const float2*>(p.rope + ((size_t)pos * (p.hd >> 1) + (d >> 1)) * 2);
+        const float y0 = a * cs.x - b * cs.y, y1 = b * cs.x + a * cs.y;
+        a = y0;
+        b = y1;
+      }
+      float* o;
+      if (n < qn) {
+        o = p.out + (size_t)m * p.os + n;
+      } else {
+        float* cache = n < qn + kn ? p.kc : p.vc;
+        o = cache + (((size_t)bb * p.Hkv + nn / p.hd) * p.S_cap + pos) * p.hd + d;
+      }
+      *reinterpret_cast<float2*>(o) = make_float2(a, b);
+      break;
+    }
+  }
+}
 
 struct EmbedParams {
   const int* tok;        // [M][K+1] prompt tokens (or null)
@@ -114,3 +175,17 @@ void launch_sample(const SampleParams& p, int wdt, int B, hipStream_t st);
 void launch_advance(const AdvanceParams& p, hipStream_t st);
 
 void launch_empty(int blocks, int* p, hipStream_t st);
+
+// ---- int4 (q4_kernels.hip)
+// quantize rows [0, n_rows) of a dense [n_rows][K] f32/bf16 device matrix into rows row0 + r*rstep of a
+// quantized matrix with Ntot rows (MLX affine rule; oracle/quant_oracle.py)
+void launch_q4_quantize(const void* src, int src_wdt, int n_rows, int K, void* dst, int Ntot, int row0, int rstep,
+                        hipStream_t st);
+// MLX scales / biases [n_rows][K/64] (f32 or bf16, device) -> sb words of rows row0 + r*rstep
+void launch_q4_set_sb(const void* sc, const void* bi, int src_wdt, int n_rows, int K, void* dst, int Ntot, int row0,
+                      int rstep, hipStream_t st);
+void launch_q4_to_f32(const void* base, int Ntot, int K, int r0, int n, float* dst, hipStream_t st);
+void launch_embed_q4(const EmbedParams& p, int n_text_rows, int M, hipStream_t st);
+void launch_gemv_q4(const GemvParams& p, bool nt, hipStream_t st);
+int gemv_q4_rows_per_block(int N, int K, int M);
+bool gemv_q4_supported(int N, int K);

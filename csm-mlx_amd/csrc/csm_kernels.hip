@@ -69,65 +69,6 @@ __global__ __launch_bounds__(256) void embed_rows_kernel(EmbedParams p) {
 // the 16-67 MB projections.  NORM fuses RMSNorm of x (weight nw) as a per-row scale applied
 // after the reduction; the epilogue (store / residual add / SiLU*up / GELU / RoPE + KV append)
 // runs on row pairs so RoPE pairs and interleaved gate/up rows stay in one thread.
-__device__ void gemv_epilogue_pair(const GemvParams& p, int m, int n, float a, float b) {
-  switch (p.epi) {
-    case EPI_STORE: {
-      float* o = p.out + (size_t)m * p.os + n;
-      o[0] = a;
-      o[1] = b;
-      break;
-    }
-    case EPI_GELU: {
-      float* o = p.out + (size_t)m * p.os + n;
-      o[0] = p.gelu_erf ? gelu_erf_f(a) : gelu_tanh_f(a);
-      o[1] = p.gelu_erf ? gelu_erf_f(b) : gelu_tanh_f(b);
-      break;
-    }
-    case EPI_ADD: {
-      float* o = p.out + (size_t)m * p.os + n;
-      if (p.scale) {
-        a *= p.scale[n];
-        b *= p.scale[n + 1];
-      }
-      o[0] += a;
-      o[1] += b;
-      break;
-    }
-    case EPI_ARGMAX: {  // logits (c0 / ci heads); the packed block arg-max is reduced by the caller
-      float* o = p.out + (size_t)m * p.os + n;
-      o[0] = a;
-      o[1] = b;
-      break;
-    }
-    case EPI_SILU_MUL:  // rows 2j (gate), 2j+1 (up) -> out[j]  (mlx_lm MLP: down(silu(gate)*up))
-      p.out[(size_t)m * p.os + (n >> 1)] = silu_f(a) * b;
-      break;
-    case EPI_QKV: {
-      // rows [q: Hq*hd | k: Hkv*hd | v: Hkv*hd]; RoPE on interleaved pairs (2i, 2i+1)
-      // (attention.py:157-177) from the cos/sin table; K/V appended at pos (KVCache.update_and_fetch)
-      const int qn = p.Hq * p.hd, kn = p.Hkv * p.hd;
-      const int bb = p.rm.b(m), pos = p.rm.pos(m);
-      const int nn = n < qn ? n : (n < qn + kn ? n - qn : n - qn - kn);
-      const int d = nn % p.hd;
-      if (n < qn + kn) {
-        const float2 cs = *reinterpret_cast<const float2*>(p.rope + ((size_t)pos * (p.hd >> 1) + (d >> 1)) * 2);
-        const float y0 = a * cs.x - b * cs.y, y1 = b * cs.x + a * cs.y;
-        a = y0;
-        b = y1;
-      }
-      float* o;
-      if (n < qn) {
-        o = p.out + (size_t)m * p.os + n;
-      } else {
-        float* cache = n < qn + kn ? p.kc : p.vc;
-        o = cache + (((size_t)bb * p.Hkv + nn / p.hd) * p.S_cap + pos) * p.hd + d;
-      }
-      *reinterpret_cast<float2*>(o) = make_float2(a, b);
-      break;
-    }
-  }
-}
-
 template <typename WT, int G, int RPT, int MT, int TAG>
 __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
   constexpr int NG = 256 / G;
@@ -1011,7 +952,9 @@ void launch_gemv(const GemvParams& p0, int wdt, int epi, int norm, hipStream_t s
   p.epi = epi;
   if (!norm) p.nw = nullptr;
   const bool nt = (gemv_nt_mask() >> tag) & 1;
-  if (wdt == WDT_BF16) {
+  if (wdt == WDT_Q4) {
+    launch_gemv_q4(p, nt, st);
+  } else if (wdt == WDT_BF16) {
     if (tag == 1) nt ? launch_gemv_t<bf16_t, 5>(p, st) : launch_gemv_t<bf16_t, 1>(p, st);
     else if (tag == 2) nt ? launch_gemv_t<bf16_t, 6>(p, st) : launch_gemv_t<bf16_t, 2>(p, st);
     else nt ? launch_gemv_t<bf16_t, 4>(p, st) : launch_gemv_t<bf16_t, 0>(p, st);

@@ -37,7 +37,9 @@ enum csm_status {
   CSM_ERR_TOO_LONG = -4   /* prompt + frames exceed the 2048-position window (generation.py:132-137) */
 };
 
-enum csm_dtype { CSM_F32 = 0, CSM_BF16 = 1 };
+/* CSM_Q4: MLX affine int4, group 64 (nn.quantize(model, 64, 4)); as a host source dtype, CSM_U32 marks
+ * MLX-packed int4 weights (8 nibbles per uint32, element j at bits 4*(j%8)). */
+enum csm_dtype { CSM_F32 = 0, CSM_BF16 = 1, CSM_Q4 = 2, CSM_U32 = 3 };
 
 typedef struct csm_llama_dims {
   int n_layers, hidden, n_heads, n_kv_heads, head_dim, intermediate;
@@ -55,7 +57,10 @@ typedef struct csm_engine csm_engine;
 const char* csm_last_error(void);
 int csm_device_count(int* n);
 
-/* weight_dtype: storage of every Linear/Embedding weight (CSM_F32 parity mode, CSM_BF16 perf). */
+/* weight_dtype: storage of every Linear/Embedding weight (CSM_F32 parity mode, CSM_BF16 perf, CSM_Q4 int4
+ * g64: float weights loaded into it are quantized on the device; MLX-quantized checkpoints load as
+ * <name>.weight (CSM_U32 [n][K/8]) + <name>.scales + <name>.biases ([n][K/64] f32 or bf16)).
+ * audio_head is never quantized (bf16 in a CSM_Q4 engine). */
 int csm_engine_create(const csm_dims* dims, int device, int weight_dtype, int max_batch, int max_frames,
                       csm_engine** out);
 int csm_engine_destroy(csm_engine* e);
@@ -66,6 +71,10 @@ int csm_load_tensor(csm_engine* e, const char* name, const void* host, int src_d
 int csm_set_rope_table(csm_engine* e, int which, const float* table, int n_pos, int head_dim);
 /* returns CSM_ERR_STATE and names the first missing tensor when weights are incomplete */
 int csm_weights_ready(csm_engine* e);
+/* nn.quantize(model, group_size, bits) (run_streaming_csm_mlx.py:811-818; README.md:108-111): convert every
+ * loaded Linear / Embedding weight to int4 in place (MLX affine rule, oracle/quant_oracle.py).  Only
+ * group_size 64, bits 4.  audio_head and the norms keep their dtype. */
+int csm_quantize(csm_engine* e, int group_size, int bits);
 
 /* Start a batch of B utterances.  temperature 0 = greedy (generation.py:51); top_k 0 = off.
  * seeds[B]: per-utterance sampling seeds (build's counter-based Gumbel sampler). */
@@ -78,7 +87,9 @@ int csm_run_frames(csm_engine* e, int nframes, int* all_done);
 /* hist [F][B][K] int32 of the frames generated so far, n_frames[B] emitted frames (EOS excluded),
  * done[B].  Any pointer may be NULL. */
 int csm_read_codes(csm_engine* e, int32_t* hist, int32_t* n_frames, uint8_t* done, int* frames_run);
-/* Debug / parity taps: "h_last" [B][D], "c0_logits" [B][Vpad], "ci_logits" [K-1][B][Vpad], "codes" [B][K] */
+/* Debug / parity taps: "h_last" [B][D], "c0_logits" [B][Vpad], "ci_logits" [K-1][B][Vpad], "codes" [B][K],
+ * "weight:<MLX name>" a whole (unfused) Linear / Embedding matrix in its device layout (int4: nibbles
+ * [N][K/2] then {scale, bias} bf16 pairs [N][K/64]). */
 int csm_debug_read(csm_engine* e, const char* what, void* host, int64_t nbytes, int64_t* needed);
 /* Device pointer of the code history [F][B][K] (for on-device Mimi decode) */
 int csm_codes_device_ptr(csm_engine* e, void** dev_ptr);

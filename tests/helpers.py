@@ -15,9 +15,15 @@ def csm_weights(args_key, seed=0):
     return args, synthetic_csm_weights(args, seed)
 
 
-def oracle_for(args, weights, bf16=False):
+def oracle_for(args, weights, bf16=False, q4=False):
+    """bf16: every weight rounded to bf16 (CSM dtype "bf16").  q4: nn.quantize'd CSM (dtype "q4"):
+    Linear / Embedding weights quantize->dequantize (oracle/quant_oracle.py), audio_head bf16."""
     from oracle.csm_oracle import OracleCSM
+    from oracle.quant_oracle import quantize_dequantize_weights
     w = {k: bf16_round(v) for k, v in weights.items()} if bf16 else weights
+    if q4:
+        w = quantize_dequantize_weights(weights)
+        w["audio_head"] = bf16_round(weights["audio_head"])
     return OracleCSM(args, w, BB[args.backbone_name], DC[args.decoder_name])
 
 
