@@ -236,11 +236,8 @@ void embed(csm_engine* e, const EmbedParams& ep, int M, hipStream_t st) {
   else launch_embed(ep, e->wdt, M, st);
 }
 
-// GEMV rows per block for an (N, K) matrix of the given storage dtype (arg-max partial counts)
-int head_blocks(int N, int K, int M, int wdt) {
-  const int rpb = wdt == WDT_Q4 ? gemv_q4_rows_per_block(N, K, M) : gemv_rows_per_block(N, K, M);
-  return (N + rpb - 1) / rpb;
-}
+// arg-max partial slots per row of a head launch (GEMV or MFMA path, dense or int4)
+int head_blocks(int N, int K, int M, int wdt) { return gemv_partials(N, K, M, wdt); }
 
 void enqueue_body(csm_engine* e, hipStream_t st) {
   const int B = e->B;
@@ -279,13 +276,30 @@ void enqueue_head(csm_engine* e, hipStream_t st) {
     g.W = e->proj; g.N = Dd; g.K = D; g.x = e->h_last; g.xs = D; g.M = M; g.out = e->dx; g.os = Dd;
     g.xpart = part(i - 1); g.xpart_stride = e->part_stride; g.xpart_n = greedy ? (i == 1 ? n0 : ni) : 1;
     g.xtab = e->audio_emb; g.xV = V; g.xcb = i - 1; g.x_step1 = (i == 1); g.x_codes = e->codes; g.x_codes_K = K;
-    g.xtab_q4_rows = V * K;
+    g.xtab_q4_rows = e->wdt == WDT_Q4 ? V * K : 0;
     const bool folded = i >= 2 && e->proj_tab && e->fold_proj;
-    if (!folded) launch_gemv(g, e->wdt, EPI_STORE, 0, st);
     GemvParams g0 = g;  // steps >= 2: layer 0 gathers projection(E_a[c]) from the folded table
-    g0.xtab = e->proj_tab; g0.xtab_f32 = 1;
+    g0.xtab = e->proj_tab; g0.xtab_f32 = 1; g0.xtab_q4_rows = 0;
     RowMap rm = (i == 1) ? RowMap{2, 0, nullptr, 0} : RowMap{1, 0, nullptr, i};
-    run_stack(e, e->dec, e->dx, M, e->dq, e->datt, e->dmlp, rm, st, folded ? &g0 : nullptr);
+    if (gemm_mfma_eligible(Dd, D, M, e->wdt) || gemm_mfma_eligible(e->dec.qkv_rows(), Dd, M, e->wdt)) {
+      // batched: materialise the gathered rows densely, then every projection runs on the matrix cores
+      if (!folded) {
+        GemvParams gr = g;
+        gr.K = D; gr.out = e->din; gr.os = D;
+        launch_gather_rows(gr, e->wdt, st);
+        GemvParams gp = GemvParams{};
+        gp.W = e->proj; gp.N = Dd; gp.K = D; gp.x = e->din; gp.xs = D; gp.M = M; gp.out = e->dx; gp.os = Dd;
+        launch_gemv(gp, e->wdt, EPI_STORE, 0, st);
+      } else {
+        GemvParams gr = g0;
+        gr.K = Dd; gr.out = e->dx; gr.os = Dd;
+        launch_gather_rows(gr, e->wdt, st);
+      }
+      run_stack(e, e->dec, e->dx, M, e->dq, e->datt, e->dmlp, rm, st, nullptr);
+    } else {
+      if (!folded) launch_gemv(g, e->wdt, EPI_STORE, 0, st);
+      run_stack(e, e->dec, e->dx, M, e->dq, e->datt, e->dmlp, rm, st, folded ? &g0 : nullptr);
+    }
     // ci_logits = norm(hidden[:, -1]) @ audio_head[i-1]  (generation.py:79)
     g = GemvParams{};
     g.W = (const char*)e->audio_head + (size_t)(i - 1) * Vp * Dd * (e->head_wdt == WDT_F32 ? 4 : 2); g.N = Vp; g.K = Dd;
@@ -353,6 +367,15 @@ void ensure_batch(csm_engine* e, int B) {
   // partial slots per row: enough for any head tiling (c0 / ci heads, dense or q4; >= Vp/2 blocks never occur)
   e->part_stride = (int)(Vp / 2);
   e->part = (unsigned long long*)e->balloc(K * Bm * (size_t)e->part_stride * 8);
+  // split-K scratch of the MFMA path for every projection shape at its largest row count
+  for (Stack* s : {&e->bb, &e->dec}) {
+    const int Dm = s->d.hidden, F = s->d.intermediate, rows = (s == &e->bb) ? std::max(e->M_cap, (int)Bm) : 2 * (int)Bm;
+    gemm_reserve(s->qkv_rows(), Dm, rows);
+    gemm_reserve(Dm, s->q_dim(), rows);
+    gemm_reserve(2 * F, Dm, rows);
+    gemm_reserve(Dm, F, rows);
+  }
+  gemm_reserve((int)Dd, (int)D, 2 * (int)Bm);
 }
 
 // proj_tab[cb] = projection(E_a rows of codebook cb), computed by the projection GEMV itself

@@ -39,6 +39,10 @@ struct GemvParams {
   int xtab_f32;         // gathered table rows are fp32 (else the weight type)
   int xtab_q4_rows;     // int4 weights: total rows of the (quantized) gathered table
   float* x_copy;        // if set: block 0 also stores the raw (un-normed) x rows here [M][K]
+  // MFMA path split-K (set by launch_gemm_mfma): slice partials [ksplit][M][N], sum-of-squares [ksplit][M]
+  float* kpart;          // [tile][m chunk][slice][64][33] slice partials (+ sum x^2), written sc1
+  unsigned* kticket;     // [tile][m chunk] arrival tickets (zero between launches)
+  int ksplit;
 };
 
 __device__ __forceinline__ unsigned long long pack_argmax(float v, int idx) {
@@ -189,3 +193,14 @@ void launch_embed_q4(const EmbedParams& p, int n_text_rows, int M, hipStream_t s
 void launch_gemv_q4(const GemvParams& p, bool nt, hipStream_t st);
 int gemv_q4_rows_per_block(int N, int K, int M);
 bool gemv_q4_supported(int N, int K);
+
+// ---- batched projections on MFMA (gemm_kernels.hip)
+constexpr int GEMM_MFMA_MIN_M = 8;  // rows at which a bf16 projection leaves the GEMV for the matrix cores
+bool gemm_mfma_eligible(int N, int K, int M, int wdt);
+int gemm_blocks(int N);  // row-tile blocks (= arg-max partials per row)
+void launch_gemm_mfma(const GemvParams& p, bool nt, hipStream_t st);
+void gemm_reserve(int N, int K, int M);  // pre-size the split-K scratch (outside graph capture)
+// dense decoder-input rows from a table (codes resolved from arg-max partials), see gather_rows_kernel
+void launch_gather_rows(const GemvParams& p, int wdt, hipStream_t st);
+// arg-max partial slots per row written by launch_gemv for this shape / dtype / row count
+int gemv_partials(int N, int K, int M, int wdt);

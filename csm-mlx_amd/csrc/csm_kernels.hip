@@ -928,6 +928,12 @@ static void launch_gemv_t(const GemvParams& p, hipStream_t st) {
 #undef GEMV_L
 }
 
+int gemv_partials(int N, int K, int M, int wdt) {
+  if (gemm_mfma_eligible(N, K, M, wdt)) return gemm_blocks(N);
+  const int rpb = wdt == WDT_Q4 ? gemv_q4_rows_per_block(N, K, M) : gemv_rows_per_block(N, K, M);
+  return (N + rpb - 1) / rpb;
+}
+
 int gemv_rows_per_block(int N, int K, int M) {
   int G, RPT;
   gemv_tiling(N, K, M, G, RPT);
@@ -952,7 +958,9 @@ void launch_gemv(const GemvParams& p0, int wdt, int epi, int norm, hipStream_t s
   p.epi = epi;
   if (!norm) p.nw = nullptr;
   const bool nt = (gemv_nt_mask() >> tag) & 1;
-  if (wdt == WDT_Q4) {
+  if (!p.xpart && !p.x_copy && gemm_mfma_eligible(p.N, p.K, p.M, wdt)) {
+    launch_gemm_mfma(p, nt, st);
+  } else if (wdt == WDT_Q4) {
     launch_gemv_q4(p, nt, st);
   } else if (wdt == WDT_BF16) {
     if (tag == 1) nt ? launch_gemv_t<bf16_t, 5>(p, st) : launch_gemv_t<bf16_t, 1>(p, st);
