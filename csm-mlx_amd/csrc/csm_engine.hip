@@ -79,6 +79,12 @@ struct csm_engine {
   // input row from it instead of running the projection GEMV.
   float* proj_tab = nullptr;
   bool proj_tab_dirty = true;
+  // decoder layer 0's QKV folded too: qkv0_tab[cb][code] = RoPE'd (q, k | v) of layer 0 for input row
+  // proj_tab[cb][code] at position cb + 1 (fp32, built by the same QKV GEMV); codebook steps >= 2 then
+  // skip layer 0's QKV launch and its attention gathers the row (AttnParams::g_tab).
+  float* qkv0_tab = nullptr;
+  bool use_qkv0_tab = true;  // csm_set_option "qkv0_tab"
+  bool qkv0_built = false;
   std::set<std::string> loaded;
   std::vector<std::string> required;
   // activations
@@ -188,7 +194,7 @@ int ablate() {
 // gather0: x-gather fields for layer 0's QKV GEMV (its input rows come from a table; the GEMV also
 // writes them to x as the residual stream).
 void run_stack(csm_engine* e, Stack& s, float* x, int M, float* q, float* att, float* mlp, const RowMap& rm,
-               hipStream_t st, const GemvParams* gather0 = nullptr) {
+               hipStream_t st, const GemvParams* gather0 = nullptr, const AttnParams* attn0 = nullptr) {
   const csm_llama_dims& d = s.d;
   const int tag = (&s == &e->dec) ? 1 : 0;
   const int D = d.hidden, F = d.intermediate, hd = d.head_dim, Hq = d.n_heads, Hkv = d.n_kv_heads;
@@ -205,15 +211,16 @@ void run_stack(csm_engine* e, Stack& s, float* x, int M, float* q, float* att, f
       g.xtab = gather0->xtab; g.xtab_f32 = gather0->xtab_f32; g.xV = gather0->xV; g.xcb = gather0->xcb;
       g.x_codes = gather0->x_codes; g.x_codes_K = gather0->x_codes_K; g.x_copy = x;
     }
-    if (!(ab & 2)) launch_gemv(g, e->wdt, EPI_QKV, 1, st, tag);
+    const bool gathered = (i == 0 && attn0);  // layer 0 QKV from the folded table (attention gathers it)
+    if (!(ab & 2) && !gathered) launch_gemv(g, e->wdt, EPI_QKV, 1, st, tag);
     // attention (+ o_proj + residual fused for the short depth-decoder KV)
-    AttnParams a{};
+    AttnParams a = gathered ? *attn0 : AttnParams{};
     a.q = q; a.qs = s.q_dim(); a.M = M; a.kc = l.kc; a.vc = l.vc; a.Hq = Hq; a.Hkv = Hkv; a.S_cap = s.S_cap;
     a.scale = 1.0f / sqrtf((float)hd); a.mode = ATTN_CAUSAL; a.window = 0; a.rm = rm; a.out = att;
     a.os = s.q_dim();
     g = GemvParams{};
     g.W = l.wo; g.N = D; g.K = s.q_dim(); g.x = att; g.xs = s.q_dim(); g.M = M; g.out = x; g.os = D;
-    if (tag == 1 && e->fuse_attn && !(ab & 5) && dec_attn_oproj_supported(g, a, hd)) {
+    if (tag == 1 && e->fuse_attn && !gathered && !(ab & 5) && dec_attn_oproj_supported(g, a, hd)) {
       launch_dec_attn_oproj(g, a, e->wdt, st, tag);
     } else {
       if (!(ab & 1)) launch_attn(a, hd, st);
@@ -296,6 +303,13 @@ void enqueue_head(csm_engine* e, hipStream_t st) {
         launch_gather_rows(gr, e->wdt, st);
       }
       run_stack(e, e->dec, e->dx, M, e->dq, e->datt, e->dmlp, rm, st, nullptr);
+    } else if (folded && e->use_qkv0_tab && e->qkv0_built) {
+      AttnParams a0{};
+      a0.g_tab = e->qkv0_tab + (size_t)(i - 1) * V * e->dec.qkv_rows(); a0.g_row = e->dec.qkv_rows();
+      a0.g_part = g.xpart; a0.g_part_stride = g.xpart_stride; a0.g_part_n = g.xpart_n; a0.g_V = V;
+      a0.g_codes = e->codes; a0.g_codes_K = K; a0.g_cb = i - 1;
+      a0.g_xtab = e->proj_tab + (size_t)(i - 1) * V * Dd; a0.g_xout = e->dx; a0.g_D = Dd;
+      run_stack(e, e->dec, e->dx, M, e->dq, e->datt, e->dmlp, rm, st, nullptr, &a0);
     } else {
       if (!folded) launch_gemv(g, e->wdt, EPI_STORE, 0, st);
       run_stack(e, e->dec, e->dx, M, e->dq, e->datt, e->dmlp, rm, st, folded ? &g0 : nullptr);
@@ -394,6 +408,22 @@ void build_proj_table(csm_engine* e) {
   HIPCHK(hipStreamSynchronize(e->st));
   HIPCHK(hipGetLastError());
   e->proj_tab_dirty = false;
+  // layer-0 QKV of every folded decoder input row, by the frame's own QKV GEMV (4 rows per launch:
+  // per-row arithmetic identical to the 1-row launch of the frame)
+  const Stack& s = e->dec;
+  const LayerW& l0 = s.L[0];
+  for (int cb = 1; cb < e->K - 1; ++cb)
+    for (int m0 = 0; m0 < V; m0 += 4) {
+      GemvParams g{};
+      g.W = l0.wqkv; g.N = s.qkv_rows(); g.K = Dd; g.x = e->proj_tab + ((size_t)cb * V + m0) * Dd; g.xs = Dd;
+      g.M = std::min(4, V - m0); g.nw = l0.n1; g.eps = s.d.eps; g.Hq = s.d.n_heads; g.Hkv = s.d.n_kv_heads;
+      g.hd = s.d.head_dim; g.S_cap = s.S_cap; g.rope = s.rope; g.rm = RowMap{1, 0, nullptr, cb + 1};
+      g.qkv_tab = e->qkv0_tab + ((size_t)cb * V + m0) * s.qkv_rows();
+      launch_gemv(g, e->wdt, EPI_QKV, 1, e->st, 1);
+    }
+  HIPCHK(hipStreamSynchronize(e->st));
+  HIPCHK(hipGetLastError());
+  e->qkv0_built = true;
 }
 
 
@@ -573,6 +603,7 @@ int csm_engine_create(const csm_dims* dims, int device, int weight_dtype, int ma
     e->c0_head = e->alloc(e->wbytes(Vp, D));
     e->audio_head = e->alloc((K - 1) * Vp * Dd * (e->head_wdt == WDT_F32 ? 4 : 2));
     e->proj_tab = (float*)e->alloc((K - 1) * (size_t)e->V * Dd * 4);
+    e->qkv0_tab = (float*)e->alloc((K - 1) * (size_t)e->V * e->dec.qkv_rows() * 4);
     for (const char* n : {"text_embeddings.weight", "audio_embeddings.weight", "projection.weight",
                           "codebook0_head.weight", "audio_head"})
       e->required.push_back(n);
@@ -620,6 +651,7 @@ int csm_load_tensor(csm_engine* e, const char* cname, const void* host, int src_
     auto expect = [&](std::initializer_list<int64_t> want) {
       if (shp != std::vector<int64_t>(want)) throw CsmError(CSM_ERR_ARG, "shape mismatch for " + name);
     };
+    if (name.rfind("decoder.layers.0.", 0) == 0) e->proj_tab_dirty = true;  // feeds the folded layer-0 QKV table
     if (e->wdt == WDT_Q4 && load_q4(e, name, host, src_dtype, shp)) return CSM_OK;
     if (src_dtype == CSM_U32) throw CsmError(CSM_ERR_ARG, "packed int4 tensor " + name + " needs a CSM_Q4 engine");
     const size_t es = e->wsz;
@@ -1033,6 +1065,10 @@ int csm_set_option(csm_engine* e, const char* key, int value) {
     else if (k == "fold_proj") {
       if (!e) throw CsmError(CSM_ERR_ARG, "fold_proj needs an engine");
       e->fold_proj = value != 0;
+    }
+    else if (k == "qkv0_tab") {
+      if (!e) throw CsmError(CSM_ERR_ARG, "qkv0_tab needs an engine");
+      e->use_qkv0_tab = value != 0;
     }
     else throw CsmError(CSM_ERR_ARG, "unknown option " + k);
     if (e) e->g_B = -1;  // re-capture the frame graphs with the new setting

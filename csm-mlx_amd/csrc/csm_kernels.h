@@ -39,6 +39,7 @@ struct GemvParams {
   int xtab_f32;         // gathered table rows are fp32 (else the weight type)
   int xtab_q4_rows;     // int4 weights: total rows of the (quantized) gathered table
   float* x_copy;        // if set: block 0 also stores the raw (un-normed) x rows here [M][K]
+  float* qkv_tab;       // EPI_QKV table build: rows [M][(Hq + 2 Hkv) hd] instead of q / KV cache
   // MFMA path split-K (set by launch_gemm_mfma): slice partials [ksplit][M][N], sum-of-squares [ksplit][M]
   float* kpart;          // [tile][m chunk][slice][64][33] slice partials (+ sum x^2), written sc1
   unsigned* kticket;     // [tile][m chunk] arrival tickets (zero between launches)
@@ -100,7 +101,9 @@ __device__ __forceinline__ void gemv_epilogue_pair(const GemvParams& p, int m, i
         b = y1;
       }
       float* o;
-      if (n < qn) {
+      if (p.qkv_tab) {  // table build: the whole (RoPE'd q, k | v) row of row m
+        o = p.qkv_tab + (size_t)m * (qn + 2 * kn) + n;
+      } else if (n < qn) {
         o = p.out + (size_t)m * p.os + n;
       } else {
         float* cache = n < qn + kn ? p.kc : p.vc;
@@ -134,6 +137,20 @@ struct AttnParams {
   RowMap rm;
   float* out;
   int os;
+  // Decoder layer 0 at codebook steps >= 2 (g_tab != null): the step's QKV rows are not computed but
+  // gathered -- g_tab[code] = RoPE'd (q, k | v) of layer 0 for decoder input row proj_tab[cb][code]
+  // (built at csm_begin by the QKV GEMV itself).  code = arg-max of the head partials g_part; the
+  // block writes its kv head's K/V row at pos into the cache, kv head 0's block also writes
+  // codes[b][g_cb] and the residual row g_xtab[code] -> g_xout[m].
+  const float* g_tab;
+  int g_row;  // floats per g_tab row = (Hq + 2 Hkv) * hd
+  const unsigned long long* g_part;
+  int g_part_stride, g_part_n, g_V;
+  int* g_codes;
+  int g_codes_K, g_cb;
+  const float* g_xtab;
+  float* g_xout;
+  int g_D;
 };
 
 struct SampleParams {

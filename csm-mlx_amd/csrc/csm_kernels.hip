@@ -238,14 +238,15 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
 // LDS once, reducing sum(x^2) per row once per block, (3) runs the dot products from LDS.  Per
 // thread the weight K-slices, accumulation order and pair epilogues are those of gemv_kernel.
 constexpr int XL_KMAX = 2048;
+constexpr int XL_KMAX_WIDE = 8192;  // down projections (K = 8192) at M = 1: 32 KB of LDS
 
-template <typename WT, int G, int RPT, int MT, int TAG>
+template <typename WT, int G, int RPT, int MT, int TAG, int KMAX = XL_KMAX>
 __global__ __launch_bounds__(256) void gemv_xl_kernel(GemvParams p) {
   constexpr int NG = 256 / G;
   constexpr int RPB = NG * RPT;
-  constexpr int NKM = XL_KMAX / (G * 8);  // K-steps per thread at most
+  constexpr int NKM = KMAX / (G * 8);  // K-steps per thread at most
   constexpr bool NT = (TAG & 4) != 0;
-  __shared__ __attribute__((aligned(16))) float xl[MT][XL_KMAX];
+  __shared__ __attribute__((aligned(16))) float xl[MT][KMAX];
   __shared__ float red[4][MT][RPT];
   __shared__ float rss[4][MT];
   __shared__ int gcode[MT];
@@ -502,6 +503,42 @@ __device__ __forceinline__ void attn_block(const AttnParams& p, int m, int kvh, 
     k0 = max(0, off - p.window);
     k1 = off + p.rm.T - 1;
   }
+  const float* qrow = p.q + (size_t)m * p.qs;
+  if (p.g_tab) {  // decoder layer 0, steps >= 2: gather this row's QKV from the layer-0 table
+    __shared__ int gcode;
+    if (wave == 0) {
+      unsigned long long best = 0;
+      for (int i = lane; i < p.g_part_n; i += 64) {
+        const unsigned long long v = p.g_part[(size_t)b * p.g_part_stride + i];
+        best = v > best ? v : best;
+      }
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long v = __shfl_xor(best, o, 64);
+        best = v > best ? v : best;
+      }
+      if (lane == 0) gcode = min(max(unpack_argmax(best), 0), p.g_V - 1);
+    }
+    __syncthreads();
+    const int c = gcode;
+    const float* trow = p.g_tab + (size_t)c * p.g_row;
+    qrow = trow;
+    const int qd = p.Hq * HD, kvd = p.Hkv * HD;
+    float* kd = const_cast<float*>(p.kc) + (((size_t)b * p.Hkv + kvh) * p.S_cap + pos) * HD;
+    float* vd = const_cast<float*>(p.vc) + (((size_t)b * p.Hkv + kvh) * p.S_cap + pos) * HD;
+    for (int d = tid; d < HD; d += 256) {
+      kd[d] = trow[qd + kvh * HD + d];
+      vd[d] = trow[qd + kvd + kvh * HD + d];
+    }
+    if (kvh == 0) {
+      if (tid == 0) p.g_codes[(size_t)b * p.g_codes_K + p.g_cb] = c;
+      const float* xs = p.g_xtab + (size_t)c * p.g_D;
+      float* xo = p.g_xout + (size_t)m * p.g_D;
+      for (int d = tid * 4; d < p.g_D; d += 256 * 4)
+        *reinterpret_cast<float4*>(xo + d) = *reinterpret_cast<const float4*>(xs + d);
+    }
+    __syncthreads();  // the K/V row at pos is visible to this block's fetches below
+  }
   const float* K = p.kc + ((size_t)b * p.Hkv + kvh) * p.S_cap * HD;
   const float* V = p.vc + ((size_t)b * p.Hkv + kvh) * p.S_cap * HD;
   // chunk loads through registers; rows past the live range re-read the last live row (always a
@@ -520,7 +557,7 @@ __device__ __forceinline__ void attn_block(const AttnParams& p, int m, int kvh, 
   };
   fetch(k0);  // first chunk in flight together with q
   if (head_ok) {
-    const float* q = p.q + (size_t)m * p.qs + h * HD;
+    const float* q = qrow + h * HD;
     for (int d = lane; d < HD; d += 64) L.qs[wave][d] = q[d] * p.scale;
   }
   constexpr int NO = HD / 64;
@@ -893,7 +930,10 @@ void gemv_set_override(int G, int RPT) {
 // row group (G = 64: no cross-wave reduction, 2-4 K-steps per thread); the K = 8192 down
 // projections want the whole block on a row pair (G = 256 at N = 1024, 128 at N = 2048); every
 // other shape is latency-bound and best at G = 128 (K >= 1024).  RPT = 2 wins everywhere at M = 1.
-static int g_gemv_xl = 1;  // LDS-staged activations for the decode regime (gemv_xl_kernel)
+// LDS-staged activations for the decode regime (gemv_xl_kernel): 1 = on for K <= 2048, 3 = also the
+// K = 8192 down projections (measured slower: dec down 5.96 vs 5.77 us, 231.6 vs 234.8 frames/s),
+// 0 = off.  CSM_GEMV_XL overrides the default (A/B runs).
+static int g_gemv_xl = [] { const char* e = getenv("CSM_GEMV_XL"); return e ? atoi(e) : 1; }();
 void gemv_set_xl(int on) { g_gemv_xl = on; }
 
 static void gemv_tiling(int N, int K, int M, int& G, int& RPT) {
@@ -913,6 +953,17 @@ static void launch_gemv_t(const GemvParams& p, hipStream_t st) {
   const int blocks = p.N / ((256 / G) * RPT);
   const bool mt1 = p.M == 1;
   const bool xl = g_gemv_xl && p.M <= 4 && p.K <= XL_KMAX && p.K % 8 == 0;
+  // K = 8192 at M = 1 (down projections): LDS-staged x, every weight K-step in flight first
+  const bool xlw = (g_gemv_xl & 2) != 0 && mt1 && p.K > XL_KMAX && p.K <= XL_KMAX_WIDE && p.K % 8 == 0 &&
+                   G >= 128;
+  if (xlw && G == 256 && RPT == 2) {
+    hipLaunchKernelGGL((gemv_xl_kernel<WT, 256, 2, 1, TAG, XL_KMAX_WIDE>), dim3(blocks), dim3(256), 0, st, p);
+    return;
+  }
+  if (xlw && G == 128 && RPT == 2) {
+    hipLaunchKernelGGL((gemv_xl_kernel<WT, 128, 2, 1, TAG, XL_KMAX_WIDE>), dim3(blocks), dim3(256), 0, st, p);
+    return;
+  }
 #define GEMV_L(G_, R_, M_)                                                                            \
   do {                                                                                                \
     if (xl) hipLaunchKernelGGL((gemv_xl_kernel<WT, G_, R_, M_, TAG>), dim3(blocks), dim3(256), 0, st, p); \

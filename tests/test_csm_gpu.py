@@ -188,3 +188,27 @@ def test_fused_decoder_attention_matches_two_launches(tiny, which, dtype, batch,
         assert np.array_equal(n_got, n_ref)
         assert np.array_equal(got, ref), f"first diff at {np.argwhere(got != ref)[0]}"
     del model
+
+
+@pytest.mark.parametrize("which,dtype", [("tiny", "float32"), ("tiny", "bf16"), ("1b", "bf16")])
+def test_folded_layer0_qkv_table_matches_gemv(tiny, which, dtype):
+    """Decoder steps >= 2 gather layer 0's (RoPE'd q, k | v) from the table built at csm_begin by the
+    same QKV GEMV: codes must be bit-identical to running the GEMV every step."""
+    from csm_mlx import _lib
+    from csm_mlx.generation import generate_codes_batch
+    from csm_mlx.sampling import Sampler
+    from csm_mlx.tokenizers import tokenize_text_segment
+    args, w = tiny if which == "tiny" else csm_weights("1b")
+    model = _model(args, w, dtype, max_batch=2)
+    K = args.n_audio_codebooks
+    ids = [tiny_prompt_ids(40 + b, 3 + b) if which == "tiny" else prompt_ids(40 + b) for b in range(2)]
+    prompts = [tokenize_text_segment(i, 0, K) for i in ids]
+    L = _lib.lib()
+    frames = 12 if which == "tiny" else 6
+    _lib.check(L.csm_set_option(model.engine, b"qkv0_tab", 0))
+    ref, n_ref, _ = generate_codes_batch(model, prompts, frames, sampler=Sampler(0.0, 0))
+    _lib.check(L.csm_set_option(model.engine, b"qkv0_tab", 1))
+    got, n_got, _ = generate_codes_batch(model, prompts, frames, sampler=Sampler(0.0, 0))
+    assert np.array_equal(n_got, n_ref)
+    assert np.array_equal(got, ref), f"first diff at {np.argwhere(got != ref)[0]}"
+    del model
