@@ -220,7 +220,7 @@ void run_stack(csm_engine* e, Stack& s, float* x, int M, float* q, float* att, f
     a.os = s.q_dim();
     g = GemvParams{};
     g.W = l.wo; g.N = D; g.K = s.q_dim(); g.x = att; g.xs = s.q_dim(); g.M = M; g.out = x; g.os = D;
-    if (tag == 1 && e->fuse_attn && !gathered && !(ab & 5) && dec_attn_oproj_supported(g, a, hd)) {
+    if (tag == 1 && e->fuse_attn && !(ab & 5) && dec_attn_oproj_supported(g, a, hd)) {
       launch_dec_attn_oproj(g, a, e->wdt, st, tag);
     } else {
       if (!(ab & 1)) launch_attn(a, hd, st);

@@ -590,6 +590,137 @@ __device__ __forceinline__ void attn_block(const AttnParams& p, int m, int kvh, 
   }
 }
 
+// Short causal attention (depth decoder: <= 32 cached positions, generation.py:70-77): one wave per
+// (row, q head); lanes (key j, half of the head dims) compute the scores, lane d owns output dims
+// d + 64 i.  Every K half-row and V column slice is loaded up front (16-B / 4-B loads straight to
+// VGPRs) -- one memory round trip instead of attn_block's staged chunk pipeline.  fp32 throughout:
+// scores, softmax (max-subtracted, one pass: all keys fit one wave), P.V in key order.  With g_tab
+// set (decoder layer 0, codebook steps >= 2) the row's q and its key/value at pos come from the
+// folded layer-0 table (see AttnParams).
+template <int HD, int NMAX>
+__device__ __forceinline__ void attn_short_head(const AttnParams& p, int m, int h, int lane, float* qsh,
+                                                float (&o)[HD / 64], bool write_kv, bool write_code, bool copy_res,
+                                                int* code_out) {
+  constexpr int V4 = HD / 4, NO = HD / 64;
+  const int G = p.Hq / p.Hkv, kvh = h / G;
+  const int b = p.rm.b(m), pos = p.rm.pos(m);
+  const int n = pos + 1;
+  const float* K = p.kc + ((size_t)b * p.Hkv + kvh) * p.S_cap * HD;
+  const float* V = p.vc + ((size_t)b * p.Hkv + kvh) * p.S_cap * HD;
+  const bool gath = p.g_tab != nullptr;
+  const int jc = gath ? pos : n;  // keys read from the cache (the gathered row's own key comes from the table)
+  // cached keys / values first (independent of the gathered code).  Scores: lane = (key kj = lane & 31,
+  // half hh = lane >> 5 of the head dims); the two halves' partial dots are added with one shuffle.
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  constexpr int H4 = V4 / 2;
+  const int kj = lane & 31, hh = lane >> 5;
+  f32x4 kr[H4];
+  const int jl = min(kj, max(jc - 1, 0));
+  const f32x4* ksrc = reinterpret_cast<const f32x4*>(K + (size_t)jl * HD + hh * (HD / 2));
+#pragma unroll
+  for (int d4 = 0; d4 < H4; ++d4) kr[d4] = ksrc[d4];
+  float vv[NMAX][NO];
+#pragma unroll
+  for (int j = 0; j < NMAX; ++j)
+#pragma unroll
+    for (int i = 0; i < NO; ++i) vv[j][i] = (j < jc) ? V[(size_t)j * HD + lane + 64 * i] : 0.f;
+  const float* qrow = p.q + (size_t)m * p.qs;
+  if (gath) {
+    unsigned long long best = 0;
+    for (int i = lane; i < p.g_part_n; i += 64) {
+      const unsigned long long v = p.g_part[(size_t)b * p.g_part_stride + i];
+      best = v > best ? v : best;
+    }
+#pragma unroll
+    for (int o2 = 32; o2 > 0; o2 >>= 1) {
+      const unsigned long long v = __shfl_xor(best, o2, 64);
+      best = v > best ? v : best;
+    }
+    const int c = min(max(unpack_argmax(best), 0), p.g_V - 1);
+    if (code_out) *code_out = c;
+    const float* trow = p.g_tab + (size_t)c * p.g_row;
+    qrow = trow;
+    const int qd = p.Hq * HD, kvd = p.Hkv * HD;
+    const float* tk = trow + qd + kvh * HD;
+    const float* tv = trow + qd + kvd + kvh * HD;
+    if (kj == pos) {
+      const f32x4* t4 = reinterpret_cast<const f32x4*>(tk + hh * (HD / 2));
+#pragma unroll
+      for (int d4 = 0; d4 < H4; ++d4) kr[d4] = t4[d4];
+    }
+#pragma unroll
+    for (int j = 0; j < NMAX; ++j)
+      if (j == pos)
+#pragma unroll
+        for (int i = 0; i < NO; ++i) vv[j][i] = tv[lane + 64 * i];
+    if (write_kv && h % G == 0) {  // this kv head's K/V row at pos -> cache (read by the later codebook steps)
+      float* kd = const_cast<float*>(K) + (size_t)pos * HD;
+      float* vd = const_cast<float*>(V) + (size_t)pos * HD;
+      for (int d = lane; d < HD; d += 64) {
+        kd[d] = tk[d];
+        vd[d] = tv[d];
+      }
+    }
+    if (write_code && h == 0 && lane == 0) p.g_codes[(size_t)b * p.g_codes_K + p.g_cb] = c;
+    if (copy_res && h == 0) {
+      const float* xs = p.g_xtab + (size_t)c * p.g_D;
+      float* xo = p.g_xout + (size_t)m * p.g_D;
+      for (int d = lane * 4; d < p.g_D; d += 64 * 4)
+        *reinterpret_cast<float4*>(xo + d) = *reinterpret_cast<const float4*>(xs + d);
+    }
+  }
+  for (int d = lane; d < HD; d += 64) qsh[d] = qrow[h * HD + d] * p.scale;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // scores (fp32), softmax over the n live keys, P.V in key order
+  float s;
+  {
+    const f32x4* qr = reinterpret_cast<const f32x4*>(qsh + hh * (HD / 2));
+    float d0 = 0.f, d1 = 0.f, d2 = 0.f, d3 = 0.f;
+#pragma unroll
+    for (int d4 = 0; d4 < H4; ++d4) {
+      const f32x4 a = kr[d4], q4 = qr[d4];
+      d0 = fmaf(q4.x, a.x, d0);
+      d1 = fmaf(q4.y, a.y, d1);
+      d2 = fmaf(q4.z, a.z, d2);
+      d3 = fmaf(q4.w, a.w, d3);
+    }
+    const float part = (d0 + d1) + (d2 + d3);
+    const float other = __shfl_xor(part, 32, 64);
+    s = hh == 0 ? part + other : other + part;  // half 0 + half 1 on both lanes of a key
+    if (kj >= n) s = -INFINITY;
+  }
+  const float new_m = wave_max(s);
+  const float pj = (kj < n) ? expf(s - new_m) : 0.f;
+  const float l_run = wave_sum(hh == 0 ? pj : 0.f);
+#pragma unroll
+  for (int i = 0; i < NO; ++i) o[i] = 0.f;
+  const int pji = __float_as_int(pj);
+#pragma unroll
+  for (int j = 0; j < NMAX; ++j) {
+    if (j < n) {
+      const float pb = __int_as_float(__builtin_amdgcn_readlane(pji, j));
+#pragma unroll
+      for (int i = 0; i < NO; ++i) o[i] = fmaf(pb, vv[j][i], o[i]);
+    }
+  }
+  const float inv = 1.f / l_run;
+#pragma unroll
+  for (int i = 0; i < NO; ++i) o[i] = o[i] * inv;
+}
+
+template <int HD, int NMAX>
+__global__ __launch_bounds__(64) void attn_short_kernel(AttnParams p) {
+  __shared__ __attribute__((aligned(16))) float qsh[HD];
+  const int m = blockIdx.x / p.Hq, h = blockIdx.x % p.Hq;
+  float o[HD / 64];
+  attn_short_head<HD, NMAX>(p, m, h, threadIdx.x, qsh, o, true, true, true, nullptr);
+  float* out = p.out + (size_t)m * p.os + h * HD;
+#pragma unroll
+  for (int i = 0; i < HD / 64; ++i) out[threadIdx.x + 64 * i] = o[i];
+}
+
 template <int HD>
 __global__ __launch_bounds__(256) void attn_kernel(AttnParams p) {
   __shared__ __attribute__((aligned(16))) AttnLds<HD> L;
@@ -597,120 +728,65 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnParams p) {
 }
 
 // ============================================================================ decoder attention + o_proj
-// The depth decoder attends over <= 32 cached positions (generation.py:70-77: one position per
-// codebook step), ~66K FMAs over <= 64 KB of K/V -- far less than the cost of a kernel boundary
-// plus a latency-bound attention launch.  Every o_proj block therefore recomputes the attention
-// of all heads itself: (1) it puts its o_proj weights in flight, (2) stages q (pre-scaled) and the
-// live K/V rows of every kv head into LDS, (3) runs each (row, head) exactly as attn_block does for
-// a single 64-key chunk (same operation order: bit-identical outputs), writing the attention
-// output into LDS, (4) runs the o_proj GEMV (+ residual) from LDS with gemv_kernel's K-slicing and
-// reduction order (G = 128: bit-identical to the two-launch path for any RPT).  RPT = 8 keeps the
-// grid at N/16 blocks, bounding the redundant attention work.
-constexpr int DA_NMAX = 32;   // cached positions
-constexpr int DA_HKV = 2;     // kv heads
-constexpr int DA_QD = 1024;   // Hq * head_dim
+// The depth decoder attends over <= 32 cached positions (generation.py:70-77).  One launch does the
+// attention of every head AND the o_proj GEMV (+ residual): 8 waves; wave h runs attn_short_head for
+// (row, head h) into LDS (K rows / V columns straight from L2 into VGPRs, one round trip), while the
+// block's o_proj weight rows are already in flight; then the o_proj dot products run from LDS with
+// gemv_xl_kernel's G = 128 K-slicing and reduction order.  Attention and projection arithmetic are
+// those of attn_short_kernel + gemv_xl_kernel, so outputs are bit-identical to the two launches.
+// Every block recomputes the attention (M <= 2 rows x 8 heads x <= 32 keys: ~64 KB of K/V from L2).
+// With g_tab (layer 0, steps >= 2) the residual row is fused: x = proj_tab[cb][code] + o_proj(att).
 constexpr int DA_M = 2;       // rows (decoder step 1: [h_last, c0] rows)
+constexpr int DA_QD = 1024;   // Hq * head_dim
+constexpr int DA_HQ = 8;      // q heads (one wave each)
 
-template <typename WT, int HD, int RPT, int TAG>
-__global__ __launch_bounds__(256) void dec_attn_oproj_kernel(GemvParams p, AttnParams a) {
-  constexpr int G = 128;
-  constexpr int NG = 256 / G;
-  constexpr int RPB = NG * RPT;
-  constexpr int KP = HD + 4;
-  constexpr int V4 = HD / 4;
-  constexpr int NKM = DA_QD / (G * 8);
+template <typename WT, int RPT, int TAG>
+__global__ __launch_bounds__(512) void dec_attn_oproj_kernel(GemvParams p, AttnParams a) {
+  constexpr int HD = 128, G = 128, NG = 512 / G, RPB = NG * RPT, NO = HD / 64;
   constexpr bool NT = (TAG & 4) != 0;
-  __shared__ __attribute__((aligned(16))) float Ks[DA_HKV * DA_NMAX * KP];
-  __shared__ __attribute__((aligned(16))) float Vs[DA_HKV * DA_NMAX * HD];
-  __shared__ __attribute__((aligned(16))) float qs[DA_M][DA_QD];  // q * scale
+  __shared__ __attribute__((aligned(16))) float qsh[DA_HQ][HD];
   __shared__ __attribute__((aligned(16))) float xo[DA_M][DA_QD];  // attention output = o_proj input
-  __shared__ float red[4][DA_M][RPT];
+  __shared__ float red[8][DA_M][RPT];
+  __shared__ int gcode[DA_M];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int grp = tid / G, gt = tid % G;
   const int row0 = blockIdx.x * RPB + grp * RPT;
-  const WT* W = (const WT*)p.W;
-  // (1) o_proj weights in flight
-  Raw8<WT> wr[NKM][RPT];
+  // (1) o_proj weights in flight (K = 1024 = one G*8 step per thread)
+  Raw8<WT> wr[RPT];
 #pragma unroll
-  for (int s = 0; s < NKM; ++s) {
-    const int k = gt * 8 + s * G * 8;
-    if (k < p.K) {
-#pragma unroll
-      for (int r = 0; r < RPT; ++r) wr[s][r].template load<NT>(W + (size_t)(row0 + r) * p.K + k);
-    }
-  }
-  // (2) stage q rows (scaled, as attn_block) and K/V rows [0, n_live) of utterance b(0)
-  const int qd = a.Hq * HD;
-  for (int t = tid; t < p.M * (qd / 4); t += 256) {
-    const int m = t / (qd / 4), c = (t % (qd / 4)) * 4;
-    const float4 v = *reinterpret_cast<const float4*>(a.q + (size_t)m * a.qs + c);
-    *reinterpret_cast<float4*>(&qs[m][c]) = make_float4(v.x * a.scale, v.y * a.scale, v.z * a.scale, v.w * a.scale);
-  }
-  const int b0 = a.rm.b(0);
-  const int n_live = a.rm.pos(p.M - 1) + 1;  // the last row has the largest position
-  const int total = a.Hkv * n_live * V4;
-  for (int t0 = 0; t0 < total; t0 += 256 * 8) {
-    float4 kr[8], vr[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int t = min(t0 + u * 256 + tid, total - 1);  // clamped: always a valid row
-      const int kv = t / (n_live * V4), rem = t % (n_live * V4);
-      const size_t src = (((size_t)b0 * a.Hkv + kv) * a.S_cap + rem / V4) * HD + (rem % V4) * 4;
-      kr[u] = *reinterpret_cast<const float4*>(a.kc + src);
-      vr[u] = *reinterpret_cast<const float4*>(a.vc + src);
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int t = t0 + u * 256 + tid;
-      if (t < total) {
-        const int kv = t / (n_live * V4), rem = t % (n_live * V4);
-        const int j = rem / V4, d4 = rem % V4;
-        *reinterpret_cast<float4*>(&Ks[(kv * DA_NMAX + j) * KP + d4 * 4]) = kr[u];
-        *reinterpret_cast<float4*>(&Vs[(kv * DA_NMAX + j) * HD + d4 * 4]) = vr[u];
-      }
-    }
-  }
-  __syncthreads();
-  // (3) attention, one wave per (row, head): attn_block's single-chunk arithmetic
-  constexpr int NO = HD / 64;
-  for (int idx = wave; idx < p.M * a.Hq; idx += 4) {
+  for (int r = 0; r < RPT; ++r) wr[r].template load<NT>((const WT*)p.W + (size_t)(row0 + r) * p.K + gt * 8);
+  // (2) attention: wave -> (row, head) pairs
+  for (int idx = wave; idx < p.M * a.Hq; idx += 8) {
     const int m = idx / a.Hq, h = idx % a.Hq;
-    const int kv = h / (a.Hq / a.Hkv);
-    const int n = a.rm.pos(m) + 1;
-    float m_run = -INFINITY, l_run = 0.f;
     float o[NO];
+    int c = 0;
+    const bool side = blockIdx.x == 0;  // cache row + code written once
+    attn_short_head<HD, 32>(a, m, h, lane, qsh[wave], o, side, side, false, &c);
 #pragma unroll
-    for (int q = 0; q < NO; ++q) o[q] = 0.f;
-    attn_chunk<HD>(&qs[m][h * HD], &Ks[kv * DA_NMAX * KP], &Vs[kv * DA_NMAX * HD], n, lane, m_run, l_run, o);
-    const float inv = 1.f / l_run;
-#pragma unroll
-    for (int i = 0; i < NO; ++i) xo[m][h * HD + lane + 64 * i] = o[i] * inv;
+    for (int i = 0; i < NO; ++i) xo[m][h * HD + lane + 64 * i] = o[i];
+    if (h == 0 && lane == 0) gcode[m] = c;
   }
   __syncthreads();
-  // (4) o_proj GEMV from LDS (+ residual)
+  // (3) o_proj from LDS
   float acc[DA_M][RPT];
 #pragma unroll
   for (int i = 0; i < DA_M; ++i)
 #pragma unroll
     for (int r = 0; r < RPT; ++r) acc[i][r] = 0.f;
+  {
+    float w[RPT][8];
 #pragma unroll
-  for (int s = 0; s < NKM; ++s) {
-    const int k = gt * 8 + s * G * 8;
-    if (k < p.K) {
-      float w[RPT][8];
+    for (int r = 0; r < RPT; ++r) wr[r].get(w[r]);
 #pragma unroll
-      for (int r = 0; r < RPT; ++r) wr[s][r].get(w[r]);
+    for (int i = 0; i < DA_M; ++i) {
+      if (i < p.M) {
+        const float4 x0 = *reinterpret_cast<const float4*>(&xo[i][gt * 8]);
+        const float4 x1 = *reinterpret_cast<const float4*>(&xo[i][gt * 8 + 4]);
+        const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
 #pragma unroll
-      for (int i = 0; i < DA_M; ++i) {
-        if (i < p.M) {
-          const float4 x0 = *reinterpret_cast<const float4*>(&xo[i][k]);
-          const float4 x1 = *reinterpret_cast<const float4*>(&xo[i][k + 4]);
-          const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+        for (int r = 0; r < RPT; ++r)
 #pragma unroll
-          for (int r = 0; r < RPT; ++r)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) acc[i][r] = fmaf(w[r][j], xv[j], acc[i][r]);
-        }
+          for (int j = 0; j < 8; ++j) acc[i][r] = fmaf(w[r][j], xv[j], acc[i][r]);
       }
     }
   }
@@ -729,13 +805,21 @@ __global__ __launch_bounds__(256) void dec_attn_oproj_kernel(GemvParams p, AttnP
     const int rem = tid % (DA_M * (RPT / 2));
     const int i = rem / (RPT / 2), rp = (rem % (RPT / 2)) * 2;
     if (i < p.M) {
-      float va = 0.f, vb2 = 0.f;
+      float va = 0.f, vb = 0.f;
 #pragma unroll
       for (int w2 = 0; w2 < WPG; ++w2) {
         va += red[g * WPG + w2][i][rp];
-        vb2 += red[g * WPG + w2][i][rp + 1];
+        vb += red[g * WPG + w2][i][rp + 1];
       }
-      gemv_epilogue_pair(p, i, blockIdx.x * RPB + g * RPT + rp, va, vb2);
+      const int n = blockIdx.x * RPB + g * RPT + rp;
+      if (a.g_tab) {  // residual = the folded decoder input row
+        const float* xs = a.g_xtab + (size_t)gcode[i] * a.g_D;
+        float* o = p.out + (size_t)i * p.os + n;
+        o[0] = xs[n] + va;
+        o[1] = xs[n + 1] + vb;
+      } else {
+        gemv_epilogue_pair(p, i, n, va, vb);
+      }
     }
   }
 }
@@ -1045,7 +1129,13 @@ void launch_embed(const EmbedParams& p, int wdt, int M, hipStream_t st) {
   else hipLaunchKernelGGL(embed_rows_kernel<float>, dim3(M), dim3(256), 0, st, p);
 }
 
+static bool g_attn_short = [] { const char* e = getenv("CSM_ATTN_SHORT"); return !(e && e[0] == '0'); }();
+
 void launch_attn(const AttnParams& p, int hd, hipStream_t st) {
+  if (g_attn_short && hd == 128 && p.mode == ATTN_CAUSAL && p.S_cap <= 32) {  // depth decoder
+    hipLaunchKernelGGL((attn_short_kernel<128, 32>), dim3(p.M * p.Hq), dim3(64), 0, st, p);
+    return;
+  }
   const int blocks = p.M * p.Hkv;
   if (hd == 64) hipLaunchKernelGGL(attn_kernel<64>, dim3(blocks), dim3(256), 0, st, p);
   else if (hd == 128) hipLaunchKernelGGL(attn_kernel<128>, dim3(blocks), dim3(256), 0, st, p);
@@ -1066,25 +1156,30 @@ void launch_advance(const AdvanceParams& p, hipStream_t st) {
 }
 
 bool dec_attn_oproj_supported(const GemvParams& p, const AttnParams& a, int hd) {
-  // one utterance's rows, <= 32 positions, <= 2 kv heads, q_dim <= 1024, o_proj at G = 128
-  int G, RPT;
-  gemv_tiling(p.N, p.K, p.M, G, RPT);
-  return G == 128 && hd == 128 && p.M <= DA_M && a.rm.T >= p.M && a.S_cap <= DA_NMAX && a.Hkv <= DA_HKV &&
-         a.Hq * hd <= DA_QD && p.K == a.Hq * hd && p.N % 16 == 0 && a.mode == ATTN_CAUSAL;
+  // rows of one step (<= 2), <= 32 positions, 8 q heads of 128, o_proj K = 1024 (one G = 128 step)
+  return hd == 128 && p.M <= DA_M && a.S_cap <= 32 && a.Hq == DA_HQ && a.Hq * hd == DA_QD && p.K == DA_QD &&
+         p.N % 32 == 0 && a.mode == ATTN_CAUSAL;
 }
+
+static int g_da_rpt = [] { const char* e = getenv("CSM_DA_RPT"); return e ? atoi(e) : 4; }();
 
 void launch_dec_attn_oproj(const GemvParams& p0, const AttnParams& a, int wdt, hipStream_t st, int tag) {
   GemvParams p = p0;
   p.epi = EPI_ADD;
   p.nw = nullptr;
-  const int blocks = p.N / 16;  // G = 128, RPT = 8
   const bool nt = (gemv_nt_mask() >> tag) & 1;
+  const int rpt = g_da_rpt == 2 ? 2 : (g_da_rpt == 8 ? 8 : 4);
+  const int blocks = p.N / (4 * rpt);
+#define DA_L(WT_, R_, T_) hipLaunchKernelGGL((dec_attn_oproj_kernel<WT_, R_, T_>), dim3(blocks), dim3(512), 0, st, p, a)
+#define DA_R(WT_, T_) do { if (rpt == 2) DA_L(WT_, 2, T_); else if (rpt == 8) DA_L(WT_, 8, T_); else DA_L(WT_, 4, T_); } while (0)
   if (wdt == WDT_BF16) {
-    if (nt) hipLaunchKernelGGL((dec_attn_oproj_kernel<bf16_t, 128, 8, 5>), dim3(blocks), dim3(256), 0, st, p, a);
-    else hipLaunchKernelGGL((dec_attn_oproj_kernel<bf16_t, 128, 8, 1>), dim3(blocks), dim3(256), 0, st, p, a);
+    if (nt) DA_R(bf16_t, 5);
+    else DA_R(bf16_t, 1);
   } else {
-    hipLaunchKernelGGL((dec_attn_oproj_kernel<float, 128, 8, 1>), dim3(blocks), dim3(256), 0, st, p, a);
+    DA_R(float, 1);
   }
+#undef DA_R
+#undef DA_L
 }
 
 // ============================================================================ launch-floor probe
