@@ -113,6 +113,42 @@ def cpu_baseline(frames: int = 2):
                       f"{frames} frames, codes only, {dt:.1f} s"}
 
 
+CONFIGS = {
+    # BASELINE.json configs[1..4]; configs[0] (MLX CPU stream) is the oracle's plumbing case (tests)
+    2: dict(batch=1, dtype="bf16", temperature=0.0, top_k=0, stream=False, context=False,
+            workload="configs[1]: csm_1b greedy generate(), B=1, 10 s utterance + Mimi decode"),
+    3: dict(batch=32, dtype="bf16", temperature=0.8, top_k=50, stream=True, context=False,
+            workload="configs[2]: csm_1b temp=0.8 top_k=50 stream_generate (per-frame Mimi decode_step), B=32"),
+    4: dict(batch=32, dtype="bf16", temperature=0.0, top_k=0, stream=False, context=False,
+            workload="configs[3]: csm_1b greedy, 256 utterances over 8 GPUs = 32 per GPU, 10 s + Mimi decode"),
+    5: dict(batch=64, dtype="q4", temperature=0.0, top_k=0, stream=False, context=True,
+            workload="configs[4]: csm_1b int4 g64 (nn.quantize), 3-Segment context (Mimi encode), B=64 + decode"),
+}
+
+
+def context_audio(g: int, seg: int, seconds: float = 5.0):
+    """seeded sum of 3 sines (100-400 Hz) + N(0, 0.01) noise, amplitude 0.1, 24 kHz."""
+    rng = np.random.default_rng(50_000 + 97 * g + seg)
+    t = np.arange(int(seconds * 24000), dtype=np.float64) / 24000.0
+    f = rng.uniform(100.0, 400.0, 3)
+    ph = rng.uniform(0, 2 * np.pi, 3)
+    x = sum(np.sin(2 * np.pi * fi * t + pi) for fi, pi in zip(f, ph)) / 3.0
+    return (0.1 * x + rng.normal(0.0, 0.01, t.shape)).astype(np.float32)
+
+
+def context_prompts(mine, K: int = 32):
+    """Config 5 prompts: 3 context Segments (12 text ids + 5 s audio, Mimi-encoded) + the 12-id text."""
+    from csm_mlx.segment import Segment
+    from csm_mlx.tokenizers import tokenize_segments_batch, tokenize_text_segment
+    out = []
+    for g in mine:
+        segs = [Segment(seg % 2, prompt_ids(10_000 + 10 * g + seg), context_audio(g, seg)) for seg in range(3)]
+        parts = tokenize_segments_batch(segs, n_audio_codebooks=K)
+        parts.append(tokenize_text_segment(prompt_ids(g), 0, K))
+        out.append((np.concatenate([t for t, _ in parts], 0), np.concatenate([m for _, m in parts], 0)))
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -125,9 +161,15 @@ def main():
     ap.add_argument("--no-decode", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=96, help="oracle frames timed for cpu_baseline (~10 s on 16 cores)")
+    ap.add_argument("--config", type=int, default=0, choices=[0, 2, 3, 4, 5],
+                    help="run BASELINE.json configs[N-1] (batch, dtype, sampling, streaming, context) instead of "
+                         "the default configs[1] line; the metric stays audio frames/s")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (RCCL over xGMI) for real runs; gloo rehearses N ranks on fewer GPUs")
     args = ap.parse_args()
+    cfg = dict(CONFIGS[args.config or 2])
+    if args.config:
+        args.batch, args.dtype = cfg["batch"], cfg["dtype"]
 
     rank, world, local = dist_env()
     dev = None
@@ -161,14 +203,26 @@ def main():
 
     model = build_model(args.dtype, args.batch, device=device)
     decode = not args.no_decode
-    if decode:
+    if decode or cfg["stream"] or cfg["context"]:
         build_codec(device=device)
     mine = shard(args.batch * world, world, rank)
-    prompts = [tokenize_text_segment(prompt_ids(g), 0, 32) for g in mine]
     ms = args.frames * 80
+    seeds = [1234 + g for g in mine]
+    if not cfg["context"]:
+        prompts = [tokenize_text_segment(prompt_ids(g), 0, 32) for g in mine]
 
     def step():
-        out = generate_batch(model, prompts, ms, temperature=0.0, decode=decode)
+        # config 5: the context Segments' Mimi encode is part of every step (generation.py:108-125)
+        pr = context_prompts(mine) if cfg["context"] else prompts
+        if cfg["stream"]:
+            from csm_mlx.generation import stream_generate_batch
+            n = 0
+            for pcm, done in stream_generate_batch(model, pr, ms, temperature=cfg["temperature"],
+                                                   top_k=cfg["top_k"], seeds=seeds):
+                n += int((~done).sum())
+            return n
+        out = generate_batch(model, pr, ms, temperature=cfg["temperature"], top_k=cfg["top_k"], seeds=seeds,
+                             decode=decode)
         if decode:
             return sum(len(w) // FRAME_SAMPLES for w in out)
         return sum(len(c) for c in out)
@@ -218,8 +272,11 @@ def main():
             "vs_baseline": None,
             "dtype": args.dtype,
             "data": "synthetic",
-            "config": {"workload": "csm_1b greedy generate(), 10 s utterances (125 frames) + Mimi decode"
-                                   if decode else "csm_1b greedy generate(), 10 s utterances (125 frames), codes only",
+            "config": {"workload": (cfg["workload"] if args.config else
+                                    "csm_1b greedy generate(), 10 s utterances (125 frames) + Mimi decode")
+                                   if decode else cfg["workload"] + " (codes only)",
+                       "temperature": cfg["temperature"], "top_k": cfg["top_k"], "stream": cfg["stream"],
+                       "context_segments": 3 if cfg["context"] else 0,
                        "model": "csm_1b (synthetic seed-0 weights)", "global_batch": args.batch * world,
                        "per_gpu_batch": args.batch, "frames": args.frames, "mimi_decode": decode,
                        "parallelism": f"dp{world}", "rtf": round(total_frames / max_dt / 12.5, 2)},

@@ -84,6 +84,11 @@ class FrameCache:
         _lib.check(self.L.csm_read_codes(self.model.engine, _lib.ptr(hist), _lib.ptr(n), _lib.ptr(d), None))
         return hist, n, d
 
+    def done(self) -> np.ndarray:
+        d = np.zeros(self.B, np.uint8)
+        _lib.check(self.L.csm_read_codes(self.model.engine, None, None, _lib.ptr(d), None))
+        return d.astype(bool)
+
     def last_codes(self) -> np.ndarray:
         out = np.zeros((self.B, self.model.n_audio_codebooks), np.int32)
         _lib.check(self.L.csm_debug_read(self.model.engine, b"codes", _lib.ptr(out), out.nbytes, None))
@@ -205,6 +210,31 @@ def generate_batch(model: CSM, prompts: Sequence[Tuple[np.ndarray, np.ndarray]],
     if not decode:
         return [hist[: n_frames[b], b] for b in range(len(prompts))]
     return _decode_batch(model, hist, n_frames)
+
+
+def stream_generate_batch(model: CSM, prompts: Sequence[Tuple[np.ndarray, np.ndarray]],
+                          max_audio_length_ms: float = 10_000, *, temperature: float = 0.8, top_k: int = 0,
+                          sampler=None, seeds=None) -> Generator[Tuple[np.ndarray, np.ndarray], None, None]:
+    """Batched extension of ``stream_generate`` (generation.py:181-258): per frame yields
+    (pcm (B, 1920) float32 from the codec's streaming ``decode_step``, done (B,) bool).  An
+    utterance's rows after its EOS frame are not audio (its ``done`` flag is set)."""
+    max_audio_frames = int(max_audio_length_ms / 80)
+    for t, _ in prompts:
+        _check_window(model, t.shape[0], max_audio_frames)
+    smp = _resolve_sampler(temperature, sampler, top_k)
+    B = len(prompts)
+    codec = get_audio_tokenizer(model.n_audio_codebooks)
+    cache = FrameCache(model, B, smp, seeds)
+    for b, (t, m) in enumerate(prompts):
+        cache.prefill(b, t, m)
+    codec.reset_state(B)
+    try:
+        for _ in range(max_audio_frames):
+            if cache.run(1):
+                break                                                              # every utterance hit EOS
+            yield codec.decode_step(cache.last_codes())[:, 0], cache.done()
+    finally:
+        codec.reset_state(B)
 
 
 def stream_generate(model: CSM, text, speaker: int, context: List[Segment], max_audio_length_ms: float = 90_000,

@@ -215,7 +215,7 @@ bool gemv_q4_supported(int N, int K);
 constexpr int GEMM_MFMA_MIN_M = 8;  // rows at which a bf16 projection leaves the GEMV for the matrix cores
 bool gemm_mfma_eligible(int N, int K, int M, int wdt);
 int gemm_blocks(int N);  // row-tile blocks (= arg-max partials per row)
-void launch_gemm_mfma(const GemvParams& p, bool nt, hipStream_t st);
+void launch_gemm_mfma(const GemvParams& p, int wdt, bool nt, hipStream_t st);
 void gemm_reserve(int N, int K, int M);  // pre-size the split-K scratch (outside graph capture)
 // dense decoder-input rows from a table (codes resolved from arg-max partials), see gather_rows_kernel
 void launch_gather_rows(const GemvParams& p, int wdt, hipStream_t st);

@@ -1094,7 +1094,7 @@ void launch_gemv(const GemvParams& p0, int wdt, int epi, int norm, hipStream_t s
   if (!norm) p.nw = nullptr;
   const bool nt = (gemv_nt_mask() >> tag) & 1;
   if (!p.xpart && !p.x_copy && gemm_mfma_eligible(p.N, p.K, p.M, wdt)) {
-    launch_gemm_mfma(p, nt, st);
+    launch_gemm_mfma(p, wdt, nt, st);
   } else if (wdt == WDT_Q4) {
     launch_gemv_q4(p, nt, st);
   } else if (wdt == WDT_BF16) {

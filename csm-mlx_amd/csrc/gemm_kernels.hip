@@ -42,6 +42,21 @@ constexpr int GM_KS = 128;     // K per sub-chunk (8 MFMA steps)
 
 __device__ __forceinline__ unsigned short bf16_bits_rne(float v) { return (unsigned short)st_cast<bf16_t>(v); }
 
+constexpr int GK_MAX_SLICES = 16;
+// Split-K combine: element e of every slice partial (sc1 loads, all issued before the first add so
+// the slices cost one round trip), summed in slice order.
+__device__ __forceinline__ float slab_sum(const gfloat* slab, size_t slab_f, size_t e, int ks) {
+  float v[GK_MAX_SLICES];
+#pragma unroll
+  for (int sl = 0; sl < GK_MAX_SLICES; ++sl)
+    v[sl] = sl < ks ? __hip_atomic_load(slab + (size_t)sl * slab_f + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
+  float sum = 0.f;
+#pragma unroll
+  for (int sl = 0; sl < GK_MAX_SLICES; ++sl)
+    if (sl < ks) sum += v[sl];
+  return sum;
+}
+
 template <int MT, bool NT>
 __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemvParams p) {
   // activation fragments of one sub-chunk: [hi/lo][tile][step][lane] x 8 bf16 (16 B)
@@ -162,9 +177,7 @@ __global__ __launch_bounds__(256) void gemm_bf16_kernel(GemvParams p) {
       __syncthreads();
       if (!last) continue;  // uniform per block
       for (int e = tid; e < mrows * (GM_WROWS + 1); e += 256) {
-        float v = 0.f;
-        for (int sl = 0; sl < p.ksplit; ++sl)
-          v += __hip_atomic_load(slab + (size_t)sl * slab_f + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const float v = slab_sum(slab, slab_f, e, p.ksplit);
         const int ml = e / (GM_WROWS + 1), j = e % (GM_WROWS + 1);
         if (j < GM_WROWS) ct[ml][j] = v;
         else ssb[ml] = v;
@@ -319,12 +332,10 @@ __global__ __launch_bounds__(256) void gemm_bf16_wk_kernel(GemvParams p) {
       float a, b, sq;
       if (slab) {
         a = 0.f; b = 0.f; sq = 0.f;
-        for (int sl = 0; sl < p.ksplit; ++sl) {
-          const gfloat* q = slab + (size_t)sl * slab_f + mi * (GW_ROWS + 1);
-          a += __hip_atomic_load(q + rp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          b += __hip_atomic_load(q + rp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          sq += __hip_atomic_load(q + GW_ROWS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        const size_t e0 = (size_t)mi * (GW_ROWS + 1);
+        a = slab_sum(slab, slab_f, e0 + rp, p.ksplit);
+        b = slab_sum(slab, slab_f, e0 + rp + 1, p.ksplit);
+        sq = slab_sum(slab, slab_f, e0 + GW_ROWS, p.ksplit);
       } else {
         a = (red[0][mi][rp] + red[1][mi][rp]) + (red[2][mi][rp] + red[3][mi][rp]);
         b = (red[0][mi][rp + 1] + red[1][mi][rp + 1]) + (red[2][mi][rp + 1] + red[3][mi][rp + 1]);
@@ -359,17 +370,243 @@ __global__ __launch_bounds__(256) void gemm_bf16_wk_kernel(GemvParams p) {
   }
 }
 
+// Variant "pipe" (default): the block's weight tile AND activation tile go through LDS with
+// coalesced global loads, double-buffered so stage c+1's loads are in flight while stage c runs on
+// the matrix cores.  Block = 64 weight rows x 32*MT batch rows over one K slice, stages of 64 K
+// (4 MFMA steps); every fragment is stored in MFMA-lane order (one conflict-free ds_read_b128 per
+// operand).  MT = 2: 2 x 2 waves over (row tile, batch tile); MT = 1: 2 waves per row tile split
+// each stage's K steps and are summed in a fixed order.  int4 weights (Q4) are dequantized while
+// staging (w = scale * q + bias in fp32, split hi/lo like the activations) and run three products
+// (hi*hi, hi*lo, lo*hi).  Split-K fixup and epilogues as the kernels above.
+constexpr int GP_ROWS = 64, GP_KC = 64;
+typedef unsigned short u16x4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void split4(const float (&v)[4], u32x2_t& hi, u32x2_t& lo) {
+  unsigned short h[4], l[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    h[q] = bf16_bits_rne(v[q]);
+    l[q] = bf16_bits_rne(v[q] - __uint_as_float((unsigned)h[q] << 16));
+  }
+  hi = u32x2_t{h[0] | ((unsigned)h[1] << 16), h[2] | ((unsigned)h[3] << 16)};
+  lo = u32x2_t{l[0] | ((unsigned)l[1] << 16), l[2] | ((unsigned)l[3] << 16)};
+}
+
+template <bool Q4, int MT, bool NT>
+__global__ __launch_bounds__(256) void gemm_pipe_kernel(GemvParams p) {
+  constexpr int NB = MT * 32, NA = Q4 ? 2 : 1;
+  constexpr int A_BYTES = 2 * NA * 2 * 4 * 64 * 16, B_BYTES = 2 * 2 * MT * 4 * 64 * 16;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[A_BYTES + B_BYTES];
+  __shared__ float ssb[NB];
+  __shared__ int last;
+  // As[buf][hi/lo][row tile][step][lane], Bs[buf][hi/lo][batch tile][step][lane] (16 B each)
+  auto As = [&](int buf, int hl, int t, int s) { return reinterpret_cast<u32x4_t*>(smem) + (((buf * NA + hl) * 2 + t) * 4 + s) * 64; };
+  auto Bs = [&](int buf, int hl, int t, int s) {
+    return reinterpret_cast<u32x4_t*>(smem + A_BYTES) + (((buf * 2 + hl) * MT + t) * 4 + s) * 64;
+  };
+  float (*ct)[GP_ROWS + 1] = reinterpret_cast<float (*)[GP_ROWS + 1]>(smem);  // after the K loop
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const int wr = wave & 1, wc = wave >> 1;  // MT = 2: batch tile; MT = 1: K-step half
+  const int tile = blockIdx.x, n0 = tile * GP_ROWS;
+  const int mc = blockIdx.z, m0 = mc * NB, nchunks = gridDim.z;
+  const int Kblk = p.K / p.ksplit, kslice = blockIdx.y * Kblk, nst = Kblk / GP_KC;
+  const bool norm = p.nw != nullptr;
+  // staging maps
+  const int a_row = Q4 ? (tid >> 1) : (tid >> 2), a_seg = Q4 ? (tid & 1) : (tid & 3);
+  const bool a_on = !Q4 || tid < 128;
+  const size_t a_grow = (size_t)min(n0 + a_row, p.N - 1);
+  const uint8_t* Wq = (const uint8_t*)p.W;
+  const uint32_t* SB = Q4 ? reinterpret_cast<const uint32_t*>(Wq + q4_sb_offset(p.N, p.K)) : nullptr;
+  const int x_c = tid >> 4, x_k4 = (tid & 15) * 4;
+  float ss[NB / 16];
+#pragma unroll
+  for (int i = 0; i < NB / 16; ++i) ss[i] = 0.f;
+  u32x4_t ar[2];
+  uint32_t asb = 0;
+  f32x4_t xr[NB / 16];
+  f32x4_t nwr = {1.f, 1.f, 1.f, 1.f};
+  auto load = [&](int kc) {
+    if (a_on) {
+      if constexpr (Q4) {
+        const u32x4_t* src = reinterpret_cast<const u32x4_t*>(Wq + a_grow * (p.K / 2) + (kc + 32 * a_seg) / 2);
+        ar[0] = NT ? __builtin_nontemporal_load(src) : *src;
+        asb = SB[a_grow * (p.K / Q4_GROUP) + kc / Q4_GROUP];
+      } else {
+        const u32x4_t* src = reinterpret_cast<const u32x4_t*>((const bf16_t*)p.W + a_grow * p.K + kc + 16 * a_seg);
+        ar[0] = NT ? __builtin_nontemporal_load(src) : src[0];
+        ar[1] = NT ? __builtin_nontemporal_load(src + 1) : src[1];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NB / 16; ++i) {
+      const int m = min(m0 + x_c + 16 * i, p.M - 1);
+      xr[i] = *(const gcf32x4*)(p.x + (size_t)m * p.xs + kc + x_k4);
+    }
+    if (norm) nwr = *(const gcf32x4*)(p.nw + kc + x_k4);
+  };
+  auto store = [&](int buf) {
+    if (a_on) {
+      const int t = a_row >> 5, ln = a_row & 31;
+      if constexpr (Q4) {
+        const float sc = bf16_lo(asb), bi = bf16_hi(asb);
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {  // 8 consecutive k per word: step 2*seg + w/2, half w&1
+          const uint32_t u = ar[0][w];
+          float v[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = fmaf(sc, (float)((u >> (4 * j)) & 15u), bi);
+          u32x2_t h0, l0, h1, l1;
+          const float v0[4] = {v[0], v[1], v[2], v[3]}, v1[4] = {v[4], v[5], v[6], v[7]};
+          split4(v0, h0, l0);
+          split4(v1, h1, l1);
+          const int s = 2 * a_seg + (w >> 1), hh = w & 1;
+          As(buf, 0, t, s)[ln + 32 * hh] = u32x4_t{h0.x, h0.y, h1.x, h1.y};
+          As(buf, 1, t, s)[ln + 32 * hh] = u32x4_t{l0.x, l0.y, l1.x, l1.y};
+        }
+      } else {
+        As(buf, 0, t, a_seg)[ln] = ar[0];
+        As(buf, 0, t, a_seg)[ln + 32] = ar[1];
+      }
+    }
+    const int s = x_k4 >> 4, hh = (x_k4 >> 3) & 1, j0 = x_k4 & 7;
+#pragma unroll
+    for (int i = 0; i < NB / 16; ++i) {
+      const int c = x_c + 16 * i;
+      float v[4] = {xr[i].x, xr[i].y, xr[i].z, xr[i].w};
+      if (norm) {
+        const float nw4[4] = {nwr.x, nwr.y, nwr.z, nwr.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          ss[i] = fmaf(v[q], v[q], ss[i]);
+          v[q] *= nw4[q];
+        }
+      }
+      u32x2_t hi, lo;
+      split4(v, hi, lo);
+      const int ln = (c & 31) + 32 * hh;
+      *(reinterpret_cast<u32x2_t*>(&Bs(buf, 0, c >> 5, s)[ln]) + (j0 >> 2)) = hi;
+      *(reinterpret_cast<u32x2_t*>(&Bs(buf, 1, c >> 5, s)[ln]) + (j0 >> 2)) = lo;
+    }
+  };
+  f32x16_t acc = f32x16_t{};
+  load(kslice);
+  store(0);
+  __syncthreads();
+  for (int it = 0; it < nst; ++it) {
+    const int buf = it & 1;
+    if (it + 1 < nst) load(kslice + (it + 1) * GP_KC);
+    const int s0 = MT == 2 ? 0 : 2 * wc, s1 = MT == 2 ? 4 : 2 * wc + 2;
+    const int bt = MT == 2 ? wc : 0;
+#pragma unroll
+    for (int s = s0; s < s1; ++s) {
+      const bf16x8_t a = __builtin_bit_cast(bf16x8_t, As(buf, 0, wr, s)[lane]);
+      const bf16x8_t bh = __builtin_bit_cast(bf16x8_t, Bs(buf, 0, bt, s)[lane]);
+      const bf16x8_t bl = __builtin_bit_cast(bf16x8_t, Bs(buf, 1, bt, s)[lane]);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bh, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bl, acc, 0, 0, 0);
+      if constexpr (Q4) {
+        const bf16x8_t al = __builtin_bit_cast(bf16x8_t, As(buf, 1, wr, s)[lane]);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
+      }
+    }
+    if (it + 1 < nst) store(buf ^ 1);
+    __syncthreads();
+  }
+  // sum of squares per batch row: the 16 threads of a row share it
+  if (norm) {
+#pragma unroll
+    for (int i = 0; i < NB / 16; ++i) {
+      float v = ss[i];
+#pragma unroll
+      for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      if ((tid & 15) == 0) ssb[x_c + 16 * i] = v;
+    }
+  }
+  // accumulators -> C tile [batch row][weight row]
+  if (MT == 2 || wc == 0) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) ct[32 * (MT == 2 ? wc : 0) + r][32 * wr + (j & 3) + 8 * (j >> 2) + 4 * h] = acc[j];
+  }
+  __syncthreads();
+  if (MT == 1 && wc == 1) {  // second K-step half, added in a fixed order
+#pragma unroll
+    for (int j = 0; j < 16; ++j) ct[r][32 * wr + (j & 3) + 8 * (j >> 2) + 4 * h] += acc[j];
+  }
+  __syncthreads();
+  const int mrows = min(NB, p.M - m0);
+  if (p.ksplit > 1) {
+    const size_t slab_f = (size_t)NB * (GP_ROWS + 1);
+    gfloat* slab = (gfloat*)p.kpart + ((size_t)(tile * nchunks + mc) * p.ksplit) * slab_f;
+    gfloat* mine = slab + (size_t)blockIdx.y * slab_f;
+    for (int e = tid; e < mrows * (GP_ROWS + 1); e += 256) {
+      const int ml = e / (GP_ROWS + 1), j = e % (GP_ROWS + 1);
+      __hip_atomic_store(mine + e, j < GP_ROWS ? ct[ml][j] : (norm ? ssb[ml] : 0.f), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      gu32* tk = (gu32*)p.kticket + tile * nchunks + mc;
+      const unsigned old = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = (old == (unsigned)p.ksplit - 1);
+      if (last) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!last) return;
+    for (int e = tid; e < mrows * (GP_ROWS + 1); e += 256) {
+      const float v = slab_sum(slab, slab_f, e, p.ksplit);
+      const int ml = e / (GP_ROWS + 1), j = e % (GP_ROWS + 1);
+      if (j < GP_ROWS) ct[ml][j] = v;
+      else ssb[ml] = v;
+    }
+    __syncthreads();
+  }
+  for (int e = tid; e < mrows * (GP_ROWS / 2); e += 256) {
+    const int ml = e / (GP_ROWS / 2), rp = (e % (GP_ROWS / 2)) * 2;
+    const int n = n0 + rp;
+    float va = ct[ml][rp], vb = ct[ml][rp + 1];
+    if (norm) {
+      const float sc = rsqrtf(ssb[ml] / (float)p.K + p.eps);
+      va *= sc;
+      vb *= sc;
+    }
+    if (n < p.N) gemv_epilogue_pair(p, m0 + ml, n, va, vb);
+    if (p.epi == EPI_ARGMAX) {
+      ct[ml][rp] = va;
+      ct[ml][rp + 1] = vb;
+    }
+  }
+  if (p.epi == EPI_ARGMAX) {
+    __syncthreads();
+    if (tid < mrows) {
+      unsigned long long best = 0;
+      for (int j = 0; j < GP_ROWS; ++j) {
+        const int n = n0 + j;
+        if (n < p.n_valid) {
+          const unsigned long long key = pack_argmax(ct[tid][j], n);
+          best = key > best ? key : best;
+        }
+      }
+      p.part[(size_t)(m0 + tid) * p.part_stride + blockIdx.x] = best;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------- host side
-static int gemm_variant() {  // 0 = "wk" (default), 1 = "lds" (CSM_GEMM=lds)
+static int gemm_variant() {  // 2 = "pipe" (default), 0 = "wk" (CSM_GEMM=wk), 1 = "lds" (CSM_GEMM=lds)
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("CSM_GEMM");
-    v = (e && e[0] == 'l') ? 1 : 0;
+    v = (e && e[0] == 'l') ? 1 : ((e && e[0] == 'w') ? 0 : 2);
   }
   return v;
 }
-static int gemm_rows() { return gemm_variant() == 1 ? GM_WROWS : GW_ROWS; }
+static int gemm_rows() { return gemm_variant() == 1 ? GM_WROWS : (gemm_variant() == 2 ? GP_ROWS : GW_ROWS); }
 constexpr int GW_PF = 4;  // wk: MFMA steps in flight per wave
+// pipe: K slices are added until the grid has this many blocks (several blocks per CU hide each
+// block's one-stage-deep pipeline); CSM_PIPE_BLOCKS overrides (lab sweeps)
+static int g_pipe_target = [] { const char* e = getenv("CSM_PIPE_BLOCKS"); return e ? atoi(e) : 512; }();
 
 // K slices: doubled while the grid has < 256 blocks (wk: while each wave keeps >= 2 rings of PF
 // steps; lds: up to 8); the arg-max heads keep whole rows.
@@ -379,7 +616,9 @@ static void gemm_plan(int N, int K, int M, int epi, int& ks) {
   const int chunks = (M + 63) / 64;
   ks = 1;
   if (epi == EPI_ARGMAX) return;
-  if (gemm_variant() == 1) {
+  if (gemm_variant() == 2) {
+    while (tiles * chunks * ks < g_pipe_target && ks < 16 && K % (GP_KC * ks * 2) == 0 && K / (ks * 2) >= 2 * GP_KC) ks *= 2;
+  } else if (gemm_variant() == 1) {
     while (tiles * chunks * ks < 256 && ks < 8 && K % (GM_KS * ks * 2) == 0) ks *= 2;
   } else {
     while (tiles * chunks * ks < 512 && K % (ks * 2 * 4 * 16 * GW_PF * 2) == 0) ks *= 2;
@@ -389,7 +628,9 @@ static void gemm_plan(int N, int K, int M, int epi, int& ks) {
 static size_t gemm_slab_floats(int MT) { return (size_t)MT * 32 * (gemm_rows() + 1); }
 
 bool gemm_mfma_eligible(int N, int K, int M, int wdt) {
-  return wdt == WDT_BF16 && M >= GEMM_MFMA_MIN_M && K % (4 * 16 * GW_PF) == 0 && K % GM_KS == 0 && N % 2 == 0;
+  if (M < GEMM_MFMA_MIN_M || N % 2) return false;
+  if (gemm_variant() == 2) return (wdt == WDT_BF16 || wdt == WDT_Q4) && K % GP_KC == 0;
+  return wdt == WDT_BF16 && K % (4 * 16 * GW_PF) == 0 && K % GM_KS == 0;
 }
 
 int gemm_blocks(int N) { return (N + gemm_rows() - 1) / gemm_rows(); }
@@ -402,13 +643,14 @@ static size_t g_ktickets_n = 0;
 static size_t gemm_need(int N, int K, int M, size_t& tk) {
   int ks;
   gemm_plan(N, K, M, EPI_STORE, ks);
-  const int MT = M > 32 ? 2 : 1;
+  const int MT = (M > 32 || gemm_variant() == 2) ? 2 : 1;
   const size_t tiles = gemm_blocks(N), chunks = (M + MT * 32 - 1) / (MT * 32);
   tk = tiles * chunks;
   return ks > 1 ? tiles * chunks * ks * gemm_slab_floats(MT) * 4 : 0;
 }
 
-void launch_gemm_mfma(const GemvParams& p0, bool nt, hipStream_t st) {
+void launch_gemm_mfma(const GemvParams& p0, int wdt, bool nt, hipStream_t st) {
+  const bool p_is_q4 = wdt == WDT_Q4;
   GemvParams p = p0;
   int ks;
   gemm_plan(p.N, p.K, p.M, p.epi, ks);
@@ -422,6 +664,16 @@ void launch_gemm_mfma(const GemvParams& p0, bool nt, hipStream_t st) {
     }
     p.kpart = g_kscratch;
     p.kticket = g_ktickets;
+  }
+  if (gemm_variant() == 2) {  // pipe: batch chunks of 64 (MT 2) or one chunk of 32 (MT 1) on grid.z
+    const int MT = p.M > 32 ? 2 : 1;
+    const dim3 g3(gemm_blocks(p.N), ks, (p.M + MT * 32 - 1) / (MT * 32));
+#define GP_L(Q_, MT_) do { if (nt) hipLaunchKernelGGL((gemm_pipe_kernel<Q_, MT_, true>), g3, dim3(256), 0, st, p); \
+                          else hipLaunchKernelGGL((gemm_pipe_kernel<Q_, MT_, false>), g3, dim3(256), 0, st, p); } while (0)
+    if (p_is_q4) { if (MT == 2) GP_L(true, 2); else GP_L(true, 1); }
+    else { if (MT == 2) GP_L(false, 2); else GP_L(false, 1); }
+#undef GP_L
+    return;
   }
   const dim3 grid(gemm_blocks(p.N), ks);
   static const int lab_hl = [] { const char* e = getenv("CSM_GEMM_HL"); return e ? atoi(e) : 2; }();
