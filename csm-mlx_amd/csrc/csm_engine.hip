@@ -32,6 +32,7 @@ struct LayerW {
   void* wo = nullptr;    // [D][Hq*hd]
   void* wgu = nullptr;   // [2F][D] rows interleaved gate_j, up_j
   void* wd = nullptr;    // [D][F]
+  void* wdc = nullptr;   // bf16 engines: down_proj re-laid chunk-major [F/R][D][R] for the fused MLP
   float* n1 = nullptr;
   float* n2 = nullptr;
   float* kc = nullptr;   // [B][Hkv][S][hd]
@@ -44,6 +45,7 @@ struct Stack {
   float* norm = nullptr;
   float* rope = nullptr;  // [S][hd/2][2]
   int S_cap = 0;
+  long long* acc[2] = {nullptr, nullptr};  // fused-MLP fixed-point accumulators (ping-pong by layer parity)
   int qkv_rows() const { return (d.n_heads + 2 * d.n_kv_heads) * d.head_dim; }
   int q_dim() const { return d.n_heads * d.head_dim; }
 };
@@ -119,6 +121,12 @@ struct csm_engine {
   // (6.1 + 5.3 us) plus the boundary it removes -- 205 vs 227 frames/s.
   bool fuse_attn = false;
   bool fold_proj = true;  // csm_set_option "fold_proj": decoder steps >= 2 read the folded table
+  // csm_set_option "fuse_mlp" / CSM_FUSE_MLP=1: one-launch MLP (gate/up + SiLU*up + down, 64-bit
+  // fixed-point atomics) for <= 4 rows.  Off: the atomics' memory-side serialization (512 blocks add
+  // into the same D outputs) costs more than the launch it saves -- 197.9 vs 235.0 frames/s; with
+  // the atomics removed (invalid results) the one-launch MLP ran at 264 frames/s.
+  bool fuse_mlp = [] { const char* v = getenv("CSM_FUSE_MLP"); return v && v[0] == '1'; }();
+  int acc_rows = 0;  // rows of the fused-MLP accumulators (the fused path runs for M <= acc_rows)
 
   void* balloc(size_t bytes) {
     void* p = nullptr;
@@ -166,6 +174,7 @@ void alloc_stack(csm_engine* e, Stack& s, const csm_llama_dims& d, int S_cap, co
     l.wo = e->alloc(e->wbytes(D, s.q_dim()));
     l.wgu = e->alloc(e->wbytes(2 * F, D));
     l.wd = e->alloc(e->wbytes(D, F));
+    if (e->wdt == WDT_BF16 && fused_mlp_chunk((int)D) && F % fused_mlp_chunk((int)D) == 0) l.wdc = e->alloc(D * F * 2);
     l.n1 = (float*)e->alloc(D * 4);
     l.n2 = (float*)e->alloc(D * 4);
     const std::string p = std::string(prefix) + ".layers." + std::to_string(i);
@@ -193,12 +202,19 @@ int ablate() {
 // One Llama block stack over M rows of the residual stream x (in place).
 // gather0: x-gather fields for layer 0's QKV GEMV (its input rows come from a table; the GEMV also
 // writes them to x as the residual stream).
-void run_stack(csm_engine* e, Stack& s, float* x, int M, float* q, float* att, float* mlp, const RowMap& rm,
-               hipStream_t st, const GemvParams* gather0 = nullptr, const AttnParams* attn0 = nullptr) {
+// Returns the fused-MLP accumulator still pending after the last layer (its reader -- the heads or
+// the final norm -- must add it), or null when the stack ran the two-launch MLP.
+// Fused MLP bookkeeping: layer i's MLP adds into acc[i & 1]; layer i+1's QKV reads x + acc[i & 1]
+// and its o_proj folds acc[i & 1] into x and zeroes it; layer 0's o_proj zeroes acc[1] (left by the
+// previous call's last layer, already consumed).
+long long* run_stack(csm_engine* e, Stack& s, float* x, int M, float* q, float* att, float* mlp, const RowMap& rm,
+                     hipStream_t st, const GemvParams* gather0 = nullptr, const AttnParams* attn0 = nullptr) {
   const csm_llama_dims& d = s.d;
   const int tag = (&s == &e->dec) ? 1 : 0;
   const int D = d.hidden, F = d.intermediate, hd = d.head_dim, Hq = d.n_heads, Hkv = d.n_kv_heads;
   const int ab = tag ? ablate() : (ablate() >> 8) & 31;  // bits 0-4 decoder, 8-12 backbone
+  const bool fused = e->fuse_mlp && e->wdt == WDT_BF16 && s.L[0].wdc && s.acc[0] && M <= e->acc_rows &&
+                     fused_mlp_supported(D, F, M) && !(ab & 24);
   for (int i = 0; i < d.n_layers; ++i) {
     LayerW& l = s.L[i];
     GemvParams g{};
@@ -206,6 +222,8 @@ void run_stack(csm_engine* e, Stack& s, float* x, int M, float* q, float* att, f
     g.W = l.wqkv; g.N = s.qkv_rows(); g.K = D; g.x = x; g.xs = D; g.M = M; g.nw = l.n1; g.eps = d.eps;
     g.out = q; g.os = s.q_dim(); g.Hq = Hq; g.Hkv = Hkv; g.hd = hd; g.S_cap = s.S_cap; g.rope = s.rope;
     g.kc = l.kc; g.vc = l.vc; g.rm = rm;
+    if (fused && i > 0) g.xacc = s.acc[(i - 1) & 1];
+    g.acc_ss = e->acc_rows * D;
     if (i == 0 && gather0) {
       g.xpart = gather0->xpart; g.xpart_stride = gather0->xpart_stride; g.xpart_n = gather0->xpart_n;
       g.xtab = gather0->xtab; g.xtab_f32 = gather0->xtab_f32; g.xV = gather0->xV; g.xcb = gather0->xcb;
@@ -220,11 +238,23 @@ void run_stack(csm_engine* e, Stack& s, float* x, int M, float* q, float* att, f
     a.os = s.q_dim();
     g = GemvParams{};
     g.W = l.wo; g.N = D; g.K = s.q_dim(); g.x = att; g.xs = s.q_dim(); g.M = M; g.out = x; g.os = D;
+    if (fused) {
+      g.oacc = s.acc[(i + 1) & 1];
+      g.oacc_add = i > 0;
+      g.acc_ss = e->acc_rows * D;
+    }
     if (tag == 1 && e->fuse_attn && !(ab & 5) && dec_attn_oproj_supported(g, a, hd)) {
       launch_dec_attn_oproj(g, a, e->wdt, st, tag);
     } else {
       if (!(ab & 1)) launch_attn(a, hd, st);
       if (!(ab & 4)) launch_gemv(g, e->wdt, EPI_ADD, 0, st, tag);
+    }
+    if (fused) {  // norm2 + gate/up + SiLU*up + down in one launch, into acc[i & 1]
+      MlpParams mp{};
+      mp.x = x; mp.xs = D; mp.M = M; mp.nw = l.n2; mp.eps = d.eps; mp.wgu = l.wgu; mp.wdc = l.wdc;
+      mp.acc = s.acc[i & 1]; mp.F = F; mp.acc_ss = e->acc_rows * D;
+      launch_fused_mlp(mp, D, gemv_nt(tag), st);
+      continue;
     }
     // norm2 + gate/up + SiLU*up
     g = GemvParams{};
@@ -236,6 +266,7 @@ void run_stack(csm_engine* e, Stack& s, float* x, int M, float* q, float* att, f
     g.W = l.wd; g.N = D; g.K = F; g.x = mlp; g.xs = F; g.M = M; g.out = x; g.os = D;
     if (!(ab & 16)) launch_gemv(g, e->wdt, EPI_ADD, 0, st, tag);
   }
+  return fused ? s.acc[(d.n_layers - 1) & 1] : nullptr;
 }
 
 void embed(csm_engine* e, const EmbedParams& ep, int M, hipStream_t st) {
@@ -253,8 +284,8 @@ void enqueue_body(csm_engine* e, hipStream_t st) {
   ep.D = e->D; ep.out = e->x; ep.pos_inc = e->pos;
   embed(e, ep, B, st);
   RowMap rm{1, 0, e->pos, 0};
-  run_stack(e, e->bb, e->x, B, e->q, e->att, e->mlp, rm, st);
-  launch_rmsnorm_rows(e->x, e->D, e->bb.norm, e->bb.d.eps, e->D, e->h_last, e->D, B, st);
+  const long long* pend = run_stack(e, e->bb, e->x, B, e->q, e->att, e->mlp, rm, st);
+  launch_rmsnorm_rows(e->x, e->D, e->bb.norm, e->bb.d.eps, e->D, e->h_last, e->D, B, st, pend, e->acc_rows * e->D);
 }
 
 void enqueue_head(csm_engine* e, hipStream_t st) {
@@ -288,6 +319,7 @@ void enqueue_head(csm_engine* e, hipStream_t st) {
     GemvParams g0 = g;  // steps >= 2: layer 0 gathers projection(E_a[c]) from the folded table
     g0.xtab = e->proj_tab; g0.xtab_f32 = 1; g0.xtab_q4_rows = 0;
     RowMap rm = (i == 1) ? RowMap{2, 0, nullptr, 0} : RowMap{1, 0, nullptr, i};
+    const long long* pend = nullptr;  // fused-MLP output of the last decoder layer, read by the head
     if (gemm_mfma_eligible(Dd, D, M, e->wdt) || gemm_mfma_eligible(e->dec.qkv_rows(), Dd, M, e->wdt)) {
       // batched: materialise the gathered rows densely, then every projection runs on the matrix cores
       if (!folded) {
@@ -302,17 +334,17 @@ void enqueue_head(csm_engine* e, hipStream_t st) {
         gr.K = Dd; gr.out = e->dx; gr.os = Dd;
         launch_gather_rows(gr, e->wdt, st);
       }
-      run_stack(e, e->dec, e->dx, M, e->dq, e->datt, e->dmlp, rm, st, nullptr);
+      pend = run_stack(e, e->dec, e->dx, M, e->dq, e->datt, e->dmlp, rm, st, nullptr);
     } else if (folded && e->use_qkv0_tab && e->qkv0_built) {
       AttnParams a0{};
       a0.g_tab = e->qkv0_tab + (size_t)(i - 1) * V * e->dec.qkv_rows(); a0.g_row = e->dec.qkv_rows();
       a0.g_part = g.xpart; a0.g_part_stride = g.xpart_stride; a0.g_part_n = g.xpart_n; a0.g_V = V;
       a0.g_codes = e->codes; a0.g_codes_K = K; a0.g_cb = i - 1;
       a0.g_xtab = e->proj_tab + (size_t)(i - 1) * V * Dd; a0.g_xout = e->dx; a0.g_D = Dd;
-      run_stack(e, e->dec, e->dx, M, e->dq, e->datt, e->dmlp, rm, st, nullptr, &a0);
+      pend = run_stack(e, e->dec, e->dx, M, e->dq, e->datt, e->dmlp, rm, st, nullptr, &a0);
     } else {
       if (!folded) launch_gemv(g, e->wdt, EPI_STORE, 0, st);
-      run_stack(e, e->dec, e->dx, M, e->dq, e->datt, e->dmlp, rm, st, folded ? &g0 : nullptr);
+      pend = run_stack(e, e->dec, e->dx, M, e->dq, e->datt, e->dmlp, rm, st, folded ? &g0 : nullptr);
     }
     // ci_logits = norm(hidden[:, -1]) @ audio_head[i-1]  (generation.py:79)
     g = GemvParams{};
@@ -320,6 +352,10 @@ void enqueue_head(csm_engine* e, hipStream_t st) {
     g.x = e->dx + (i == 1 ? Dd : 0); g.xs = (i == 1 ? 2 * Dd : Dd); g.M = B; g.nw = e->dec.norm;
     g.eps = e->dec.d.eps; g.out = e->ci_logits + (size_t)(i - 1) * B * Vp; g.os = Vp;
     g.part = part(i); g.part_stride = e->part_stride; g.n_valid = V;
+    if (pend) {
+      g.xacc = pend + (i == 1 ? Dd : 0);
+      g.acc_ss = e->acc_rows * Dd;
+    }
     if (!(ablate() & 64)) launch_gemv(g, e->head_wdt, greedy ? EPI_ARGMAX : EPI_STORE, 1, st);
     if (!greedy) {
       sp.logits = e->ci_logits + (size_t)(i - 1) * B * Vp; sp.cb = i; sp.part = part(i);
@@ -381,6 +417,10 @@ void ensure_batch(csm_engine* e, int B) {
   // partial slots per row: enough for any head tiling (c0 / ci heads, dense or q4; >= Vp/2 blocks never occur)
   e->part_stride = (int)(Vp / 2);
   e->part = (unsigned long long*)e->balloc(K * Bm * (size_t)e->part_stride * 8);
+  // fused-MLP accumulators (zeroed here; kept zero between uses by the o_proj that folds them)
+  e->acc_rows = 4;
+  for (Stack* s : {&e->bb, &e->dec})
+    for (int k = 0; k < 2; ++k) s->acc[k] = (long long*)e->balloc((size_t)ACC_SLOTS * e->acc_rows * s->d.hidden * 8);
   // split-K scratch of the MFMA path for every projection shape at its largest row count
   for (Stack* s : {&e->bb, &e->dec}) {
     const int Dm = s->d.hidden, F = s->d.intermediate, rows = (s == &e->bb) ? std::max(e->M_cap, (int)Bm) : 2 * (int)Bm;
@@ -701,6 +741,15 @@ int csm_load_tensor(csm_engine* e, const char* cname, const void* host, int src_
         expect({D, F});
         auto h = conv(numel());
         HIPCHK(hipMemcpy(l.wd, h.data(), h.size(), hipMemcpyHostToDevice));
+        if (l.wdc) {  // fused MLP: columns chunk-major [F/R][D][R] (bf16)
+          const int R = fused_mlp_chunk(D);
+          const uint16_t* src = reinterpret_cast<const uint16_t*>(h.data());
+          std::vector<uint16_t> t2((size_t)D * F);
+          for (int c = 0; c < F / R; ++c)
+            for (int n = 0; n < D; ++n)
+              memcpy(&t2[((size_t)c * D + n) * R], src + (size_t)n * F + (size_t)c * R, R * 2);
+          HIPCHK(hipMemcpy(l.wdc, t2.data(), t2.size() * 2, hipMemcpyHostToDevice));
+        }
       } else if (t == "input_layernorm.weight" || t == "post_attention_layernorm.weight") {
         expect({D});
         auto h = conv_f32(D);
@@ -840,9 +889,10 @@ int csm_prefill(csm_engine* e, int b, int T, const int32_t* tokens, const uint8_
     ep.K = K; ep.D = e->D; ep.out = e->x;
     embed(e, ep, T, e->st);
     RowMap rm{T, b, nullptr, start};
-    run_stack(e, e->bb, e->x, T, e->q, e->att, e->mlp, rm, e->st);
+    const long long* pend = run_stack(e, e->bb, e->x, T, e->q, e->att, e->mlp, rm, e->st);
     launch_rmsnorm_rows(e->x + (size_t)(T - 1) * e->D, e->D, e->bb.norm, e->bb.d.eps, e->D,
-                        e->h_last + (size_t)b * e->D, e->D, 1, e->st);
+                        e->h_last + (size_t)b * e->D, e->D, 1, e->st, pend ? pend + (size_t)(T - 1) * e->D : nullptr,
+                        e->acc_rows * e->D);
     e->pos_host[b] = start + T - 1;  // position of the last processed backbone row
     HIPCHK(hipMemcpyAsync(e->pos + b, &e->pos_host[b], 4, hipMemcpyHostToDevice, e->st));
     HIPCHK(hipStreamSynchronize(e->st));
@@ -1069,6 +1119,10 @@ int csm_set_option(csm_engine* e, const char* key, int value) {
     else if (k == "qkv0_tab") {
       if (!e) throw CsmError(CSM_ERR_ARG, "qkv0_tab needs an engine");
       e->use_qkv0_tab = value != 0;
+    }
+    else if (k == "fuse_mlp") {
+      if (!e) throw CsmError(CSM_ERR_ARG, "fuse_mlp needs an engine");
+      e->fuse_mlp = value != 0;
     }
     else throw CsmError(CSM_ERR_ARG, "unknown option " + k);
     if (e) e->g_B = -1;  // re-capture the frame graphs with the new setting

@@ -6,6 +6,21 @@ enum { WDT_F32 = 0, WDT_BF16 = 1, WDT_Q4 = 2 };  // WDT_Q4: MLX affine int4, gro
 enum { EPI_STORE = 0, EPI_ADD = 1, EPI_SILU_MUL = 2, EPI_QKV = 3, EPI_GELU = 4, EPI_ARGMAX = 5 };
 enum { ATTN_CAUSAL = 0, ATTN_WINDOW = 1, ATTN_BLOCK = 2 };
 
+// Residual contributions of the fused MLP are summed as 64-bit fixed point (units of 2^-32) with
+// integer atomics: integer addition is associative, so the total is independent of block order.
+// The accumulator is replicated ACC_SLOTS times (block c adds into slot c % ACC_SLOTS): the memory-side
+// atomic units serialize adds to one 64-B line, so spreading the F/R blocks over slots divides that
+// serialization; readers sum the slots (integer, exact) in slot order.
+constexpr double ACC_ONE = 4294967296.0;
+constexpr int ACC_SLOTS = 1;  // 8 slots measured slower (184.7 vs 197.9 frames/s fused; consumers pay the slot reads)
+__device__ __forceinline__ float acc_to_f(long long v) { return (float)((double)v * (1.0 / ACC_ONE)); }
+__device__ __forceinline__ long long acc_slots_sum(const long long* a, size_t ss) {
+  long long t = 0;
+#pragma unroll
+  for (int s = 0; s < ACC_SLOTS; ++s) t += a[(size_t)s * ss];
+  return t;
+}
+
 struct GemvParams {
   const void* W;      // [N][K] weight (bf16 or f32)
   int N, K;
@@ -40,6 +55,11 @@ struct GemvParams {
   int xtab_q4_rows;     // int4 weights: total rows of the (quantized) gathered table
   float* x_copy;        // if set: block 0 also stores the raw (un-normed) x rows here [M][K]
   float* qkv_tab;       // EPI_QKV table build: rows [M][(Hq + 2 Hkv) hd] instead of q / KV cache
+  // fused-MLP residual accumulator (64-bit fixed point, ACC_ONE units; see fused_mlp_kernel):
+  const long long* xacc;  // staging reads x + acc (row m at xacc + m * xs, as x): the pending MLP output
+  long long* oacc;        // EPI_ADD: out = (out + acc) + a when oacc_add (else out += a); acc zeroed
+  int oacc_add;
+  int acc_ss;             // elements between accumulator slots
   // MFMA path split-K (set by launch_gemm_mfma): slice partials [ksplit][M][N], sum-of-squares [ksplit][M]
   float* kpart;          // [tile][m chunk][slice][64][33] slice partials (+ sum x^2), written sc1
   unsigned* kticket;     // [tile][m chunk] arrival tickets (zero between launches)
@@ -74,8 +94,24 @@ __device__ __forceinline__ void gemv_epilogue_pair(const GemvParams& p, int m, i
         a *= p.scale[n];
         b *= p.scale[n + 1];
       }
-      o[0] += a;
-      o[1] += b;
+      if (p.oacc) {  // fold the pending fused-MLP output into the residual and clear it
+        long long* ac = p.oacc + (size_t)m * p.os + n;
+        if (p.oacc_add) {
+          o[0] = (o[0] + acc_to_f(acc_slots_sum(ac, p.acc_ss))) + a;
+          o[1] = (o[1] + acc_to_f(acc_slots_sum(ac + 1, p.acc_ss))) + b;
+        } else {
+          o[0] += a;
+          o[1] += b;
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < ACC_SLOTS; ++s2) {
+          ac[(size_t)s2 * p.acc_ss] = 0;
+          ac[(size_t)s2 * p.acc_ss + 1] = 0;
+        }
+      } else {
+        o[0] += a;
+        o[1] += b;
+      }
       break;
     }
     case EPI_ARGMAX: {  // logits (c0 / ci heads); the packed block arg-max is reduced by the caller
@@ -190,8 +226,26 @@ bool dec_attn_oproj_supported(const GemvParams& p, const AttnParams& a, int hd);
 void launch_dec_attn_oproj(const GemvParams& p, const AttnParams& a, int wdt, hipStream_t st, int tag);
 void gemv_set_nt_mask(int mask);
 void gemv_set_xl(int on);
+// xacc (optional): pending fused-MLP accumulator added to x (same layout as x)
 void launch_rmsnorm_rows(const float* x, int xs, const float* w, float eps, int D, float* out, int os, int M,
-                         hipStream_t st);
+                         hipStream_t st, const long long* xacc = nullptr, int acc_ss = 0);
+
+// ---- fused MLP (decode regime, bf16): x + down(silu(gate(norm(x))) * up(norm(x))) in one launch
+struct MlpParams {
+  const float* x;          // [M][xs] residual rows (attention already added)
+  int xs, M;
+  const float* nw;         // post_attention_layernorm weight
+  float eps;
+  const void* wgu;         // [2F][D] gate/up rows interleaved (row 2j gate_j, 2j+1 up_j)
+  const void* wdc;         // down_proj columns chunk-major: [F/R][D][R] (R = fused_mlp_chunk(D))
+  long long* acc;          // [ACC_SLOTS][M][xs] fixed-point accumulator of down(h), zero on entry
+  int F;
+  int acc_ss;              // elements between slots
+};
+int fused_mlp_chunk(int D);                  // intermediate rows per block (0: shape unsupported)
+bool fused_mlp_supported(int D, int F, int M);
+void launch_fused_mlp(const MlpParams& p, int D, bool nt, hipStream_t st);
+bool gemv_nt(int tag);                       // non-temporal weight loads for this stack tag
 void launch_sample(const SampleParams& p, int wdt, int B, hipStream_t st);
 void launch_advance(const AdvanceParams& p, hipStream_t st);
 

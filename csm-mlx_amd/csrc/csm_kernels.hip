@@ -301,10 +301,20 @@ __global__ __launch_bounds__(256) void gemv_xl_kernel(GemvParams p) {
       const WT* xw = g16 ? (const WT*)p.xtab + trow : nullptr;
       const float* xf = gathered ? (const float*)p.xtab + trow : p.x + (size_t)(p.x_step1 ? (i >> 1) : i) * p.xs;
       float* xc = (p.x_copy && blockIdx.x == 0) ? p.x_copy + (size_t)i * p.K : nullptr;
+      const long long* xa = p.xacc ? p.xacc + (size_t)(p.x_step1 ? (i >> 1) : i) * p.xs : nullptr;
       for (int k = tid * 8; k < p.K; k += 256 * 8) {
         float xv[8];
         if (g16) W8<WT>::load(xw + k, xv);
         else W8<float>::load(xf + k, xv);
+        if (xa) {  // residual + the pending fused-MLP output (slots summed in order)
+          long long t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+          for (int s2 = 0; s2 < ACC_SLOTS; ++s2)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) t[j] += xa[(size_t)s2 * p.acc_ss + k + j];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) xv[j] += acc_to_f(t[j]);
+        }
         if (xc) {
           *reinterpret_cast<float4*>(xc + k) = make_float4(xv[0], xv[1], xv[2], xv[3]);
           *reinterpret_cast<float4*>(xc + k + 4) = make_float4(xv[4], xv[5], xv[6], xv[7]);
@@ -817,6 +827,12 @@ __global__ __launch_bounds__(512) void dec_attn_oproj_kernel(GemvParams p, AttnP
         float* o = p.out + (size_t)i * p.os + n;
         o[0] = xs[n] + va;
         o[1] = xs[n + 1] + vb;
+        if (p.oacc) {  // the previous step's last-layer MLP accumulator: consumed, clear it
+          for (int s2 = 0; s2 < ACC_SLOTS; ++s2) {
+            p.oacc[(size_t)s2 * p.acc_ss + (size_t)i * p.os + n] = 0;
+            p.oacc[(size_t)s2 * p.acc_ss + (size_t)i * p.os + n + 1] = 0;
+          }
+        }
       } else {
         gemv_epilogue_pair(p, i, n, va, vb);
       }
@@ -827,18 +843,20 @@ __global__ __launch_bounds__(512) void dec_attn_oproj_kernel(GemvParams p, AttnP
 // ============================================================================ rmsnorm rows
 // out[m] = rmsnorm(x[row(m)]) ; optionally also scatter to dec_in[2m] (decoder step-1 rows).
 __global__ __launch_bounds__(256) void rmsnorm_rows_kernel(const float* x, int xs, const float* w, float eps, int D,
-                                                            float* out, int os) {
+                                                            float* out, int os, const long long* xacc, int acc_ss) {
   __shared__ float red[4];
   const int m = blockIdx.x;
   const float* xr = x + (size_t)m * xs;
+  const long long* xa = xacc ? xacc + (size_t)m * xs : nullptr;
+  auto xv = [&](int d) { return xa ? xr[d] + acc_to_f(acc_slots_sum(xa + d, acc_ss)) : xr[d]; };
   float ss = 0.f;
-  for (int d = threadIdx.x; d < D; d += blockDim.x) ss += xr[d] * xr[d];
+  for (int d = threadIdx.x; d < D; d += blockDim.x) ss += xv(d) * xv(d);
   ss = wave_sum(ss);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
   __syncthreads();
   const float tot = red[0] + red[1] + red[2] + red[3];
   const float sc = rsqrtf(tot / (float)D + eps);
-  for (int d = threadIdx.x; d < D; d += blockDim.x) out[(size_t)m * os + d] = xr[d] * sc * w[d];
+  for (int d = threadIdx.x; d < D; d += blockDim.x) out[(size_t)m * os + d] = xv(d) * sc * w[d];
 }
 
 // ============================================================================ sampling
@@ -1142,8 +1160,174 @@ void launch_attn(const AttnParams& p, int hd, hipStream_t st) {
 }
 
 void launch_rmsnorm_rows(const float* x, int xs, const float* w, float eps, int D, float* out, int os, int M,
-                         hipStream_t st) {
-  hipLaunchKernelGGL(rmsnorm_rows_kernel, dim3(M), dim3(256), 0, st, x, xs, w, eps, D, out, os);
+                         hipStream_t st, const long long* xacc, int acc_ss) {
+  hipLaunchKernelGGL(rmsnorm_rows_kernel, dim3(M), dim3(256), 0, st, x, xs, w, eps, D, out, os, xacc, acc_ss);
+}
+
+// ============================================================================ fused MLP (decode)
+// One Llama MLP (mlx_lm MLP wired by models.py:50-51) for M <= MT rows in ONE launch:
+//   x += down(silu(gate(norm2(x))) * up(norm2(x)))
+// Block c owns R consecutive intermediate rows j (gate/up weight rows 2j, 2j+1 -- the engine's
+// interleaved layout) and the matching R columns of down_proj, re-laid chunk-major at load
+// (wdc[c][n][0..R)).  (1) Every weight byte of the block (2R gate/up rows, D x R down slice) is put
+// in flight first; (2) x * norm weight is staged in LDS exactly as gemv_xl_kernel stages it, and the
+// gate/up dots use its K-slicing, wave reduction and epilogue (G = 64): h is bit-identical to the
+// two-launch path; (3) h (R values per row) goes to LDS; (4) the block's partial down product for
+// all D outputs is added to a 64-bit fixed-point accumulator (units 2^-32) with integer atomics --
+// associative, so the sum over the F/R blocks is deterministic whatever the arrival order.  The
+// next reader of the residual (QKV / head staging, final norm) adds the accumulator; the next
+// o_proj folds it into x and zeroes it (GemvParams::xacc / oacc).  Saves the down launch and the
+// h round trip through HBM/L2 per layer.
+template <int D, int R, int MT, bool NT>
+__global__ __launch_bounds__(256) void fused_mlp_kernel(MlpParams p) {
+  constexpr int G = 64, NG = 4, RPT = 2 * R / NG;  // one wave per group of RPT gate/up rows
+  constexpr int KS = D / (G * 8);                   // K steps per lane
+  constexpr int NQ = D / 256;                       // down outputs per thread
+  constexpr int LN = R / 8;                         // 16-B loads per down row slice
+  static_assert(RPT % 2 == 0 && KS >= 1 && NQ >= 1 && LN >= 1, "fused MLP tiling");
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  __shared__ __attribute__((aligned(16))) float xl[MT][D];
+  __shared__ float rss[4][MT];
+  __shared__ float hs[MT][R];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c = blockIdx.x;
+  const int row0 = c * 2 * R + wave * RPT;
+  // (1) all weight loads in flight
+  const bf16_t* Wg = (const bf16_t*)p.wgu;
+  Raw8<bf16_t> wr[KS][RPT];
+#pragma unroll
+  for (int s = 0; s < KS; ++s)
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) wr[s][r].template load<NT>(Wg + (size_t)(row0 + r) * D + lane * 8 + s * G * 8);
+  const bf16_t* Wd = (const bf16_t*)p.wdc + (size_t)c * D * R;
+  u32x4 wd[NQ][LN];
+#pragma unroll
+  for (int q = 0; q < NQ; ++q)
+#pragma unroll
+    for (int l = 0; l < LN; ++l) {
+      const u32x4* src = reinterpret_cast<const u32x4*>(Wd + (size_t)(tid + 256 * q) * R + l * 8);
+      if constexpr (NT) wd[q][l] = __builtin_nontemporal_load(src);
+      else wd[q][l] = *src;
+    }
+  // (2) stage x * nw (gemv_xl_kernel (2b), dense rows)
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    float ssp = 0.f;
+    if (i < p.M) {
+      const float* xf = p.x + (size_t)i * p.xs;
+      for (int k = tid * 8; k < D; k += 256 * 8) {
+        float xv[8], nw[8];
+        W8<float>::load(xf + k, xv);
+        W8<float>::load(p.nw + k, nw);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          ssp = fmaf(xv[j], xv[j], ssp);
+          xv[j] *= nw[j];
+        }
+        *reinterpret_cast<float4*>(&xl[i][k]) = make_float4(xv[0], xv[1], xv[2], xv[3]);
+        *reinterpret_cast<float4*>(&xl[i][k + 4]) = make_float4(xv[4], xv[5], xv[6], xv[7]);
+      }
+    }
+    const float v = wave_sum(ssp);
+    if (lane == 0) rss[wave][i] = v;
+  }
+  __syncthreads();
+  // (3) gate/up dots from LDS, wave reduction, SiLU(gate) * up -> hs
+  float acc[MT][RPT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) acc[i][r] = 0.f;
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int k = lane * 8 + s * G * 8;
+    float w[RPT][8];
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) wr[s][r].get(w[r]);
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      if (i < p.M) {
+        const float4 x0 = *reinterpret_cast<const float4*>(&xl[i][k]);
+        const float4 x1 = *reinterpret_cast<const float4*>(&xl[i][k + 4]);
+        const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+        for (int r = 0; r < RPT; ++r)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) acc[i][r] = fmaf(w[r][j], xv[j], acc[i][r]);
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int r = 0; r < RPT; ++r) acc[i][r] = wave_sum(acc[i][r]);
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      if (i < p.M) {
+        const float sq = (rss[0][i] + rss[1][i]) + (rss[2][i] + rss[3][i]);
+        const float sc = rsqrtf(sq / (float)D + p.eps);
+#pragma unroll
+        for (int rp = 0; rp < RPT; rp += 2) {
+          const float a = (0.f + acc[i][rp]) * sc, b = (0.f + acc[i][rp + 1]) * sc;
+          hs[i][(wave * RPT + rp) >> 1] = silu_f(a) * b;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // (4) partial down product of this block's R intermediate rows -> fixed-point atomics
+#pragma unroll
+  for (int q = 0; q < NQ; ++q) {
+    const int n = tid + 256 * q;
+    float wf[R];
+#pragma unroll
+    for (int l = 0; l < LN; ++l) {
+      const u32x4 u = wd[q][l];
+      wf[l * 8 + 0] = bf16_lo(u.x); wf[l * 8 + 1] = bf16_hi(u.x); wf[l * 8 + 2] = bf16_lo(u.y);
+      wf[l * 8 + 3] = bf16_hi(u.y); wf[l * 8 + 4] = bf16_lo(u.z); wf[l * 8 + 5] = bf16_hi(u.z);
+      wf[l * 8 + 6] = bf16_lo(u.w); wf[l * 8 + 7] = bf16_hi(u.w);
+    }
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      if (i < p.M) {
+        float pv = 0.f;
+#pragma unroll
+        for (int j = 0; j < R; ++j) pv = fmaf(wf[j], hs[i][j], pv);
+        const long long fx = __double2ll_rn((double)pv * ACC_ONE);
+        if (p.F > 0)
+          atomicAdd(reinterpret_cast<unsigned long long*>(p.acc + (size_t)(c % ACC_SLOTS) * p.acc_ss + (size_t)i * p.xs + n),
+                    (unsigned long long)fx);
+        else if (fx == 0x123456789ll) p.acc[0] = fx;  // lab: atomics skipped (results invalid)
+      }
+    }
+  }
+}
+
+int fused_mlp_chunk(int D) { return D == 1024 ? 16 : (D == 2048 ? 8 : 0); }
+
+bool fused_mlp_supported(int D, int F, int M) {
+  const int R = fused_mlp_chunk(D);
+  return R && M >= 1 && M <= 4 && F % R == 0;
+}
+
+bool gemv_nt(int tag) { return (gemv_nt_mask() >> tag) & 1; }
+
+static bool g_mlp_lab_noatomic = [] { const char* e = getenv("CSM_LAB_MLP_NOATOMIC"); return e && e[0] == '1'; }();
+
+void launch_fused_mlp(const MlpParams& p0, int D, bool nt, hipStream_t st) {
+  const int R = fused_mlp_chunk(D);
+  const dim3 grid(p0.F / R);
+  MlpParams p = p0;
+  if (g_mlp_lab_noatomic) p.F = -p.F;
+#define FM_L(D_, R_, MT_) do { if (nt) hipLaunchKernelGGL((fused_mlp_kernel<D_, R_, MT_, true>), grid, dim3(256), 0, st, p); \
+                               else hipLaunchKernelGGL((fused_mlp_kernel<D_, R_, MT_, false>), grid, dim3(256), 0, st, p); } while (0)
+  if (D == 1024) {
+    if (p.M == 1) FM_L(1024, 16, 1); else FM_L(1024, 16, 4);
+  } else {
+    if (p.M == 1) FM_L(2048, 8, 1); else FM_L(2048, 8, 4);
+  }
+#undef FM_L
 }
 
 void launch_sample(const SampleParams& p, int wdt, int B, hipStream_t st) {

@@ -212,3 +212,28 @@ def test_folded_layer0_qkv_table_matches_gemv(tiny, which, dtype):
     assert np.array_equal(n_got, n_ref)
     assert np.array_equal(got, ref), f"first diff at {np.argwhere(got != ref)[0]}"
     del model
+
+
+def test_fused_mlp_matches_two_launches():
+    """One-launch MLP (gate/up + SiLU*up + down with a 64-bit fixed-point accumulator) against the
+    gate/up + down launches: h is bit-identical, the down sum differs only in rounding (< 1e-6
+    relative), so codes must match (bf16 weights, B = 2: decoder step 1 runs 4 rows)."""
+    from csm_mlx import _lib
+    from csm_mlx.generation import generate_codes_batch
+    from csm_mlx.sampling import Sampler
+    from csm_mlx.tokenizers import tokenize_text_segment
+    args, w = csm_weights("1b")  # the tiny widths (256) have no fused-MLP tiling
+    model = _model(args, w, "bf16", max_batch=2)
+    K = args.n_audio_codebooks
+    ids = [prompt_ids(60 + b) for b in range(2)]
+    prompts = [tokenize_text_segment(i, 0, K) for i in ids]
+    L = _lib.lib()
+    _lib.check(L.csm_set_option(model.engine, b"fuse_mlp", 0))
+    ref, n_ref, _ = generate_codes_batch(model, prompts, 6, sampler=Sampler(0.0, 0))
+    _lib.check(L.csm_set_option(model.engine, b"fuse_mlp", 1))
+    got, n_got, _ = generate_codes_batch(model, prompts, 6, sampler=Sampler(0.0, 0))
+    assert np.array_equal(n_got, n_ref)
+    assert np.array_equal(got, ref), f"first diff at {np.argwhere(got != ref)[0]}"
+    got2, _, _ = generate_codes_batch(model, prompts, 6, sampler=Sampler(0.0, 0))
+    assert np.array_equal(got2, got), "fused MLP must be deterministic run to run"
+    del model
