@@ -22,33 +22,45 @@ __global__ __launch_bounds__(256) void gemm64_kernel(P p) {
   for (int r = 0; r < 4; ++r)
 #pragma unroll
     for (int c = 0; c < 4; ++c) acc[r][c] = 0.f;
-  for (int k0 = 0; k0 < KD; k0 += 16) {
+  // the next K tile is fetched into registers while the current one is multiplied (one tile of
+  // prefetch hides the global-load latency that a load -> sync -> compute loop exposes per step)
+  float va[4], vb[4];
+  auto fetch = [&](int k0) {
     {
       const int i = tid >> 2, kb = (tid & 3) * 4;
-      float v[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        v[e] = (i0 + i < p.M && k0 + kb + e < KD) ? p.a(z, i0 + i, k0 + kb + e) : 0.f;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) As[kb + e][i] = v[e];
+        va[e] = (i0 + i < p.M && k0 + kb + e < KD) ? p.a(z, i0 + i, k0 + kb + e) : 0.f;
     }
     if constexpr (P::B_KCONTIG) {
       const int j = tid >> 2, kb = (tid & 3) * 4;
-      float v[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        v[e] = (j0 + j < p.N && k0 + kb + e < KD) ? p.b(z, k0 + kb + e, j0 + j) : 0.f;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) Bs[kb + e][j] = v[e];
+        vb[e] = (j0 + j < p.N && k0 + kb + e < KD) ? p.b(z, k0 + kb + e, j0 + j) : 0.f;
     } else {
       const int kk = tid >> 4, jb = (tid & 15) * 4;
-      float v[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        v[e] = (k0 + kk < KD && j0 + jb + e < p.N) ? p.b(z, k0 + kk, j0 + jb + e) : 0.f;
-      *reinterpret_cast<float4*>(&Bs[kk][jb]) = make_float4(v[0], v[1], v[2], v[3]);
+        vb[e] = (k0 + kk < KD && j0 + jb + e < p.N) ? p.b(z, k0 + kk, j0 + jb + e) : 0.f;
+    }
+  };
+  fetch(0);
+  for (int k0 = 0; k0 < KD; k0 += 16) {
+    {
+      const int i = tid >> 2, kb = (tid & 3) * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) As[kb + e][i] = va[e];
+    }
+    if constexpr (P::B_KCONTIG) {
+      const int j = tid >> 2, kb = (tid & 3) * 4;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) Bs[kb + e][j] = vb[e];
+    } else {
+      const int kk = tid >> 4, jb = (tid & 15) * 4;
+      *reinterpret_cast<float4*>(&Bs[kk][jb]) = make_float4(vb[0], vb[1], vb[2], vb[3]);
     }
     __syncthreads();
+    if (k0 + 16 < KD) fetch(k0 + 16);
 #pragma unroll
     for (int kk = 0; kk < 16; ++kk) {
       const float4 a = *reinterpret_cast<const float4*>(&As[kk][ty * 4]);
