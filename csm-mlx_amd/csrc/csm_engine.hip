@@ -430,6 +430,8 @@ void ensure_batch(csm_engine* e, int B) {
     gemm_reserve(Dm, F, rows);
   }
   gemm_reserve((int)Dd, (int)D, 2 * (int)Bm);
+  gemm_reserve((int)Vp, (int)D, (int)Bm);   // c0 head
+  gemm_reserve((int)Vp, (int)Dd, (int)Bm);  // ci heads
 }
 
 // proj_tab[cb] = projection(E_a rows of codebook cb), computed by the projection GEMV itself

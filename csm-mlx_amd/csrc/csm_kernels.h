@@ -61,7 +61,7 @@ struct GemvParams {
   int oacc_add;
   int acc_ss;             // elements between accumulator slots
   // MFMA path split-K (set by launch_gemm_mfma): slice partials [ksplit][M][N], sum-of-squares [ksplit][M]
-  float* kpart;          // [tile][m chunk][slice][64][33] slice partials (+ sum x^2), written sc1
+  float* kpart;          // [tile][m chunk][slice][slab] split-K slice partials (+ sum x^2), written sc1
   unsigned* kticket;     // [tile][m chunk] arrival tickets (zero between launches)
   int ksplit;
 };

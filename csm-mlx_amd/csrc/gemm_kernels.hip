@@ -371,13 +371,15 @@ __global__ __launch_bounds__(256) void gemm_bf16_wk_kernel(GemvParams p) {
 }
 
 // Variant "pipe" (default): the block's weight tile AND activation tile go through LDS with
-// coalesced global loads, double-buffered so stage c+1's loads are in flight while stage c runs on
-// the matrix cores.  Block = 64 weight rows x 32*MT batch rows over one K slice, stages of 64 K
+// coalesced global loads into a register ring of PD stages (loads of stages c+1..c+PD in flight
+// while stage c runs on the matrix cores from a double-buffered LDS tile; PD = 1 / 2 / 4 by the
+// stage count).  Block = 64 weight rows x 32*MT batch rows over one K slice, stages of 64 K
 // (4 MFMA steps); every fragment is stored in MFMA-lane order (one conflict-free ds_read_b128 per
 // operand).  MT = 2: 2 x 2 waves over (row tile, batch tile); MT = 1: 2 waves per row tile split
 // each stage's K steps and are summed in a fixed order.  int4 weights (Q4) are dequantized while
 // staging (w = scale * q + bias in fp32, split hi/lo like the activations) and run three products
-// (hi*hi, hi*lo, lo*hi).  Split-K fixup and epilogues as the kernels above.
+// (hi*hi, hi*lo, lo*hi).  Split-K fixup as the kernels above, except the combine (gp_combine: 16-B
+// loads, 16 in flight per thread); arg-max heads are split too (the last slice runs the arg-max).
 constexpr int GP_ROWS = 64, GP_KC = 64;
 typedef unsigned short u16x4_t __attribute__((ext_vector_type(4)));
 
@@ -392,7 +394,53 @@ __device__ __forceinline__ void split4(const float (&v)[4], u32x2_t& hi, u32x2_t
   lo = u32x2_t{l[0] | ((unsigned)l[1] << 16), l[2] | ((unsigned)l[3] << 16)};
 }
 
-template <bool Q4, int MT, bool NT>
+// Split-K combine of the pipe kernel (the last slice of a tile to arrive): every slice's partial is
+// read with 16-B sc1 buffer loads, KS * U of them in flight per thread before the first add (one
+// round trip per 4096 floats at U * KS = 16), and summed in slice order (deterministic, the same
+// order as slab_sum).
+constexpr int GP_RSRC3 = 0x00020000;  // buffer descriptor word 3 (raw 32-bit format)
+constexpr int GP_SC1 = 16;            // cache policy: sc1 (agent-coherent, as __hip_atomic_load/store)
+template <int KS, int NB>
+__device__ __forceinline__ void gp_combine(__amdgpu_buffer_rsrc_t rs, float (*ct)[GP_ROWS + 1], float* ssb,
+                                           int mrows, bool norm, int slab_f, int tid) {
+  constexpr int U = KS >= 16 ? 1 : 16 / KS;
+  const int nq = mrows * (GP_ROWS / 4);
+  for (int q0 = tid; q0 < nq; q0 += 256 * U) {
+    f32x4_t v[U][KS];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int q = min(q0 + 256 * u, nq - 1);
+#pragma unroll
+      for (int s = 0; s < KS; ++s) v[u][s] = __builtin_amdgcn_raw_buffer_load_b128(rs, q * 16, s * slab_f * 4, GP_SC1);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int q = q0 + 256 * u;
+      if (q < nq) {
+        f32x4_t sum = v[u][0];
+#pragma unroll
+        for (int s = 1; s < KS; ++s) sum += v[u][s];
+        const int ml = q / (GP_ROWS / 4), j = (q % (GP_ROWS / 4)) * 4;
+        ct[ml][j] = sum.x;
+        ct[ml][j + 1] = sum.y;
+        ct[ml][j + 2] = sum.z;
+        ct[ml][j + 3] = sum.w;
+      }
+    }
+  }
+  if (norm && tid < mrows) {
+    float v[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s)
+      v[s] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (NB * GP_ROWS + tid) * 4, s * slab_f * 4, GP_SC1));
+    float sum = v[0];
+#pragma unroll
+    for (int s = 1; s < KS; ++s) sum += v[s];
+    ssb[tid] = sum;
+  }
+}
+
+template <bool Q4, int MT, bool NT, int PD>
 __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemvParams p) {
   constexpr int NB = MT * 32, NA = Q4 ? 2 : 1;
   constexpr int A_BYTES = 2 * NA * 2 * 4 * 64 * 16, B_BYTES = 2 * 2 * MT * 4 * 64 * 16;
@@ -422,37 +470,48 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemvParams p) {
   float ss[NB / 16];
 #pragma unroll
   for (int i = 0; i < NB / 16; ++i) ss[i] = 0.f;
-  u32x4_t ar[2];
-  uint32_t asb = 0;
-  f32x4_t xr[NB / 16];
-  f32x4_t nwr = {1.f, 1.f, 1.f, 1.f};
-  auto load = [&](int kc) {
+  // register ring: PD stages in flight while one is multiplied (nst % PD == 0, host-checked)
+  struct Stage {
+    u32x4_t ar[2];
+    uint32_t asb;
+    f32x4_t xr[NB / 16];
+    f32x4_t nwr;
+  };
+  Stage sg[PD];
+  // stage st >= nst is a placeholder: weights from the (L2-hot) activation row, nothing used
+  const float* nwp = norm ? p.nw : p.x;
+  auto load = [&](int st, Stage& g) {
+    const bool junk = st >= nst;
+    const int kc = kslice + min(st, nst - 1) * GP_KC;
     if (a_on) {
       if constexpr (Q4) {
-        const u32x4_t* src = reinterpret_cast<const u32x4_t*>(Wq + a_grow * (p.K / 2) + (kc + 32 * a_seg) / 2);
-        ar[0] = NT ? __builtin_nontemporal_load(src) : *src;
-        asb = SB[a_grow * (p.K / Q4_GROUP) + kc / Q4_GROUP];
+        const u32x4_t* src = junk ? reinterpret_cast<const u32x4_t*>(p.x)
+                                  : reinterpret_cast<const u32x4_t*>(Wq + a_grow * (p.K / 2) + (kc + 32 * a_seg) / 2);
+        g.ar[0] = NT ? __builtin_nontemporal_load(src) : *src;
+        const uint32_t* sbp = junk ? reinterpret_cast<const uint32_t*>(p.x) : SB + a_grow * (p.K / Q4_GROUP) + kc / Q4_GROUP;
+        g.asb = *sbp;
       } else {
-        const u32x4_t* src = reinterpret_cast<const u32x4_t*>((const bf16_t*)p.W + a_grow * p.K + kc + 16 * a_seg);
-        ar[0] = NT ? __builtin_nontemporal_load(src) : src[0];
-        ar[1] = NT ? __builtin_nontemporal_load(src + 1) : src[1];
+        const u32x4_t* src = junk ? reinterpret_cast<const u32x4_t*>(p.x)
+                                  : reinterpret_cast<const u32x4_t*>((const bf16_t*)p.W + a_grow * p.K + kc + 16 * a_seg);
+        g.ar[0] = NT ? __builtin_nontemporal_load(src) : src[0];
+        g.ar[1] = NT ? __builtin_nontemporal_load(src + 1) : src[1];
       }
     }
 #pragma unroll
     for (int i = 0; i < NB / 16; ++i) {
       const int m = min(m0 + x_c + 16 * i, p.M - 1);
-      xr[i] = *(const gcf32x4*)(p.x + (size_t)m * p.xs + kc + x_k4);
+      g.xr[i] = *(const gcf32x4*)(p.x + (size_t)m * p.xs + kc + x_k4);
     }
-    if (norm) nwr = *(const gcf32x4*)(p.nw + kc + x_k4);
+    g.nwr = *(const gcf32x4*)(nwp + kc + x_k4);
   };
-  auto store = [&](int buf) {
+  auto store = [&](const Stage& g, int buf, bool live) {
     if (a_on) {
       const int t = a_row >> 5, ln = a_row & 31;
       if constexpr (Q4) {
-        const float sc = bf16_lo(asb), bi = bf16_hi(asb);
+        const float sc = bf16_lo(g.asb), bi = bf16_hi(g.asb);
 #pragma unroll
         for (int w = 0; w < 4; ++w) {  // 8 consecutive k per word: step 2*seg + w/2, half w&1
-          const uint32_t u = ar[0][w];
+          const uint32_t u = g.ar[0][w];
           float v[8];
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[j] = fmaf(sc, (float)((u >> (4 * j)) & 15u), bi);
@@ -465,20 +524,20 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemvParams p) {
           As(buf, 1, t, s)[ln + 32 * hh] = u32x4_t{l0.x, l0.y, l1.x, l1.y};
         }
       } else {
-        As(buf, 0, t, a_seg)[ln] = ar[0];
-        As(buf, 0, t, a_seg)[ln + 32] = ar[1];
+        As(buf, 0, t, a_seg)[ln] = g.ar[0];
+        As(buf, 0, t, a_seg)[ln + 32] = g.ar[1];
       }
     }
     const int s = x_k4 >> 4, hh = (x_k4 >> 3) & 1, j0 = x_k4 & 7;
 #pragma unroll
     for (int i = 0; i < NB / 16; ++i) {
       const int c = x_c + 16 * i;
-      float v[4] = {xr[i].x, xr[i].y, xr[i].z, xr[i].w};
+      float v[4] = {g.xr[i].x, g.xr[i].y, g.xr[i].z, g.xr[i].w};
       if (norm) {
-        const float nw4[4] = {nwr.x, nwr.y, nwr.z, nwr.w};
+        const float nw4[4] = {g.nwr.x, g.nwr.y, g.nwr.z, g.nwr.w};
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          ss[i] = fmaf(v[q], v[q], ss[i]);
+          ss[i] = live ? fmaf(v[q], v[q], ss[i]) : ss[i];
           v[q] *= nw4[q];
         }
       }
@@ -490,28 +549,32 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemvParams p) {
     }
   };
   f32x16_t acc = f32x16_t{};
-  load(kslice);
-  store(0);
-  __syncthreads();
-  for (int it = 0; it < nst; ++it) {
-    const int buf = it & 1;
-    if (it + 1 < nst) load(kslice + (it + 1) * GP_KC);
-    const int s0 = MT == 2 ? 0 : 2 * wc, s1 = MT == 2 ? 4 : 2 * wc + 2;
-    const int bt = MT == 2 ? wc : 0;
 #pragma unroll
-    for (int s = s0; s < s1; ++s) {
-      const bf16x8_t a = __builtin_bit_cast(bf16x8_t, As(buf, 0, wr, s)[lane]);
-      const bf16x8_t bh = __builtin_bit_cast(bf16x8_t, Bs(buf, 0, bt, s)[lane]);
-      const bf16x8_t bl = __builtin_bit_cast(bf16x8_t, Bs(buf, 1, bt, s)[lane]);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bh, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bl, acc, 0, 0, 0);
-      if constexpr (Q4) {
-        const bf16x8_t al = __builtin_bit_cast(bf16x8_t, As(buf, 1, wr, s)[lane]);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
+  for (int d = 0; d < PD; ++d) load(d, sg[d]);
+  store(sg[0], 0, true);
+  __syncthreads();
+  const int s0 = MT == 2 ? 0 : 2 * wc, s1 = MT == 2 ? 4 : 2 * wc + 2;
+  const int bt = MT == 2 ? wc : 0;
+  for (int it0 = 0; it0 < nst; it0 += PD) {
+#pragma unroll
+    for (int d = 0; d < PD; ++d) {
+      const int it = it0 + d, buf = it & 1;
+      load(it + PD, sg[d]);  // slot d's stage (it) is already in LDS
+#pragma unroll
+      for (int s = s0; s < s1; ++s) {
+        const bf16x8_t a = __builtin_bit_cast(bf16x8_t, As(buf, 0, wr, s)[lane]);
+        const bf16x8_t bh = __builtin_bit_cast(bf16x8_t, Bs(buf, 0, bt, s)[lane]);
+        const bf16x8_t bl = __builtin_bit_cast(bf16x8_t, Bs(buf, 1, bt, s)[lane]);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bh, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bl, acc, 0, 0, 0);
+        if constexpr (Q4) {
+          const bf16x8_t al = __builtin_bit_cast(bf16x8_t, As(buf, 1, wr, s)[lane]);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
+        }
       }
+      store(sg[(d + 1) % PD], buf ^ 1, it + 1 < nst);  // the last one stores a placeholder
+      __syncthreads();
     }
-    if (it + 1 < nst) store(buf ^ 1);
-    __syncthreads();
   }
   // sum of squares per batch row: the 16 threads of a row share it
   if (norm) {
@@ -536,14 +599,17 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemvParams p) {
   __syncthreads();
   const int mrows = min(NB, p.M - m0);
   if (p.ksplit > 1) {
-    const size_t slab_f = (size_t)NB * (GP_ROWS + 1);
-    gfloat* slab = (gfloat*)p.kpart + ((size_t)(tile * nchunks + mc) * p.ksplit) * slab_f;
-    gfloat* mine = slab + (size_t)blockIdx.y * slab_f;
-    for (int e = tid; e < mrows * (GP_ROWS + 1); e += 256) {
-      const int ml = e / (GP_ROWS + 1), j = e % (GP_ROWS + 1);
-      __hip_atomic_store(mine + e, j < GP_ROWS ? ct[ml][j] : (norm ? ssb[ml] : 0.f), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
+    // slice partial = [NB][64] tile values, then [NB] sums of squares; 16-B write-through stores
+    const int slab_f = NB * (GP_ROWS + 1);
+    float* slab = p.kpart + ((size_t)(tile * nchunks + mc) * p.ksplit) * slab_f;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(slab, 0, p.ksplit * slab_f * 4, GP_RSRC3);
+    const int mine = blockIdx.y * slab_f * 4;
+    for (int q = tid; q < mrows * (GP_ROWS / 4); q += 256) {
+      const int ml = q / (GP_ROWS / 4), j = (q % (GP_ROWS / 4)) * 4;
+      const f32x4_t v = {ct[ml][j], ct[ml][j + 1], ct[ml][j + 2], ct[ml][j + 3]};
+      __builtin_amdgcn_raw_buffer_store_b128(v, rs, q * 16, mine, GP_SC1);
     }
+    if (norm && tid < mrows) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ssb[tid]), rs, (NB * GP_ROWS + tid) * 4, mine, GP_SC1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
@@ -554,11 +620,11 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemvParams p) {
     }
     __syncthreads();
     if (!last) return;
-    for (int e = tid; e < mrows * (GP_ROWS + 1); e += 256) {
-      const float v = slab_sum(slab, slab_f, e, p.ksplit);
-      const int ml = e / (GP_ROWS + 1), j = e % (GP_ROWS + 1);
-      if (j < GP_ROWS) ct[ml][j] = v;
-      else ssb[ml] = v;
+    switch (p.ksplit) {
+      case 2: gp_combine<2, NB>(rs, ct, ssb, mrows, norm, slab_f, tid); break;
+      case 4: gp_combine<4, NB>(rs, ct, ssb, mrows, norm, slab_f, tid); break;
+      case 8: gp_combine<8, NB>(rs, ct, ssb, mrows, norm, slab_f, tid); break;
+      default: gp_combine<16, NB>(rs, ct, ssb, mrows, norm, slab_f, tid); break;
     }
     __syncthreads();
   }
@@ -604,20 +670,25 @@ static int gemm_variant() {  // 2 = "pipe" (default), 0 = "wk" (CSM_GEMM=wk), 1 
 }
 static int gemm_rows() { return gemm_variant() == 1 ? GM_WROWS : (gemm_variant() == 2 ? GP_ROWS : GW_ROWS); }
 constexpr int GW_PF = 4;  // wk: MFMA steps in flight per wave
-// pipe: K slices are added until the grid has this many blocks (several blocks per CU hide each
-// block's one-stage-deep pipeline); CSM_PIPE_BLOCKS overrides (lab sweeps)
-static int g_pipe_target = [] { const char* e = getenv("CSM_PIPE_BLOCKS"); return e ? atoi(e) : 512; }();
+// pipe: K slices are added until the grid has this many blocks (measured best: 256 for <= 32 batch
+// rows, 512 above -- configs 4 / 5); CSM_PIPE_BLOCKS overrides (lab sweeps)
+static int g_pipe_target_env = [] { const char* e = getenv("CSM_PIPE_BLOCKS"); return e ? atoi(e) : 0; }();
+static int pipe_target(int M) { return g_pipe_target_env > 0 ? g_pipe_target_env : (M > 32 ? 512 : 256); }
+// pipe: deepest register prefetch ring (stages in flight, 1 / 2 / 4: 4 for <= 32 batch rows, 2 above,
+// where the 64-row stages cost twice the registers); CSM_PIPE_PD overrides
+static int g_pipe_pd_env = [] { const char* e = getenv("CSM_PIPE_PD"); return e ? atoi(e) : 0; }();
+static int pipe_pd_cap(int M) { return g_pipe_pd_env > 0 ? g_pipe_pd_env : (M > 32 ? 2 : 4); }
 
 // K slices: doubled while the grid has < 256 blocks (wk: while each wave keeps >= 2 rings of PF
-// steps; lds: up to 8); the arg-max heads keep whole rows.
+// steps; lds: up to 8); wk / lds arg-max heads keep whole rows.
 static void gemm_plan(int N, int K, int M, int epi, int& ks) {
   const int rows = gemm_rows();
   const int tiles = (N + rows - 1) / rows;
   const int chunks = (M + 63) / 64;
   ks = 1;
-  if (epi == EPI_ARGMAX) return;
+  if (epi == EPI_ARGMAX && gemm_variant() != 2) return;  // pipe: the last slice runs the arg-max epilogue
   if (gemm_variant() == 2) {
-    while (tiles * chunks * ks < g_pipe_target && ks < 16 && K % (GP_KC * ks * 2) == 0 && K / (ks * 2) >= 2 * GP_KC) ks *= 2;
+    while (tiles * chunks * ks < pipe_target(M) && ks < 16 && K % (GP_KC * ks * 2) == 0 && K / (ks * 2) >= 2 * GP_KC) ks *= 2;
   } else if (gemm_variant() == 1) {
     while (tiles * chunks * ks < 256 && ks < 8 && K % (GM_KS * ks * 2) == 0) ks *= 2;
   } else {
@@ -668,11 +739,16 @@ void launch_gemm_mfma(const GemvParams& p0, int wdt, bool nt, hipStream_t st) {
   if (gemm_variant() == 2) {  // pipe: batch chunks of 64 (MT 2) or one chunk of 32 (MT 1) on grid.z
     const int MT = p.M > 32 ? 2 : 1;
     const dim3 g3(gemm_blocks(p.N), ks, (p.M + MT * 32 - 1) / (MT * 32));
-#define GP_L(Q_, MT_) do { if (nt) hipLaunchKernelGGL((gemm_pipe_kernel<Q_, MT_, true>), g3, dim3(256), 0, st, p); \
-                          else hipLaunchKernelGGL((gemm_pipe_kernel<Q_, MT_, false>), g3, dim3(256), 0, st, p); } while (0)
+    const int nst = p.K / ks / GP_KC;
+    const int cap = pipe_pd_cap(p.M);
+    const int pd = (nst % 4 == 0 && cap >= 4) ? 4 : ((nst % 2 == 0 && cap >= 2) ? 2 : 1);
+#define GP_K(Q_, MT_, PD_) do { if (nt) hipLaunchKernelGGL((gemm_pipe_kernel<Q_, MT_, true, PD_>), g3, dim3(256), 0, st, p); \
+                                else hipLaunchKernelGGL((gemm_pipe_kernel<Q_, MT_, false, PD_>), g3, dim3(256), 0, st, p); } while (0)
+#define GP_L(Q_, MT_) do { if (pd == 4) GP_K(Q_, MT_, 4); else if (pd == 2) GP_K(Q_, MT_, 2); else GP_K(Q_, MT_, 1); } while (0)
     if (p_is_q4) { if (MT == 2) GP_L(true, 2); else GP_L(true, 1); }
     else { if (MT == 2) GP_L(false, 2); else GP_L(false, 1); }
 #undef GP_L
+#undef GP_K
     return;
   }
   const dim3 grid(gemm_blocks(p.N), ks);
