@@ -72,6 +72,28 @@ __device__ __forceinline__ unsigned long long pack_argmax(float v, int idx) {
   return ((unsigned long long)key << 32) | (unsigned long long)(0xFFFFFFFFu - (uint32_t)idx);
 }
 __device__ __forceinline__ int unpack_argmax(unsigned long long p) { return (int)(0xFFFFFFFFu - (uint32_t)p); }
+// Arg-max over n packed block partials pp[0..n) by one wave: each lane's loads (up to 16 per round)
+// are all issued before the first compare -- one memory round trip for a head's ~500 partials --
+// then a shuffle max.  Every lane returns the result.
+__device__ __forceinline__ unsigned long long wave_argmax_partials(const unsigned long long* pp, int n, int lane) {
+  unsigned long long best = 0;
+  for (int i0 = 0; i0 < n; i0 += 64 * 16) {
+    unsigned long long v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int i = i0 + lane + 64 * u;
+      v[u] = i < n ? pp[i] : 0ull;
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) best = v[u] > best ? v[u] : best;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long v = __shfl_xor(best, o, 64);
+    best = v > best ? v : best;
+  }
+  return best;
+}
 
 // Pair epilogue shared by every GEMV kernel (rows n, n+1 of output row m).
 __device__ __forceinline__ void gemv_epilogue_pair(const GemvParams& p, int m, int n, float a, float b) {

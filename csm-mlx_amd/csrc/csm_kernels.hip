@@ -86,16 +86,7 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvParams p) {
     for (int m = wave; m < p.M; m += 4) {
       const int bb = p.x_step1 ? (m >> 1) : m;
       if (p.x_step1 && !(m & 1)) continue;
-      unsigned long long best = 0;
-      for (int i = lane; i < p.xpart_n; i += 64) {
-        const unsigned long long v = p.xpart[(size_t)bb * p.xpart_stride + i];
-        best = v > best ? v : best;
-      }
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        const unsigned long long v = __shfl_xor(best, o, 64);
-        best = v > best ? v : best;
-      }
+      const unsigned long long best = wave_argmax_partials(p.xpart + (size_t)bb * p.xpart_stride, p.xpart_n, lane);
       if (lane == 0) {
         const int c = min(max(unpack_argmax(best), 0), p.xV - 1);
         gcode[m] = c;
@@ -271,16 +262,7 @@ __global__ __launch_bounds__(256) void gemv_xl_kernel(GemvParams p) {
     for (int m = wave; m < p.M; m += 4) {
       const int bb = p.x_step1 ? (m >> 1) : m;
       if (p.x_step1 && !(m & 1)) continue;
-      unsigned long long best = 0;
-      for (int i = lane; i < p.xpart_n; i += 64) {
-        const unsigned long long v = p.xpart[(size_t)bb * p.xpart_stride + i];
-        best = v > best ? v : best;
-      }
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        const unsigned long long v = __shfl_xor(best, o, 64);
-        best = v > best ? v : best;
-      }
+      const unsigned long long best = wave_argmax_partials(p.xpart + (size_t)bb * p.xpart_stride, p.xpart_n, lane);
       if (lane == 0) {
         const int c = min(max(unpack_argmax(best), 0), p.xV - 1);
         gcode[m] = c;
@@ -517,16 +499,7 @@ __device__ __forceinline__ void attn_block(const AttnParams& p, int m, int kvh, 
   if (p.g_tab) {  // decoder layer 0, steps >= 2: gather this row's QKV from the layer-0 table
     __shared__ int gcode;
     if (wave == 0) {
-      unsigned long long best = 0;
-      for (int i = lane; i < p.g_part_n; i += 64) {
-        const unsigned long long v = p.g_part[(size_t)b * p.g_part_stride + i];
-        best = v > best ? v : best;
-      }
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        const unsigned long long v = __shfl_xor(best, o, 64);
-        best = v > best ? v : best;
-      }
+      const unsigned long long best = wave_argmax_partials(p.g_part + (size_t)b * p.g_part_stride, p.g_part_n, lane);
       if (lane == 0) gcode = min(max(unpack_argmax(best), 0), p.g_V - 1);
     }
     __syncthreads();
@@ -636,16 +609,7 @@ __device__ __forceinline__ void attn_short_head(const AttnParams& p, int m, int 
     for (int i = 0; i < NO; ++i) vv[j][i] = (j < jc) ? V[(size_t)j * HD + lane + 64 * i] : 0.f;
   const float* qrow = p.q + (size_t)m * p.qs;
   if (gath) {
-    unsigned long long best = 0;
-    for (int i = lane; i < p.g_part_n; i += 64) {
-      const unsigned long long v = p.g_part[(size_t)b * p.g_part_stride + i];
-      best = v > best ? v : best;
-    }
-#pragma unroll
-    for (int o2 = 32; o2 > 0; o2 >>= 1) {
-      const unsigned long long v = __shfl_xor(best, o2, 64);
-      best = v > best ? v : best;
-    }
+    const unsigned long long best = wave_argmax_partials(p.g_part + (size_t)b * p.g_part_stride, p.g_part_n, lane);
     const int c = min(max(unpack_argmax(best), 0), p.g_V - 1);
     if (code_out) *code_out = c;
     const float* trow = p.g_tab + (size_t)c * p.g_row;
@@ -988,16 +952,7 @@ __global__ void advance_kernel(AdvanceParams p) {
   if (p.last_part) {  // greedy: arg-max of the last head's block partials -> codes[b][K-1]
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (int b = wave; b < p.B; b += blockDim.x / 64) {
-      unsigned long long best = 0;
-      for (int i = lane; i < p.last_n; i += 64) {
-        const unsigned long long v = p.last_part[(size_t)b * p.last_stride + i];
-        best = v > best ? v : best;
-      }
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        const unsigned long long v = __shfl_xor(best, o, 64);
-        best = v > best ? v : best;
-      }
+      const unsigned long long best = wave_argmax_partials(p.last_part + (size_t)b * p.last_stride, p.last_n, lane);
       if (lane == 0) p.codes[(size_t)b * p.K + p.K - 1] = min(max(unpack_argmax(best), 0), p.V - 1);
     }
     __syncthreads();

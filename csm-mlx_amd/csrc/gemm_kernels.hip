@@ -812,16 +812,7 @@ __global__ __launch_bounds__(256) void gather_rows_kernel(GemvParams p) {
   const bool dense = p.x_step1 && !(m & 1);
   if (!dense && threadIdx.x < 64) {
     const int lane = threadIdx.x;
-    unsigned long long best = 0;
-    for (int i = lane; i < p.xpart_n; i += 64) {
-      const unsigned long long v = p.xpart[(size_t)bb * p.xpart_stride + i];
-      best = v > best ? v : best;
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const unsigned long long v = __shfl_xor(best, o, 64);
-      best = v > best ? v : best;
-    }
+    const unsigned long long best = wave_argmax_partials(p.xpart + (size_t)bb * p.xpart_stride, p.xpart_n, lane);
     if (lane == 0) {
       const int c = min(max(unpack_argmax(best), 0), p.xV - 1);
       code = c;

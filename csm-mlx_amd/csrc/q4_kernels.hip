@@ -218,16 +218,7 @@ __global__ __launch_bounds__(256) void gemv_q4_kernel(GemvParams p) {
         const int m = m0 + i;
         const int bb = p.x_step1 ? (m >> 1) : m;
         if (p.x_step1 && !(m & 1)) continue;
-        unsigned long long best = 0;
-        for (int t = lane; t < p.xpart_n; t += 64) {
-          const unsigned long long v = p.xpart[(size_t)bb * p.xpart_stride + t];
-          best = v > best ? v : best;
-        }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-          const unsigned long long v = __shfl_xor(best, o, 64);
-          best = v > best ? v : best;
-        }
+        const unsigned long long best = wave_argmax_partials(p.xpart + (size_t)bb * p.xpart_stride, p.xpart_n, lane);
         if (lane == 0) {
           const int c = min(max(unpack_argmax(best), 0), p.xV - 1);
           gcode[i] = c;
