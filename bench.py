@@ -140,11 +140,12 @@ def context_prompts(mine, K: int = 32):
     """Config 5 prompts: 3 context Segments (12 text ids + 5 s audio, Mimi-encoded) + the 12-id text."""
     from csm_mlx.segment import Segment
     from csm_mlx.tokenizers import tokenize_segments_batch, tokenize_text_segment
+    # every utterance's context audio goes through ONE batched Mimi encode (same-length segments)
+    segs = [Segment(seg % 2, prompt_ids(10_000 + 10 * g + seg), context_audio(g, seg)) for g in mine for seg in range(3)]
+    enc = tokenize_segments_batch(segs, n_audio_codebooks=K)
     out = []
-    for g in mine:
-        segs = [Segment(seg % 2, prompt_ids(10_000 + 10 * g + seg), context_audio(g, seg)) for seg in range(3)]
-        parts = tokenize_segments_batch(segs, n_audio_codebooks=K)
-        parts.append(tokenize_text_segment(prompt_ids(g), 0, K))
+    for u, g in enumerate(mine):
+        parts = enc[3 * u:3 * u + 3] + [tokenize_text_segment(prompt_ids(g), 0, K)]
         out.append((np.concatenate([t for t, _ in parts], 0), np.concatenate([m for _, m in parts], 0)))
     return out
 

@@ -362,8 +362,114 @@ __global__ __launch_bounds__(256) void rvq_encode_kernel(float* r, int T, int cd
   }
   for (int d = tid; d < cd; d += 256) r[(size_t)m * cd + d] = rs[d];
 }
+
+// Tiled encode for many rows: a block owns 16 latent rows (wave w: rows 4w..4w+3) and streams each
+// codebook through LDS in [32 dims][256 codes] tiles shared by all its rows -- the codebook is read
+// once per block instead of once per row.  Lane l of a wave scores codes 4l..4l+3 of every tile
+// against the wave's 4 rows (16 fp32 accumulators: one 16-B code read and one 16-B residual read
+// per 16 FMAs); the residuals sit transposed ([dim][row]) in LDS.  Every (row, code) dot is one
+// fmaf chain over the dims in order -- rvq_encode_kernel's arithmetic, so codes and residuals are
+// identical; the arg-min keeps the first minimum.
+constexpr int RVQ_RB = 16, RVQ_CC = 256, RVQ_DC = 32, RVQ_CDMAX = 512;
+__global__ __launch_bounds__(256) void rvq_encode_tiled_kernel(float* r, int M, int T, int cd, const float* cb,
+                                                               const float* c2half, int bins, int k0, int k1,
+                                                               int n_q, int* codes) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  __shared__ __attribute__((aligned(16))) float rsT[RVQ_CDMAX][RVQ_RB];   // residuals [dim][row]
+  __shared__ __attribute__((aligned(16))) float ct[RVQ_DC][RVQ_CC];       // codebook tile [dim][code]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int m0 = blockIdx.x * RVQ_RB;
+  for (int e = tid; e < RVQ_RB * cd; e += 256) {
+    const int i = e / cd, d = e % cd;
+    rsT[d][i] = r[(size_t)min(m0 + i, M - 1) * cd + d];
+  }
+  __syncthreads();
+  for (int k = k0; k < k1; ++k) {
+    const float* cbk = cb + (size_t)k * bins * cd;
+    float best[4];
+    int bi[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      best[i] = INFINITY;
+      bi[i] = 0x7fffffff;
+    }
+    for (int c0 = 0; c0 < bins; c0 += RVQ_CC) {
+      float acc[4][4];  // [row][code]
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = 0.f;
+      for (int d0 = 0; d0 < cd; d0 += RVQ_DC) {
+        const int dn = min(RVQ_DC, cd - d0);
+        __syncthreads();  // previous tile consumed
+        for (int e = tid; e < RVQ_CC * RVQ_DC; e += 256) {  // coalesced along dims
+          const int cc = e / RVQ_DC, dd = e % RVQ_DC;
+          const int c = c0 + cc;
+          ct[dd][cc] = (c < bins && dd < dn) ? cbk[(size_t)c * cd + d0 + dd] : 0.f;
+        }
+        __syncthreads();
+        for (int dd = 0; dd < dn; ++dd) {
+          const f4 a = *reinterpret_cast<const f4*>(&ct[dd][4 * lane]);
+          const f4 x = *reinterpret_cast<const f4*>(&rsT[d0 + dd][4 * wave]);
+          const float av[4] = {a.x, a.y, a.z, a.w}, xv[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = fmaf(av[j], xv[i], acc[i][j]);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = c0 + 4 * lane + j;
+        if (c < bins) {
+          const float c2 = c2half[(size_t)k * bins + c];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float dist = c2 - acc[i][j];
+            if (dist < best[i]) {  // codes visited in increasing order: first minimum kept
+              best[i] = dist;
+              bi[i] = c;
+            }
+          }
+        }
+      }
+    }
+    // per row: first minimum over the wave's lanes, then the wave updates its rows' residuals
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float bv = best[i];
+      int bx = bi[i];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const float ov = __shfl_xor(bv, o, 64);
+        const int oi = __shfl_xor(bx, o, 64);
+        if (ov < bv || (ov == bv && oi < bx)) {
+          bv = ov;
+          bx = oi;
+        }
+      }
+      bx = min(max(bx, 0), bins - 1);
+      const int m = m0 + 4 * wave + i;
+      if (lane == 0 && m < M) codes[((size_t)(m / T) * n_q + k) * T + m % T] = bx;
+      for (int d = lane; d < cd; d += 64) rsT[d][4 * wave + i] = rsT[d][4 * wave + i] - cbk[(size_t)bx * cd + d];
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < RVQ_RB * cd; e += 256) {
+    const int i = e / cd, d = e % cd;
+    if (m0 + i < M) r[(size_t)(m0 + i) * cd + d] = rsT[d][i];
+  }
+}
+
 void launch_rvq_encode(float* r, int M, int T, int cd, const float* cb, const float* c2half, int bins, int k0, int k1,
                        int n_q, int* codes, hipStream_t st) {
+  const char* env = getenv("CSM_RVQ_TILED");  // read per call (encode is never graph-captured): A/B tests
+  const int mode = env ? atoi(env) : 1;
+  if (mode && cd <= RVQ_CDMAX && M >= 1024) {  // tiled once there are >= 64 blocks of 16 rows
+    hipLaunchKernelGGL(rvq_encode_tiled_kernel, dim3((M + RVQ_RB - 1) / RVQ_RB), dim3(256), 0, st, r, M, T, cd, cb,
+                       c2half, bins, k0, k1, n_q, codes);
+    return;
+  }
   hipLaunchKernelGGL(rvq_encode_kernel, dim3(M), dim3(256), 0, st, r, T, cd, cb, c2half, bins, k0, k1, n_q, codes);
 }
 

@@ -22,7 +22,7 @@ def _model(args, weights, dtype, max_batch):
     return m
 
 
-def _batch_vs_oracle(args, w, id_sets, frames, rtol, dtype="bf16"):
+def _batch_vs_oracle(args, w, id_sets, frames, rtol, dtype="bf16", check=None):
     from csm_mlx.generation import FrameCache
     from csm_mlx.sampling import Sampler
     from csm_mlx.tokenizers import tokenize_text_segment
@@ -41,6 +41,8 @@ def _batch_vs_oracle(args, w, id_sets, frames, rtol, dtype="bf16"):
         logs.append((cache.debug("c0_logits", (B, Vp))[:, :V], cache.debug("ci_logits", (K - 1, B, Vp))[:, :, :V]))
     hist, n, _ = cache.codes()
     for b, ids in enumerate(id_sets):
+        if check is not None and b not in check:
+            continue
         ref, ref_logs = o.generate_codes(*text_frame(ids, K), frames, collect_logits=True)
         div = first_divergence(hist[: n[b], b], ref)
         upto = len(ref_logs) if div is None else div
@@ -75,6 +77,15 @@ def test_csm_1b_bf16_batched_mfma():
     args, w = csm_weights("1b")
     id_sets = [prompt_ids(200 + b, 4 + b) for b in range(8)]
     _batch_vs_oracle(args, w, id_sets, 2, 2e-3)
+
+
+def test_csm_1b_bf16_batched_mfma_two_tiles():
+    """csm_1b at B = 40: 64-row batch tiles (MT = 2, 2-stage prefetch ring), split-K up to 16 slices
+    combined in one launch, the step-1 decoder at M = 80 (two batch chunks); utterances from both
+    tiles and both chunks are compared (all 40 run in the batch)."""
+    args, w = csm_weights("1b")
+    id_sets = [prompt_ids(500 + b, 3 + b % 9) for b in range(40)]
+    _batch_vs_oracle(args, w, id_sets, 2, 2e-3, check={0, 17, 31, 39})
 
 
 @pytest.mark.parametrize("B", [9, 33])

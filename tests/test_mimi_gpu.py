@@ -84,3 +84,18 @@ def test_encode_decode_batch_equals_single():
     y2 = codec.decode(both)
     y1 = codec.decode(both[1:2])
     assert _rms(y2[1:2], y1) <= 1e-6
+
+
+def test_encode_tiled_rvq_matches_per_row_kernel(monkeypatch):
+    """>= 1024 latent rows take the tiled RVQ kernel (16 rows per block, codebook tiles in LDS); its
+    codes must equal the per-row kernel's (same fmaf chains) and the oracle's."""
+    m, codec, o = _pair("mimi_202407", "mlx", max_batch=24)
+    pcm = np.stack([_pcm(24000 * 4, 40 + b) for b in range(24)])  # 24 x 50 frames = 1200 rows
+    monkeypatch.setenv("CSM_RVQ_TILED", "0")
+    ref_rows = codec.encode(pcm[:, None, :])
+    monkeypatch.setenv("CSM_RVQ_TILED", "1")
+    tiled = codec.encode(pcm[:, None, :])
+    assert tiled.shape == ref_rows.shape and tiled.shape[0] * tiled.shape[2] >= 1024
+    assert np.array_equal(tiled, ref_rows), f"first diff at {np.argwhere(tiled != ref_rows)[:3].tolist()}"
+    ref = o.encode(pcm[[0, 23], None, :])
+    assert np.array_equal(tiled[[0, 23]], ref)
