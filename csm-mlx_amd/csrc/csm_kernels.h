@@ -64,6 +64,7 @@ struct GemvParams {
   float* kpart;          // [tile][m chunk][slice][slab] split-K slice partials (+ sum x^2), written sc1
   unsigned* kticket;     // [tile][m chunk] arrival tickets (zero between launches)
   int ksplit;
+  int no_mfma;           // keep the GEMV's per-row arithmetic at any M (folded-table builds)
 };
 
 __device__ __forceinline__ unsigned long long pack_argmax(float v, int idx) {
@@ -236,6 +237,9 @@ struct AdvanceParams {
 };
 
 void launch_gemv(const GemvParams& p, int wdt, int epi, int norm, hipStream_t st, int tag = 2);
+// folded-table builds: rows per call launch_gemv_table takes (same per-row arithmetic as launch_gemv)
+int gemv_table_rows(int N, int K, int wdt, int tag);
+void launch_gemv_table(const GemvParams& p, int wdt, int epi, int norm, hipStream_t st, int tag);
 void launch_embed(const EmbedParams& p, int wdt, int M, hipStream_t st);
 // dst[i] = float(src[i]) for n elements (n % 8 == 0)
 void launch_to_f32(const void* src, int wdt, float* dst, size_t n, hipStream_t st);

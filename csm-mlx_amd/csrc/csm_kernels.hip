@@ -1061,12 +1061,38 @@ static int gemv_nt_mask() {
   return g_nt_mask;
 }
 
+// Folded-table builds (csm_engine.hip build_proj_table): XL_TAB_MT rows per launch through
+// gemv_xl_kernel<WT, 128, 2, XL_TAB_MT, 1, 1024> (56 KB of LDS) -- per row the arithmetic of the
+// frame's own launch (same K-slices, reduction order and epilogue for every MT), 3.5x fewer launches
+// than the M <= 4 decode instantiation.  Shapes outside (G, RPT) = (128, 2), K <= 1024, decoder
+// tag 1 with default loads go through launch_gemv (M <= 4 per call).
+constexpr int XL_TAB_MT = 14;
+int gemv_table_rows(int N, int K, int wdt, int tag) {
+  int G, RPT;
+  gemv_tiling(N, K, 1, G, RPT);
+  const bool ok = g_gemv_xl && (wdt == WDT_BF16 || wdt == WDT_F32) && K <= 1024 && K % 8 == 0 && G == 128 &&
+                  RPT == 2 && tag == 1 && !((gemv_nt_mask() >> tag) & 1);
+  return ok ? XL_TAB_MT : 4;
+}
+void launch_gemv_table(const GemvParams& p0, int wdt, int epi, int norm, hipStream_t st, int tag) {
+  if (p0.M <= 4 || gemv_table_rows(p0.N, p0.K, wdt, tag) != XL_TAB_MT || p0.M > XL_TAB_MT || p0.xpart) {
+    launch_gemv(p0, wdt, epi, norm, st, tag);
+    return;
+  }
+  GemvParams p = p0;
+  p.epi = epi;
+  if (!norm) p.nw = nullptr;
+  const int blocks = p.N / ((256 / 128) * 2);
+  if (wdt == WDT_BF16) hipLaunchKernelGGL((gemv_xl_kernel<bf16_t, 128, 2, XL_TAB_MT, 1, 1024>), dim3(blocks), dim3(256), 0, st, p);
+  else hipLaunchKernelGGL((gemv_xl_kernel<float, 128, 2, XL_TAB_MT, 1, 1024>), dim3(blocks), dim3(256), 0, st, p);
+}
+
 void launch_gemv(const GemvParams& p0, int wdt, int epi, int norm, hipStream_t st, int tag) {
   GemvParams p = p0;
   p.epi = epi;
   if (!norm) p.nw = nullptr;
   const bool nt = (gemv_nt_mask() >> tag) & 1;
-  if (!p.xpart && !p.x_copy && gemm_mfma_eligible(p.N, p.K, p.M, wdt)) {
+  if (!p.xpart && !p.x_copy && !p.no_mfma && gemm_mfma_eligible(p.N, p.K, p.M, wdt)) {
     launch_gemm_mfma(p, wdt, nt, st);
   } else if (wdt == WDT_Q4) {
     launch_gemv_q4(p, nt, st);
