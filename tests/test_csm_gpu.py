@@ -237,3 +237,27 @@ def test_fused_mlp_matches_two_launches():
     got2, _, _ = generate_codes_batch(model, prompts, 6, sampler=Sampler(0.0, 0))
     assert np.array_equal(got2, got), "fused MLP must be deterministic run to run"
     del model
+
+
+def test_eos_first_frame_stops_generation(tiny):
+    """generation.py:151-152 / :163-165: an all-zero frame is EOS -- it is not appended, and with no
+    samples generate() returns zeros((0,)).  Zeroed heads make every logit 0, so the first-max greedy
+    pick is code 0 in every codebook (the reference's argmax tie rule) for every utterance."""
+    from csm_mlx.generation import generate, generate_codes_batch
+    from csm_mlx.sampling import Sampler
+    from csm_mlx.tokenizers import tokenize_text_segment
+    args, w = tiny
+    w = dict(w)
+    for k in ("codebook0_head.weight", "audio_head"):
+        w[k] = np.zeros_like(w[k])
+    model = _model(args, w, "float32", max_batch=3)
+    o = oracle_for(args, w)
+    from oracle.csm_oracle import text_frame
+    ref = o.generate_codes(*text_frame(tiny_prompt_ids(7, 4), args.n_audio_codebooks), 10)
+    assert len(ref) == 0
+    prompts = [tokenize_text_segment(tiny_prompt_ids(7 + b, 3 + b), 0, args.n_audio_codebooks) for b in range(3)]
+    hist, n, _ = generate_codes_batch(model, prompts, 10, sampler=Sampler(0.0, 0))
+    assert n.tolist() == [0, 0, 0]
+    audio = generate(model, text=tiny_prompt_ids(7, 4), speaker=0, context=[], max_audio_length_ms=800, temperature=0.0)
+    assert audio.shape == (0,) and audio.dtype == np.float32
+    del model
