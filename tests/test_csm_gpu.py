@@ -261,3 +261,35 @@ def test_eos_first_frame_stops_generation(tiny):
     audio = generate(model, text=tiny_prompt_ids(7, 4), speaker=0, context=[], max_audio_length_ms=800, temperature=0.0)
     assert audio.shape == (0,) and audio.dtype == np.float32
     del model
+
+
+def test_eos_per_utterance_in_batch(tiny):
+    """Batched EOS: with the ci heads zeroed and only c0-head row 0 non-zero, a frame is all-zero
+    (EOS) exactly when that row's logit is positive for the utterance's backbone state -- so some
+    utterances stop at different frames while the others keep generating.  Every utterance must match
+    its own oracle run (codes and frame count)."""
+    from csm_mlx.generation import generate_codes_batch
+    from csm_mlx.sampling import Sampler
+    from csm_mlx.tokenizers import tokenize_text_segment
+    from oracle.csm_oracle import text_frame
+    args, w = tiny
+    w = dict(w)
+    rng = np.random.default_rng(3)
+    c0 = np.zeros_like(w["codebook0_head.weight"])
+    c0[0] = rng.normal(0, 1.0, c0.shape[1]).astype(c0.dtype)
+    w["codebook0_head.weight"] = c0
+    w["audio_head"] = np.zeros_like(w["audio_head"])
+    K = args.n_audio_codebooks
+    B, F = 8, 6
+    model = _model(args, w, "float32", max_batch=B)
+    o = oracle_for(args, w)
+    ids = [tiny_prompt_ids(90 + b, 2 + b % 5) for b in range(B)]
+    hist, n, _ = generate_codes_batch(model, [tokenize_text_segment(i, 0, K) for i in ids], F, sampler=Sampler(0.0, 0))
+    lens = []
+    for b in range(B):
+        ref = o.generate_codes(*text_frame(ids[b], K), F)
+        lens.append(len(ref))
+        assert n[b] == len(ref), f"utterance {b}: {n[b]} frames vs oracle {len(ref)}"
+        assert np.array_equal(hist[: n[b], b], np.asarray(ref).reshape(-1, K))
+    assert 0 < sum(1 for x in lens if x < F) < B, f"want a mix of stopped / running utterances, got {lens}"
+    del model
