@@ -1051,7 +1051,8 @@ int csm_bench_gemv(csm_engine* e, int which, int M, int iters, float* avg_us, do
     GemvParams g = params(0, epi, norm);
     size_t nbytes = e->wbytes(g.N, g.K);
     nbytes += (size_t)M * g.K * 4 + (size_t)M * (epi == EPI_SILU_MUL ? F : D) * 4 * (epi == EPI_ADD ? 2 : 1);
-    const int nl = s.d.n_layers;
+    const char* lenv = getenv("CSM_BENCH_LAYERS");  // lab: rotate over fewer layers (cache residency)
+    const int nl = lenv ? std::max(1, std::min(atoi(lenv), s.d.n_layers)) : s.d.n_layers;
     for (int i = 0; i < nl; ++i) { GemvParams gi = params(i, epi, norm); launch_gemv(gi, e->wdt, epi, norm, e->st, tag); }
     hipEvent_t a, b;
     HIPCHK(hipEventCreate(&a));
