@@ -172,7 +172,25 @@ struct LinProblem {
   }
 };
 
+// Few rows (streaming decode_step: one row per utterance): gemm64's 64 x 64 tiles leave most of the
+// chip idle (8-32 blocks), so row-major linears of <= 32 rows go through the decode GEMV instead
+// (fp32 weights, same epilogues: y = gelu(v) / out += scale * v).  Measured: config 3 (B = 32
+// decode_step) 2083 -> 2123 frames/s; at 125 rows (one-shot decode of a 10 s utterance) neutral, and
+// 16 rows per weight pass was slower (2001).  CSM_MIMI_GEMV_M sets the largest row count (0 = never).
+static int mimi_gemv_rows() {
+  static const int v = [] { const char* e = getenv("CSM_MIMI_GEMV_M"); return e ? atoi(e) : 32; }();
+  return v;
+}
+
 void launch_linear(const LinParams& p, hipStream_t st) {
+  if (!p.conv_T && p.M <= mimi_gemv_rows() && p.N % 8 == 0 && p.K % 8 == 0 &&
+      p.N % gemv_rows_per_block(p.N, p.K, p.M) == 0 && gemv_rows_per_block(p.N, p.K, p.M) % 2 == 0) {
+    GemvParams g{};
+    g.W = p.W; g.N = p.N; g.K = p.K; g.x = p.x; g.xs = p.xs; g.M = p.M; g.out = p.out; g.os = p.os;
+    g.scale = p.scale; g.gelu_erf = p.gelu_erf;
+    launch_gemv(g, WDT_F32, p.epi, 0, st, 3);  // tag 3: default cache policy
+    return;
+  }
   LinProblem pr{p, p.N, p.M};
   dim3 grid((p.M + 63) / 64, (p.N + 63) / 64, 1);
   hipLaunchKernelGGL(gemm64_kernel<LinProblem>, grid, dim3(256), 0, st, pr);
