@@ -864,9 +864,11 @@ __device__ __forceinline__ int block_argmax(T v, int i, T* sv, int* si) {
 // over logits*(1/temp) restricted to values >= the top_k-th largest (radix select) -- mlx_lm
 // make_sampler(temp, top_k) semantics with the build's counter-based RNG.  The chosen code's
 // audio embedding (embed_audio, models.py:79-80) is gathered into the next decoder input row.
+constexpr int SAMPLE_NPT = 16;  // logits per thread: V <= 4096 (checked at launch)
 template <typename WT>
 __global__ __launch_bounds__(256) void sample_kernel(SampleParams p) {
   __shared__ uint32_t hist[256];
+  __shared__ uint32_t wsum[4];
   __shared__ uint32_t sh_prefix, sh_remain;
   __shared__ double sdv[4];
   __shared__ float sfv[4];
@@ -888,34 +890,46 @@ __global__ __launch_bounds__(256) void sample_kernel(SampleParams p) {
     }
     code = block_argmax<float>(best, bi, sfv, si);
   } else {
+    // the row's logits stay in registers for the radix passes and the Gumbel pass
+    float lv[SAMPLE_NPT];
+#pragma unroll
+    for (int i = 0; i < SAMPLE_NPT; ++i) {
+      const int v = tid + 256 * i;
+      lv[i] = v < V ? lg[v] : 0.f;
+    }
     float thr = -INFINITY;
     if (p.top_k > 0 && p.top_k < V) {
-      uint32_t prefix = 0, maskbits = 0;
-      if (tid == 0) sh_remain = (uint32_t)p.top_k;
+      // radix select of the top_k-th largest key, 8 bits per pass; the digit is found by a parallel
+      // suffix count over the 256 bins (thread t holds digit 255 - t), not a serial scan
+      uint32_t prefix = 0, maskbits = 0, rem = (uint32_t)p.top_k;
+      const int lane = tid & 63, wave = tid >> 6;
       for (int shift = 24; shift >= 0; shift -= 8) {
         hist[tid] = 0;
         __syncthreads();
-        for (int v = tid; v < V; v += 256) {
-          const uint32_t key = f2key(lg[v]);
-          if ((key & maskbits) == prefix) atomicAdd(&hist[(key >> shift) & 255u], 1u);
+#pragma unroll
+        for (int i = 0; i < SAMPLE_NPT; ++i) {
+          const uint32_t key = f2key(lv[i]);
+          if (tid + 256 * i < V && (key & maskbits) == prefix) atomicAdd(&hist[(key >> shift) & 255u], 1u);
         }
         __syncthreads();
-        if (tid == 0) {
-          uint32_t cum = 0, rem = sh_remain;
-          int dsel = 0;
-          for (int dgt = 255; dgt >= 0; --dgt) {
-            if (cum + hist[dgt] >= rem) {
-              dsel = dgt;
-              rem -= cum;
-              break;
-            }
-            cum += hist[dgt];
-          }
-          sh_remain = rem;
-          sh_prefix = prefix | ((uint32_t)dsel << shift);
+        const uint32_t h = hist[255 - tid];
+        uint32_t c = h;  // inclusive prefix over t = count of keys with digit >= 255 - t
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t u = __shfl_up(c, o, 64);
+          if (lane >= o) c += u;
+        }
+        if (lane == 63) wsum[wave] = c;
+        __syncthreads();
+        for (int w = 0; w < wave; ++w) c += wsum[w];
+        const uint32_t above = c - h;
+        if (h > 0 && above < rem && rem <= c) {  // exactly one digit
+          sh_prefix = prefix | ((uint32_t)(255 - tid) << shift);
+          sh_remain = rem - above;
         }
         __syncthreads();
         prefix = sh_prefix;
+        rem = sh_remain;
         maskbits |= 255u << shift;
       }
       thr = key2f(prefix);
@@ -925,9 +939,11 @@ __global__ __launch_bounds__(256) void sample_kernel(SampleParams p) {
     const float inv_t = 1.0f / p.temperature;
     double best = -INFINITY;
     int bi = 0x7fffffff;
-    for (int v = tid; v < V; v += 256) {
-      const float l = lg[v];
-      if (!(l >= thr)) continue;
+#pragma unroll
+    for (int i = 0; i < SAMPLE_NPT; ++i) {
+      const int v = tid + 256 * i;
+      const float l = lv[i];
+      if (v >= V || !(l >= thr)) continue;
       const uint64_t h = splitmix64(key ^ (uint64_t)v);
       const double u = ((double)(h >> 11) + 0.5) * 1.1102230246251565e-16;  // 2^-53
       const double val = (double)(l * inv_t) + (-log(-log(u)));
@@ -1312,6 +1328,10 @@ void launch_fused_mlp(const MlpParams& p0, int D, bool nt, hipStream_t st) {
 }
 
 void launch_sample(const SampleParams& p, int wdt, int B, hipStream_t st) {
+  if (p.V > 256 * SAMPLE_NPT) {
+    fprintf(stderr, "csm: sampler supports V <= %d (got %d)\n", 256 * SAMPLE_NPT, p.V);
+    abort();
+  }
   if (wdt == WDT_BF16) hipLaunchKernelGGL(sample_kernel<bf16_t>, dim3(B), dim3(256), 0, st, p);
   else hipLaunchKernelGGL(sample_kernel<float>, dim3(B), dim3(256), 0, st, p);
 }

@@ -94,6 +94,20 @@ def test_tiny_topk_sampling_parity(tiny):
     _compare(eng, orc, 8, 2e-4)
 
 
+@pytest.mark.parametrize("top_k", [50, 0])
+def test_csm_1b_topk_sampling_parity(top_k):
+    """configs[2] sampler at csm_1b size (V = 2051: nine logits per thread, a 4-digit radix select of
+    the top-50 threshold, or no top-k): codes identical to the oracle's restatement of the RNG."""
+    args, w = csm_weights("1b")
+    model = _model(args, w, "float32")
+    o = oracle_for(args, w)
+    ids = prompt_ids(5)
+    eng = _engine_frames(model, ids, 2, temperature=0.8, top_k=top_k, seed=77)
+    orc = _oracle_frames(o, ids, 2, args.n_audio_codebooks, temperature=0.8, top_k=top_k, seed=77)
+    _compare(eng, orc, 2, 2e-4)
+    del model
+
+
 def test_tiny_batched_ragged_prompts(tiny):
     """B utterances with different prompt lengths == each utterance run alone."""
     from csm_mlx.generation import generate_codes_batch
