@@ -68,9 +68,11 @@ class FrameCache:
         m = np.ascontiguousarray(mask, np.uint8)
         _lib.check(self.L.csm_prefill(self.model.engine, b, t.shape[0], _lib.ptr(t), _lib.ptr(m)))
 
-    def run(self, nframes: int) -> bool:
+    def run(self, nframes: int, sync: bool = True) -> bool:
+        """Enqueue nframes frame graphs; with sync, wait and return whether every utterance is done
+        (without, return False at once: the caller polls ``done()``, which waits for the frames)."""
         done = ctypes.c_int(0)
-        _lib.check(self.L.csm_run_frames(self.model.engine, nframes, ctypes.byref(done)))
+        _lib.check(self.L.csm_run_frames(self.model.engine, nframes, ctypes.byref(done) if sync else None))
         self.frames += nframes
         return bool(done.value)
 
@@ -212,6 +214,25 @@ def generate_batch(model: CSM, prompts: Sequence[Tuple[np.ndarray, np.ndarray]],
     return _decode_batch(model, hist, n_frames)
 
 
+def _overlapped_frames(cache: "FrameCache", codec, max_audio_frames: int):
+    """The streaming loop of generation.py:232-256 with frame f+1 computing on the engine's stream
+    while the codec decodes frame f on its own: enqueue f+1, decode + yield f, then wait for f+1 and
+    test EOS (an all-done frame is not decoded or yielded, as the reference breaks before its
+    decode_step).  Yields (pcm (B, 1920), done (B,)) in frame order."""
+    prev = None  # (codes, done) of the last finished, not yet decoded frame
+    for _ in range(max_audio_frames):
+        cache.run(1, sync=False)
+        if prev is not None:
+            yield codec.decode_step(prev[0])[:, 0], prev[1]
+        d = cache.done()                                                           # waits for the frame
+        if d.all():
+            prev = None
+            break                                                                  # EOS (generation.py:239)
+        prev = (cache.last_codes(), d)
+    if prev is not None:
+        yield codec.decode_step(prev[0])[:, 0], prev[1]
+
+
 def stream_generate_batch(model: CSM, prompts: Sequence[Tuple[np.ndarray, np.ndarray]],
                           max_audio_length_ms: float = 10_000, *, temperature: float = 0.8, top_k: int = 0,
                           sampler=None, seeds=None) -> Generator[Tuple[np.ndarray, np.ndarray], None, None]:
@@ -229,10 +250,7 @@ def stream_generate_batch(model: CSM, prompts: Sequence[Tuple[np.ndarray, np.nda
         cache.prefill(b, t, m)
     codec.reset_state(B)
     try:
-        for _ in range(max_audio_frames):
-            if cache.run(1):
-                break                                                              # every utterance hit EOS
-            yield codec.decode_step(cache.last_codes())[:, 0], cache.done()
+        yield from _overlapped_frames(cache, codec, max_audio_frames)
     finally:
         codec.reset_state(B)
 
@@ -255,10 +273,7 @@ def stream_generate(model: CSM, text, speaker: int, context: List[Segment], max_
     cache.prefill(0, t, m)
     codec.reset_state(1)
     try:
-        for _ in range(max_audio_frames):
-            if cache.run(1):
-                break                                                              # EOS (generation.py:239)
-            codes = cache.last_codes()
-            yield codec.decode_step(codes)[0, 0]
+        for pcm, _ in _overlapped_frames(cache, codec, max_audio_frames):
+            yield pcm[0]
     finally:
         codec.reset_state(1)
