@@ -445,27 +445,25 @@ void build_proj_table(csm_engine* e) {
     GemvParams g{};
     g.W = e->proj; g.N = Dd; g.K = D; g.x = scratch; g.xs = D; g.M = V;
     g.out = e->proj_tab + (size_t)cb * V * Dd; g.os = Dd;
-    g.no_mfma = 1;  // the GEMV (no norm: gemv_kernel's rows equal gemv_xl_kernel's), not the matrix cores
-    launch_gemv(g, e->wdt, EPI_STORE, 0, e->st);
+    g.no_mfma = 1;  // the GEMV's per-row arithmetic (the step-1 launch's), never the matrix cores
+    launch_gemv_table(g, e->wdt, EPI_STORE, 0, e->st, 1);
   }
   HIPCHK(hipStreamSynchronize(e->st));
   HIPCHK(hipGetLastError());
   e->proj_tab_dirty = false;
-  // layer-0 QKV of every folded decoder input row, by the frame's own QKV GEMV (14 rows per launch
-  // where the shape allows, else 4: per-row arithmetic identical to the 1-row launch of the frame)
+  // layer-0 QKV of every folded decoder input row, by the frame's own QKV GEMV (one launch per
+  // codebook where the shape allows, else 4 rows per launch: per-row arithmetic of the 1-row launch)
   if (!e->use_qkv0_tab) return;  // built at the next csm_begin after csm_set_option("qkv0_tab", 1)
   const Stack& s = e->dec;
   const LayerW& l0 = s.L[0];
-  const int rows = gemv_table_rows(s.qkv_rows(), Dd, e->wdt, 1);
-  for (int cb = 1; cb < e->K - 1; ++cb)
-    for (int m0 = 0; m0 < V; m0 += rows) {
-      GemvParams g{};
-      g.W = l0.wqkv; g.N = s.qkv_rows(); g.K = Dd; g.x = e->proj_tab + ((size_t)cb * V + m0) * Dd; g.xs = Dd;
-      g.M = std::min(rows, V - m0); g.nw = l0.n1; g.eps = s.d.eps; g.Hq = s.d.n_heads; g.Hkv = s.d.n_kv_heads;
-      g.hd = s.d.head_dim; g.S_cap = s.S_cap; g.rope = s.rope; g.rm = RowMap{1, 0, nullptr, cb + 1};
-      g.qkv_tab = e->qkv0_tab + ((size_t)cb * V + m0) * s.qkv_rows();
-      launch_gemv_table(g, e->wdt, EPI_QKV, 1, e->st, 1);
-    }
+  for (int cb = 1; cb < e->K - 1; ++cb) {
+    GemvParams g{};
+    g.W = l0.wqkv; g.N = s.qkv_rows(); g.K = Dd; g.x = e->proj_tab + (size_t)cb * V * Dd; g.xs = Dd;
+    g.M = V; g.nw = l0.n1; g.eps = s.d.eps; g.Hq = s.d.n_heads; g.Hkv = s.d.n_kv_heads;
+    g.hd = s.d.head_dim; g.S_cap = s.S_cap; g.rope = s.rope; g.rm = RowMap{1, 0, nullptr, cb + 1};
+    g.qkv_tab = e->qkv0_tab + (size_t)cb * V * s.qkv_rows();
+    launch_gemv_table(g, e->wdt, EPI_QKV, 1, e->st, 1);
+  }
   HIPCHK(hipStreamSynchronize(e->st));
   HIPCHK(hipGetLastError());
   e->qkv0_built = true;

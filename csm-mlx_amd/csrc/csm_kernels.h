@@ -65,6 +65,7 @@ struct GemvParams {
   unsigned* kticket;     // [tile][m chunk] arrival tickets (zero between launches)
   int ksplit;
   int no_mfma;           // keep the GEMV's per-row arithmetic at any M (folded-table builds)
+  int row_chunk;         // gemv_xl_kernel: blockIdx.y takes rows [y*row_chunk, +row_chunk) (table builds)
 };
 
 __device__ __forceinline__ unsigned long long pack_argmax(float v, int idx) {

@@ -233,6 +233,13 @@ constexpr int XL_KMAX_WIDE = 8192;  // down projections (K = 8192) at M = 1: 32 
 
 template <typename WT, int G, int RPT, int MT, int TAG, int KMAX = XL_KMAX>
 __global__ __launch_bounds__(256) void gemv_xl_kernel(GemvParams p) {
+  if (p.row_chunk) {  // table builds: one launch covers every row, MT rows per grid row
+    const int y0 = blockIdx.y * p.row_chunk;
+    p.x += (size_t)y0 * p.xs;
+    if (p.out) p.out += (size_t)y0 * p.os;
+    if (p.qkv_tab) p.qkv_tab += (size_t)y0 * p.N;
+    p.M = min(p.row_chunk, p.M - y0);
+  }
   constexpr int NG = 256 / G;
   constexpr int RPB = NG * RPT;
   constexpr int NKM = KMAX / (G * 8);  // K-steps per thread at most
@@ -1077,30 +1084,40 @@ static int gemv_nt_mask() {
   return g_nt_mask;
 }
 
-// Folded-table builds (csm_engine.hip build_proj_table): XL_TAB_MT rows per launch through
-// gemv_xl_kernel<WT, 128, 2, XL_TAB_MT, 1, 1024> (56 KB of LDS) -- per row the arithmetic of the
-// frame's own launch (same K-slices, reduction order and epilogue for every MT), 3.5x fewer launches
-// than the M <= 4 decode instantiation.  Shapes outside (G, RPT) = (128, 2), K <= 1024, decoder
-// tag 1 with default loads go through launch_gemv (M <= 4 per call).
-constexpr int XL_TAB_MT = 14;
+// Folded-table builds (csm_engine.hip build_proj_table): every row of a table in ONE launch of
+// gemv_xl_kernel<WT, 128, 2, MT, 1, KMAX> with grid.y over chunks of MT rows (MT = 14 at K <= 1024,
+// 7 at K <= 2048: <= 56 KB of LDS) -- per row the arithmetic of the frame's own launch (same
+// K-slices, reduction order and epilogue for every MT; without a norm also gemv_kernel's).  Other
+// shapes / weight types fall back to launch_gemv in chunks of 4 rows.
 int gemv_table_rows(int N, int K, int wdt, int tag) {
   int G, RPT;
   gemv_tiling(N, K, 1, G, RPT);
-  const bool ok = g_gemv_xl && (wdt == WDT_BF16 || wdt == WDT_F32) && K <= 1024 && K % 8 == 0 && G == 128 &&
+  const bool ok = g_gemv_xl && (wdt == WDT_BF16 || wdt == WDT_F32) && K <= 2048 && K % 8 == 0 && G == 128 &&
                   RPT == 2 && tag == 1 && !((gemv_nt_mask() >> tag) & 1);
-  return ok ? XL_TAB_MT : 4;
+  return ok ? (K <= 1024 ? 14 : 7) : 4;
 }
 void launch_gemv_table(const GemvParams& p0, int wdt, int epi, int norm, hipStream_t st, int tag) {
-  if (p0.M <= 4 || gemv_table_rows(p0.N, p0.K, wdt, tag) != XL_TAB_MT || p0.M > XL_TAB_MT || p0.xpart) {
-    launch_gemv(p0, wdt, epi, norm, st, tag);
+  const int rows = gemv_table_rows(p0.N, p0.K, wdt, tag);
+  if (rows == 4 || p0.xpart) {
+    for (int m0 = 0; m0 < p0.M; m0 += 4) {
+      GemvParams g = p0;
+      g.M = std::min(4, p0.M - m0);
+      g.x = p0.x + (size_t)m0 * p0.xs;
+      if (g.out) g.out = p0.out + (size_t)m0 * p0.os;
+      if (g.qkv_tab) g.qkv_tab = p0.qkv_tab + (size_t)m0 * p0.N;
+      launch_gemv(g, wdt, epi, norm, st, tag);
+    }
     return;
   }
   GemvParams p = p0;
   p.epi = epi;
   if (!norm) p.nw = nullptr;
-  const int blocks = p.N / ((256 / 128) * 2);
-  if (wdt == WDT_BF16) hipLaunchKernelGGL((gemv_xl_kernel<bf16_t, 128, 2, XL_TAB_MT, 1, 1024>), dim3(blocks), dim3(256), 0, st, p);
-  else hipLaunchKernelGGL((gemv_xl_kernel<float, 128, 2, XL_TAB_MT, 1, 1024>), dim3(blocks), dim3(256), 0, st, p);
+  p.row_chunk = rows;
+  const dim3 grid(p.N / ((256 / 128) * 2), (p.M + rows - 1) / rows);
+#define TAB_L(WT_, MT_, KM_) hipLaunchKernelGGL((gemv_xl_kernel<WT_, 128, 2, MT_, 1, KM_>), grid, dim3(256), 0, st, p)
+  if (rows == 14) { if (wdt == WDT_BF16) TAB_L(bf16_t, 14, 1024); else TAB_L(float, 14, 1024); }
+  else { if (wdt == WDT_BF16) TAB_L(bf16_t, 7, 2048); else TAB_L(float, 7, 2048); }
+#undef TAB_L
 }
 
 void launch_gemv(const GemvParams& p0, int wdt, int epi, int norm, hipStream_t st, int tag) {
