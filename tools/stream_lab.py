@@ -21,9 +21,10 @@ for rep in range(3):
     n = sum(1 for _ in stream_generate(model, ids, 0, [], max_audio_length_ms=10_000, sampler=smp))
     dt = time.perf_counter() - t0
     print(f"stream_generate sampled: {n} frames in {dt * 1e3:.1f} ms -> {n / dt:.1f} frames/s", flush=True)
-for rep in range(2):
+for rep in range(4):
+    smp = make_sampler(0.8, top_k=50 if rep < 2 else 0)
     t0 = time.perf_counter()
     a = generate(model, ids, 0, [], max_audio_length_ms=10_000, sampler=smp)
     dt = time.perf_counter() - t0
-    print(f"generate sampled: {a.shape[0] / 1920:.0f} frames in {dt * 1e3:.1f} ms -> {a.shape[0] / 1920 / dt:.1f} frames/s",
+    print(f"generate sampled top_k={smp.top_k}: {a.shape[0] / 1920:.0f} frames in {dt * 1e3:.1f} ms -> {a.shape[0] / 1920 / dt:.1f} frames/s",
           flush=True)
