@@ -84,6 +84,7 @@ class CSM:
         self._max_batch = max_batch
         self._engine = None
         self._loaded = set()
+        self._sources = []     # checkpoint paths / dicts given to load_weights (load_adapters re-reads them)
 
     # ------------------------------------------------------------------ engine
     def _dims(self) -> _lib.CsmDims:
@@ -118,8 +119,10 @@ class CSM:
         """MLX ``Module.load_weights``: a .safetensors/.npz path or (name, array) pairs."""
         if isinstance(file_or_weights, (str, os.PathLike)):
             items = _read_weight_file(str(file_or_weights))
+            self._sources.append(str(file_or_weights))
         elif isinstance(file_or_weights, dict):
             items = file_or_weights.items()
+            self._sources.append(file_or_weights)
         else:
             items = file_or_weights
         L = _lib.lib()
@@ -134,6 +137,24 @@ class CSM:
         if strict:
             _lib.check(L.csm_weights_ready(eng))
         return self
+
+    def base_weight_lookup(self, extra=None):
+        """name -> host array of the most recently loaded value, from the paths / dicts given to
+        ``load_weights`` (the resident copy is in kernel layout on the GPU)."""
+        sources = list(self._sources) + ([] if extra is None else
+                                         [str(extra) if isinstance(extra, (str, os.PathLike)) else extra])
+
+        def lookup(name: str) -> np.ndarray:
+            for src in reversed(sources):
+                if isinstance(src, dict):
+                    if name in src:
+                        return src[name]
+                else:
+                    for _, v in _read_weight_file(src, only=name):
+                        return v
+            raise KeyError(f"base weight {name} not found among the loaded checkpoints "
+                           f"(pass base_weights= to load_adapters)")
+        return lookup
 
     def quantize(self, group_size: int = 64, bits: int = 4):
         """``nn.quantize(model, group_size, bits)`` (run_streaming_csm_mlx.py:811-818, README.md:108-111).
@@ -158,16 +179,19 @@ class CSM:
         raise NotImplementedError("embeddings are gathered inside the HIP frame graph (models.py:82-92)")
 
 
-def _read_weight_file(path: str):
+def _read_weight_file(path: str, only: Optional[str] = None):
     if path.endswith(".npz"):
         with np.load(path, allow_pickle=False) as z:
             for k in z.files:
-                yield k, z[k]
+                if only is None or k == only:
+                    yield k, z[k]
         return
     from safetensors import safe_open
     with safe_open(path, framework="pt") as f:
         import torch
         for k in f.keys():
+            if only is not None and k != only:
+                continue
             t = f.get_tensor(k)
             if t.dtype == torch.bfloat16:
                 yield k, t.view(torch.uint16).numpy()

@@ -17,6 +17,9 @@ sources line by line as a spec:
   * GQA attention         /root/reference/csm_mlx/attention.py:180-253
   * Llama block / RMSNorm mlx_lm.models.llama (TransformerBlock, MLP) as wired
                           by /root/reference/csm_mlx/models.py:50-77
+  * LoRA / DoRA adapters  mlx_lm.tuner LoRALinear / DoRALinear / LoRAEmbedding /
+                          DoRAEmbedding forwards (unfused), as wrapped by
+                          /root/reference/csm_mlx/finetune/utils.py:16-108
 
 Sampling with temperature cannot reproduce MLX's RNG; it restates the build's
 own counter-based Gumbel-max sampler (``gumbel_u``) so GPU sampled codes can be
@@ -85,6 +88,32 @@ def linear(x: np.ndarray, w: np.ndarray) -> np.ndarray:
     return np.matmul(x, w.T).astype(F32)
 
 
+def adapted_linear(x: np.ndarray, w: np.ndarray, ad: Optional[dict]) -> np.ndarray:
+    """mlx_lm LoRALinear / DoRALinear forward, unfused (finetune/utils.py:33-50 wraps the layer):
+    LoRA  y = x W^T + scale (x A) B;  DoRA  y = (m / ||W + scale B^T A^T||_row) (x W^T + scale (x A) B).
+    ad: {"a": (in, r), "b": (r, out), "scale": s, "m": (out,) or None}."""
+    y = linear(x, w)
+    if ad is None:
+        return y
+    z = (y + F32(ad["scale"]) * np.matmul(np.matmul(x, ad["a"]), ad["b"])).astype(F32)
+    if ad.get("m") is not None:
+        wf = w + (F32(ad["scale"]) * ad["b"].T) @ ad["a"].T
+        z = (ad["m"] / np.linalg.norm(wf, axis=1).astype(F32)).astype(F32) * z
+    return z.astype(F32)
+
+
+def adapted_embedding(idx: np.ndarray, w: np.ndarray, ad: Optional[dict]) -> np.ndarray:
+    """mlx_lm LoRAEmbedding / DoRAEmbedding forward: y = E[i] + scale A[i] B, DoRA rows rescaled
+    by m[i] / ||E[i] + scale A[i] B||."""
+    y = w[idx]
+    if ad is None:
+        return y
+    z = (y + np.matmul(ad["a"][idx], F32(ad["scale"]) * ad["b"])).astype(F32)
+    if ad.get("m") is not None:
+        z = (ad["m"][idx] / np.linalg.norm(z, axis=-1).astype(F32))[..., None] * z
+    return z.astype(F32)
+
+
 def silu(x):
     return (x / (F32(1) + np.exp(-x))).astype(F32)
 
@@ -121,8 +150,9 @@ class KVCacheRef:
 class LlamaRef:
     """mlx_lm LlamaModel with embed_tokens=Identity and the reference Attention patched in."""
 
-    def __init__(self, w: Dict[str, np.ndarray], prefix: str, args):
+    def __init__(self, w: Dict[str, np.ndarray], prefix: str, args, adapters: Optional[Dict[str, dict]] = None):
         self.w, self.p, self.a = w, prefix, args
+        self.adapters = adapters or {}
         rs = args.rope_scaling
         theta = llama3_rope_theta(args.head_dim, args.rope_theta, rs.get("factor", 1.0),
                                   1.0, 4.0, 8192)   # attention.py:201-205 passes only base/scale_factor
@@ -132,9 +162,9 @@ class LlamaRef:
         a, w, p = self.a, self.w, f"{self.p}.layers.{i}.self_attn"
         b, t, _ = x.shape
         hd, H, Hkv = a.head_dim, a.num_attention_heads, a.num_key_value_heads
-        q = linear(x, w[f"{p}.q_proj.weight"]).reshape(b, t, H, hd)
-        k = linear(x, w[f"{p}.k_proj.weight"]).reshape(b, t, Hkv, hd)
-        v = linear(x, w[f"{p}.v_proj.weight"]).reshape(b, t, Hkv, hd)
+        q = self.lin(x, f"{p}.q_proj").reshape(b, t, H, hd)
+        k = self.lin(x, f"{p}.k_proj").reshape(b, t, Hkv, hd)
+        v = self.lin(x, f"{p}.v_proj").reshape(b, t, Hkv, hd)
         off = cache.offset
         q = rope_apply(q, self.rope, off)
         k = rope_apply(k, self.rope, off)
@@ -145,7 +175,10 @@ class LlamaRef:
         v = np.repeat(v, rep, axis=1)
         o = sdpa(q, k, v, hd ** -0.5, off)
         o = np.swapaxes(o, 1, 2).reshape(b, t, H * hd)
-        return linear(o, w[f"{p}.o_proj.weight"])
+        return self.lin(o, f"{p}.o_proj")
+
+    def lin(self, x, path):
+        return adapted_linear(x, self.w[path + ".weight"], self.adapters.get(path))
 
     def __call__(self, x, caches: List[KVCacheRef]):
         a, w = self.a, self.w
@@ -155,9 +188,9 @@ class LlamaRef:
             r = self.attention(i, rms_norm(h, w[f"{p}.input_layernorm.weight"], a.rms_norm_eps), caches[i])
             h = (h + r).astype(F32)
             n = rms_norm(h, w[f"{p}.post_attention_layernorm.weight"], a.rms_norm_eps)
-            g = linear(n, w[f"{p}.mlp.gate_proj.weight"])
-            u = linear(n, w[f"{p}.mlp.up_proj.weight"])
-            h = (h + linear((silu(g) * u).astype(F32), w[f"{p}.mlp.down_proj.weight"])).astype(F32)
+            g = self.lin(n, f"{p}.mlp.gate_proj")
+            u = self.lin(n, f"{p}.mlp.up_proj")
+            h = (h + self.lin((silu(g) * u).astype(F32), f"{p}.mlp.down_proj")).astype(F32)
         return rms_norm(h, w[f"{self.p}.norm.weight"], a.rms_norm_eps)
 
 
@@ -209,11 +242,14 @@ def sample_one(logits: np.ndarray, temperature: float, top_k: int, seed: int, st
 class OracleCSM:
     """Restatement of ``CSM`` (models.py:31-92) + ``generate_frame`` (generation.py:21-92)."""
 
-    def __init__(self, args, weights: Dict[str, np.ndarray], bb_args, dec_args):
+    def __init__(self, args, weights: Dict[str, np.ndarray], bb_args, dec_args,
+                 adapters: Optional[Dict[str, dict]] = None):
+        """adapters: module path -> LoRA/DoRA tensors (see ``adapted_linear``), applied unfused."""
         self.args = args
         self.w = {k: np.asarray(v, dtype=F32) for k, v in weights.items()}
-        self.backbone = LlamaRef(self.w, "backbone", bb_args)
-        self.decoder = LlamaRef(self.w, "decoder", dec_args)
+        self.ad = adapters or {}
+        self.backbone = LlamaRef(self.w, "backbone", bb_args, self.ad)
+        self.decoder = LlamaRef(self.w, "decoder", dec_args, self.ad)
         self.bb_args, self.dec_args = bb_args, dec_args
         self.V, self.K = args.n_audio_vocab, args.n_audio_codebooks
         self.debug = {}
@@ -222,12 +258,15 @@ class OracleCSM:
         return [KVCacheRef() for _ in range(self.bb_args.num_hidden_layers)]
 
     def embed_audio(self, codebook: int, tokens: np.ndarray) -> np.ndarray:
-        return self.w["audio_embeddings.weight"][tokens + codebook * self.V]     # models.py:79-80
+        return adapted_embedding(tokens + codebook * self.V, self.w["audio_embeddings.weight"],
+                                 self.ad.get("audio_embeddings"))                    # models.py:79-80
 
     def embed_tokens(self, tokens: np.ndarray) -> np.ndarray:                   # models.py:82-92
-        text = self.w["text_embeddings.weight"][tokens[:, :, -1]][:, :, None, :]
+        text = adapted_embedding(tokens[:, :, -1], self.w["text_embeddings.weight"],
+                                 self.ad.get("text_embeddings"))[:, :, None, :]
         audio_tokens = tokens[:, :, :-1] + self.V * np.arange(self.K)
-        audio = self.w["audio_embeddings.weight"][audio_tokens.reshape(-1)].reshape(*tokens.shape[:2], self.K, -1)
+        audio = adapted_embedding(audio_tokens.reshape(-1), self.w["audio_embeddings.weight"],
+                                  self.ad.get("audio_embeddings")).reshape(*tokens.shape[:2], self.K, -1)
         return np.concatenate([audio, text], axis=-2)
 
     def frame(self, tokens, mask, cache, temperature=0.0, top_k=0, seeds=None, frame_idx=0):
@@ -239,7 +278,7 @@ class OracleCSM:
             x = x + emb[:, :, j]
         h = self.backbone(x, cache)                                                # :39
         h_last = h[:, -1, :]                                                       # :40
-        c0_logits = linear(h_last, self.w["codebook0_head.weight"])                # :42
+        c0_logits = adapted_linear(h_last, self.w["codebook0_head.weight"], self.ad.get("codebook0_head"))  # :42
         self.debug["c0_logits"] = c0_logits
         self.debug["h_last"] = h_last
         seeds = seeds if seeds is not None else [0] * B
@@ -251,7 +290,8 @@ class OracleCSM:
         dcache = [KVCacheRef() for _ in range(self.dec_args.num_hidden_layers)]   # :70 fresh per frame
         ci_logits_all = []
         for i in range(1, self.K):                                                 # :72
-            z = self.decoder(linear(dec_in, self.w["projection.weight"]), dcache)  # :74-77
+            z = self.decoder(adapted_linear(dec_in, self.w["projection.weight"], self.ad.get("projection")),
+                             dcache)                                               # :74-77
             logits = np.matmul(z[:, -1, :], self.w["audio_head"][i - 1]).astype(F32)   # :79 (in,out) layout
             ci_logits_all.append(logits)
             ci = np.array([sample_one(logits[b], temperature, top_k, seeds[b], frame_idx * self.K + i)

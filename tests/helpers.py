@@ -44,3 +44,39 @@ def first_divergence(a: np.ndarray, b: np.ndarray):
         if not np.array_equal(a[i], b[i]):
             return i
     return None if len(a) == len(b) else n
+
+
+def make_adapters(model_handle, weights, fine_tune_type="lora", keys=("attn",), rank=4, scale=2.0,
+                  seed=7, b_std=0.05):
+    """Synthetic trained adapters for ``keys`` (mlx_lm LoRALinear naming: <module>.lora_a (in, r),
+    .lora_b (r, out); LoRAEmbedding: lora_a (n, r), lora_b (r, d); DoRA adds .m).  Returns
+    (adapter_config dict, flat tensors for adapters.safetensors, oracle adapters {path: dict})."""
+    from csm_mlx.adapters import converted_modules
+    rng = np.random.default_rng(seed)
+    tensors, oracle_ad = {}, {}
+    for path, kind in converted_modules(model_handle, list(keys)).items():
+        w = np.asarray(weights[path + ".weight"], np.float32)
+        n_in = w.shape[1] if kind == "linear" else w.shape[0]
+        n_out = w.shape[0] if kind == "linear" else w.shape[1]
+        bound = 1.0 / np.sqrt(n_in) if kind == "linear" else 1.0 / np.sqrt(rank)
+        a = rng.uniform(-bound, bound, (n_in, rank)).astype(np.float32)
+        b = (rng.standard_normal((rank, n_out)) * b_std).astype(np.float32)
+        tensors[path + ".lora_a"], tensors[path + ".lora_b"] = a, b
+        ad = {"a": a, "b": b, "scale": scale, "m": None}
+        if fine_tune_type == "dora":
+            m = (np.linalg.norm(w, axis=1) * rng.uniform(0.8, 1.2, w.shape[0])).astype(np.float32)
+            tensors[path + ".m"] = m
+            ad["m"] = m
+        oracle_ad[path] = ad
+    config = {"fine_tune_type": fine_tune_type,
+              "lora_parameters": {"rank": rank, "scale": scale, "dropout": 0.0, "keys": list(keys)}}
+    return config, tensors, oracle_ad
+
+
+def write_adapter_dir(path, config, tensors):
+    import json
+    from safetensors.numpy import save_file
+    path.mkdir(parents=True, exist_ok=True)
+    (path / "adapter_config.json").write_text(json.dumps(config))
+    save_file({k: np.ascontiguousarray(v) for k, v in tensors.items()}, str(path / "adapters.safetensors"))
+    return path
