@@ -76,6 +76,24 @@ class FrameCache:
         self.frames += nframes
         return bool(done.value)
 
+    def run_processed(self, processors: Sequence[Callable], c0_history: Optional[list]) -> bool:
+        """One frame with host ``logits_processors`` applied to the c0 logits (generation.py:42-61):
+        the engine stops after codebook0_head, each processor maps (stack(c0_history) or zeros((0,)),
+        logits (B, V)) -> logits, and the frame finishes on the GPU from the processed logits.
+        Appends this frame's c0 (B, 1) to ``c0_history``; returns whether every utterance is done."""
+        V = self.model.n_audio_vocab
+        logits = np.zeros((self.B, V), np.float32)
+        _lib.check(self.L.csm_frame_c0_logits(self.model.engine, _lib.ptr(logits)))
+        hist = np.stack(c0_history, 0) if c0_history else np.zeros((0,), np.int32)
+        for proc in processors:
+            logits = np.ascontiguousarray(np.asarray(proc(hist, logits), np.float32).reshape(self.B, V))
+        done = ctypes.c_int(0)
+        _lib.check(self.L.csm_frame_finish(self.model.engine, _lib.ptr(logits), ctypes.byref(done)))
+        self.frames += 1
+        if c0_history is not None:
+            c0_history.append(self.last_codes()[:, :1].copy())
+        return bool(done.value)
+
     def codes(self) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
         """(history [F,B,K], n_frames [B], done [B])."""
         F = ctypes.c_int(0)
@@ -112,9 +130,8 @@ def generate_frame(model: CSM, tokens, *, temperature: float = 0.8, token_mask=N
     """generation.py:21-92.  tokens (B, T, K+1); returns codes (B, K) int32.
 
     The rows are appended to the backbone KV held by ``cache`` (a fresh one when None),
-    then one frame (c0 + 31 decoder steps) runs on the GPU."""
-    if logits_processors:
-        raise NotImplementedError("logits_processors run on host logits; not supported by the GPU frame graph")
+    then one frame (c0 + 31 decoder steps) runs on the GPU.  With ``logits_processors`` the frame
+    pauses after codebook0_head for them (``FrameCache.run_processed``)."""
     tokens = np.asarray(tokens, np.int32)
     mask = np.ones_like(tokens, dtype=bool) if token_mask is None else np.asarray(token_mask).astype(bool)
     B = tokens.shape[0]
@@ -122,6 +139,9 @@ def generate_frame(model: CSM, tokens, *, temperature: float = 0.8, token_mask=N
         cache = make_frame_cache(model, B, temperature=temperature, sampler=sampler, seed=seed)
     for b in range(B):
         cache.prefill(b, tokens[b], mask[b])
+    if logits_processors:
+        cache.run_processed(logits_processors, c0_history)
+        return cache.last_codes()
     cache.run(1)
     codes = cache.last_codes()
     if c0_history is not None:
@@ -150,8 +170,10 @@ def _check_window(model: CSM, L: int, max_audio_frames: int):
 
 
 def generate_codes_batch(model: CSM, prompts: Sequence[Tuple[np.ndarray, np.ndarray]], max_audio_frames: int, *,
-                         sampler: Sampler, seeds=None, chunk: int = 16):
-    """Run the frame loop for B prompts.  Returns (hist [F,B,K], n_frames [B], cache)."""
+                         sampler: Sampler, seeds=None, chunk: int = 16,
+                         logits_processors: Optional[List[Callable]] = None):
+    """Run the frame loop for B prompts.  Returns (hist [F,B,K], n_frames [B], cache).  With
+    ``logits_processors`` every frame pauses after codebook0_head for them (generation.py:44-49)."""
     B = len(prompts)
     for t, _ in prompts:
         _check_window(model, t.shape[0], max_audio_frames)
@@ -159,6 +181,12 @@ def generate_codes_batch(model: CSM, prompts: Sequence[Tuple[np.ndarray, np.ndar
     for b, (t, m) in enumerate(prompts):
         cache.prefill(b, t, m)
     left = max_audio_frames
+    if logits_processors:
+        c0_history: list = []                                                    # generation.py:128
+        for _ in range(max_audio_frames):
+            if cache.run_processed(logits_processors, c0_history):
+                break
+        left = 0
     while left > 0:
         n = min(chunk, left)
         all_done = cache.run(n)                                                  # EOS poll (generation.py:151)
@@ -192,12 +220,11 @@ def generate(model: CSM, text, speaker: int, context: List[Segment], max_audio_l
              temperature: float = 0.8, logits_processors: Optional[List[Callable]] = None,
              stream: Any = default_stream, sampler=None, seed=None) -> np.ndarray:
     """generation.py:95-178: returns the (F*1920,) float32 waveform (or zeros((0,)) + warning)."""
-    if logits_processors:
-        raise NotImplementedError("logits_processors are not supported by the GPU frame graph")
     max_audio_frames = int(max_audio_length_ms / 80)
     prompt = build_prompt(model, text, speaker, context)
     smp = _resolve_sampler(temperature, sampler)
-    hist, n_frames, _ = generate_codes_batch(model, [prompt], max_audio_frames, sampler=smp, seeds=seed)
+    hist, n_frames, _ = generate_codes_batch(model, [prompt], max_audio_frames, sampler=smp, seeds=seed,
+                                             logits_processors=logits_processors)
     if n_frames[0] == 0:
         print("[WARN] No samples generated.")
         return np.zeros((0,), dtype=np.float32)
@@ -233,6 +260,16 @@ def _overlapped_frames(cache: "FrameCache", codec, max_audio_frames: int):
         yield codec.decode_step(prev[0])[:, 0], prev[1]
 
 
+def _processed_frames(cache: "FrameCache", codec, max_audio_frames: int, processors):
+    """The streaming loop with host logits processors: each frame pauses after codebook0_head, so
+    there is nothing to overlap; EOS is tested before the frame is decoded (generation.py:237-251)."""
+    c0_history: list = []
+    for _ in range(max_audio_frames):
+        if cache.run_processed(processors, c0_history):
+            break
+        yield codec.decode_step(cache.last_codes())[:, 0], cache.done()
+
+
 def stream_generate_batch(model: CSM, prompts: Sequence[Tuple[np.ndarray, np.ndarray]],
                           max_audio_length_ms: float = 10_000, *, temperature: float = 0.8, top_k: int = 0,
                           sampler=None, seeds=None) -> Generator[Tuple[np.ndarray, np.ndarray], None, None]:
@@ -262,8 +299,6 @@ def stream_generate(model: CSM, text, speaker: int, context: List[Segment], max_
 
     Codec streaming state is per call (the reference resets a process-global Mimi,
     generation.py:224-225, :258)."""
-    if logits_processors:
-        raise NotImplementedError("logits_processors are not supported by the GPU frame graph")
     max_audio_frames = int(max_audio_length_ms / 80)
     t, m = build_prompt(model, text, speaker, context)
     _check_window(model, t.shape[0], max_audio_frames)
@@ -273,7 +308,9 @@ def stream_generate(model: CSM, text, speaker: int, context: List[Segment], max_
     cache.prefill(0, t, m)
     codec.reset_state(1)
     try:
-        for pcm, _ in _overlapped_frames(cache, codec, max_audio_frames):
+        frames = (_processed_frames(cache, codec, max_audio_frames, logits_processors) if logits_processors
+                  else _overlapped_frames(cache, codec, max_audio_frames))
+        for pcm, _ in frames:
             yield pcm[0]
     finally:
         codec.reset_state(1)

@@ -81,6 +81,7 @@ struct csm_engine {
   // input row from it instead of running the projection GEMV.
   float* proj_tab = nullptr;
   bool proj_tab_dirty = true;
+  bool c0_pending = false;  // csm_frame_c0_logits ran; csm_frame_finish must follow
   // decoder layer 0's QKV folded too: qkv0_tab[cb][code] = RoPE'd (q, k | v) of layer 0 for input row
   // proj_tab[cb][code] at position cb + 1 (fp32, built by the same QKV GEMV); codebook steps >= 2 then
   // skip layer 0's QKV launch and its attention gathers the row (AttnParams::g_tab).
@@ -288,9 +289,14 @@ void enqueue_body(csm_engine* e, hipStream_t st) {
   launch_rmsnorm_rows(e->x, e->D, e->bb.norm, e->bb.d.eps, e->D, e->h_last, e->D, B, st, pend, e->acc_rows * e->D);
 }
 
-void enqueue_head(csm_engine* e, hipStream_t st) {
+// phase 0: the whole head (what the frame graph captures).  phase 1: c0 logits only, stored for the
+// host (logits processors, generation.py:44-49).  phase 2: the rest of the frame from c0 logits the
+// host wrote back: c0 is picked by the sample kernel (arg-max when greedy, published as one partial),
+// then steps 1..K-1 as in phase 0.
+void enqueue_head_phase(csm_engine* e, hipStream_t st, int phase) {
   const int B = e->B, K = e->K, D = e->D, Dd = e->Dd, V = e->V, Vp = e->Vpad;
   const bool greedy = e->temperature <= 0.f;
+  const bool c0_sampled = !greedy || phase == 2;  // c0 published by sample_kernel as a single partial
   const int n0 = head_blocks(Vp, D, B, e->wdt);        // c0-head blocks (partials per row)
   const int ni = head_blocks(Vp, Dd, B, e->head_wdt);  // ci-head blocks
   auto part = [&](int cb) { return e->part + (size_t)cb * e->B_max * e->part_stride; };
@@ -301,8 +307,9 @@ void enqueue_head(csm_engine* e, hipStream_t st) {
   GemvParams g{};
   g.W = e->c0_head; g.N = Vp; g.K = D; g.x = e->h_last; g.xs = D; g.M = B; g.out = e->c0_logits; g.os = Vp;
   g.part = part(0); g.part_stride = e->part_stride; g.n_valid = V;
-  launch_gemv(g, e->wdt, greedy ? EPI_ARGMAX : EPI_STORE, 0, st);
-  if (!greedy) {
+  if (phase != 2) launch_gemv(g, e->wdt, (greedy && phase == 0) ? EPI_ARGMAX : EPI_STORE, 0, st);
+  if (phase == 1) return;
+  if (c0_sampled) {
     sp.logits = e->c0_logits; sp.cb = 0; sp.part = part(0);
     launch_sample(sp, e->wdt, B, st);
   }
@@ -312,7 +319,7 @@ void enqueue_head(csm_engine* e, hipStream_t st) {
     // rows itself -- [h_last, E_a[c0]] at step 1 (:62-64), E_a[c_{i-1} + V*(i-1)] after (:87-89)
     g = GemvParams{};
     g.W = e->proj; g.N = Dd; g.K = D; g.x = e->h_last; g.xs = D; g.M = M; g.out = e->dx; g.os = Dd;
-    g.xpart = part(i - 1); g.xpart_stride = e->part_stride; g.xpart_n = greedy ? (i == 1 ? n0 : ni) : 1;
+    g.xpart = part(i - 1); g.xpart_stride = e->part_stride; g.xpart_n = i == 1 ? (c0_sampled ? 1 : n0) : (greedy ? ni : 1);
     g.xtab = e->audio_emb; g.xV = V; g.xcb = i - 1; g.x_step1 = (i == 1); g.x_codes = e->codes; g.x_codes_K = K;
     g.xtab_q4_rows = e->wdt == WDT_Q4 ? V * K : 0;
     const bool folded = i >= 2 && e->proj_tab && e->fold_proj;
@@ -370,6 +377,8 @@ void enqueue_head(csm_engine* e, hipStream_t st) {
   }
   launch_advance(ap, st);
 }
+
+void enqueue_head(csm_engine* e, hipStream_t st) { enqueue_head_phase(e, st, 0); }
 
 hipGraphExec_t capture(csm_engine* e, void (*fn)(csm_engine*, hipStream_t)) {
   hipGraph_t graph;
@@ -852,6 +861,7 @@ int csm_quantize(csm_engine* e, int group_size, int bits) {
 
 int csm_begin(csm_engine* e, int B, const uint64_t* seeds, float temperature, int top_k) {
   CSM_TRY {
+    e->c0_pending = false;
     if (B <= 0) throw CsmError(CSM_ERR_ARG, "batch size out of range");
     if (temperature < 0.f) throw CsmError(CSM_ERR_ARG, "temperature must be >= 0");
     HIPCHK(hipSetDevice(e->dev));
@@ -908,6 +918,7 @@ int csm_prefill(csm_engine* e, int b, int T, const int32_t* tokens, const uint8_
 
 int csm_run_frames(csm_engine* e, int nframes, int* all_done) {
   CSM_TRY {
+    if (e->c0_pending) throw CsmError(CSM_ERR_STATE, "csm_frame_finish pending");
     for (int b = 0; b < e->B; ++b)
       if (e->prompt_len[b] < 0) throw CsmError(CSM_ERR_STATE, "csm_prefill not called for every utterance");
     HIPCHK(hipSetDevice(e->dev));
@@ -961,6 +972,61 @@ int csm_run_frames(csm_engine* e, int nframes, int* all_done) {
       int all = 1;
       for (auto v : d) all &= (v != 0);
       *all_done = all;
+    }
+  }
+  CSM_CATCH
+}
+
+// One frame in two halves around a host hook on the c0 logits (generation.py:42-49): eager launches
+// of the same kernels the frame graph holds.
+int csm_frame_c0_logits(csm_engine* e, float* logits) {
+  CSM_TRY {
+    for (int b = 0; b < e->B; ++b)
+      if (e->prompt_len[b] < 0) throw CsmError(CSM_ERR_STATE, "csm_prefill not called for every utterance");
+    if (e->c0_pending) throw CsmError(CSM_ERR_STATE, "csm_frame_c0_logits called again before csm_frame_finish");
+    if (!logits) throw CsmError(CSM_ERR_ARG, "null logits buffer");
+    HIPCHK(hipSetDevice(e->dev));
+    if (e->frames_run + 1 > e->F_cap) throw CsmError(CSM_ERR_STATE, "frame capacity reached");
+    int maxpos = 0;
+    for (int b = 0; b < e->B; ++b) maxpos = std::max(maxpos, e->pos_host[b]);
+    if (maxpos + 1 + (e->need_body ? 1 : 0) > e->dims.max_seq_len)
+      throw CsmError(CSM_ERR_TOO_LONG, "frames exceed the 2048-position window");
+    if (e->need_body) {
+      enqueue_body(e, e->st);
+      for (int b = 0; b < e->B; ++b) e->pos_host[b] += 1;
+      e->need_body = false;
+    }
+    enqueue_head_phase(e, e->st, 1);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpy2DAsync(logits, (size_t)e->V * 4, e->c0_logits, (size_t)e->Vpad * 4, (size_t)e->V * 4, e->B,
+                            hipMemcpyDeviceToHost, e->st));
+    HIPCHK(hipStreamSynchronize(e->st));
+    e->c0_pending = true;
+  }
+  CSM_CATCH
+}
+
+int csm_frame_finish(csm_engine* e, const float* logits, int* all_done) {
+  CSM_TRY {
+    if (!e->c0_pending) throw CsmError(CSM_ERR_STATE, "csm_frame_finish without csm_frame_c0_logits");
+    if (!logits) throw CsmError(CSM_ERR_ARG, "null logits buffer");
+    HIPCHK(hipSetDevice(e->dev));
+    HIPCHK(hipMemcpy2DAsync(e->c0_logits, (size_t)e->Vpad * 4, logits, (size_t)e->V * 4, (size_t)e->V * 4, e->B,
+                            hipMemcpyHostToDevice, e->st));
+    enqueue_head_phase(e, e->st, 2);
+    HIPCHK(hipGetLastError());
+    e->c0_pending = false;
+    e->need_body = true;
+    e->frames_run++;
+    if (all_done) {
+      std::vector<uint8_t> d(e->B);
+      HIPCHK(hipMemcpyAsync(d.data(), e->done, e->B, hipMemcpyDeviceToHost, e->st));
+      HIPCHK(hipStreamSynchronize(e->st));
+      int all = 1;
+      for (auto v : d) all &= (v != 0);
+      *all_done = all;
+    } else {
+      HIPCHK(hipStreamSynchronize(e->st));  // the host logits buffer may be released on return
     }
   }
   CSM_CATCH

@@ -84,6 +84,13 @@ int csm_prefill(csm_engine* e, int b, int T, const int32_t* tokens, const uint8_
 /* Generate up to nframes frames for the whole batch (one HIP graph replay per frame).
  * *all_done (optional) = 1 when every utterance hit EOS. */
 int csm_run_frames(csm_engine* e, int nframes, int* all_done);
+/* One frame split around a host hook on the c0 logits (logits_processors, generation.py:42-49):
+ * csm_frame_c0_logits runs the backbone step + codebook0_head and copies logits [B][V] out;
+ * csm_frame_finish takes the (processed) logits [B][V] back, picks c0 (arg-max when greedy, else the
+ * engine's sampler) and runs the 31 decoder steps.  Replaces generate_frame's processor loop
+ * (generation.py:44-49) -- called once per frame instead of csm_run_frames. */
+int csm_frame_c0_logits(csm_engine* e, float* logits);
+int csm_frame_finish(csm_engine* e, const float* logits, int* all_done);
 /* hist [F][B][K] int32 of the frames generated so far, n_frames[B] emitted frames (EOS excluded),
  * done[B].  Any pointer may be NULL. */
 int csm_read_codes(csm_engine* e, int32_t* hist, int32_t* n_frames, uint8_t* done, int* frames_run);

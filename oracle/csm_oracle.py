@@ -269,8 +269,11 @@ class OracleCSM:
                                   self.ad.get("audio_embeddings")).reshape(*tokens.shape[:2], self.K, -1)
         return np.concatenate([audio, text], axis=-2)
 
-    def frame(self, tokens, mask, cache, temperature=0.0, top_k=0, seeds=None, frame_idx=0):
-        """generation.py:21-92.  tokens/mask (B,T,33).  Returns codes (B,K) int32."""
+    def frame(self, tokens, mask, cache, temperature=0.0, top_k=0, seeds=None, frame_idx=0,
+              processors=None, c0_history=None):
+        """generation.py:21-92.  tokens/mask (B,T,33).  Returns codes (B,K) int32.
+        processors: logits processors on c0 (:44-49), called with (stack(c0_history) or zeros((0,)),
+        logits); c0 (B,1) is appended to c0_history when it is a list (:60-61)."""
         B = tokens.shape[0]
         emb = self.embed_tokens(tokens) * mask[..., None].astype(F32)              # :34-35
         x = np.zeros(emb.shape[:2] + emb.shape[3:], F32)
@@ -279,6 +282,9 @@ class OracleCSM:
         h = self.backbone(x, cache)                                                # :39
         h_last = h[:, -1, :]                                                       # :40
         c0_logits = adapted_linear(h_last, self.w["codebook0_head.weight"], self.ad.get("codebook0_head"))  # :42
+        for proc in processors or []:                                              # :44-49
+            hist = np.stack(c0_history, 0) if c0_history else np.zeros((0,), np.int32)
+            c0_logits = np.asarray(proc(hist, c0_logits), F32)
         self.debug["c0_logits"] = c0_logits
         self.debug["h_last"] = h_last
         seeds = seeds if seeds is not None else [0] * B
@@ -286,6 +292,8 @@ class OracleCSM:
                        for b in range(B)], dtype=np.int64)                        # :51-54
         out = np.zeros((B, self.K), np.int32)
         out[:, 0] = c0
+        if c0_history is not None:
+            c0_history.append(c0[:, None].astype(np.int32))
         dec_in = np.stack([h_last, self.embed_audio(0, c0)], axis=1)               # :57-64
         dcache = [KVCacheRef() for _ in range(self.dec_args.num_hidden_layers)]   # :70 fresh per frame
         ci_logits_all = []
@@ -302,7 +310,8 @@ class OracleCSM:
         return out
 
     def generate_codes(self, prompt_tokens: np.ndarray, prompt_mask: np.ndarray, max_frames: int,
-                       temperature=0.0, top_k=0, seed=0, max_seq_len=2048, collect_logits=False):
+                       temperature=0.0, top_k=0, seed=0, max_seq_len=2048, collect_logits=False,
+                       processors=None):
         """generation.py:95-178 up to (not including) decode_audio.  prompt (L,33).
 
         Returns (codes (F,K) int32 up to EOS, logits list if requested)."""
@@ -312,9 +321,9 @@ class OracleCSM:
                              f"{max_seq_len - max_frames}")
         cache = self.new_backbone_cache()
         inp, msk = prompt_tokens[None].astype(np.int64), prompt_mask[None].astype(bool)
-        samples, logs = [], []
+        samples, logs, c0_history = [], [], []                                     # :128
         for f in range(max_frames):                                                # :139
-            s = self.frame(inp, msk, cache, temperature, top_k, [seed], f)
+            s = self.frame(inp, msk, cache, temperature, top_k, [seed], f, processors, c0_history)
             if collect_logits:
                 logs.append((self.debug["c0_logits"][0].copy(), self.debug["ci_logits"][0].copy()))
             if not s.any():                                                        # :151 EOS
