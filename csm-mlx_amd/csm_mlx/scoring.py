@@ -1,0 +1,120 @@
+"""Teacher-forced scoring -- the forward half of ``CSMTrainer.compute_loss``
+(/root/reference/csm_mlx/finetune/trainer.py:203-318).
+
+The reference runs the backbone over the whole (B, S-1) sequence, then the decoder over
+(B*(S-1), 33) rows [h_t, E_0(c_0), ..., E_31(c_31)] of the next frame, and takes the cross entropy
+of every code.  On the GPU the same numbers come out of the frame engine run in teacher-forcing
+mode: the prompt prefix is prefilled, then every scored row is one ``csm_frame_forced`` call (the
+backbone consumes the previous row, codebook0_head and the 31 decoder steps store their logits and
+feed the *given* codes forward, exactly the causal inputs compute_loss builds).  Cross entropy and
+the masked means are reduced on the host from the returned logits.
+
+Layout accepted by ``compute_loss``: per utterance, rows before the first row with a loss are any
+prompt (text and context audio, prefilled); from that row on every row is an audio row (text
+column masked) -- trailing all-masked rows are padding.  Other layouts raise NotImplementedError.
+"""
+from __future__ import annotations
+
+from typing import Dict, List, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from .generation import FrameCache, _check_window
+from .sampling import Sampler
+
+
+def cross_entropy(logits: np.ndarray, targets: np.ndarray) -> np.ndarray:
+    """mlx.nn.losses.cross_entropy(reduction="none"): logsumexp(logits) - logits[target], fp32."""
+    lg = logits.astype(np.float32)
+    mx_ = lg.max(-1, keepdims=True)
+    lse = (np.log(np.exp(lg - mx_).sum(-1, dtype=np.float32)) + mx_[..., 0]).astype(np.float32)
+    picked = np.take_along_axis(lg, targets[..., None].astype(np.int64), -1)[..., 0]
+    return (lse - picked).astype(np.float32)
+
+
+def score_frames(model, prompts: Sequence[Tuple[np.ndarray, np.ndarray]], frames: Sequence[np.ndarray]):
+    """Teacher-forced logits of B utterances: prompt b (tokens (L_b, K+1), mask) followed by the
+    audio frames ``frames[b]`` (F_b, K).  Returns logits (B, F, K, V) float32, F = max F_b; row f of
+    utterance b predicts frames[b][f] (rows past F_b are padding)."""
+    B, K, V = len(prompts), model.n_audio_codebooks, model.n_audio_vocab
+    F = max((len(f) for f in frames), default=0)
+    for t, _ in prompts:
+        _check_window(model, t.shape[0], F)
+    forced = np.zeros((F, B, K), np.int32)
+    for b, fr in enumerate(frames):
+        fr = np.asarray(fr, np.int32).reshape(-1, K)
+        forced[: len(fr), b] = fr
+    cache = FrameCache(model, B, Sampler(0.0, 0), [0] * B)
+    for b, (t, m) in enumerate(prompts):
+        cache.prefill(b, t, m)
+    L = _lib.lib()
+    out = np.zeros((B, F, K, V), np.float32)
+    c0 = np.zeros((B, V), np.float32)
+    ci = np.zeros((K - 1, B, V), np.float32)
+    for f in range(F):
+        codes = np.ascontiguousarray(forced[f])
+        _lib.check(L.csm_frame_forced(model.engine, _lib.ptr(codes), _lib.ptr(c0), _lib.ptr(ci)))
+        out[:, f, 0] = c0
+        out[:, f, 1:] = ci.transpose(1, 0, 2)
+    return out
+
+
+def _split(tokens: np.ndarray, masks: np.ndarray, loss_masks: np.ndarray, K: int):
+    """Per utterance: first scored row r0 (>= 1) and the checks of the accepted layout."""
+    B, S, _ = tokens.shape
+    scored = (masks[:, :, :K] & loss_masks[:, :, :K]).any(-1)          # (B, S)
+    r0 = []
+    for b in range(B):
+        rows = np.nonzero(scored[b, 1:])[0]
+        r = int(rows[0]) + 1 if len(rows) else S
+        tail = masks[b, r:]
+        if tail[:, K].any():
+            raise NotImplementedError("text rows after the first scored row are not supported")
+        full = tail[:, :K].all(-1)
+        empty = ~tail[:, :K].any(-1)
+        if not (full | empty).all() or (len(full) and np.any(np.diff(empty.astype(int)) < 0)):
+            raise NotImplementedError("scored audio rows must be fully unmasked; padding only trailing")
+        r0.append(r)
+    return r0
+
+
+def compute_loss(model, batch: Dict[str, np.ndarray], *, per_sample: bool = False, cause_mismatch: bool = False,
+                 **kwargs):
+    """trainer.py:203-318 on the GPU frame engine (teacher forcing); returns the scalar loss, or the
+    (B,) per-sample losses with ``per_sample``.  Masked means divide by the mask sums as the
+    reference does (0/0 gives nan)."""
+    tokens = np.asarray(batch["tokens"], np.int32)
+    masks = np.asarray(batch["masks"]).astype(bool)
+    loss_masks = np.asarray(batch["loss_masks"]).astype(bool)
+    w0 = np.float32(batch["first_codebook_weight_multiplier"])
+    B, S, n_cb = tokens.shape
+    K = n_cb - 1
+    r0 = _split(tokens, masks, loss_masks, K)
+    prompts = [(tokens[b, : r0[b]], masks[b, : r0[b]]) for b in range(B)]
+    frames = [tokens[b, r0[b]:, :K] for b in range(B)]
+    logits = score_frames(model, prompts, frames)                       # (B, F, K, V)
+    # targets / loss masks on the reference's shifted grid (row t = 1..S-1 predicts row t)
+    tgt = tokens[:, 1:, :K]                                              # :220-221
+    if cause_mismatch:                                                   # :266-269
+        tgt = np.concatenate([tgt[:, 1:], tgt[:, :1]], axis=1)
+    lm = masks[:, 1:, :K] & loss_masks[:, 1:, :K]                        # :263-265
+    ce = np.zeros((B, S - 1, K), np.float32)
+    for b in range(B):
+        n = S - r0[b]
+        if n > 0:
+            ce[b, r0[b] - 1:] = cross_entropy(logits[b, :n], tgt[b, r0[b] - 1:])
+    ce = np.where(lm, ce, np.float32(0))
+    lmf = lm.astype(np.float32)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        if per_sample:
+            c0 = ce[:, :, 0].sum(-1) / lmf[:, :, 0].sum(-1) * w0
+            total = c0 / np.float32(K)
+            for i in range(1, K):
+                total = total + (ce[:, :, i].sum(-1) / lmf[:, :, i].sum(-1)) / np.float32(K)
+        else:
+            c0 = ce[:, :, 0].sum() / lmf[:, :, 0].sum() * w0
+            total = c0 / np.float32(K)
+            for i in range(1, K):
+                total = total + (ce[:, :, i].sum() / lmf[:, :, i].sum()) / np.float32(K)
+    return np.asarray(total, np.float32)

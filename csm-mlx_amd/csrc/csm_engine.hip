@@ -93,6 +93,7 @@ struct csm_engine {
   // activations
   float *x = nullptr, *q = nullptr, *att = nullptr, *mlp = nullptr;
   float *h_last = nullptr, *c0_logits = nullptr, *ci_logits = nullptr;
+  int* force = nullptr;  // [B_max][K] teacher-forced codes (csm_frame_forced)
   float *dx = nullptr, *din = nullptr, *dq = nullptr, *datt = nullptr, *dmlp = nullptr;
   int32_t* tok = nullptr;
   uint8_t* msk = nullptr;
@@ -293,9 +294,11 @@ void enqueue_body(csm_engine* e, hipStream_t st) {
 // host (logits processors, generation.py:44-49).  phase 2: the rest of the frame from c0 logits the
 // host wrote back: c0 is picked by the sample kernel (arg-max when greedy, published as one partial),
 // then steps 1..K-1 as in phase 0.
+// phase 3: teacher forcing -- every head stores its logits and the code fed forward is the caller's
+// (e->force [B][K]), as compute_loss feeds the target frame (trainer.py:233-262).
 void enqueue_head_phase(csm_engine* e, hipStream_t st, int phase) {
   const int B = e->B, K = e->K, D = e->D, Dd = e->Dd, V = e->V, Vp = e->Vpad;
-  const bool greedy = e->temperature <= 0.f;
+  const bool greedy = e->temperature <= 0.f && phase != 3;
   const bool c0_sampled = !greedy || phase == 2;  // c0 published by sample_kernel as a single partial
   const int n0 = head_blocks(Vp, D, B, e->wdt);        // c0-head blocks (partials per row)
   const int ni = head_blocks(Vp, Dd, B, e->head_wdt);  // ci-head blocks
@@ -303,6 +306,7 @@ void enqueue_head_phase(csm_engine* e, hipStream_t st, int phase) {
   SampleParams sp{};
   sp.ls = Vp; sp.V = V; sp.temperature = e->temperature; sp.top_k = e->top_k; sp.seeds = e->seeds;
   sp.frame_ctr = e->frame_ctr; sp.K = K; sp.codes = e->codes; sp.part_stride = e->part_stride;
+  sp.forced = phase == 3 ? e->force : nullptr;
   // c0 = codebook0_head(h_last) (generation.py:42); greedy arg-max fused into the GEMV epilogue
   GemvParams g{};
   g.W = e->c0_head; g.N = Vp; g.K = D; g.x = e->h_last; g.xs = D; g.M = B; g.out = e->c0_logits; g.os = Vp;
@@ -411,6 +415,7 @@ void ensure_batch(csm_engine* e, int B) {
   }
   e->h_last = (float*)e->balloc(Bm * D * 4);
   e->c0_logits = (float*)e->balloc(Bm * Vp * 4);
+  e->force = (int*)e->balloc(Bm * K * 4);
   e->ci_logits = (float*)e->balloc((K - 1) * Bm * Vp * 4);
   e->dx = (float*)e->balloc(2 * Bm * Dd * 4);
   e->din = (float*)e->balloc(2 * Bm * D * 4);
@@ -1028,6 +1033,40 @@ int csm_frame_finish(csm_engine* e, const float* logits, int* all_done) {
     } else {
       HIPCHK(hipStreamSynchronize(e->st));  // the host logits buffer may be released on return
     }
+  }
+  CSM_CATCH
+}
+
+int csm_frame_forced(csm_engine* e, const int32_t* codes, float* c0_logits, float* ci_logits) {
+  CSM_TRY {
+    for (int b = 0; b < e->B; ++b)
+      if (e->prompt_len[b] < 0) throw CsmError(CSM_ERR_STATE, "csm_prefill not called for every utterance");
+    if (e->c0_pending) throw CsmError(CSM_ERR_STATE, "csm_frame_finish pending");
+    if (!codes) throw CsmError(CSM_ERR_ARG, "null codes");
+    HIPCHK(hipSetDevice(e->dev));
+    if (e->frames_run + 1 > e->F_cap) throw CsmError(CSM_ERR_STATE, "frame capacity reached");
+    int maxpos = 0;
+    for (int b = 0; b < e->B; ++b) maxpos = std::max(maxpos, e->pos_host[b]);
+    if (maxpos + 1 + (e->need_body ? 1 : 0) > e->dims.max_seq_len)
+      throw CsmError(CSM_ERR_TOO_LONG, "frames exceed the 2048-position window");
+    for (int i = 0; i < e->B * e->K; ++i)
+      if (codes[i] < 0 || codes[i] >= e->V) throw CsmError(CSM_ERR_ARG, "forced code out of range");
+    HIPCHK(hipMemcpyAsync(e->force, codes, (size_t)e->B * e->K * 4, hipMemcpyHostToDevice, e->st));
+    if (e->need_body) {
+      enqueue_body(e, e->st);
+      for (int b = 0; b < e->B; ++b) e->pos_host[b] += 1;
+    }
+    enqueue_head_phase(e, e->st, 3);
+    HIPCHK(hipGetLastError());
+    e->need_body = true;
+    e->frames_run++;
+    const size_t V = e->V, Vp = e->Vpad, B = e->B;
+    if (c0_logits)
+      HIPCHK(hipMemcpy2DAsync(c0_logits, V * 4, e->c0_logits, Vp * 4, V * 4, B, hipMemcpyDeviceToHost, e->st));
+    if (ci_logits)
+      HIPCHK(hipMemcpy2DAsync(ci_logits, V * 4, e->ci_logits, Vp * 4, V * 4, (size_t)(e->K - 1) * B,
+                              hipMemcpyDeviceToHost, e->st));
+    HIPCHK(hipStreamSynchronize(e->st));
   }
   CSM_CATCH
 }

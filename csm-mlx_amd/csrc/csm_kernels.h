@@ -224,6 +224,7 @@ struct SampleParams {
   int* codes;           // [B][K]
   unsigned long long* part;  // optional: publish the code as partial [b * part_stride]
   int part_stride;
+  const int* forced;    // optional [B][K]: teacher forcing -- the code is forced[b][cb], logits untouched
 };
 
 struct AdvanceParams {

@@ -885,6 +885,14 @@ __global__ __launch_bounds__(256) void sample_kernel(SampleParams p) {
   const float* lg = p.logits + (size_t)b * p.ls;
   const int V = p.V;
   int code;
+  if (p.forced) {  // block-uniform: no barrier below is reached by part of the block
+    if (tid == 0) {
+      code = min(max(p.forced[(size_t)b * p.K + p.cb], 0), V - 1);
+      p.codes[(size_t)b * p.K + p.cb] = code;
+      if (p.part) p.part[(size_t)b * p.part_stride] = pack_argmax(0.f, code);
+    }
+    return;
+  }
   if (p.temperature <= 0.f) {
     float best = -INFINITY;
     int bi = 0x7fffffff;

@@ -91,6 +91,11 @@ int csm_run_frames(csm_engine* e, int nframes, int* all_done);
  * (generation.py:44-49) -- called once per frame instead of csm_run_frames. */
 int csm_frame_c0_logits(csm_engine* e, float* logits);
 int csm_frame_finish(csm_engine* e, const float* logits, int* all_done);
+/* Teacher-forced frame (the scoring form of trainer.py:203-318 compute_loss): the backbone step
+ * consumes the previous frame, then every head stores its logits while the code fed forward is
+ * codes[B][K] (the target frame).  c0_logits [B][V] and ci_logits [K-1][B][V] (optional, may be
+ * NULL) receive the logits that predict codes[b][0] and codes[b][1..K-1]. */
+int csm_frame_forced(csm_engine* e, const int32_t* codes, float* c0_logits, float* ci_logits);
 /* hist [F][B][K] int32 of the frames generated so far, n_frames[B] emitted frames (EOS excluded),
  * done[B].  Any pointer may be NULL. */
 int csm_read_codes(csm_engine* e, int32_t* hist, int32_t* n_frames, uint8_t* done, int* frames_run);

@@ -354,3 +354,47 @@ def audio_frame(codes_kt: np.ndarray) -> (np.ndarray, np.ndarray):
     t[:, :-1] = c.T
     m[:, :-1] = True
     return t, m
+
+
+# ----------------------------------------------------------------------------- compute_loss
+def compute_loss_ref(o: "OracleCSM", batch, per_sample: bool = False, cause_mismatch: bool = False):
+    """/root/reference/csm_mlx/finetune/trainer.py:203-318, whole-sequence form: one causal backbone
+    call over rows [0, S-1), codebook0_head on every position, one causal decoder call over the
+    (B*(S-1), K+1) rows [h_t, E_0(c_0), ..., E_{K-1}(c_{K-1})] of the next frame, masked means of
+    the cross entropies."""
+    tokens = np.asarray(batch["tokens"]).astype(np.int64)
+    masks = np.asarray(batch["masks"]).astype(bool)
+    loss_masks = np.asarray(batch["loss_masks"]).astype(bool)
+    w0 = F32(batch["first_codebook_weight_multiplier"])
+    B, S, n_cb = tokens.shape
+    K = n_cb - 1
+    tgt = tokens[:, 1:, :K]                                                        # :220-221
+    lm = masks[:, 1:, :K] & loss_masks[:, 1:, :K]                                  # :263-265
+    emb = o.embed_tokens(tokens) * masks[..., None].astype(F32)                    # :232-233
+    x = np.zeros(emb.shape[:2] + emb.shape[3:], F32)
+    for j in range(emb.shape[2]):
+        x = x + emb[:, :, j]
+    h = o.backbone(x[:, :-1], o.new_backbone_cache())                              # :234-239
+    c0_logits = adapted_linear(h, o.w["codebook0_head.weight"], o.ad.get("codebook0_head"))
+    ci = np.stack([o.embed_audio(i, tgt[:, :, i]) for i in range(K)], axis=-2)     # :243-249
+    dec_in = np.concatenate([h[:, :, None, :], ci], axis=-2).reshape(-1, n_cb, h.shape[-1])
+    dcache = [KVCacheRef() for _ in range(o.dec_args.num_hidden_layers)]
+    proj = adapted_linear(dec_in, o.w["projection.weight"], o.ad.get("projection"))
+    dh = o.decoder(proj, dcache).reshape(B, S - 1, n_cb, -1)[:, :, 1:-1, :]        # :257-262
+    if cause_mismatch:                                                             # :266-269
+        tgt = np.concatenate([tgt[:, 1:], tgt[:, :1]], axis=1)
+
+    def ce(logits, t):
+        lg = logits.astype(np.float64)
+        m = lg.max(-1, keepdims=True)
+        lse = np.log(np.exp(lg - m).sum(-1)) + m[..., 0]
+        return lse - np.take_along_axis(lg, t[..., None], -1)[..., 0]
+
+    def masked_mean(v, msk):
+        return (v * msk).sum(-1) / msk.sum(-1) if per_sample else (v * msk).sum() / msk.sum()
+    with np.errstate(invalid="ignore", divide="ignore"):
+        total = masked_mean(ce(c0_logits, tgt[:, :, 0]), lm[:, :, 0]) * w0 / K         # :271-289
+        for i in range(1, K):                                                          # :291-312
+            logits = np.matmul(dh[:, :, i - 1, :], o.w["audio_head"][i - 1])
+            total = total + masked_mean(ce(logits, tgt[:, :, i]), lm[:, :, i]) / K
+    return total

@@ -99,3 +99,25 @@ def test_adapter_dir_errors(tmp_path):
     from csm_mlx.adapters import read_adapter_dir
     with pytest.raises(FileNotFoundError):
         read_adapter_dir(tmp_path / "missing")
+
+
+def test_scoring_layout_checks_and_cross_entropy():
+    """csm_mlx.scoring host logic: the accepted compute_loss layout and mlx cross_entropy."""
+    from csm_mlx.scoring import _split, cross_entropy
+    K = 4
+    toks = np.zeros((1, 6, K + 1), np.int32)
+    m = np.zeros((1, 6, K + 1), bool)
+    m[0, :2, K] = True                       # text rows
+    m[0, 2:5, :K] = True                     # audio rows, then one padding row
+    lm = np.zeros_like(m)
+    lm[0, 3:5] = True
+    assert _split(toks, m, lm, K) == [3]
+    m2 = m.copy()
+    m2[0, 4, K] = True                       # text after the first scored row
+    with pytest.raises(NotImplementedError):
+        _split(toks, m2, lm, K)
+    rng = np.random.default_rng(0)
+    lg = rng.standard_normal((3, 7)).astype(np.float32) * 4
+    t = np.array([0, 6, 3])
+    ref = np.log(np.exp(lg.astype(np.float64)).sum(-1)) - lg[np.arange(3), t]
+    np.testing.assert_allclose(cross_entropy(lg, t), ref, rtol=1e-6)

@@ -1,0 +1,73 @@
+"""GPU parity of teacher-forced scoring (csm_frame_forced) against the oracle's whole-sequence
+restatement of compute_loss (trainer.py:203-318): one causal backbone call, one causal decoder call
+over (B*(S-1), K+1) rows.  fp32 weights; losses within 1e-4 relative."""
+import numpy as np
+import pytest
+
+from helpers import csm_weights, oracle_for
+
+pytestmark = pytest.mark.gpu
+
+
+def _batch(args, seed=0):
+    """Two utterances padded to one length: (text prompt, scored audio) and
+    (text, unscored context audio, text, scored audio); loss masks on the scored audio rows."""
+    from csm_mlx.tokenizers import tokenize_text_segment
+    rng = np.random.default_rng(seed)
+    K = args.n_audio_codebooks
+
+    def audio(n):
+        t = np.zeros((n, K + 1), np.int32)
+        t[:, :K] = rng.integers(0, 64, (n, K))
+        m = np.zeros((n, K + 1), bool)
+        m[:, :K] = True
+        return t, m
+    rows = []
+    t1, m1 = tokenize_text_segment([998, 5, 6, 7, 999], 0, K)
+    a1, am1 = audio(6)
+    rows.append((np.concatenate([t1, a1]), np.concatenate([m1, am1]), np.r_[np.zeros(len(t1)), np.ones(6)]))
+    t2, m2 = tokenize_text_segment([998, 11, 999], 1, K)
+    c2, cm2 = audio(2)
+    t3, m3 = tokenize_text_segment([998, 12, 13, 999], 0, K)
+    a2, am2 = audio(8)
+    toks = np.concatenate([t2, c2, t3, a2])
+    rows.append((toks, np.concatenate([m2, cm2, m3, am2]), np.r_[np.zeros(len(toks) - 8), np.ones(8)]))
+    S = max(len(r[0]) for r in rows)
+    T = np.zeros((2, S, K + 1), np.int32)
+    M = np.zeros((2, S, K + 1), bool)
+    LM = np.zeros((2, S, K + 1), bool)
+    for b, (t, m, lm) in enumerate(rows):
+        T[b, : len(t)], M[b, : len(t)] = t, m
+        LM[b, : len(t)] = lm[:, None].astype(bool)
+    return {"tokens": T, "masks": M, "loss_masks": LM, "first_codebook_weight_multiplier": 1.5}
+
+
+@pytest.mark.parametrize("per_sample,mismatch", [(False, False), (True, False), (False, True)])
+def test_compute_loss_matches_oracle(per_sample, mismatch):
+    from csm_mlx.models import CSM
+    from csm_mlx.scoring import compute_loss
+    from oracle.csm_oracle import compute_loss_ref
+    args, w = csm_weights("tiny")
+    model = CSM(args, dtype="float32", max_batch=2)
+    model.load_weights(w)
+    batch = _batch(args)
+    got = compute_loss(model, batch, per_sample=per_sample, cause_mismatch=mismatch)
+    ref = compute_loss_ref(oracle_for(args, w), batch, per_sample=per_sample, cause_mismatch=mismatch)
+    assert np.all(np.isfinite(got)) and np.shape(got) == np.shape(ref)
+    np.testing.assert_allclose(got, ref, rtol=1e-4)
+
+
+def test_score_frames_greedy_codes_are_argmax():
+    """Forcing the greedy generator's own codes reproduces its logits: arg-max of every scored
+    row equals the forced code."""
+    from csm_mlx.generation import generate_batch
+    from csm_mlx.models import CSM
+    from csm_mlx.scoring import score_frames
+    from csm_mlx.tokenizers import tokenize_text_segment
+    args, w = csm_weights("tiny")
+    model = CSM(args, dtype="float32", max_batch=2)
+    model.load_weights(w)
+    p = [tokenize_text_segment([998, 21, 22, 999], 0, args.n_audio_codebooks)]
+    codes = generate_batch(model, p, 8 * 80, temperature=0.0, decode=False)[0]
+    logits = score_frames(model, p, [codes])
+    assert np.array_equal(logits[0, : len(codes)].argmax(-1), codes)
