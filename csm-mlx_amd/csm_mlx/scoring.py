@@ -6,8 +6,10 @@ The reference runs the backbone over the whole (B, S-1) sequence, then the decod
 of every code.  On the GPU the same numbers come out of the frame engine run in teacher-forcing
 mode: the prompt prefix is prefilled, then every scored row is one ``csm_frame_forced`` call (the
 backbone consumes the previous row, codebook0_head and the 31 decoder steps store their logits and
-feed the *given* codes forward, exactly the causal inputs compute_loss builds).  Cross entropy and
-the masked means are reduced on the host from the returned logits.
+feed the *given* codes forward, exactly the causal inputs compute_loss builds).  The cross entropy
+of every forced code is reduced on the GPU (``forced_ce_kernel``: B*K floats leave the device per
+row); only ``cause_mismatch`` (targets differ from the fed codes) copies logits to the host.  The
+masked means are taken on the host.
 
 Layout accepted by ``compute_loss``: per utterance, rows before the first row with a loss are any
 prompt (text and context audio, prefilled); from that row on every row is an audio row (text
@@ -33,10 +35,12 @@ def cross_entropy(logits: np.ndarray, targets: np.ndarray) -> np.ndarray:
     return (lse - picked).astype(np.float32)
 
 
-def score_frames(model, prompts: Sequence[Tuple[np.ndarray, np.ndarray]], frames: Sequence[np.ndarray]):
-    """Teacher-forced logits of B utterances: prompt b (tokens (L_b, K+1), mask) followed by the
-    audio frames ``frames[b]`` (F_b, K).  Returns logits (B, F, K, V) float32, F = max F_b; row f of
-    utterance b predicts frames[b][f] (rows past F_b are padding)."""
+def score_frames(model, prompts: Sequence[Tuple[np.ndarray, np.ndarray]], frames: Sequence[np.ndarray],
+                 logits: bool = True):
+    """Teacher-forced scoring of B utterances: prompt b (tokens (L_b, K+1), mask) followed by the
+    audio frames ``frames[b]`` (F_b, K).  F = max F_b; row f of utterance b predicts frames[b][f]
+    (rows past F_b are padding).  Returns logits (B, F, K, V) float32, or with ``logits=False`` the
+    cross entropy of every forced code (B, F, K), reduced on the GPU (no logits leave the device)."""
     B, K, V = len(prompts), model.n_audio_codebooks, model.n_audio_vocab
     F = max((len(f) for f in frames), default=0)
     for t, _ in prompts:
@@ -49,12 +53,18 @@ def score_frames(model, prompts: Sequence[Tuple[np.ndarray, np.ndarray]], frames
     for b, (t, m) in enumerate(prompts):
         cache.prefill(b, t, m)
     L = _lib.lib()
+    if not logits:
+        ce = np.zeros((F, B, K), np.float32)
+        for f in range(F):
+            codes = np.ascontiguousarray(forced[f])
+            _lib.check(L.csm_frame_forced(model.engine, _lib.ptr(codes), None, None, _lib.ptr(ce[f])))
+        return np.ascontiguousarray(ce.transpose(1, 0, 2))
     out = np.zeros((B, F, K, V), np.float32)
     c0 = np.zeros((B, V), np.float32)
     ci = np.zeros((K - 1, B, V), np.float32)
     for f in range(F):
         codes = np.ascontiguousarray(forced[f])
-        _lib.check(L.csm_frame_forced(model.engine, _lib.ptr(codes), _lib.ptr(c0), _lib.ptr(ci)))
+        _lib.check(L.csm_frame_forced(model.engine, _lib.ptr(codes), _lib.ptr(c0), _lib.ptr(ci), None))
         out[:, f, 0] = c0
         out[:, f, 1:] = ci.transpose(1, 0, 2)
     return out
@@ -93,17 +103,23 @@ def compute_loss(model, batch: Dict[str, np.ndarray], *, per_sample: bool = Fals
     r0 = _split(tokens, masks, loss_masks, K)
     prompts = [(tokens[b, : r0[b]], masks[b, : r0[b]]) for b in range(B)]
     frames = [tokens[b, r0[b]:, :K] for b in range(B)]
-    logits = score_frames(model, prompts, frames)                       # (B, F, K, V)
     # targets / loss masks on the reference's shifted grid (row t = 1..S-1 predicts row t)
     tgt = tokens[:, 1:, :K]                                              # :220-221
-    if cause_mismatch:                                                   # :266-269
-        tgt = np.concatenate([tgt[:, 1:], tgt[:, :1]], axis=1)
     lm = masks[:, 1:, :K] & loss_masks[:, 1:, :K]                        # :263-265
     ce = np.zeros((B, S - 1, K), np.float32)
-    for b in range(B):
-        n = S - r0[b]
-        if n > 0:
-            ce[b, r0[b] - 1:] = cross_entropy(logits[b, :n], tgt[b, r0[b] - 1:])
+    if cause_mismatch:   # targets differ from the fed codes (:266-269): cross entropy from the logits
+        tgt = np.concatenate([tgt[:, 1:], tgt[:, :1]], axis=1)
+        logits = score_frames(model, prompts, frames)                    # (B, F, K, V)
+        for b in range(B):
+            n = S - r0[b]
+            if n > 0:
+                ce[b, r0[b] - 1:] = cross_entropy(logits[b, :n], tgt[b, r0[b] - 1:])
+    else:                # targets are the fed codes: cross entropy reduced on the GPU
+        dev = score_frames(model, prompts, frames, logits=False)         # (B, F, K)
+        for b in range(B):
+            n = S - r0[b]
+            if n > 0:
+                ce[b, r0[b] - 1:] = dev[b, :n]
     ce = np.where(lm, ce, np.float32(0))
     lmf = lm.astype(np.float32)
     with np.errstate(invalid="ignore", divide="ignore"):

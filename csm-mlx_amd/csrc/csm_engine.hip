@@ -94,6 +94,7 @@ struct csm_engine {
   float *x = nullptr, *q = nullptr, *att = nullptr, *mlp = nullptr;
   float *h_last = nullptr, *c0_logits = nullptr, *ci_logits = nullptr;
   int* force = nullptr;  // [B_max][K] teacher-forced codes (csm_frame_forced)
+  float* force_ce = nullptr;  // [B_max][K] their cross entropies
   float *dx = nullptr, *din = nullptr, *dq = nullptr, *datt = nullptr, *dmlp = nullptr;
   int32_t* tok = nullptr;
   uint8_t* msk = nullptr;
@@ -416,6 +417,7 @@ void ensure_batch(csm_engine* e, int B) {
   e->h_last = (float*)e->balloc(Bm * D * 4);
   e->c0_logits = (float*)e->balloc(Bm * Vp * 4);
   e->force = (int*)e->balloc(Bm * K * 4);
+  e->force_ce = (float*)e->balloc(Bm * K * 4);
   e->ci_logits = (float*)e->balloc((K - 1) * Bm * Vp * 4);
   e->dx = (float*)e->balloc(2 * Bm * Dd * 4);
   e->din = (float*)e->balloc(2 * Bm * D * 4);
@@ -1037,7 +1039,7 @@ int csm_frame_finish(csm_engine* e, const float* logits, int* all_done) {
   CSM_CATCH
 }
 
-int csm_frame_forced(csm_engine* e, const int32_t* codes, float* c0_logits, float* ci_logits) {
+int csm_frame_forced(csm_engine* e, const int32_t* codes, float* c0_logits, float* ci_logits, float* ce) {
   CSM_TRY {
     for (int b = 0; b < e->B; ++b)
       if (e->prompt_len[b] < 0) throw CsmError(CSM_ERR_STATE, "csm_prefill not called for every utterance");
@@ -1057,6 +1059,7 @@ int csm_frame_forced(csm_engine* e, const int32_t* codes, float* c0_logits, floa
       for (int b = 0; b < e->B; ++b) e->pos_host[b] += 1;
     }
     enqueue_head_phase(e, e->st, 3);
+    if (ce) launch_forced_ce(e->c0_logits, e->ci_logits, e->force, e->force_ce, e->B, e->K, e->V, e->Vpad, e->st);
     HIPCHK(hipGetLastError());
     e->need_body = true;
     e->frames_run++;
@@ -1066,6 +1069,7 @@ int csm_frame_forced(csm_engine* e, const int32_t* codes, float* c0_logits, floa
     if (ci_logits)
       HIPCHK(hipMemcpy2DAsync(ci_logits, V * 4, e->ci_logits, Vp * 4, V * 4, (size_t)(e->K - 1) * B,
                               hipMemcpyDeviceToHost, e->st));
+    if (ce) HIPCHK(hipMemcpyAsync(ce, e->force_ce, B * e->K * 4, hipMemcpyDeviceToHost, e->st));
     HIPCHK(hipStreamSynchronize(e->st));
   }
   CSM_CATCH

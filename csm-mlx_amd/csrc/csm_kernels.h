@@ -276,6 +276,10 @@ void launch_fused_mlp(const MlpParams& p, int D, bool nt, hipStream_t st);
 bool gemv_nt(int tag);                       // non-temporal weight loads for this stack tag
 void launch_sample(const SampleParams& p, int wdt, int B, hipStream_t st);
 void launch_advance(const AdvanceParams& p, hipStream_t st);
+// Teacher-forced cross entropy (mlx cross_entropy, trainer.py:271-312): out[b][cb] =
+// logsumexp(logits[:V]) - logits[forced[b][cb]] for c0 rows [B][Vp] and ci rows [K-1][B][Vp].
+void launch_forced_ce(const float* c0, const float* ci, const int* forced, float* out, int B, int K, int V, int Vp,
+                      hipStream_t st);
 
 void launch_empty(int blocks, int* p, hipStream_t st);
 

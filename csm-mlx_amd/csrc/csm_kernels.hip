@@ -1361,6 +1361,37 @@ void launch_sample(const SampleParams& p, int wdt, int B, hipStream_t st) {
   else hipLaunchKernelGGL(sample_kernel<float>, dim3(B), dim3(256), 0, st, p);
 }
 
+// One block per (codebook, utterance) row: max, then sum of exp(l - max) in fp32 (wave shuffles +
+// a 4-entry LDS combine), lse - l[target].
+__global__ __launch_bounds__(256) void forced_ce_kernel(const float* c0, const float* ci, const int* forced,
+                                                        float* out, int B, int K, int V, int Vp) {
+  __shared__ float red[4];
+  const int cb = blockIdx.x / B, b = blockIdx.x % B;
+  const float* lg = cb == 0 ? c0 + (size_t)b * Vp : ci + ((size_t)(cb - 1) * B + b) * Vp;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float m = -INFINITY;
+  for (int v = tid; v < V; v += 256) m = fmaxf(m, lg[v]);
+  m = wave_max(m);
+  if (lane == 0) red[wave] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  __syncthreads();
+  float sum = 0.f;
+  for (int v = tid; v < V; v += 256) sum += expf(lg[v] - m);
+  sum = wave_sum(sum);
+  if (lane == 0) red[wave] = sum;
+  __syncthreads();
+  if (tid == 0) {
+    const int t = min(max(forced[(size_t)b * K + cb], 0), V - 1);
+    out[(size_t)b * K + cb] = (logf((red[0] + red[1]) + (red[2] + red[3])) + m) - lg[t];
+  }
+}
+
+void launch_forced_ce(const float* c0, const float* ci, const int* forced, float* out, int B, int K, int V, int Vp,
+                      hipStream_t st) {
+  hipLaunchKernelGGL(forced_ce_kernel, dim3(B * K), dim3(256), 0, st, c0, ci, forced, out, B, K, V, Vp);
+}
+
 void launch_advance(const AdvanceParams& p, hipStream_t st) {
   hipLaunchKernelGGL(advance_kernel, dim3(1), dim3(256), 0, st, p);
 }

@@ -94,8 +94,9 @@ int csm_frame_finish(csm_engine* e, const float* logits, int* all_done);
 /* Teacher-forced frame (the scoring form of trainer.py:203-318 compute_loss): the backbone step
  * consumes the previous frame, then every head stores its logits while the code fed forward is
  * codes[B][K] (the target frame).  c0_logits [B][V] and ci_logits [K-1][B][V] (optional, may be
- * NULL) receive the logits that predict codes[b][0] and codes[b][1..K-1]. */
-int csm_frame_forced(csm_engine* e, const int32_t* codes, float* c0_logits, float* ci_logits);
+ * NULL) receive the logits that predict codes[b][0] and codes[b][1..K-1]; ce [B][K] (optional)
+ * their cross entropies logsumexp(logits) - logits[code], reduced on the device. */
+int csm_frame_forced(csm_engine* e, const int32_t* codes, float* c0_logits, float* ci_logits, float* ce);
 /* hist [F][B][K] int32 of the frames generated so far, n_frames[B] emitted frames (EOS excluded),
  * done[B].  Any pointer may be NULL. */
 int csm_read_codes(csm_engine* e, int32_t* hist, int32_t* n_frames, uint8_t* done, int* frames_run);

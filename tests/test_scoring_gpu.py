@@ -71,3 +71,22 @@ def test_score_frames_greedy_codes_are_argmax():
     codes = generate_batch(model, p, 8 * 80, temperature=0.0, decode=False)[0]
     logits = score_frames(model, p, [codes])
     assert np.array_equal(logits[0, : len(codes)].argmax(-1), codes)
+
+
+def test_device_cross_entropy_matches_logits():
+    """score_frames(logits=False) (forced_ce_kernel) equals the host cross entropy of the logits."""
+    from csm_mlx.models import CSM
+    from csm_mlx.scoring import cross_entropy, score_frames
+    from csm_mlx.tokenizers import tokenize_text_segment
+    args, w = csm_weights("tiny")
+    model = CSM(args, dtype="float32", max_batch=3)
+    model.load_weights(w)
+    rng = np.random.default_rng(5)
+    K = args.n_audio_codebooks
+    p = [tokenize_text_segment([998, 30 + b, 999], 0, K) for b in range(3)]
+    fr = [rng.integers(0, 64, (n, K)).astype(np.int32) for n in (5, 7, 6)]
+    lg = score_frames(model, p, fr)
+    ce = score_frames(model, p, fr, logits=False)
+    for b in range(3):
+        n = len(fr[b])
+        np.testing.assert_allclose(ce[b, :n], cross_entropy(lg[b, :n], fr[b]), rtol=1e-5, atol=1e-5)
