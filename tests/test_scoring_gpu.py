@@ -90,3 +90,22 @@ def test_device_cross_entropy_matches_logits():
     for b in range(3):
         n = len(fr[b])
         np.testing.assert_allclose(ce[b, :n], cross_entropy(lg[b, :n], fr[b]), rtol=1e-5, atol=1e-5)
+
+
+def test_csm_1b_device_cross_entropy():
+    """forced_ce_kernel at csm_1b's vocabulary (V = 2051: nine logits per thread) against the host
+    cross entropy of the same logits; bf16 weights, B = 2, 4 forced rows."""
+    from csm_mlx.models import CSM
+    from csm_mlx.scoring import cross_entropy, score_frames
+    from csm_mlx.tokenizers import tokenize_text_segment
+    from helpers import prompt_ids
+    args, w = csm_weights("1b")
+    model = CSM(args, dtype="bf16", max_batch=2)
+    model.load_weights(w)
+    rng = np.random.default_rng(6)
+    p = [tokenize_text_segment(prompt_ids(s), 0, 32) for s in (1, 2)]
+    fr = [rng.integers(0, 2051, (4, 32)).astype(np.int32) for _ in range(2)]
+    lg = score_frames(model, p, fr)
+    ce = score_frames(model, p, fr, logits=False)
+    for b in range(2):
+        np.testing.assert_allclose(ce[b], cross_entropy(lg[b], fr[b]), rtol=1e-5, atol=1e-4)
