@@ -118,3 +118,31 @@ def test_stream_generate_with_processor(tiny_model):
     assert len(chunks) == len(ref)
     for a, b in zip(chunks, ref):
         assert float(np.sqrt(np.mean((a - b) ** 2))) <= 1e-4
+
+
+def test_stream_generate_from_worker_thread(tiny_model):
+    """The demo's consumer contract (run_streaming_csm_mlx.py:830-872, ThreadPoolExecutor worker
+    :145, :984-1000): stream_generate with logits_processors iterated on a worker thread yields the
+    same chunks as on the calling thread."""
+    from concurrent.futures import ThreadPoolExecutor
+    from csm_mlx import stream_generate
+    from csm_mlx.config import MIMI_CONFIGURATION
+    from csm_mlx.mimi import MimiCodec
+    from csm_mlx.tokenizers import set_audio_tokenizer
+    from csm_mlx.weights import synthetic_mimi_weights
+    model, _, args = tiny_model
+    mm = MIMI_CONFIGURATION["tiny"]
+    codec = MimiCodec(mm, max_batch=4, max_frames=300)
+    codec.load_weights(synthetic_mimi_weights(mm))
+    set_audio_tokenizer(codec, args.n_audio_codebooks)
+    ids = tiny_prompt_ids(11)
+
+    def run():
+        return [np.array(c, np.float32) for c in stream_generate(model, ids, 0, [], max_audio_length_ms=5 * 80,
+                                                                  temperature=0.0, logits_processors=[penalty])]
+    here = run()
+    with ThreadPoolExecutor(max_workers=1) as ex:
+        there = ex.submit(run).result(timeout=60)
+    assert len(here) == len(there) > 0
+    for a, b in zip(here, there):
+        assert np.array_equal(a, b)
