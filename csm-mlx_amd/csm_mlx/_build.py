@@ -27,7 +27,7 @@ def _sources():
 
 def _headers_mtime():
     hs = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")]
-    hs.append(os.path.join(os.path.dirname(ROOT), "include", "csm_hip.h"))
+    hs += [os.path.join(os.path.dirname(ROOT), "include", h) for h in ("csm_hip.h", "csm_hip_prof.h")]
     return max(os.path.getmtime(h) for h in hs if os.path.exists(h))
 
 

@@ -15,6 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # CSM_HIP_LIB: A/B-test another in-tree build of the same ABI (profiling only)
 LIB_PATH = os.environ.get("CSM_HIP_LIB") or os.path.join(_HERE, "libcsm_hip.so")
 HEADER_PATH = os.path.join(os.path.dirname(os.path.dirname(_HERE)), "include", "csm_hip.h")
+PROF_HEADER_PATH = os.path.join(os.path.dirname(HEADER_PATH), "csm_hip_prof.h")  # tuning / profiling hooks
 
 CSM_OK, CSM_ERR_ARG, CSM_ERR_HIP, CSM_ERR_STATE, CSM_ERR_TOO_LONG = 0, -1, -2, -3, -4
 CSM_F32, CSM_BF16, CSM_Q4, CSM_U32 = 0, 1, 2, 3
@@ -51,10 +52,13 @@ class CsmHipError(RuntimeError):
 _lib = None
 
 
-def declared_symbols():
-    """Function names declared in include/csm_hip.h."""
-    src = open(HEADER_PATH).read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+((?:csm|mimi)_\w+)\s*\(", src, re.M)))
+def declared_symbols(headers=(HEADER_PATH, PROF_HEADER_PATH)):
+    """Function names declared in include/csm_hip.h (the reference-facing ABI) and
+    include/csm_hip_prof.h (profiling hooks)."""
+    out = set()
+    for h in headers:
+        out |= set(re.findall(r"^\s*(?:int|const char\*)\s+((?:csm|mimi)_\w+)\s*\(", open(h).read(), re.M))
+    return sorted(out)
 
 
 def lib():
@@ -83,11 +87,7 @@ def lib():
             "csm_debug_read": ([P, ctypes.c_char_p, P, I64, ctypes.POINTER(I64)], I),
             "csm_codes_device_ptr": ([P, ctypes.POINTER(P)], I),
             "csm_synchronize": ([P], I),
-            "csm_set_gemv_config": ([I, I], I),
             "csm_set_option": ([P, ctypes.c_char_p, I], I),
-            "csm_lab_stream": ([I, ctypes.c_double, ctypes.c_double, I, I, I, ctypes.POINTER(F)], I),
-            "csm_lab_gemv": ([I, I, I, I, ctypes.c_double, I, I, I, ctypes.POINTER(F)], I),
-            "csm_bench_floor": ([P, I, I, I, ctypes.POINTER(F)], I),
             "csm_bench_gemv": ([P, I, I, I, ctypes.POINTER(F), ctypes.POINTER(ctypes.c_double)], I),
             "mimi_create": ([ctypes.POINTER(MimiDims), I, I, I, ctypes.POINTER(P)], I),
             "mimi_destroy": ([P], I),

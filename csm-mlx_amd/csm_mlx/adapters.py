@@ -151,7 +151,13 @@ def fuse_adapters(model, config: dict, tensors: Dict[str, np.ndarray],
         if (a is None or b is None) and m is None:
             continue                     # never trained: LoRA's zero-init lora_b leaves W unchanged
         name = path + ".weight"
-        yield name, fuse_module(base_weight(name), kind, a, b, scale, m, model.dtype)
+        base = base_weight(name)
+        if dora and m is None:
+            # DoRALinear / DoRAEmbedding.from_base set m = ||W_base|| per row and load_weights(strict=False)
+            # keeps it when the file has no .m: the fused rows are rescaled back to the base norms
+            w = bf16_round(_as_f32(base)) if model.dtype == "bf16" else _as_f32(base)
+            m = np.sqrt(np.sum(w.astype(np.float64) ** 2, axis=1)).astype(np.float32)
+        yield name, fuse_module(base, kind, a, b, scale, m, model.dtype)
 
 
 def load_adapters(model, adapter_path, base_weights=None):

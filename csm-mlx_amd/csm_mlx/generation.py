@@ -52,7 +52,13 @@ def _seed_list(seed, B: int) -> np.ndarray:
 
 class FrameCache:
     """Replaces the per-layer mlx_lm ``KVCache`` list: a batch slot in the engine
-    (KV caches, positions, code history live on the GPU)."""
+    (KV caches, positions, code history live on the GPU).
+
+    The engine holds ONE active generation per model: creating a FrameCache (or calling
+    ``generate`` / ``stream_generate`` / ``score_frames``, which create one) starts a new batch and
+    overwrites the KV caches.  An older FrameCache of the same model then raises on every call
+    instead of silently reading the new state (the reference's KVCache lists are independent
+    objects; here the caches live in the engine)."""
 
     def __init__(self, model: CSM, batch_size: int, sampler: Sampler, seeds=None):
         self.model = model
@@ -61,9 +67,17 @@ class FrameCache:
         self.seeds = _seed_list(seeds, batch_size)
         self.L = _lib.lib()
         _lib.check(self.L.csm_begin(model.engine, batch_size, _lib.ptr(self.seeds), sampler.temp, sampler.top_k))
+        model._generation = getattr(model, "_generation", 0) + 1
+        self._gen = model._generation
         self.frames = 0
 
+    def _check(self):
+        if getattr(self.model, "_generation", 0) != self._gen:
+            raise RuntimeError("this FrameCache was superseded: a newer generation started on the same model "
+                               "(the engine holds one active generation per model)")
+
     def prefill(self, b: int, tokens: np.ndarray, mask: np.ndarray):
+        self._check()
         t = np.ascontiguousarray(tokens, np.int32)
         m = np.ascontiguousarray(mask, np.uint8)
         _lib.check(self.L.csm_prefill(self.model.engine, b, t.shape[0], _lib.ptr(t), _lib.ptr(m)))
@@ -71,6 +85,7 @@ class FrameCache:
     def run(self, nframes: int, sync: bool = True) -> bool:
         """Enqueue nframes frame graphs; with sync, wait and return whether every utterance is done
         (without, return False at once: the caller polls ``done()``, which waits for the frames)."""
+        self._check()
         done = ctypes.c_int(0)
         _lib.check(self.L.csm_run_frames(self.model.engine, nframes, ctypes.byref(done) if sync else None))
         self.frames += nframes
@@ -81,6 +96,7 @@ class FrameCache:
         the engine stops after codebook0_head, each processor maps (stack(c0_history) or zeros((0,)),
         logits (B, V)) -> logits, and the frame finishes on the GPU from the processed logits.
         Appends this frame's c0 (B, 1) to ``c0_history``; returns whether every utterance is done."""
+        self._check()
         V = self.model.n_audio_vocab
         logits = np.zeros((self.B, V), np.float32)
         _lib.check(self.L.csm_frame_c0_logits(self.model.engine, _lib.ptr(logits)))
@@ -96,6 +112,7 @@ class FrameCache:
 
     def codes(self) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
         """(history [F,B,K], n_frames [B], done [B])."""
+        self._check()
         F = ctypes.c_int(0)
         _lib.check(self.L.csm_read_codes(self.model.engine, None, None, None, ctypes.byref(F)))
         hist = np.zeros((F.value, self.B, self.model.n_audio_codebooks), np.int32)
@@ -105,16 +122,19 @@ class FrameCache:
         return hist, n, d
 
     def done(self) -> np.ndarray:
+        self._check()
         d = np.zeros(self.B, np.uint8)
         _lib.check(self.L.csm_read_codes(self.model.engine, None, None, _lib.ptr(d), None))
         return d.astype(bool)
 
     def last_codes(self) -> np.ndarray:
+        self._check()
         out = np.zeros((self.B, self.model.n_audio_codebooks), np.int32)
         _lib.check(self.L.csm_debug_read(self.model.engine, b"codes", _lib.ptr(out), out.nbytes, None))
         return out
 
     def debug(self, what: str, shape) -> np.ndarray:
+        self._check()
         out = np.zeros(shape, np.float32)
         _lib.check(self.L.csm_debug_read(self.model.engine, what.encode(), _lib.ptr(out), out.nbytes, None))
         return out
@@ -137,6 +157,14 @@ def generate_frame(model: CSM, tokens, *, temperature: float = 0.8, token_mask=N
     B = tokens.shape[0]
     if cache is None:
         cache = make_frame_cache(model, B, temperature=temperature, sampler=sampler, seed=seed)
+    else:
+        # the sampler is fixed when the cache starts its batch (csm_begin); the reference applies the
+        # temperature of every call (generation.py:51-54), so a different one cannot be honoured
+        want = _resolve_sampler(temperature, sampler)
+        if (want.temp, want.top_k) != (cache.sampler.temp, cache.sampler.top_k):
+            raise ValueError(f"generate_frame(temperature={want.temp}, top_k={want.top_k}) differs from the "
+                             f"cache's sampler (temperature={cache.sampler.temp}, top_k={cache.sampler.top_k}); "
+                             f"create the cache with make_frame_cache(model, temperature=...)")
     for b in range(B):
         cache.prefill(b, tokens[b], mask[b])
     if logits_processors:

@@ -11,9 +11,14 @@ of every forced code is reduced on the GPU (``forced_ce_kernel``: B*K floats lea
 row); only ``cause_mismatch`` (targets differ from the fed codes) copies logits to the host.  The
 masked means are taken on the host.
 
-Layout accepted by ``compute_loss``: per utterance, rows before the first row with a loss are any
-prompt (text and context audio, prefilled); from that row on every row is an audio row (text
-column masked) -- trailing all-masked rows are padding.  Other layouts raise NotImplementedError.
+Layouts: per utterance, rows before the first row with a loss are any prompt (text and context
+audio, prefilled).  When every later row is a full audio row (audio columns unmasked, text column
+masked; trailing all-masked rows are padding) the whole batch is scored together.  Otherwise
+(multi-segment conversations: text rows or partially masked rows after the first scored row, as
+``tokenize_segments_with_loss_mask`` builds them) that utterance is scored on its own: every row
+t >= r0 is a forced frame predicting row t, and a row the engine cannot feed back as
+``[codes, 0]`` / ``[1]*K + [0]`` is appended to the backbone with its own tokens and mask by
+``csm_prefill`` -- the backbone input compute_loss builds for it (trainer.py:232-239).
 """
 from __future__ import annotations
 
@@ -70,23 +75,54 @@ def score_frames(model, prompts: Sequence[Tuple[np.ndarray, np.ndarray]], frames
     return out
 
 
+def _standard_row(mask_row: np.ndarray, K: int) -> bool:
+    """A row the engine feeds back itself after a forced frame: audio columns on, text column off."""
+    return bool(mask_row[:K].all()) and not bool(mask_row[K])
+
+
 def _split(tokens: np.ndarray, masks: np.ndarray, loss_masks: np.ndarray, K: int):
-    """Per utterance: first scored row r0 (>= 1) and the checks of the accepted layout."""
+    """Per utterance: first scored row r0 (>= 1) and whether the rows from r0 on are full audio rows
+    followed only by trailing padding (the batched path)."""
     B, S, _ = tokens.shape
     scored = (masks[:, :, :K] & loss_masks[:, :, :K]).any(-1)          # (B, S)
-    r0 = []
+    r0, simple = [], []
     for b in range(B):
         rows = np.nonzero(scored[b, 1:])[0]
         r = int(rows[0]) + 1 if len(rows) else S
         tail = masks[b, r:]
-        if tail[:, K].any():
-            raise NotImplementedError("text rows after the first scored row are not supported")
-        full = tail[:, :K].all(-1)
-        empty = ~tail[:, :K].any(-1)
-        if not (full | empty).all() or (len(full) and np.any(np.diff(empty.astype(int)) < 0)):
-            raise NotImplementedError("scored audio rows must be fully unmasked; padding only trailing")
+        full = tail[:, :K].all(-1) & ~tail[:, K]
+        empty = ~tail.any(-1)
+        ok = bool((full | empty).all()) and not (len(full) and np.any(np.diff(empty.astype(int)) < 0))
         r0.append(r)
-    return r0
+        simple.append(ok)
+    return r0, simple
+
+
+def _score_utterance(model, tokens: np.ndarray, masks: np.ndarray, r0: int, logits: bool):
+    """One utterance of any layout: rows [0, r0) prefilled, then a forced frame per row t >= r0 (its
+    c0 / ci predictions from h_{t-1}); rows that are not full audio rows are appended to the backbone
+    with their own mask.  Returns (S - r0, K, V) logits or (S - r0, K) cross entropies."""
+    S, n_cb = tokens.shape
+    K, V = n_cb - 1, model.n_audio_vocab
+    L = _lib.lib()
+    cache = FrameCache(model, 1, Sampler(0.0, 0), [0])
+    cache.prefill(0, tokens[:r0], masks[:r0])
+    out = np.zeros((S - r0, K, V) if logits else (S - r0, K), np.float32)
+    c0 = np.zeros((1, V), np.float32)
+    ci = np.zeros((K - 1, 1, V), np.float32)
+    for t in range(r0, S):
+        codes = np.ascontiguousarray(tokens[t, :K][None], np.int32)
+        if logits:
+            _lib.check(L.csm_frame_forced(model.engine, _lib.ptr(codes), _lib.ptr(c0), _lib.ptr(ci), None))
+            out[t - r0, 0] = c0[0]
+            out[t - r0, 1:] = ci[:, 0]
+        else:
+            ce = np.zeros((1, K), np.float32)
+            _lib.check(L.csm_frame_forced(model.engine, _lib.ptr(codes), None, None, _lib.ptr(ce)))
+            out[t - r0] = ce[0]
+        if t + 1 < S and not _standard_row(masks[t], K):
+            cache.prefill(0, tokens[t:t + 1], masks[t:t + 1])   # row t with its own mask
+    return out
 
 
 def compute_loss(model, batch: Dict[str, np.ndarray], *, per_sample: bool = False, cause_mismatch: bool = False,
@@ -100,26 +136,30 @@ def compute_loss(model, batch: Dict[str, np.ndarray], *, per_sample: bool = Fals
     w0 = np.float32(batch["first_codebook_weight_multiplier"])
     B, S, n_cb = tokens.shape
     K = n_cb - 1
-    r0 = _split(tokens, masks, loss_masks, K)
-    prompts = [(tokens[b, : r0[b]], masks[b, : r0[b]]) for b in range(B)]
-    frames = [tokens[b, r0[b]:, :K] for b in range(B)]
+    r0, simple = _split(tokens, masks, loss_masks, K)
+    batched = [b for b in range(B) if simple[b]]
     # targets / loss masks on the reference's shifted grid (row t = 1..S-1 predicts row t)
     tgt = tokens[:, 1:, :K]                                              # :220-221
     lm = masks[:, 1:, :K] & loss_masks[:, 1:, :K]                        # :263-265
     ce = np.zeros((B, S - 1, K), np.float32)
     if cause_mismatch:   # targets differ from the fed codes (:266-269): cross entropy from the logits
         tgt = np.concatenate([tgt[:, 1:], tgt[:, :1]], axis=1)
-        logits = score_frames(model, prompts, frames)                    # (B, F, K, V)
-        for b in range(B):
-            n = S - r0[b]
-            if n > 0:
-                ce[b, r0[b] - 1:] = cross_entropy(logits[b, :n], tgt[b, r0[b] - 1:])
-    else:                # targets are the fed codes: cross entropy reduced on the GPU
-        dev = score_frames(model, prompts, frames, logits=False)         # (B, F, K)
-        for b in range(B):
-            n = S - r0[b]
-            if n > 0:
-                ce[b, r0[b] - 1:] = dev[b, :n]
+    res = {}
+    if batched:
+        prompts = [(tokens[b, : r0[b]], masks[b, : r0[b]]) for b in batched]
+        frames = [tokens[b, r0[b]:, :K] for b in batched]
+        got = score_frames(model, prompts, frames, logits=cause_mismatch)  # (b, F, K[, V])
+        res.update({b: got[j] for j, b in enumerate(batched)})
+    for b in range(B):
+        if not simple[b]:
+            res[b] = _score_utterance(model, tokens[b], masks[b], r0[b], cause_mismatch)
+    for b in range(B):
+        n = S - r0[b]
+        if n > 0:
+            if cause_mismatch:
+                ce[b, r0[b] - 1:] = cross_entropy(res[b][:n], tgt[b, r0[b] - 1:])
+            else:        # targets are the fed codes: cross entropy reduced on the GPU
+                ce[b, r0[b] - 1:] = res[b][:n]
     ce = np.where(lm, ce, np.float32(0))
     lmf = lm.astype(np.float32)
     with np.errstate(invalid="ignore", divide="ignore"):

@@ -12,7 +12,6 @@ only look in the local Hugging Face cache; synthetic runs register a codec with
 """
 from __future__ import annotations
 
-from functools import lru_cache
 from typing import List, Optional, Sequence, Union
 
 import numpy as np
@@ -48,16 +47,12 @@ def get_audio_tokenizer(n_audio_codebooks: int):
     return codec
 
 
-@lru_cache(maxsize=None)
-def get_text_tokenizer():
-    """tokenizers.py:24-40 (BOS/EOS template around every encode)."""
+_text_tokenizer = None
+
+
+def _with_bos_eos_template(tok):
+    """tokenizers.py:29-39: BOS/EOS TemplateProcessing around every encode (single and pair)."""
     from tokenizers.processors import TemplateProcessing
-    from transformers import AutoTokenizer
-    try:
-        tok = AutoTokenizer.from_pretrained(TOKENIZERS["text"]["repo_id"], local_files_only=True)
-    except Exception as ex:  # noqa: BLE001
-        raise RuntimeError("the Llama-3.2 tokenizer is not in the local HF cache (offline); pass pre-tokenized "
-                           "ids (a list of ints) as `text`") from ex
     bos, eos = tok.bos_token, tok.eos_token
     tok._tokenizer.post_processor = TemplateProcessing(
         single=f"{bos}:0 $A:0 {eos}:0",
@@ -65,6 +60,30 @@ def get_text_tokenizer():
         special_tokens=[(f"{bos}", tok.bos_token_id), (f"{eos}", tok.eos_token_id)],
     )
     return tok
+
+
+def set_text_tokenizer(tok):
+    """Register a text tokenizer (a transformers fast tokenizer with bos/eos tokens) in place of the
+    hub download; the reference's BOS/EOS template is applied to it."""
+    global _text_tokenizer
+    _text_tokenizer = _with_bos_eos_template(tok)
+    return _text_tokenizer
+
+
+def get_text_tokenizer():
+    """tokenizers.py:24-40 (BOS/EOS template around every encode).  Offline: a registered tokenizer
+    (``set_text_tokenizer``) or the local HF cache."""
+    global _text_tokenizer
+    if _text_tokenizer is None:
+        from transformers import AutoTokenizer
+        try:
+            tok = AutoTokenizer.from_pretrained(TOKENIZERS["text"]["repo_id"], local_files_only=True)
+        except Exception as ex:  # noqa: BLE001
+            raise RuntimeError("the Llama-3.2 tokenizer is not in the local HF cache (offline); register one "
+                               "with csm_mlx.tokenizers.set_text_tokenizer(...) or pass pre-tokenized ids "
+                               "(a list of ints) as `text`") from ex
+        _text_tokenizer = _with_bos_eos_template(tok)
+    return _text_tokenizer
 
 
 def tokenize_text_segment(text: Union[str, Sequence[int]], speaker: int, n_audio_codebooks: int = 32):
@@ -121,6 +140,26 @@ def tokenize_segments_batch(segments: List[Segment], *, n_audio_codebooks: int =
         a_tok, a_mask = audio_codes_to_frames(np.asarray(c))
         out.append((np.concatenate([t_tok, a_tok], 0), np.concatenate([t_mask, a_mask], 0)))
     return out
+
+
+def tokenize_segments_with_loss_mask(segments: List[Segment], *, n_audio_codebooks: int = 32,
+                                     mask_speaker_ids: Sequence[int], max_audio_length_ms: Optional[int]):
+    """tokenizers.py:105-145 (the fine-tuning batch layout that ``scoring.compute_loss`` scores):
+    every segment's rows concatenated, loss mask ones except the rows of segments whose speaker is in
+    ``mask_speaker_ids``, all three truncated to max_audio_length_ms / 80 rows."""
+    parts = [tokenize_segment(seg, n_audio_codebooks=n_audio_codebooks) for seg in segments]
+    tokens = np.concatenate([t for t, _ in parts], 0).astype(np.int32)
+    masks = np.concatenate([m for _, m in parts], 0).astype(bool)
+    loss_masks = np.ones_like(tokens)
+    pos = 0
+    for (t, _), seg in zip(parts, segments):
+        if seg.speaker in mask_speaker_ids:
+            loss_masks[pos:pos + t.shape[0]] = 0
+        pos += t.shape[0]
+    if max_audio_length_ms is not None:
+        n = int(max_audio_length_ms / 80)
+        tokens, masks, loss_masks = tokens[:n], masks[:n], loss_masks[:n]
+    return tokens, masks, loss_masks
 
 
 def decode_audio(audio_tokens, *, n_audio_codebooks: int = 32) -> np.ndarray:

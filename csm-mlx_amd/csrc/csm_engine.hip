@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "../../include/csm_hip.h"
+#include "../../include/csm_hip_prof.h"
 #include "csm_kernels.h"
 #include "engine_util.h"
 
@@ -130,6 +131,7 @@ struct csm_engine {
   // the atomics removed (invalid results) the one-launch MLP ran at 264 frames/s.
   bool fuse_mlp = [] { const char* v = getenv("CSM_FUSE_MLP"); return v && v[0] == '1'; }();
   int acc_rows = 0;  // rows of the fused-MLP accumulators (the fused path runs for M <= acc_rows)
+  GemmWs ws;         // split-K slabs + tickets of this engine's MFMA launches (ensure_batch sizes them)
 
   void* balloc(size_t bytes) {
     void* p = nullptr;
@@ -159,12 +161,20 @@ struct csm_engine {
     if (g_head) (void)hipGraphExecDestroy(g_head);
     for (void* p : allocs) (void)hipFree(p);
     for (void* p : batch_allocs) (void)hipFree(p);
+    gemm_ws_free(ws);
     if (st) (void)hipStreamDestroy(st);
   }
 };
 
 // ---------------------------------------------------------------------------------------------
 namespace {
+
+// GEMV / GEMM parameters bound to this engine's split-K scratch
+GemvParams gp(csm_engine* e) {
+  GemvParams g{};
+  g.ws = &e->ws;
+  return g;
+}
 
 void alloc_stack(csm_engine* e, Stack& s, const csm_llama_dims& d, int S_cap, const char* prefix) {
   s.d = d;
@@ -220,7 +230,7 @@ long long* run_stack(csm_engine* e, Stack& s, float* x, int M, float* q, float* 
                      fused_mlp_supported(D, F, M) && !(ab & 24);
   for (int i = 0; i < d.n_layers; ++i) {
     LayerW& l = s.L[i];
-    GemvParams g{};
+    GemvParams g = gp(e);
     // norm1 + QKV + RoPE + KV append
     g.W = l.wqkv; g.N = s.qkv_rows(); g.K = D; g.x = x; g.xs = D; g.M = M; g.nw = l.n1; g.eps = d.eps;
     g.out = q; g.os = s.q_dim(); g.Hq = Hq; g.Hkv = Hkv; g.hd = hd; g.S_cap = s.S_cap; g.rope = s.rope;
@@ -239,7 +249,7 @@ long long* run_stack(csm_engine* e, Stack& s, float* x, int M, float* q, float* 
     a.q = q; a.qs = s.q_dim(); a.M = M; a.kc = l.kc; a.vc = l.vc; a.Hq = Hq; a.Hkv = Hkv; a.S_cap = s.S_cap;
     a.scale = 1.0f / sqrtf((float)hd); a.mode = ATTN_CAUSAL; a.window = 0; a.rm = rm; a.out = att;
     a.os = s.q_dim();
-    g = GemvParams{};
+    g = gp(e);
     g.W = l.wo; g.N = D; g.K = s.q_dim(); g.x = att; g.xs = s.q_dim(); g.M = M; g.out = x; g.os = D;
     if (fused) {
       g.oacc = s.acc[(i + 1) & 1];
@@ -260,12 +270,12 @@ long long* run_stack(csm_engine* e, Stack& s, float* x, int M, float* q, float* 
       continue;
     }
     // norm2 + gate/up + SiLU*up
-    g = GemvParams{};
+    g = gp(e);
     g.W = l.wgu; g.N = 2 * F; g.K = D; g.x = x; g.xs = D; g.M = M; g.nw = l.n2; g.eps = d.eps; g.out = mlp;
     g.os = F;
     if (!(ab & 8)) launch_gemv(g, e->wdt, EPI_SILU_MUL, 1, st, tag);
     // down + residual
-    g = GemvParams{};
+    g = gp(e);
     g.W = l.wd; g.N = D; g.K = F; g.x = mlp; g.xs = F; g.M = M; g.out = x; g.os = D;
     if (!(ab & 16)) launch_gemv(g, e->wdt, EPI_ADD, 0, st, tag);
   }
@@ -309,7 +319,7 @@ void enqueue_head_phase(csm_engine* e, hipStream_t st, int phase) {
   sp.frame_ctr = e->frame_ctr; sp.K = K; sp.codes = e->codes; sp.part_stride = e->part_stride;
   sp.forced = phase == 3 ? e->force : nullptr;
   // c0 = codebook0_head(h_last) (generation.py:42); greedy arg-max fused into the GEMV epilogue
-  GemvParams g{};
+  GemvParams g = gp(e);
   g.W = e->c0_head; g.N = Vp; g.K = D; g.x = e->h_last; g.xs = D; g.M = B; g.out = e->c0_logits; g.os = Vp;
   g.part = part(0); g.part_stride = e->part_stride; g.n_valid = V;
   if (phase != 2) launch_gemv(g, e->wdt, (greedy && phase == 0) ? EPI_ARGMAX : EPI_STORE, 0, st);
@@ -322,7 +332,7 @@ void enqueue_head_phase(csm_engine* e, hipStream_t st, int phase) {
     const int M = (i == 1) ? 2 * B : B;
     // decoder(projection(decoder_inputs)) (generation.py:74-77): the projection gathers its input
     // rows itself -- [h_last, E_a[c0]] at step 1 (:62-64), E_a[c_{i-1} + V*(i-1)] after (:87-89)
-    g = GemvParams{};
+    g = gp(e);
     g.W = e->proj; g.N = Dd; g.K = D; g.x = e->h_last; g.xs = D; g.M = M; g.out = e->dx; g.os = Dd;
     g.xpart = part(i - 1); g.xpart_stride = e->part_stride; g.xpart_n = i == 1 ? (c0_sampled ? 1 : n0) : (greedy ? ni : 1);
     g.xtab = e->audio_emb; g.xV = V; g.xcb = i - 1; g.x_step1 = (i == 1); g.x_codes = e->codes; g.x_codes_K = K;
@@ -338,9 +348,9 @@ void enqueue_head_phase(csm_engine* e, hipStream_t st, int phase) {
         GemvParams gr = g;
         gr.K = D; gr.out = e->din; gr.os = D;
         launch_gather_rows(gr, e->wdt, st);
-        GemvParams gp = GemvParams{};
-        gp.W = e->proj; gp.N = Dd; gp.K = D; gp.x = e->din; gp.xs = D; gp.M = M; gp.out = e->dx; gp.os = Dd;
-        launch_gemv(gp, e->wdt, EPI_STORE, 0, st);
+        GemvParams gj = gp(e);
+        gj.W = e->proj; gj.N = Dd; gj.K = D; gj.x = e->din; gj.xs = D; gj.M = M; gj.out = e->dx; gj.os = Dd;
+        launch_gemv(gj, e->wdt, EPI_STORE, 0, st);
       } else {
         GemvParams gr = g0;
         gr.K = Dd; gr.out = e->dx; gr.os = Dd;
@@ -359,7 +369,7 @@ void enqueue_head_phase(csm_engine* e, hipStream_t st, int phase) {
       pend = run_stack(e, e->dec, e->dx, M, e->dq, e->datt, e->dmlp, rm, st, folded ? &g0 : nullptr);
     }
     // ci_logits = norm(hidden[:, -1]) @ audio_head[i-1]  (generation.py:79)
-    g = GemvParams{};
+    g = gp(e);
     g.W = (const char*)e->audio_head + (size_t)(i - 1) * Vp * Dd * (e->head_wdt == WDT_F32 ? 4 : 2); g.N = Vp; g.K = Dd;
     g.x = e->dx + (i == 1 ? Dd : 0); g.xs = (i == 1 ? 2 * Dd : Dd); g.M = B; g.nw = e->dec.norm;
     g.eps = e->dec.d.eps; g.out = e->ci_logits + (size_t)(i - 1) * B * Vp; g.os = Vp;
@@ -440,14 +450,14 @@ void ensure_batch(csm_engine* e, int B) {
   // split-K scratch of the MFMA path for every projection shape at its largest row count
   for (Stack* s : {&e->bb, &e->dec}) {
     const int Dm = s->d.hidden, F = s->d.intermediate, rows = (s == &e->bb) ? std::max(e->M_cap, (int)Bm) : 2 * (int)Bm;
-    gemm_reserve(s->qkv_rows(), Dm, rows);
-    gemm_reserve(Dm, s->q_dim(), rows);
-    gemm_reserve(2 * F, Dm, rows);
-    gemm_reserve(Dm, F, rows);
+    gemm_reserve(e->ws, s->qkv_rows(), Dm, rows);
+    gemm_reserve(e->ws, Dm, s->q_dim(), rows);
+    gemm_reserve(e->ws, 2 * F, Dm, rows);
+    gemm_reserve(e->ws, Dm, F, rows);
   }
-  gemm_reserve((int)Dd, (int)D, 2 * (int)Bm);
-  gemm_reserve((int)Vp, (int)D, (int)Bm);   // c0 head
-  gemm_reserve((int)Vp, (int)Dd, (int)Bm);  // ci heads
+  gemm_reserve(e->ws, (int)Dd, (int)D, 2 * (int)Bm);
+  gemm_reserve(e->ws, (int)Vp, (int)D, (int)Bm);   // c0 head
+  gemm_reserve(e->ws, (int)Vp, (int)Dd, (int)Bm);  // ci heads
 }
 
 // proj_tab[cb] = projection(E_a rows of codebook cb), computed by the projection GEMV itself
@@ -458,7 +468,7 @@ void build_proj_table(csm_engine* e) {
   for (int cb = 0; cb < e->K - 1; ++cb) {
     if (e->wdt == WDT_Q4) launch_q4_to_f32(e->audio_emb, V * e->K, D, cb * V, V, scratch, e->st);
     else launch_to_f32((const char*)e->audio_emb + (size_t)cb * V * D * e->wsz, e->wdt, scratch, (size_t)V * D, e->st);
-    GemvParams g{};
+    GemvParams g = gp(e);
     g.W = e->proj; g.N = Dd; g.K = D; g.x = scratch; g.xs = D; g.M = V;
     g.out = e->proj_tab + (size_t)cb * V * Dd; g.os = Dd;
     g.no_mfma = 1;  // the GEMV's per-row arithmetic (the step-1 launch's), never the matrix cores
@@ -473,7 +483,7 @@ void build_proj_table(csm_engine* e) {
   const Stack& s = e->dec;
   const LayerW& l0 = s.L[0];
   for (int cb = 1; cb < e->K - 1; ++cb) {
-    GemvParams g{};
+    GemvParams g = gp(e);
     g.W = l0.wqkv; g.N = s.qkv_rows(); g.K = Dd; g.x = e->proj_tab + (size_t)cb * V * Dd; g.xs = Dd;
     g.M = V; g.nw = l0.n1; g.eps = s.d.eps; g.Hq = s.d.n_heads; g.Hkv = s.d.n_kv_heads;
     g.hd = s.d.head_dim; g.S_cap = s.S_cap; g.rope = s.rope; g.rm = RowMap{1, 0, nullptr, cb + 1};
@@ -1137,7 +1147,7 @@ int csm_bench_gemv(csm_engine* e, int which, int M, int iters, float* avg_us, do
     // HBM, decoder 4 x 33.5 MB stays within the 256 MiB Infinity Cache.
     auto params = [&](int layer, int& epi, int& norm) {
       const LayerW& l = s.L[layer];
-      GemvParams g{};
+      GemvParams g = gp(e);
       if (kind == 0) {  // norm + gate/up + SiLU
         g.W = l.wgu; g.N = 2 * F; g.K = D; g.x = x; g.xs = D; g.M = M; g.nw = l.n2; g.eps = s.d.eps;
         g.out = mlp; g.os = F; epi = EPI_SILU_MUL; norm = 1;
@@ -1178,44 +1188,6 @@ int csm_bench_gemv(csm_engine* e, int which, int M, int iters, float* avg_us, do
   CSM_CATCH
 }
 
-int csm_bench_floor(csm_engine* e, int n_kernels, int blocks, int graph, float* us_per_kernel) {
-  CSM_TRY {
-    if (n_kernels <= 0 || blocks <= 0) throw CsmError(CSM_ERR_ARG, "bad floor arguments");
-    HIPCHK(hipSetDevice(e->dev));
-    int* ctr = e->frame_ctr + 2;  // scratch word (frame_ctr[2] is unused)
-    hipGraphExec_t exec = nullptr;
-    if (graph) {
-      hipGraph_t gr;
-      HIPCHK(hipStreamBeginCapture(e->st, hipStreamCaptureModeThreadLocal));
-      for (int i = 0; i < n_kernels; ++i) launch_empty(blocks, ctr, e->st);
-      HIPCHK(hipStreamEndCapture(e->st, &gr));
-      HIPCHK(hipGraphInstantiate(&exec, gr, nullptr, nullptr, 0));
-      (void)hipGraphDestroy(gr);
-      HIPCHK(hipGraphLaunch(exec, e->st));
-    }
-    HIPCHK(hipStreamSynchronize(e->st));
-    hipEvent_t a, b;
-    HIPCHK(hipEventCreate(&a));
-    HIPCHK(hipEventCreate(&b));
-    HIPCHK(hipEventRecord(a, e->st));
-    for (int r = 0; r < 5; ++r) {
-      if (graph) HIPCHK(hipGraphLaunch(exec, e->st));
-      else for (int i = 0; i < n_kernels; ++i) launch_empty(blocks, ctr, e->st);
-    }
-    HIPCHK(hipEventRecord(b, e->st));
-    HIPCHK(hipEventSynchronize(b));
-    float ms = 0.f;
-    HIPCHK(hipEventElapsedTime(&ms, a, b));
-    (void)hipEventDestroy(a);
-    (void)hipEventDestroy(b);
-    if (exec) (void)hipGraphExecDestroy(exec);
-    HIPCHK(hipMemsetAsync(ctr, 0, 4, e->st));
-    HIPCHK(hipStreamSynchronize(e->st));
-    if (us_per_kernel) *us_per_kernel = ms * 1000.f / (5.f * n_kernels);
-  }
-  CSM_CATCH
-}
-
 int csm_set_option(csm_engine* e, const char* key, int value) {
   CSM_TRY {
     const std::string k(key ? key : "");
@@ -1240,15 +1212,6 @@ int csm_set_option(csm_engine* e, const char* key, int value) {
     }
     else throw CsmError(CSM_ERR_ARG, "unknown option " + k);
     if (e) e->g_B = -1;  // re-capture the frame graphs with the new setting
-  }
-  CSM_CATCH
-}
-
-int csm_set_gemv_config(int G, int RPT) {
-  CSM_TRY {
-    if ((G && G != 64 && G != 128 && G != 256) || (RPT && RPT != 2 && RPT != 4))
-      throw CsmError(CSM_ERR_ARG, "G in {0,64,128,256}, RPT in {0,2,4}");
-    gemv_set_override(G, RPT);
   }
   CSM_CATCH
 }

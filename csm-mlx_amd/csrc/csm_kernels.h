@@ -21,6 +21,15 @@ __device__ __forceinline__ long long acc_slots_sum(const long long* a, size_t ss
   return t;
 }
 
+// Split-K scratch of the MFMA path, owned by one engine (csm_engine::ws): slice partials and arrival
+// tickets, sized by gemm_reserve outside graph capture.
+struct GemmWs {
+  float* kpart = nullptr;
+  size_t bytes = 0;
+  unsigned* tickets = nullptr;
+  size_t n = 0;
+};
+
 struct GemvParams {
   const void* W;      // [N][K] weight (bf16 or f32)
   int N, K;
@@ -60,7 +69,8 @@ struct GemvParams {
   long long* oacc;        // EPI_ADD: out = (out + acc) + a when oacc_add (else out += a); acc zeroed
   int oacc_add;
   int acc_ss;             // elements between accumulator slots
-  // MFMA path split-K (set by launch_gemm_mfma): slice partials [ksplit][M][N], sum-of-squares [ksplit][M]
+  // MFMA path split-K (set by launch_gemm_mfma from ws): slice partials [ksplit][M][N], sum-of-squares [ksplit][M]
+  GemmWs* ws;            // the calling engine's scratch (host pointer; required for split launches)
   float* kpart;          // [tile][m chunk][slice][slab] split-K slice partials (+ sum x^2), written sc1
   unsigned* kticket;     // [tile][m chunk] arrival tickets (zero between launches)
   int ksplit;
@@ -248,7 +258,6 @@ void launch_to_f32(const void* src, int wdt, float* dst, size_t n, hipStream_t s
 void launch_attn(const AttnParams& p, int hd, hipStream_t st);
 // rows per block of the GEMV launch for (N, K, M): N must be a multiple of it
 int gemv_rows_per_block(int N, int K, int M);
-void gemv_set_override(int G, int RPT);  // 0 = automatic
 // depth-decoder attention recomputed inside every o_proj block (+ residual): one launch
 bool dec_attn_oproj_supported(const GemvParams& p, const AttnParams& a, int hd);
 void launch_dec_attn_oproj(const GemvParams& p, const AttnParams& a, int wdt, hipStream_t st, int tag);
@@ -281,7 +290,6 @@ void launch_advance(const AdvanceParams& p, hipStream_t st);
 void launch_forced_ce(const float* c0, const float* ci, const int* forced, float* out, int B, int K, int V, int Vp,
                       hipStream_t st);
 
-void launch_empty(int blocks, int* p, hipStream_t st);
 
 // ---- int4 (q4_kernels.hip)
 // quantize rows [0, n_rows) of a dense [n_rows][K] f32/bf16 device matrix into rows row0 + r*rstep of a
@@ -302,7 +310,9 @@ constexpr int GEMM_MFMA_MIN_M = 8;  // rows at which a bf16 projection leaves th
 bool gemm_mfma_eligible(int N, int K, int M, int wdt);
 int gemm_blocks(int N);  // row-tile blocks (= arg-max partials per row)
 void launch_gemm_mfma(const GemvParams& p, int wdt, bool nt, hipStream_t st);
-void gemm_reserve(int N, int K, int M);  // pre-size the split-K scratch (outside graph capture)
+// pre-size ws for (N, K) at any row count <= M (outside graph capture); true if it reallocated
+bool gemm_reserve(GemmWs& ws, int N, int K, int M);
+void gemm_ws_free(GemmWs& ws);
 // dense decoder-input rows from a table (codes resolved from arg-max partials), see gather_rows_kernel
 void launch_gather_rows(const GemvParams& p, int wdt, hipStream_t st);
 // arg-max partial slots per row written by launch_gemv for this shape / dtype / row count

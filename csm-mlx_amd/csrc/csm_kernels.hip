@@ -1006,13 +1006,7 @@ __global__ void advance_kernel(AdvanceParams p) {
 }
 
 // ============================================================================ launchers
-// tiling choice (G threads per row group, RPT rows per thread); g_gemv_override lets the
-// profiling hook csm_set_gemv_config sweep alternatives.
-static int g_gemv_G = 0, g_gemv_RPT = 0;
-void gemv_set_override(int G, int RPT) {
-  g_gemv_G = G;
-  g_gemv_RPT = RPT;
-}
+// tiling choice (G threads per row group, RPT rows per thread)
 
 // Measured on MI355X (tools/gemv_sweep.py, bf16, M = 1): tall gate/up matrices want one wave per
 // row group (G = 64: no cross-wave reduction, 2-4 K-steps per thread); the K = 8192 down
@@ -1030,8 +1024,6 @@ static void gemv_tiling(int N, int K, int M, int& G, int& RPT) {
   else if (K >= 8192) G = N <= 1024 ? 256 : 128;
   else G = K >= 1024 ? 128 : 64;
   RPT = 2;
-  if (g_gemv_G) G = g_gemv_G;
-  if (g_gemv_RPT) RPT = g_gemv_RPT;
 }
 
 template <typename WT, int TAG>
@@ -1421,12 +1413,4 @@ void launch_dec_attn_oproj(const GemvParams& p0, const AttnParams& a, int wdt, h
   }
 #undef DA_R
 #undef DA_L
-}
-
-// ============================================================================ launch-floor probe
-__global__ void empty_kernel(int* p) {
-  if (p && threadIdx.x == 0 && blockIdx.x == 0) p[0] += 1;
-}
-void launch_empty(int blocks, int* p, hipStream_t st) {
-  hipLaunchKernelGGL(empty_kernel, dim3(blocks), dim3(256), 0, st, p);
 }

@@ -4,24 +4,33 @@
 // codebook heads (models.py:50-67, generation.py:42, :74-79) once the row count M makes the
 // GEMV's per-row loop (gemv_kernel re-streams the weights every MT rows) the bottleneck.
 //
-// Operands: W bf16 [N][K] as stored (MLX (out,in) layout) is the MFMA A operand (32 weight rows per
-// wave); the fp32 activations are the B operand (32 batch rows per tile), each value split into two
-// bf16 parts x = hi + lo (hi = bf16(x), lo = bf16(x - hi)) with both products accumulated in fp32:
-// the activation keeps ~16 significant bits, so results stay within the bf16-weight parity bar of
-// the fp32 GEMV (tests/test_gemm_gpu.py).  v_mfma_f32_32x32x16_bf16: lane l = (r = l & 31, h = l >> 5)
-// holds A[row r][k 8h..8h+7] and B[k 8h..8h+7][col r]; C[row (j&3) + 8(j>>2) + 4h][col r].
+// Exactness.  The greedy bar is bit-exact RVQ codes against an fp32 reference, so every product
+// must be an fp32-exact one:
+//   * activations (fp32, RMSNorm-weighted) are split into three bf16 parts x = hi + mid + lo
+//     (hi = bf16(x), mid = bf16(x - hi), lo = bf16(x - hi - mid)); the three parts hold all 24
+//     significant bits of x, and each part times a bf16 weight is exact in fp32 -- three
+//     v_mfma_f32_32x32x16_bf16 per K-step, fp32 accumulation: the arithmetic of an fp32 GEMV up to
+//     summation order;
+//   * int4 weights (MLX affine, group 64: w = scale * q + bias) are NOT dequantized: the nibbles
+//     q in [0, 15] are exact bf16 operands, so per group g the matrix cores give
+//     S_g = sum_k q_k x_k (three products per K-step as above) and the staging threads give
+//     X_g = sum_k x_k; the accumulator folds acc += scale_g * S_g + bias_g * X_g per group
+//     (scale, bias bf16 as stored).  Same operand count as a bf16 weight.
+// v_mfma_f32_32x32x16_bf16 fragments: lane l = (r = l & 31, h = l >> 5) holds A[row r][k 8h..8h+7]
+// and B[k 8h..8h+7][col r]; C[row (j&3) + 8(j>>2) + 4h][col r] in accumulator register j.
 //
-// Block = 4 waves = 128 weight rows (wave w: rows 32w..32w+31) x up to 64 batch rows per pass, over
-// one K slice of K / ksplit, in sub-chunks of 128 K: (1) the block's coalesced 16-B loads of the
-// activation sub-chunk and every wave's weight loads for it are issued together (weights straight to
-// VGPRs: each weight byte is used by one wave only), (2) the activations are RMSNorm-weighted,
-// split hi/lo and written to LDS in MFMA-fragment order (one conflict-free ds_read_b128 per
-// fragment, shared by the 4 waves), (3) 8 K-steps of MFMA.  ksplit == 1: pair epilogues straight
-// from the accumulators (rows (j, j+1) sit in registers j, j+1 of one lane).  ksplit > 1: each slice
-// publishes its accumulators write-through (sc1 stores, drained) and takes an arrival ticket; the
-// last slice of a tile to arrive reads every partial back with sc1 loads (MI355X_MICROARCH.md
-// hand-off table, single-counter row), sums them in slice order (deterministic) and runs the
-// epilogue -- no second launch.
+// Kernel "pipe": the block's weight tile AND activation tile go through LDS with coalesced global
+// loads into a register ring of PD stages (loads of stages c+1..c+PD in flight while stage c runs
+// on the matrix cores from a double-buffered LDS tile; PD = 1 / 2 / 4 by the stage count).  Block =
+// 64 weight rows x 32*MT batch rows over one K slice, stages of 64 K (4 MFMA steps = one int4
+// group); every fragment is stored in MFMA-lane order (one conflict-free ds_read_b128 per operand).
+// MT = 2: 2 x 2 waves over (row tile, batch tile); MT = 1: 2 waves per row tile split each stage's
+// K steps and are summed in a fixed order.  Split-K: each slice publishes its tile write-through
+// (16-B sc1 stores, drained), takes an arrival ticket; the last slice of a tile to arrive reads
+// every partial back with 16-B sc1 loads (MI355X_MICROARCH.md hand-off table, single-counter row),
+// sums them in slice order (deterministic) and runs the epilogue -- RoPE + KV append, residual
+// add, SiLU*up or the heads' arg-max partials -- no second launch.  The slabs and tickets belong
+// to the calling engine (GemmWs), sized outside graph capture by gemm_reserve.
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -33,371 +42,37 @@ typedef float f32x16_t __attribute__((ext_vector_type(16)));
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(1))) float gfloat;
 typedef __attribute__((address_space(1))) unsigned int gu32;
 typedef __attribute__((address_space(1))) const f32x4_t gcf32x4;
 
-constexpr int GM_WROWS = 128;  // weight rows per block (4 waves x one 32-row MFMA tile)
-constexpr int GM_KS = 128;     // K per sub-chunk (8 MFMA steps)
+constexpr int GP_ROWS = 64, GP_KC = 64;  // weight rows per block, K per stage (= Q4_GROUP)
+constexpr int GK_MAX_SLICES = 16;
+static_assert(GP_KC == Q4_GROUP, "one int4 group per stage");
 
 __device__ __forceinline__ unsigned short bf16_bits_rne(float v) { return (unsigned short)st_cast<bf16_t>(v); }
 
-constexpr int GK_MAX_SLICES = 16;
-// Split-K combine: element e of every slice partial (sc1 loads, all issued before the first add so
-// the slices cost one round trip), summed in slice order.
-__device__ __forceinline__ float slab_sum(const gfloat* slab, size_t slab_f, size_t e, int ks) {
-  float v[GK_MAX_SLICES];
-#pragma unroll
-  for (int sl = 0; sl < GK_MAX_SLICES; ++sl)
-    v[sl] = sl < ks ? __hip_atomic_load(slab + (size_t)sl * slab_f + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
-  float sum = 0.f;
-#pragma unroll
-  for (int sl = 0; sl < GK_MAX_SLICES; ++sl)
-    if (sl < ks) sum += v[sl];
-  return sum;
-}
-
-template <int MT, bool NT>
-__global__ __launch_bounds__(256) void gemm_bf16_kernel(GemvParams p) {
-  // activation fragments of one sub-chunk: [hi/lo][tile][step][lane] x 8 bf16 (16 B)
-  __shared__ __attribute__((aligned(16))) u32x4_t xs[2][MT][GM_KS / 16][64];
-  __shared__ float ssb[MT * 32];
-  __shared__ float ct[MT * 32][GM_WROWS + 1];  // C tile [batch row][weight row]
-  __shared__ int last;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int r = lane & 31, h = lane >> 5;
-  const int tile = blockIdx.x;
-  const int nw0 = tile * GM_WROWS + wave * 32;  // this wave's first weight row
-  const int Kblk = p.K / p.ksplit;
-  const int kslice = blockIdx.y * Kblk;
-  const bool norm = p.nw != nullptr;
-  const bf16_t* wrow = (const bf16_t*)p.W + (size_t)min(nw0 + r, p.N - 1) * p.K;
-  const int nchunks = (p.M + MT * 32 - 1) / (MT * 32);
-  // staging map: thread t, load i covers batch row (t >> 5) + 8i, k offset 4 * (t & 31) of the sub-chunk
-  const int sk = 4 * (tid & 31);
-  const int s_step = sk >> 4, s_h = (sk >> 3) & 1, s_j = sk & 7;
-  for (int mc = 0; mc < nchunks; ++mc) {
-    const int m0 = mc * MT * 32;
-    f32x16_t acc[MT];
-#pragma unroll
-    for (int t = 0; t < MT; ++t) acc[t] = f32x16_t{};
-    float ss[MT * 4];
-#pragma unroll
-    for (int i = 0; i < MT * 4; ++i) ss[i] = 0.f;
-    for (int kc = kslice; kc < kslice + Kblk; kc += GM_KS) {
-      // (1) activation sub-chunk (+ norm weights) and this wave's weights, all in flight
-      f32x4_t xv[MT * 4];
-#pragma unroll
-      for (int i = 0; i < MT * 4; ++i) {
-        const int m = min(m0 + (tid >> 5) + 8 * i, p.M - 1);
-        xv[i] = *(const gcf32x4*)(p.x + (size_t)m * p.xs + kc + sk);
-      }
-      f32x4_t nwv = {1.f, 1.f, 1.f, 1.f};
-      if (norm) nwv = *(const gcf32x4*)(p.nw + kc + sk);
-      u32x4_t wa[GM_KS / 16];
-#pragma unroll
-      for (int s = 0; s < GM_KS / 16; ++s) {
-        const u32x4_t* src = reinterpret_cast<const u32x4_t*>(wrow + kc + s * 16 + 8 * h);
-        if constexpr (NT) wa[s] = __builtin_nontemporal_load(src);
-        else wa[s] = *src;
-      }
-      __syncthreads();  // previous sub-chunk's fragments consumed
-      // (2) x * nw, sum(x^2), hi/lo split -> fragment-ordered LDS
-#pragma unroll
-      for (int i = 0; i < MT * 4; ++i) {
-        const int ml = (tid >> 5) + 8 * i;  // batch row inside the chunk
-        const float v4[4] = {xv[i].x, xv[i].y, xv[i].z, xv[i].w};
-        const float n4[4] = {nwv.x, nwv.y, nwv.z, nwv.w};
-        unsigned short hb[4], lb[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          float v = v4[q];
-          if (norm) {
-            ss[i] = fmaf(v, v, ss[i]);
-            v *= n4[q];
-          }
-          hb[q] = bf16_bits_rne(v);
-          lb[q] = bf16_bits_rne(v - __uint_as_float((unsigned)hb[q] << 16));
-        }
-        const int t = ml >> 5, fl = (ml & 31) + 32 * s_h;
-        unsigned int* dh = reinterpret_cast<unsigned int*>(&xs[0][t][s_step][fl]) + (s_j >> 1);
-        unsigned int* dl = reinterpret_cast<unsigned int*>(&xs[1][t][s_step][fl]) + (s_j >> 1);
-        *reinterpret_cast<u32x2_t*>(dh) = u32x2_t{hb[0] | ((unsigned)hb[1] << 16), hb[2] | ((unsigned)hb[3] << 16)};
-        *reinterpret_cast<u32x2_t*>(dl) = u32x2_t{lb[0] | ((unsigned)lb[1] << 16), lb[2] | ((unsigned)lb[3] << 16)};
-      }
-      __syncthreads();
-      // (3) MFMA over the sub-chunk
-#pragma unroll
-      for (int s = 0; s < GM_KS / 16; ++s) {
-        const bf16x8_t a = __builtin_bit_cast(bf16x8_t, wa[s]);
-#pragma unroll
-        for (int t = 0; t < MT; ++t) {
-          const bf16x8_t bh = __builtin_bit_cast(bf16x8_t, xs[0][t][s][lane]);
-          const bf16x8_t bl = __builtin_bit_cast(bf16x8_t, xs[1][t][s][lane]);
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bh, acc[t], 0, 0, 0);
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bl, acc[t], 0, 0, 0);
-        }
-      }
-    }
-    // sum(x^2) of the slice per batch row: the 32 threads of a half-wave share rows
-    if (norm) {
-#pragma unroll
-      for (int i = 0; i < MT * 4; ++i) {
-        float v = ss[i];
-#pragma unroll
-        for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-        if ((tid & 31) == 0) ssb[(tid >> 5) + 8 * i] = v;
-      }
-    }
-    // accumulators -> C tile in LDS [batch row][weight row of the block]
-#pragma unroll
-    for (int t = 0; t < MT; ++t)
-#pragma unroll
-      for (int j = 0; j < 16; ++j) ct[32 * t + r][wave * 32 + (j & 3) + 8 * (j >> 2) + 4 * h] = acc[t][j];
-    __syncthreads();
-    const int mrows = min(MT * 32, p.M - m0);
-    if (p.ksplit > 1) {
-      // publish the slice partial write-through, take a ticket; the last slice to arrive combines
-      const size_t slab_f = (size_t)MT * 32 * (GM_WROWS + 1);  // [batch row][128 rows + sum(x^2)]
-      gfloat* slab = (gfloat*)p.kpart + ((size_t)(tile * nchunks + mc) * p.ksplit) * slab_f;
-      gfloat* mine = slab + (size_t)blockIdx.y * slab_f;
-      for (int e = tid; e < mrows * (GM_WROWS + 1); e += 256) {
-        const int ml = e / (GM_WROWS + 1), j = e % (GM_WROWS + 1);
-        __hip_atomic_store(mine + e, j < GM_WROWS ? ct[ml][j] : (norm ? ssb[ml] : 0.f), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) {
-        gu32* tk = (gu32*)p.kticket + tile * nchunks + mc;
-        const unsigned old = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = (old == (unsigned)p.ksplit - 1);
-        if (last) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
-      }
-      __syncthreads();
-      if (!last) continue;  // uniform per block
-      for (int e = tid; e < mrows * (GM_WROWS + 1); e += 256) {
-        const float v = slab_sum(slab, slab_f, e, p.ksplit);
-        const int ml = e / (GM_WROWS + 1), j = e % (GM_WROWS + 1);
-        if (j < GM_WROWS) ct[ml][j] = v;
-        else ssb[ml] = v;
-      }
-      __syncthreads();
-    }
-    // pair epilogues: thread -> (batch row, weight-row pair)
-    for (int e = tid; e < mrows * (GM_WROWS / 2); e += 256) {
-      const int ml = e / (GM_WROWS / 2), rp = (e % (GM_WROWS / 2)) * 2;
-      const int n = tile * GM_WROWS + rp;
-      float a = ct[ml][rp], b = ct[ml][rp + 1];
-      if (norm) {
-        const float sc = rsqrtf(ssb[ml] / (float)p.K + p.eps);
-        a *= sc;
-        b *= sc;
-      }
-      if (n < p.N) gemv_epilogue_pair(p, m0 + ml, n, a, b);
-      if (p.epi == EPI_ARGMAX) {
-        ct[ml][rp] = a;
-        ct[ml][rp + 1] = b;
-      }
-    }
-    if (p.epi == EPI_ARGMAX) {  // block arg-max per batch row -> partial slot
-      __syncthreads();
-      if (tid < mrows) {
-        unsigned long long best = 0;
-        for (int j = 0; j < GM_WROWS; ++j) {
-          const int n = tile * GM_WROWS + j;
-          if (n < p.n_valid) {
-            const unsigned long long key = pack_argmax(ct[tid][j], n);
-            best = key > best ? key : best;
-          }
-        }
-        p.part[(size_t)(m0 + tid) * p.part_stride + blockIdx.x] = best;
-      }
-    }
-    __syncthreads();
-  }
-}
-
-// Variant "wk" (CSM_GEMM=wk): 32 weight rows per block, the four waves split the block's K slice
-// (each activation fragment read by one wave only, straight from L2 into VGPRs), loads run PF
-// MFMA steps ahead of use through a register ring (in-order vmcnt: the wait for step s leaves the
-// PF-1 younger steps in flight).  Wave tiles are summed in LDS in a fixed order; split-K as above.
-constexpr int GW_ROWS = 32;
-template <int MT, int PF, bool NT, bool LO = true>
-__global__ __launch_bounds__(256) void gemm_bf16_wk_kernel(GemvParams p) {
-  __shared__ float red[4][MT * 32][GW_ROWS + 1];
-  __shared__ float ssw[4][MT * 32];
-  __shared__ int last;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int r = lane & 31, h = lane >> 5;
-  const int tile = blockIdx.x, n0 = tile * GW_ROWS;
-  const int Kblk = p.K / p.ksplit, kw = Kblk / 4;
-  const int kbeg = blockIdx.y * Kblk + wave * kw;
-  const int nsteps = kw / 16;  // multiple of PF (plan)
-  const bool norm = p.nw != nullptr;
-  const bf16_t* wrow = (const bf16_t*)p.W + (size_t)min(n0 + r, p.N - 1) * p.K + kbeg + 8 * h;
-  const float* nwp = norm ? p.nw + kbeg + 8 * h : nullptr;
-  const int nchunks = (p.M + MT * 32 - 1) / (MT * 32);
-  for (int mc = 0; mc < nchunks; ++mc) {
-    const int m0 = mc * MT * 32;
-    const float* xr[MT];
-    f32x16_t acc[MT];
-    float ss[MT];
-#pragma unroll
-    for (int t = 0; t < MT; ++t) {
-      xr[t] = p.x + (size_t)min(m0 + t * 32 + r, p.M - 1) * p.xs + kbeg + 8 * h;
-      acc[t] = f32x16_t{};
-      ss[t] = 0.f;
-    }
-    u32x4_t wq[PF];
-    f32x4_t xq[PF][MT][2];
-    f32x4_t nq[PF][2];
-    auto issue = [&](int u, int s) {
-      const int k = s * 16;
-      if constexpr (NT) wq[u] = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(wrow + k));
-      else wq[u] = *reinterpret_cast<const u32x4_t*>(wrow + k);
-#pragma unroll
-      for (int t = 0; t < MT; ++t) {
-        xq[u][t][0] = ((gcf32x4*)(xr[t] + k))[0];
-        xq[u][t][1] = ((gcf32x4*)(xr[t] + k))[1];
-      }
-      if (norm) {
-        nq[u][0] = ((gcf32x4*)(nwp + k))[0];
-        nq[u][1] = ((gcf32x4*)(nwp + k))[1];
-      }
-    };
-#pragma unroll
-    for (int u = 0; u < PF; ++u) issue(u, u);
-    for (int s0 = 0; s0 < nsteps; s0 += PF) {
-#pragma unroll
-      for (int u = 0; u < PF; ++u) {
-        const bf16x8_t a = __builtin_bit_cast(bf16x8_t, wq[u]);
-        const float nw[8] = {nq[u][0].x, nq[u][0].y, nq[u][0].z, nq[u][0].w, nq[u][1].x, nq[u][1].y, nq[u][1].z, nq[u][1].w};
-#pragma unroll
-        for (int t = 0; t < MT; ++t) {
-          const float xv[8] = {xq[u][t][0].x, xq[u][t][0].y, xq[u][t][0].z, xq[u][t][0].w,
-                               xq[u][t][1].x, xq[u][t][1].y, xq[u][t][1].z, xq[u][t][1].w};
-          bf16x8_t bh, bl;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            float v = xv[j];
-            if (norm) {
-              ss[t] = fmaf(v, v, ss[t]);
-              v *= nw[j];
-            }
-            const __bf16 hi = (__bf16)v;
-            bh[j] = hi;
-            bl[j] = (__bf16)(v - (float)hi);
-          }
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bh, acc[t], 0, 0, 0);
-          if constexpr (LO) acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bl, acc[t], 0, 0, 0);
-        }
-        if (s0 + u + PF < nsteps) issue(u, s0 + u + PF);
-      }
-    }
-#pragma unroll
-    for (int t = 0; t < MT; ++t) {
-#pragma unroll
-      for (int j = 0; j < 16; ++j) red[wave][t * 32 + r][(j & 3) + 8 * (j >> 2) + 4 * h] = acc[t][j];
-      const float sv = ss[t] + __shfl_xor(ss[t], 32, 64);
-      if (h == 0) ssw[wave][t * 32 + r] = sv;
-    }
-    __syncthreads();
-    const int mrows = min(MT * 32, p.M - m0);
-    gfloat* slab = nullptr;
-    const size_t slab_f = (size_t)MT * 32 * (GW_ROWS + 1);
-    if (p.ksplit > 1) {
-      slab = (gfloat*)p.kpart + ((size_t)(tile * nchunks + mc) * p.ksplit) * slab_f;
-      gfloat* mine = slab + (size_t)blockIdx.y * slab_f;
-      for (int e = tid; e < mrows * (GW_ROWS + 1); e += 256) {
-        const int mi = e / (GW_ROWS + 1), j = e % (GW_ROWS + 1);
-        const float v = j < GW_ROWS ? (red[0][mi][j] + red[1][mi][j]) + (red[2][mi][j] + red[3][mi][j])
-                                    : (ssw[0][mi] + ssw[1][mi]) + (ssw[2][mi] + ssw[3][mi]);
-        __hip_atomic_store(mine + e, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) {
-        gu32* tk = (gu32*)p.kticket + tile * nchunks + mc;
-        const unsigned old = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        last = (old == (unsigned)p.ksplit - 1);
-        if (last) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      __syncthreads();
-      if (!last) continue;  // uniform per block
-    }
-    for (int e = tid; e < mrows * (GW_ROWS / 2); e += 256) {
-      const int mi = e / (GW_ROWS / 2), rp = (e % (GW_ROWS / 2)) * 2;
-      const int n = n0 + rp;
-      float a, b, sq;
-      if (slab) {
-        a = 0.f; b = 0.f; sq = 0.f;
-        const size_t e0 = (size_t)mi * (GW_ROWS + 1);
-        a = slab_sum(slab, slab_f, e0 + rp, p.ksplit);
-        b = slab_sum(slab, slab_f, e0 + rp + 1, p.ksplit);
-        sq = slab_sum(slab, slab_f, e0 + GW_ROWS, p.ksplit);
-      } else {
-        a = (red[0][mi][rp] + red[1][mi][rp]) + (red[2][mi][rp] + red[3][mi][rp]);
-        b = (red[0][mi][rp + 1] + red[1][mi][rp + 1]) + (red[2][mi][rp + 1] + red[3][mi][rp + 1]);
-        sq = (ssw[0][mi] + ssw[1][mi]) + (ssw[2][mi] + ssw[3][mi]);
-      }
-      if (norm) {
-        const float sc = rsqrtf(sq / (float)p.K + p.eps);
-        a *= sc;
-        b *= sc;
-      }
-      if (n < p.N) gemv_epilogue_pair(p, m0 + mi, n, a, b);
-      if (p.epi == EPI_ARGMAX) {
-        red[0][mi][rp] = a;
-        red[0][mi][rp + 1] = b;
-      }
-    }
-    if (p.epi == EPI_ARGMAX) {
-      __syncthreads();
-      if (tid < mrows) {
-        unsigned long long best = 0;
-        for (int j = 0; j < GW_ROWS; ++j) {
-          const int n = n0 + j;
-          if (n < p.n_valid) {
-            const unsigned long long key = pack_argmax(red[0][tid][j], n);
-            best = key > best ? key : best;
-          }
-        }
-        p.part[(size_t)(m0 + tid) * p.part_stride + blockIdx.x] = best;
-      }
-    }
-    __syncthreads();
-  }
-}
-
-// Variant "pipe" (default): the block's weight tile AND activation tile go through LDS with
-// coalesced global loads into a register ring of PD stages (loads of stages c+1..c+PD in flight
-// while stage c runs on the matrix cores from a double-buffered LDS tile; PD = 1 / 2 / 4 by the
-// stage count).  Block = 64 weight rows x 32*MT batch rows over one K slice, stages of 64 K
-// (4 MFMA steps); every fragment is stored in MFMA-lane order (one conflict-free ds_read_b128 per
-// operand).  MT = 2: 2 x 2 waves over (row tile, batch tile); MT = 1: 2 waves per row tile split
-// each stage's K steps and are summed in a fixed order.  int4 weights (Q4) are dequantized while
-// staging (w = scale * q + bias in fp32, split hi/lo like the activations) and run three products
-// (hi*hi, hi*lo, lo*hi).  Split-K fixup as the kernels above, except the combine (gp_combine: 16-B
-// loads, 16 in flight per thread); arg-max heads are split too (the last slice runs the arg-max).
-constexpr int GP_ROWS = 64, GP_KC = 64;
-typedef unsigned short u16x4_t __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ void split4(const float (&v)[4], u32x2_t& hi, u32x2_t& lo) {
-  unsigned short h[4], l[4];
+// x -> three bf16 parts holding all 24 significant bits (finite inputs; parts may be zero)
+__device__ __forceinline__ void split3_4(const float (&v)[4], u32x2_t& hi, u32x2_t& mid, u32x2_t& lo) {
+  unsigned short h[4], m[4], l[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     h[q] = bf16_bits_rne(v[q]);
-    l[q] = bf16_bits_rne(v[q] - __uint_as_float((unsigned)h[q] << 16));
+    const float r1 = v[q] - __uint_as_float((unsigned)h[q] << 16);  // exact
+    m[q] = bf16_bits_rne(r1);
+    const float r2 = r1 - __uint_as_float((unsigned)m[q] << 16);    // exact, <= 8 significant bits
+    l[q] = bf16_bits_rne(r2);
   }
   hi = u32x2_t{h[0] | ((unsigned)h[1] << 16), h[2] | ((unsigned)h[3] << 16)};
+  mid = u32x2_t{m[0] | ((unsigned)m[1] << 16), m[2] | ((unsigned)m[3] << 16)};
   lo = u32x2_t{l[0] | ((unsigned)l[1] << 16), l[2] | ((unsigned)l[3] << 16)};
 }
 
-// Split-K combine of the pipe kernel (the last slice of a tile to arrive): every slice's partial is
-// read with 16-B sc1 buffer loads, KS * U of them in flight per thread before the first add (one
-// round trip per 4096 floats at U * KS = 16), and summed in slice order (deterministic, the same
-// order as slab_sum).
+// bf16 bits of the small integer n in [0, 15] (exact)
+__device__ __forceinline__ unsigned q_bits(unsigned n) { return __float_as_uint((float)n) >> 16; }
+
+// Split-K combine (the last slice of a tile to arrive): every slice's partial is read with 16-B sc1
+// buffer loads, KS * U of them in flight per thread before the first add (one round trip per 4096
+// floats at U * KS = 16), and summed in slice order (deterministic).
 constexpr int GP_RSRC3 = 0x00020000;  // buffer descriptor word 3 (raw 32-bit format)
 constexpr int GP_SC1 = 16;            // cache policy: sc1 (agent-coherent, as __hip_atomic_load/store)
 template <int KS, int NB>
@@ -442,16 +117,19 @@ __device__ __forceinline__ void gp_combine(__amdgpu_buffer_rsrc_t rs, float (*ct
 
 template <bool Q4, int MT, bool NT, int PD>
 __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemvParams p) {
-  constexpr int NB = MT * 32, NA = Q4 ? 2 : 1;
-  constexpr int A_BYTES = 2 * NA * 2 * 4 * 64 * 16, B_BYTES = 2 * 2 * MT * 4 * 64 * 16;
+  constexpr int NB = MT * 32;
+  constexpr int A_BYTES = 2 * 2 * 4 * 64 * 16;        // [buf][row tile][step][lane] x 16 B
+  constexpr int B_BYTES = 2 * 3 * MT * 4 * 64 * 16;   // [buf][hi/mid/lo][batch tile][step][lane] x 16 B
   __shared__ __attribute__((aligned(16))) unsigned char smem[A_BYTES + B_BYTES];
+  __shared__ __attribute__((aligned(16))) uint32_t sbs[2][GP_ROWS];  // int4: {scale, bias} of the stage's group
+  __shared__ float xsum[2][NB];                                      // int4: sum of the stage's x per batch row
   __shared__ float ssb[NB];
   __shared__ int last;
-  // As[buf][hi/lo][row tile][step][lane], Bs[buf][hi/lo][batch tile][step][lane] (16 B each)
-  auto As = [&](int buf, int hl, int t, int s) { return reinterpret_cast<u32x4_t*>(smem) + (((buf * NA + hl) * 2 + t) * 4 + s) * 64; };
-  auto Bs = [&](int buf, int hl, int t, int s) {
-    return reinterpret_cast<u32x4_t*>(smem + A_BYTES) + (((buf * 2 + hl) * MT + t) * 4 + s) * 64;
+  auto As = [&](int buf, int t, int s) { return reinterpret_cast<u32x4_t*>(smem) + ((buf * 2 + t) * 4 + s) * 64; };
+  auto Bs = [&](int buf, int part, int t, int s) {
+    return reinterpret_cast<u32x4_t*>(smem + A_BYTES) + (((buf * 3 + part) * MT + t) * 4 + s) * 64;
   };
+  static_assert(NB * (GP_ROWS + 1) * 4 <= A_BYTES + B_BYTES, "C tile aliases the operand tiles");
   float (*ct)[GP_ROWS + 1] = reinterpret_cast<float (*)[GP_ROWS + 1]>(smem);  // after the K loop
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5;
@@ -478,7 +156,7 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemvParams p) {
     f32x4_t nwr;
   };
   Stage sg[PD];
-  // stage st >= nst is a placeholder: weights from the (L2-hot) activation row, nothing used
+  // stage st >= nst is a placeholder: loads from the (L2-hot) activation row, nothing used
   const float* nwp = norm ? p.nw : p.x;
   auto load = [&](int st, Stage& g) {
     const bool junk = st >= nst;
@@ -508,24 +186,19 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemvParams p) {
     if (a_on) {
       const int t = a_row >> 5, ln = a_row & 31;
       if constexpr (Q4) {
-        const float sc = bf16_lo(g.asb), bi = bf16_hi(g.asb);
 #pragma unroll
         for (int w = 0; w < 4; ++w) {  // 8 consecutive k per word: step 2*seg + w/2, half w&1
           const uint32_t u = g.ar[0][w];
-          float v[8];
+          unsigned b[8];
 #pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = fmaf(sc, (float)((u >> (4 * j)) & 15u), bi);
-          u32x2_t h0, l0, h1, l1;
-          const float v0[4] = {v[0], v[1], v[2], v[3]}, v1[4] = {v[4], v[5], v[6], v[7]};
-          split4(v0, h0, l0);
-          split4(v1, h1, l1);
+          for (int j = 0; j < 8; ++j) b[j] = q_bits((u >> (4 * j)) & 15u);
           const int s = 2 * a_seg + (w >> 1), hh = w & 1;
-          As(buf, 0, t, s)[ln + 32 * hh] = u32x4_t{h0.x, h0.y, h1.x, h1.y};
-          As(buf, 1, t, s)[ln + 32 * hh] = u32x4_t{l0.x, l0.y, l1.x, l1.y};
+          As(buf, t, s)[ln + 32 * hh] = u32x4_t{b[0] | (b[1] << 16), b[2] | (b[3] << 16), b[4] | (b[5] << 16), b[6] | (b[7] << 16)};
         }
+        if (a_seg == 0) sbs[buf][a_row] = g.asb;
       } else {
-        As(buf, 0, t, a_seg)[ln] = g.ar[0];
-        As(buf, 0, t, a_seg)[ln + 32] = g.ar[1];
+        As(buf, t, a_seg)[ln] = g.ar[0];
+        As(buf, t, a_seg)[ln + 32] = g.ar[1];
       }
     }
     const int s = x_k4 >> 4, hh = (x_k4 >> 3) & 1, j0 = x_k4 & 7;
@@ -541,11 +214,18 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemvParams p) {
           v[q] *= nw4[q];
         }
       }
-      u32x2_t hi, lo;
-      split4(v, hi, lo);
+      if constexpr (Q4) {  // sum of the group's 64 values of row c: 16 threads x 4, fixed order
+        float sum = (v[0] + v[1]) + (v[2] + v[3]);
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) sum += __shfl_xor(sum, o, 64);
+        if ((tid & 15) == 0) xsum[buf][c] = sum;
+      }
+      u32x2_t hi, mid, lo;
+      split3_4(v, hi, mid, lo);
       const int ln = (c & 31) + 32 * hh;
       *(reinterpret_cast<u32x2_t*>(&Bs(buf, 0, c >> 5, s)[ln]) + (j0 >> 2)) = hi;
-      *(reinterpret_cast<u32x2_t*>(&Bs(buf, 1, c >> 5, s)[ln]) + (j0 >> 2)) = lo;
+      *(reinterpret_cast<u32x2_t*>(&Bs(buf, 1, c >> 5, s)[ln]) + (j0 >> 2)) = mid;
+      *(reinterpret_cast<u32x2_t*>(&Bs(buf, 2, c >> 5, s)[ln]) + (j0 >> 2)) = lo;
     }
   };
   f32x16_t acc = f32x16_t{};
@@ -560,16 +240,28 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemvParams p) {
     for (int d = 0; d < PD; ++d) {
       const int it = it0 + d, buf = it & 1;
       load(it + PD, sg[d]);  // slot d's stage (it) is already in LDS
+      f32x16_t g = f32x16_t{};
 #pragma unroll
       for (int s = s0; s < s1; ++s) {
-        const bf16x8_t a = __builtin_bit_cast(bf16x8_t, As(buf, 0, wr, s)[lane]);
-        const bf16x8_t bh = __builtin_bit_cast(bf16x8_t, Bs(buf, 0, bt, s)[lane]);
-        const bf16x8_t bl = __builtin_bit_cast(bf16x8_t, Bs(buf, 1, bt, s)[lane]);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bh, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, bl, acc, 0, 0, 0);
-        if constexpr (Q4) {
-          const bf16x8_t al = __builtin_bit_cast(bf16x8_t, As(buf, 1, wr, s)[lane]);
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al, bh, acc, 0, 0, 0);
+        const bf16x8_t a = __builtin_bit_cast(bf16x8_t, As(buf, wr, s)[lane]);
+#pragma unroll
+        for (int part = 0; part < 3; ++part) {
+          const bf16x8_t b = __builtin_bit_cast(bf16x8_t, Bs(buf, part, bt, s)[lane]);
+          if constexpr (Q4) g = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, g, 0, 0, 0);
+          else acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+        }
+      }
+      if constexpr (Q4) {  // acc += scale * S_g + bias * X_g for this lane's 16 weight rows
+        const float xs = (MT == 2 || wc == 0) ? xsum[buf][32 * bt + r] : 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const u32x4_t sb = *reinterpret_cast<const u32x4_t*>(&sbs[buf][32 * wr + 8 * q + 4 * h]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int j = 4 * q + e;
+            acc[j] = fmaf(bf16_lo(sb[e]), g[j], acc[j]);
+            acc[j] = fmaf(bf16_hi(sb[e]), xs, acc[j]);
+          }
         }
       }
       store(sg[(d + 1) % PD], buf ^ 1, it + 1 < nst);  // the last one stores a placeholder
@@ -616,7 +308,7 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemvParams p) {
       gu32* tk = (gu32*)p.kticket + tile * nchunks + mc;
       const unsigned old = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       last = (old == (unsigned)p.ksplit - 1);
-      if (last) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (last) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
     }
     __syncthreads();
     if (!last) return;
@@ -660,143 +352,101 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemvParams p) {
 }
 
 // ---------------------------------------------------------------------------- host side
-static int gemm_variant() {  // 2 = "pipe" (default), 0 = "wk" (CSM_GEMM=wk), 1 = "lds" (CSM_GEMM=lds)
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("CSM_GEMM");
-    v = (e && e[0] == 'l') ? 1 : ((e && e[0] == 'w') ? 0 : 2);
-  }
-  return v;
-}
-static int gemm_rows() { return gemm_variant() == 1 ? GM_WROWS : (gemm_variant() == 2 ? GP_ROWS : GW_ROWS); }
-constexpr int GW_PF = 4;  // wk: MFMA steps in flight per wave
-// pipe: K slices are added until the grid has this many blocks (measured best: 256 for <= 32 batch
-// rows, 512 above -- configs 4 / 5); CSM_PIPE_BLOCKS overrides (lab sweeps)
+// K slices are added until the grid has this many blocks (measured best: 256 for <= 32 batch rows,
+// 512 above -- configs 4 / 5); CSM_PIPE_BLOCKS overrides (lab sweeps)
 static int g_pipe_target_env = [] { const char* e = getenv("CSM_PIPE_BLOCKS"); return e ? atoi(e) : 0; }();
 static int pipe_target(int M) { return g_pipe_target_env > 0 ? g_pipe_target_env : (M > 32 ? 512 : 256); }
-// pipe: deepest register prefetch ring (stages in flight, 1 / 2 / 4: 4 for <= 32 batch rows, 2 above,
-// where the 64-row stages cost twice the registers); CSM_PIPE_PD overrides
+// deepest register prefetch ring (stages in flight, 1 / 2 / 4: 4 for <= 32 batch rows, 2 above, where
+// the 64-row stages cost twice the registers); CSM_PIPE_PD overrides
 static int g_pipe_pd_env = [] { const char* e = getenv("CSM_PIPE_PD"); return e ? atoi(e) : 0; }();
 static int pipe_pd_cap(int M) { return g_pipe_pd_env > 0 ? g_pipe_pd_env : (M > 32 ? 2 : 4); }
 
-// K slices: doubled while the grid has < 256 blocks (wk: while each wave keeps >= 2 rings of PF
-// steps; lds: up to 8); wk / lds arg-max heads keep whole rows.
-static void gemm_plan(int N, int K, int M, int epi, int& ks) {
-  const int rows = gemm_rows();
-  const int tiles = (N + rows - 1) / rows;
-  const int chunks = (M + 63) / 64;
-  ks = 1;
-  if (epi == EPI_ARGMAX && gemm_variant() != 2) return;  // pipe: the last slice runs the arg-max epilogue
-  if (gemm_variant() == 2) {
-    while (tiles * chunks * ks < pipe_target(M) && ks < 16 && K % (GP_KC * ks * 2) == 0 && K / (ks * 2) >= 2 * GP_KC) ks *= 2;
-  } else if (gemm_variant() == 1) {
-    while (tiles * chunks * ks < 256 && ks < 8 && K % (GM_KS * ks * 2) == 0) ks *= 2;
-  } else {
-    while (tiles * chunks * ks < 512 && K % (ks * 2 * 4 * 16 * GW_PF * 2) == 0) ks *= 2;
-  }
+// K slices: doubled while the grid has fewer than pipe_target(M) blocks and every slice keeps >= 2
+// stages; arg-max heads are split too (the last slice runs the arg-max epilogue).
+static int gemm_ksplit(int N, int K, int M) {
+  const int tiles = (N + GP_ROWS - 1) / GP_ROWS, chunks = (M + 63) / 64;
+  int ks = 1;
+  while (tiles * chunks * ks < pipe_target(M) && ks < GK_MAX_SLICES && K % (GP_KC * ks * 2) == 0 &&
+         K / (ks * 2) >= 2 * GP_KC)
+    ks *= 2;
+  return ks;
 }
-
-static size_t gemm_slab_floats(int MT) { return (size_t)MT * 32 * (gemm_rows() + 1); }
 
 bool gemm_mfma_eligible(int N, int K, int M, int wdt) {
-  if (M < GEMM_MFMA_MIN_M || N % 2) return false;
-  if (gemm_variant() == 2) return (wdt == WDT_BF16 || wdt == WDT_Q4) && K % GP_KC == 0;
-  return wdt == WDT_BF16 && K % (4 * 16 * GW_PF) == 0 && K % GM_KS == 0;
+  return M >= GEMM_MFMA_MIN_M && N % 2 == 0 && (wdt == WDT_BF16 || wdt == WDT_Q4) && K % GP_KC == 0;
 }
 
-int gemm_blocks(int N) { return (N + gemm_rows() - 1) / gemm_rows(); }
+int gemm_blocks(int N) { return (N + GP_ROWS - 1) / GP_ROWS; }
 
-static float* g_kscratch = nullptr;
-static size_t g_kscratch_bytes = 0;
-static unsigned* g_ktickets = nullptr;
-static size_t g_ktickets_n = 0;
-
+// split-K slab bytes and ticket count of one (N, K, M) launch
 static size_t gemm_need(int N, int K, int M, size_t& tk) {
-  int ks;
-  gemm_plan(N, K, M, EPI_STORE, ks);
-  const int MT = (M > 32 || gemm_variant() == 2) ? 2 : 1;
+  const int ks = gemm_ksplit(N, K, M);
+  const int MT = M > 32 ? 2 : 1;
   const size_t tiles = gemm_blocks(N), chunks = (M + MT * 32 - 1) / (MT * 32);
   tk = tiles * chunks;
-  return ks > 1 ? tiles * chunks * ks * gemm_slab_floats(MT) * 4 : 0;
+  return ks > 1 ? tiles * chunks * ks * (size_t)MT * 32 * (GP_ROWS + 1) * 4 : 0;
 }
 
 void launch_gemm_mfma(const GemvParams& p0, int wdt, bool nt, hipStream_t st) {
-  const bool p_is_q4 = wdt == WDT_Q4;
   GemvParams p = p0;
-  int ks;
-  gemm_plan(p.N, p.K, p.M, p.epi, ks);
+  const int ks = gemm_ksplit(p.N, p.K, p.M);
   p.ksplit = ks;
   if (ks > 1) {
     size_t tk = 0;
     const size_t need = gemm_need(p.N, p.K, p.M, tk);
-    if (need > g_kscratch_bytes || tk > g_ktickets_n) {  // reserved by gemm_reserve outside graph capture
+    if (!p.ws || need > p.ws->bytes || tk > p.ws->n) {  // reserved by gemm_reserve outside graph capture
       fprintf(stderr, "csm: split-K scratch not reserved for N=%d K=%d M=%d\n", p.N, p.K, p.M);
       abort();
     }
-    p.kpart = g_kscratch;
-    p.kticket = g_ktickets;
+    p.kpart = p.ws->kpart;
+    p.kticket = p.ws->tickets;
   }
-  if (gemm_variant() == 2) {  // pipe: batch chunks of 64 (MT 2) or one chunk of 32 (MT 1) on grid.z
-    const int MT = p.M > 32 ? 2 : 1;
-    const dim3 g3(gemm_blocks(p.N), ks, (p.M + MT * 32 - 1) / (MT * 32));
-    const int nst = p.K / ks / GP_KC;
-    const int cap = pipe_pd_cap(p.M);
-    const int pd = (nst % 4 == 0 && cap >= 4) ? 4 : ((nst % 2 == 0 && cap >= 2) ? 2 : 1);
+  // batch chunks of 64 (MT 2) or one chunk of 32 (MT 1) on grid.z
+  const int MT = p.M > 32 ? 2 : 1;
+  const dim3 g3(gemm_blocks(p.N), ks, (p.M + MT * 32 - 1) / (MT * 32));
+  const int nst = p.K / ks / GP_KC;
+  const int cap = pipe_pd_cap(p.M);
+  const int pd = (nst % 4 == 0 && cap >= 4) ? 4 : ((nst % 2 == 0 && cap >= 2) ? 2 : 1);
 #define GP_K(Q_, MT_, PD_) do { if (nt) hipLaunchKernelGGL((gemm_pipe_kernel<Q_, MT_, true, PD_>), g3, dim3(256), 0, st, p); \
                                 else hipLaunchKernelGGL((gemm_pipe_kernel<Q_, MT_, false, PD_>), g3, dim3(256), 0, st, p); } while (0)
 #define GP_L(Q_, MT_) do { if (pd == 4) GP_K(Q_, MT_, 4); else if (pd == 2) GP_K(Q_, MT_, 2); else GP_K(Q_, MT_, 1); } while (0)
-    if (p_is_q4) { if (MT == 2) GP_L(true, 2); else GP_L(true, 1); }
-    else { if (MT == 2) GP_L(false, 2); else GP_L(false, 1); }
+  if (wdt == WDT_Q4) { if (MT == 2) GP_L(true, 2); else GP_L(true, 1); }
+  else { if (MT == 2) GP_L(false, 2); else GP_L(false, 1); }
 #undef GP_L
 #undef GP_K
-    return;
-  }
-  const dim3 grid(gemm_blocks(p.N), ks);
-  static const int lab_hl = [] { const char* e = getenv("CSM_GEMM_HL"); return e ? atoi(e) : 2; }();
-  if (gemm_variant() == 0 && lab_hl == 1 && p.M <= 32) {  // lab only: hi part alone (not parity-grade)
-    if (nt) hipLaunchKernelGGL((gemm_bf16_wk_kernel<1, GW_PF, true, false>), grid, dim3(256), 0, st, p);
-    else hipLaunchKernelGGL((gemm_bf16_wk_kernel<1, GW_PF, false, false>), grid, dim3(256), 0, st, p);
-    return;
-  }
-  if (gemm_variant() == 0) {
-    if (p.M > 32) {
-      if (nt) hipLaunchKernelGGL((gemm_bf16_wk_kernel<2, GW_PF, true>), grid, dim3(256), 0, st, p);
-      else hipLaunchKernelGGL((gemm_bf16_wk_kernel<2, GW_PF, false>), grid, dim3(256), 0, st, p);
-    } else {
-      if (nt) hipLaunchKernelGGL((gemm_bf16_wk_kernel<1, GW_PF, true>), grid, dim3(256), 0, st, p);
-      else hipLaunchKernelGGL((gemm_bf16_wk_kernel<1, GW_PF, false>), grid, dim3(256), 0, st, p);
-    }
-    return;
-  }
-  if (p.M > 32) {
-    if (nt) hipLaunchKernelGGL((gemm_bf16_kernel<2, true>), grid, dim3(256), 0, st, p);
-    else hipLaunchKernelGGL((gemm_bf16_kernel<2, false>), grid, dim3(256), 0, st, p);
-  } else {
-    if (nt) hipLaunchKernelGGL((gemm_bf16_kernel<1, true>), grid, dim3(256), 0, st, p);
-    else hipLaunchKernelGGL((gemm_bf16_kernel<1, false>), grid, dim3(256), 0, st, p);
-  }
 }
 
-// Pre-size the split-K slab and tickets for an (N, K) launched at any M <= Mmax (call outside capture).
-void gemm_reserve(int N, int K, int Mmax) {
+// Pre-size the engine's split-K slab and tickets for an (N, K) launched at any M <= Mmax (outside
+// capture).  Returns true when the buffers were reallocated (graphs holding the old ones are stale).
+bool gemm_reserve(GemmWs& ws, int N, int K, int Mmax) {
   size_t slab = 0, tk = 0;
   for (int m = GEMM_MFMA_MIN_M; m <= Mmax; ++m) {  // cheap host loop (Mmax <= a few thousand)
     size_t t = 0;
     slab = std::max(slab, gemm_need(N, K, m, t));
     tk = std::max(tk, t);
   }
-  if (slab > g_kscratch_bytes) {
-    if (g_kscratch) (void)hipFree(g_kscratch);
-    g_kscratch = nullptr;
-    g_kscratch_bytes = 0;
-    if (hipMalloc(&g_kscratch, slab) == hipSuccess) g_kscratch_bytes = slab;
+  bool moved = false;
+  if (slab > ws.bytes) {
+    if (ws.kpart) (void)hipFree(ws.kpart);
+    ws.kpart = nullptr;
+    ws.bytes = 0;
+    if (hipMalloc(&ws.kpart, slab) == hipSuccess) ws.bytes = slab;
+    moved = true;
   }
-  if (tk > g_ktickets_n) {
-    if (g_ktickets) (void)hipFree(g_ktickets);
-    g_ktickets = nullptr;
-    g_ktickets_n = 0;
-    if (hipMalloc(&g_ktickets, tk * 4) == hipSuccess && hipMemset(g_ktickets, 0, tk * 4) == hipSuccess) g_ktickets_n = tk;
+  if (tk > ws.n) {
+    if (ws.tickets) (void)hipFree(ws.tickets);
+    ws.tickets = nullptr;
+    ws.n = 0;
+    if (hipMalloc(&ws.tickets, tk * 4) == hipSuccess && hipMemset(ws.tickets, 0, tk * 4) == hipSuccess) ws.n = tk;
+    moved = true;
   }
+  return moved;
+}
+
+void gemm_ws_free(GemmWs& ws) {
+  if (ws.kpart) (void)hipFree(ws.kpart);
+  if (ws.tickets) (void)hipFree(ws.tickets);
+  ws = GemmWs{};
 }
 
 // ---------------------------------------------------------------------------- row gather

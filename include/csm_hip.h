@@ -107,29 +107,6 @@ int csm_debug_read(csm_engine* e, const char* what, void* host, int64_t nbytes, 
 /* Device pointer of the code history [F][B][K] (for on-device Mimi decode) */
 int csm_codes_device_ptr(csm_engine* e, void** dev_ptr);
 int csm_synchronize(csm_engine* e);
-/* Profiling hook: replay one GEMV of the frame (layer 0) `iters` times on the engine stream,
- * timed with HIP events.  which = stack*4 + kind, stack 0 backbone / 1 decoder,
- * kind 0 = norm+gate/up+SiLU, 1 = down+residual, 2 = norm+QKV+RoPE, 3 = o_proj+residual.
- * *bytes = algorithmic (weight) bytes per launch. */
-int csm_bench_gemv(csm_engine* e, int which, int M, int iters, float* avg_us, double* bytes);
-/* Tuning / debug switches (re-capture the frame graphs): "fuse_attn" (decoder attention recomputed
- * inside the o_proj launch, default 0), "nt_mask" (bit t: non-temporal weight loads for stack tag
- * t, default 5), "gemv_xl"
- * (decode GEMVs with LDS-staged activations, default 1), "fold_proj" (decoder steps >= 2 gather
- * projection(E_a[c]) from a table built at csm_begin instead of running the projection, default 1). */
-int csm_set_option(csm_engine* e, const char* key, int value);
-/* Profiling hook: force the GEMV tiling (threads per row group G, rows per thread RPT); 0 = auto. */
-int csm_set_gemv_config(int G, int RPT);
-/* Measurement lab (profiling only): a pure streaming read of `bytes` (blocks x 256 threads x
- * `loads` 16-B loads; nt = non-temporal) and the production GEMV on a synthetic bf16 N x K matrix
- * (kind 0 = norm + SiLU*up, 1 = store; tag = stack tag, bit 2 = nt loads), each rotating over
- * `span` bytes of distinct copies (one copy: cache-hot; >> 256 MiB: HBM-cold). */
-int csm_lab_stream(int device, double bytes, double span, int loads, int nt, int iters, float* avg_us);
-int csm_lab_gemv(int device, int N, int K, int M, double span, int kind, int tag, int iters, float* avg_us);
-/* Profiling hook: per-kernel time of n dependent near-empty kernels (blocks x 256 threads),
- * replayed as one HIP graph (graph=1) or launched eagerly (graph=0). */
-int csm_bench_floor(csm_engine* e, int n_kernels, int blocks, int graph, float* us_per_kernel);
-
 /* ------------------------------------------------------------------ Mimi codec */
 typedef struct mimi_dims {
   int channels, dimension, n_filters, n_ratios, ratios[8];

@@ -1,0 +1,36 @@
+/*
+ * csm_hip_prof.h -- tuning and profiling hooks of libcsm_hip.so.
+ *
+ * NOT part of the reference-facing ABI (include/csm_hip.h): no reference interface corresponds to
+ * these.  bench.py uses csm_bench_gemv for the live roofline of the dominant kernel; the parity
+ * tests use csm_set_option to A/B the opt-in fused paths against the default launches.
+ */
+#ifndef CSM_HIP_PROF_H
+#define CSM_HIP_PROF_H
+
+#include "csm_hip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Replay one projection of the frame `iters` times on the engine stream (one launch per layer in
+ * turn, as the frame does), timed with HIP events on that stream.  which = stack*4 + kind, stack 0
+ * backbone / 1 decoder, kind 0 = norm+gate/up+SiLU, 1 = down+residual, 2 = norm+QKV+RoPE,
+ * 3 = o_proj+residual; M rows (M >= 8 on bf16 / int4 weights: the MFMA GEMM the batched frame runs).
+ * *bytes = algorithmic bytes per launch (weights in their storage format + activations read and
+ * written). */
+int csm_bench_gemv(csm_engine* e, int which, int M, int iters, float* avg_us, double* bytes);
+
+/* Tuning / debug switches (re-capture the frame graphs): "fuse_attn" (decoder attention recomputed
+ * inside the o_proj launch, default 0), "nt_mask" (bit t: non-temporal weight loads for stack tag
+ * t, default 5), "gemv_xl" (decode GEMVs with LDS-staged activations, default 1), "fold_proj"
+ * (decoder steps >= 2 gather projection(E_a[c]) from a table built at csm_begin, default 1),
+ * "qkv0_tab" (decoder layer 0's q, k, v gathered from a table at steps >= 2, default 1),
+ * "fuse_mlp" (one-launch MLP for <= 4 rows, default 0). */
+int csm_set_option(csm_engine* e, const char* key, int value);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CSM_HIP_PROF_H */

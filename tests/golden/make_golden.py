@@ -24,6 +24,16 @@ from oracle.mimi_oracle import OracleMimi  # noqa: E402
 
 TINY_IDS = [998, 17, 401, 77, 912, 3, 999]
 
+# configs[1] prompt (bench.py prompt_ids(0)): BOS + 12 ids ~ U[0, 128000) (seed 1) + EOS
+CONFIG1_IDS = [128000] + [int(x) for x in np.random.default_rng(1).integers(0, 128000, 12)] + [128001]
+# configs[0] "[0]Hello from Sesame." under the Llama-3.2 BPE + BOS/EOS template (tokenizers.py:24-58).
+# UNVERIFIED: the tokenizer assets (unsloth/Llama-3.2-1B) are not available offline.  The ids are the
+# cl100k-compatible pieces "[", "0", "]", "Hello", " from", " Ses", "ame", "." recalled by hand; only
+# the plumbing (prompt -> 125 frames -> Mimi decode) is pinned by this fixture, not the tokenizer.
+CONFIG0_IDS = [128000, 58, 15, 60, 9906, 505, 23720, 373, 13, 128001]
+LONG_FRAMES = (0, 63, 64, 100, 124)   # frames whose logits are kept (attention crosses 64-key chunks)
+LONG_CI = (1, 2, 16, 31)              # codebooks whose ci logits are kept
+
 
 def pcm_fixture(n=9600, seed=3):
     t = np.arange(n) / 24000.0
@@ -42,6 +52,70 @@ def csm_golden():
                 ci_logits=np.stack([l[1] for l in logs]), sampled_codes=scodes)
 
 
+def _oracle(args, w, bf16):
+    from csm_mlx.weights import bf16_round
+    ww = {k: bf16_round(v) for k, v in w.items()} if bf16 else w
+    return OracleCSM(args, ww, BB[args.backbone_name], DC[args.decoder_name])
+
+
+def csm_1b_long_golden():
+    """configs[1] at full length: csm_1b B=1 greedy, 125 frames from the 14-row prompt (backbone
+    attention reaches S = 139 keys: three 64-key chunks), fp32 weights and bf16-rounded weights."""
+    from csm_mlx.models import csm_1b
+    args = csm_1b()
+    w = synthetic_csm_weights(args, 0)
+    out = dict(ids=np.array(CONFIG1_IDS, np.int32), frames=np.array(LONG_FRAMES), ci_codebooks=np.array(LONG_CI))
+    for tag, bf16 in (("fp32", False), ("bf16", True)):
+        codes, logs = _oracle(args, w, bf16).generate_codes(*text_frame(CONFIG1_IDS, 32), 125, collect_logits=True)
+        out[f"{tag}_codes"] = codes
+        out[f"{tag}_c0"] = np.stack([logs[f][0] for f in LONG_FRAMES])
+        out[f"{tag}_ci"] = np.stack([logs[f][1][[c - 1 for c in LONG_CI]] for f in LONG_FRAMES])
+        print(tag, "codes", codes.shape, flush=True)
+    return out
+
+
+def config0_golden():
+    """configs[0] plumbing: generate("[0]Hello from Sesame." ids (unverified), speaker 0, no context,
+    10 s, greedy) on the fp32 oracle -> 125 frames; the Mimi oracle's decode of them (rms + head)."""
+    from csm_mlx.models import csm_1b
+    args = csm_1b()
+    w = synthetic_csm_weights(args, 0)
+    codes = _oracle(args, w, False).generate_codes(*text_frame(CONFIG0_IDS, 32), 125)
+    m = MIMI_CONFIGURATION["mimi_202407"]
+    y = OracleMimi(m, synthetic_mimi_weights(m, 0)).decode(np.ascontiguousarray(codes.T[None]))
+    return dict(ids=np.array(CONFIG0_IDS, np.int32), codes=codes, pcm_head=y[0, 0, :1920],
+                pcm_rms=np.array(np.sqrt(np.mean(y.astype(np.float64) ** 2))), n_samples=np.array(y.shape[-1]))
+
+
+def tiny_long_prompt(seed=11):
+    """A >= 200-row tiny prompt: text, 100 audio rows + EOS row, text, 100 audio rows + EOS row, text
+    (tokenize_segment layout, tokenizers.py:61-102) -- prefill and decode past three 64-key chunks."""
+    from oracle.csm_oracle import audio_frame
+    rng = np.random.default_rng(seed)
+    parts = []
+    for i in range(3):
+        parts.append(text_frame([998] + [int(x) for x in rng.integers(0, 990, 6)] + [999], 4))
+        if i < 2:
+            parts.append(audio_frame(rng.integers(0, 64, (4, 100)).astype(np.int32)))
+    return np.concatenate([p[0] for p in parts]), np.concatenate([p[1] for p in parts])
+
+
+TINY_LONG_FRAMES = (0, 20, 39)
+
+
+def tiny_long_golden():
+    args = csm_tiny()
+    w = synthetic_csm_weights(args, 0)
+    t, m = tiny_long_prompt()
+    out = dict(tokens=t, mask=m, frames=np.array(TINY_LONG_FRAMES))
+    for tag, bf16 in (("fp32", False), ("bf16", True)):
+        codes, logs = _oracle(args, w, bf16).generate_codes(t, m, 40, collect_logits=True)
+        out[f"{tag}_codes"] = codes
+        out[f"{tag}_c0"] = np.stack([logs[f][0] for f in TINY_LONG_FRAMES])
+        out[f"{tag}_ci"] = np.stack([logs[f][1] for f in TINY_LONG_FRAMES])
+    return out
+
+
 def mimi_golden():
     out = {}
     for mode in ("mlx", "causal"):
@@ -56,7 +130,16 @@ def mimi_golden():
     return out
 
 
+FIXTURES = {
+    "csm_tiny_oracle.npz": csm_golden,
+    "mimi_tiny_oracle.npz": mimi_golden,
+    "tiny_long_prompt.npz": tiny_long_golden,
+    "csm_1b_greedy_125.npz": csm_1b_long_golden,
+    "config0_plumbing.npz": config0_golden,
+}
+
 if __name__ == "__main__":
-    np.savez_compressed(os.path.join(HERE, "csm_tiny_oracle.npz"), **csm_golden())
-    np.savez_compressed(os.path.join(HERE, "mimi_tiny_oracle.npz"), **mimi_golden())
-    print("wrote", os.listdir(HERE))
+    # python tests/golden/make_golden.py [fixture ...]   (default: all; the csm_1b ones take minutes)
+    for name in (sys.argv[1:] or list(FIXTURES)):
+        np.savez_compressed(os.path.join(HERE, name), **FIXTURES[name]())
+        print("wrote", name, flush=True)

@@ -15,9 +15,21 @@ def csm_weights(args_key, seed=0):
     return args, synthetic_csm_weights(args, seed)
 
 
+_ORACLES = {}
+
+
 def oracle_for(args, weights, bf16=False, q4=False):
     """bf16: every weight rounded to bf16 (CSM dtype "bf16").  q4: nn.quantize'd CSM (dtype "q4"):
-    Linear / Embedding weights quantize->dequantize (oracle/quant_oracle.py), audio_head bf16."""
+    Linear / Embedding weights quantize->dequantize (oracle/quant_oracle.py), audio_head bf16.
+    Memoised per weight dict (the csm_weights dicts are cached): the csm_1b bf16 / int4 conversions
+    take 10-45 s each (6 GB of fp32 per variant)."""
+    key = (id(weights), bool(bf16), bool(q4))
+    if key not in _ORACLES:
+        _ORACLES[key] = _oracle_for(args, weights, bf16, q4)
+    return _ORACLES[key]
+
+
+def _oracle_for(args, weights, bf16, q4):
     from oracle.csm_oracle import OracleCSM
     from oracle.quant_oracle import quantize_dequantize_weights
     w = {k: bf16_round(v) for k, v in weights.items()} if bf16 else weights
@@ -80,3 +92,38 @@ def write_adapter_dir(path, config, tensors):
     (path / "adapter_config.json").write_text(json.dumps(config))
     save_file({k: np.ascontiguousarray(v) for k, v in tensors.items()}, str(path / "adapters.safetensors"))
     return path
+
+
+def oracle_batch(o, prompts, frames, collect_logits=False, temperature=0.0, top_k=0, seeds=None):
+    """Greedy oracle frames for many utterances at once: prompts (tokens, mask) of equal length run as
+    one (B, L, 33) batch through OracleCSM.frame (the reference's generate_frame is batch-agnostic,
+    generation.py:21-92).  Returns per utterance (codes (F_b, K), [(c0, ci) per frame] or None);
+    an utterance that reaches EOS is re-run alone so its frame count follows generation.py:151.
+    Sampling (temperature > 0) uses the oracle's restatement of the engine's counter-based RNG with
+    one seed per utterance."""
+    seeds = [0] * len(prompts) if seeds is None else list(seeds)
+    groups = {}
+    for i, (t, _) in enumerate(prompts):
+        groups.setdefault(t.shape[0], []).append(i)
+    out = [None] * len(prompts)
+    for L, idx in groups.items():
+        toks = np.stack([prompts[i][0] for i in idx]).astype(np.int64)
+        msk = np.stack([prompts[i][1] for i in idx]).astype(bool)
+        cache = o.new_backbone_cache()
+        codes, logs = [], []
+        for f in range(frames):
+            s = o.frame(toks, msk, cache, temperature, top_k, [seeds[i] for i in idx], f)
+            codes.append(s)
+            if collect_logits:
+                logs.append((o.debug["c0_logits"].copy(), o.debug["ci_logits"].copy()))
+            toks = np.concatenate([s, np.zeros((len(idx), 1), np.int32)], 1)[:, None, :].astype(np.int64)
+            msk = np.concatenate([np.ones_like(s, bool), np.zeros((len(idx), 1), bool)], 1)[:, None, :]
+        codes = np.stack(codes, 1)                                    # (b, F, K)
+        for j, i in enumerate(idx):
+            if not codes[j].any(-1).all():                            # EOS inside the window: run alone
+                res = o.generate_codes(prompts[i][0], prompts[i][1], frames, temperature, top_k, seeds[i],
+                                       collect_logits=collect_logits)
+                out[i] = res if collect_logits else (res, None)
+            else:
+                out[i] = (codes[j], [(c0[j], ci[j]) for c0, ci in logs] if collect_logits else None)
+    return out

@@ -95,6 +95,28 @@ def test_fuse_adapters_tree(tmp_path):
     assert list(full) == ["projection.weight"]
 
 
+def test_dora_without_magnitude_keeps_base_row_norms(tmp_path):
+    """A DoRA adapter file with lora_a / lora_b but no .m: DoRALinear.from_base initialised m to the
+    base weight's row norms and load_weights(strict=False) kept it, so the fused rows must come back
+    to ||W_base|| -- the oracle's unfused DoRA forward with m = ||W_base||."""
+    from csm_mlx.adapters import fuse_adapters
+    from csm_mlx.weights import synthetic_csm_weights
+    from oracle.csm_oracle import adapted_linear
+    m = _handle("tiny")
+    w = synthetic_csm_weights(m.args, 0)
+    cfg, t, oracle_ad = make_adapters(m, w, "dora", keys=("projection",))
+    t = {k: v for k, v in t.items() if not k.endswith(".m")}
+    out = dict(fuse_adapters(m, cfg, t, lambda n: w[n]))
+    base = w["projection.weight"]
+    fused = out["projection.weight"]
+    np.testing.assert_allclose(np.linalg.norm(fused, axis=1), np.linalg.norm(base, axis=1), rtol=1e-5)
+    ad = dict(oracle_ad["projection"], m=np.linalg.norm(base, axis=1).astype(np.float32))
+    x = np.random.default_rng(1).standard_normal((3, base.shape[1])).astype(np.float32)
+    want = adapted_linear(x, base, ad)
+    np.testing.assert_allclose(x @ fused.T, want, rtol=0, atol=2e-5 * np.abs(want).max())
+    assert not np.allclose(fused, base)
+
+
 def test_adapter_dir_errors(tmp_path):
     from csm_mlx.adapters import read_adapter_dir
     with pytest.raises(FileNotFoundError):
@@ -111,11 +133,10 @@ def test_scoring_layout_checks_and_cross_entropy():
     m[0, 2:5, :K] = True                     # audio rows, then one padding row
     lm = np.zeros_like(m)
     lm[0, 3:5] = True
-    assert _split(toks, m, lm, K) == [3]
+    assert _split(toks, m, lm, K) == ([3], [True])
     m2 = m.copy()
-    m2[0, 4, K] = True                       # text after the first scored row
-    with pytest.raises(NotImplementedError):
-        _split(toks, m2, lm, K)
+    m2[0, 4, K] = True                       # text after the first scored row: the per-utterance path
+    assert _split(toks, m2, lm, K) == ([3], [False])
     rng = np.random.default_rng(0)
     lg = rng.standard_normal((3, 7)).astype(np.float32) * 4
     t = np.array([0, 6, 3])

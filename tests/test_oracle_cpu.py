@@ -161,3 +161,30 @@ def test_mimi_oracle_golden():
         assert np.array_equal(codes, g[f"{mode}_codes"])
         y = o.decode(codes)
         np.testing.assert_allclose(y[0, 0, :512], g[f"{mode}_pcm_head"], rtol=1e-5, atol=1e-6)
+
+
+def test_tiny_long_prompt_golden():
+    """The >= 200-row prompt fixture regenerates from the oracle (fp32 and bf16-rounded weights)."""
+    g = np.load(os.path.join(GOLD, "tiny_long_prompt.npz"))
+    args, w = csm_weights("tiny")
+    for tag, bf16 in (("fp32", False), ("bf16", True)):
+        codes, logs = oracle_for(args, w, bf16=bf16).generate_codes(g["tokens"], g["mask"], 40, collect_logits=True)
+        assert np.array_equal(codes, g[f"{tag}_codes"])
+        np.testing.assert_allclose(np.stack([logs[f][0] for f in g["frames"]]), g[f"{tag}_c0"], rtol=0, atol=1e-5)
+
+
+def test_csm_1b_long_fixtures_regenerate():
+    """The csm_1b fixtures (configs[1] 125 frames; configs[0] plumbing) regenerate from the oracle:
+    first frames here (the full runs are make_golden.py's), the configs[0] decode length and the
+    flagged-unverified id list."""
+    from oracle.csm_oracle import text_frame
+    g1 = np.load(os.path.join(GOLD, "csm_1b_greedy_125.npz"))
+    g0 = np.load(os.path.join(GOLD, "config0_plumbing.npz"))
+    args, w = csm_weights("1b")
+    o = oracle_for(args, w)
+    for g, key in ((g1, "fp32_codes"), (g0, "codes")):
+        assert g[key].shape == (125, 32)
+        codes = o.generate_codes(*text_frame(g["ids"].tolist(), 32), 3)
+        assert np.array_equal(codes, g[key][:3])
+    assert g0["ids"][0] == 128000 and g0["ids"][-1] == 128001 and int(g0["n_samples"]) == 125 * 1920
+    assert np.isfinite(g0["pcm_rms"]) and 0 < float(g0["pcm_rms"]) < 1

@@ -42,6 +42,59 @@ def _batch(args, seed=0):
     return {"tokens": T, "masks": M, "loss_masks": LM, "first_codebook_weight_multiplier": 1.5}
 
 
+def _batch_multiseg(args, seed=1):
+    """tokenize_segments_with_loss_mask layout (tokenizers.py:105-145): per utterance alternating
+    speaker segments [text rows, audio rows + EOS zero row], loss masks ones except the segments of a
+    masked speaker (1) -- text rows and a masked speaker's rows follow the first scored row."""
+    from csm_mlx.tokenizers import tokenize_text_segment
+    rng = np.random.default_rng(seed)
+    K = args.n_audio_codebooks
+
+    def audio(n):
+        t = np.zeros((n + 1, K + 1), np.int32)
+        t[:n, :K] = rng.integers(0, 64, (n, K))
+        m = np.zeros((n + 1, K + 1), bool)
+        m[:, :K] = True
+        return t, m
+    utts = []
+    for spec in ([(0, 3, 5), (1, 2, 4), (0, 4, 3)], [(1, 2, 2), (0, 3, 6)]):
+        toks, msks, lms = [], [], []
+        for spk, n_txt, n_aud in spec:
+            t, m = tokenize_text_segment([998] + [int(x) for x in rng.integers(0, 990, n_txt)] + [999], spk, K)
+            a, am = audio(n_aud)
+            seg_t, seg_m = np.concatenate([t, a]), np.concatenate([m, am])
+            toks.append(seg_t)
+            msks.append(seg_m)
+            lms.append(np.full(seg_t.shape, spk != 1))
+        utts.append((np.concatenate(toks), np.concatenate(msks), np.concatenate(lms)))
+    S = max(len(u[0]) for u in utts)
+    T = np.zeros((2, S, K + 1), np.int32)
+    M = np.zeros((2, S, K + 1), bool)
+    LM = np.zeros((2, S, K + 1), bool)
+    for b, (t, m, lm) in enumerate(utts):
+        T[b, : len(t)], M[b, : len(t)], LM[b, : len(t)] = t, m, lm
+    return {"tokens": T, "masks": M, "loss_masks": LM, "first_codebook_weight_multiplier": 1.0}
+
+
+@pytest.mark.parametrize("per_sample,mismatch", [(False, False), (True, False), (False, True)])
+def test_compute_loss_multi_segment_matches_oracle(per_sample, mismatch):
+    """Text rows (and masked-speaker segments) after the first scored row: every utterance is scored
+    on its own, text rows appended to the backbone with their own masks."""
+    from csm_mlx.models import CSM
+    from csm_mlx.scoring import _split, compute_loss
+    from oracle.csm_oracle import compute_loss_ref
+    args, w = csm_weights("tiny")
+    model = CSM(args, dtype="float32", max_batch=2)
+    model.load_weights(w)
+    batch = _batch_multiseg(args)
+    K = args.n_audio_codebooks
+    assert _split(batch["tokens"], batch["masks"], batch["loss_masks"], K)[1] == [False, False]
+    got = compute_loss(model, batch, per_sample=per_sample, cause_mismatch=mismatch)
+    ref = compute_loss_ref(oracle_for(args, w), batch, per_sample=per_sample, cause_mismatch=mismatch)
+    assert np.all(np.isfinite(got)) and np.shape(got) == np.shape(ref)
+    np.testing.assert_allclose(got, ref, rtol=1e-4)
+
+
 @pytest.mark.parametrize("per_sample,mismatch", [(False, False), (True, False), (False, True)])
 def test_compute_loss_matches_oracle(per_sample, mismatch):
     from csm_mlx.models import CSM
