@@ -45,8 +45,8 @@ def prompt_ids(g: int):
 
 def shard(global_batch: int, world: int, rank: int):
     """Contiguous utterance partition: rank r owns [r*B/N, (r+1)*B/N)."""
-    per = global_batch // world
-    return list(range(rank * per, (rank + 1) * per))
+    from csm_mlx.dist import shard as _shard
+    return _shard(global_batch, world, rank)
 
 
 def dist_env():
@@ -67,22 +67,22 @@ def aggregate(frames_local: float, dt_local: float, world: int, device=None):
     return float(f.item()), float(m.item())
 
 
-def build_codec(seed=0, device=None):
+def build_codec(seed=0, device=None, model_name="csm_1b"):
     from csm_mlx.config import MIMI_CONFIGURATION
     from csm_mlx.mimi import MimiCodec
     from csm_mlx.tokenizers import set_audio_tokenizer
     from csm_mlx.weights import synthetic_mimi_weights
-    m = MIMI_CONFIGURATION["mimi_202407"]
+    m = MIMI_CONFIGURATION["mimi_202407" if model_name == "csm_1b" else "tiny"]
     codec = MimiCodec(m, max_batch=64, device=device)
     codec.load_weights(synthetic_mimi_weights(m, seed))
-    set_audio_tokenizer(codec, 32)
+    set_audio_tokenizer(codec, m.n_q)
     return codec
 
 
-def build_model(dtype: str, batch: int, seed=0, device=None):
-    from csm_mlx.models import CSM, csm_1b
+def build_model(dtype: str, batch: int, seed=0, device=None, model_name="csm_1b"):
+    from csm_mlx.models import CSM, csm_1b, csm_tiny
     from csm_mlx.weights import csm_param_specs, synthetic_csm_weights
-    args = csm_1b()
+    args = csm_1b() if model_name == "csm_1b" else csm_tiny()   # tiny: test rehearsals of the N-rank path only
     model = CSM(args, dtype=dtype, max_batch=batch, device=device)
     names = list(csm_param_specs(args))
     for i in range(0, len(names), 16):      # stream tensors in groups: bounded host memory
@@ -126,6 +126,18 @@ CONFIGS = {
 }
 
 
+def model_codes(model, B):
+    """Per-utterance codes (F_b, K) of the engine's current batch (csm_read_codes)."""
+    from csm_mlx import _lib
+    L = _lib.lib()
+    F = ctypes.c_int(0)
+    _lib.check(L.csm_read_codes(model.engine, None, None, None, ctypes.byref(F)))
+    hist = np.zeros((F.value, B, model.n_audio_codebooks), np.int32)
+    n = np.zeros(B, np.int32)
+    _lib.check(L.csm_read_codes(model.engine, _lib.ptr(hist), _lib.ptr(n), None, None))
+    return [hist[: n[b], b] for b in range(B)]
+
+
 def context_audio(g: int, seg: int, seconds: float = 5.0):
     """seeded sum of 3 sines (100-400 Hz) + N(0, 0.01) noise, amplitude 0.1, 24 kHz."""
     rng = np.random.default_rng(50_000 + 97 * g + seg)
@@ -167,6 +179,9 @@ def main():
                          "the default configs[1] line; the metric stays audio frames/s")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (RCCL over xGMI) for real runs; gloo rehearses N ranks on fewer GPUs")
+    ap.add_argument("--model", default="csm_1b", choices=["csm_1b", "tiny"],
+                    help="tiny: the toy test model (multi-rank rehearsals in tests), never a bench line")
+    ap.add_argument("--dump", default="", help="rank 0 writes the gathered codes / PCM of the last step (npz)")
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config or 2])
     if args.config:
@@ -199,18 +214,27 @@ def main():
             if dev is not None:
                 torch.cuda.synchronize()
 
+    from csm_mlx.dist import gather_results
     from csm_mlx.generation import generate_batch
     from csm_mlx.tokenizers import tokenize_text_segment
 
-    model = build_model(args.dtype, args.batch, device=device)
+    model = build_model(args.dtype, args.batch, device=device, model_name=args.model)
+    K = model.n_audio_codebooks
     decode = not args.no_decode
     if decode or cfg["stream"] or cfg["context"]:
-        build_codec(device=device)
+        build_codec(device=device, model_name=args.model)
     mine = shard(args.batch * world, world, rank)
     ms = args.frames * 80
     seeds = [1234 + g for g in mine]
+
+    def ids_of(g):
+        if args.model == "csm_1b":
+            return prompt_ids(g)
+        rng = np.random.default_rng(1 if g == 0 else 1000 + g)          # tiny vocab (1000 text ids)
+        return [998] + [int(x) for x in rng.integers(0, 990, 3 + g % 4)] + [999]
     if not cfg["context"]:
-        prompts = [tokenize_text_segment(prompt_ids(g), 0, 32) for g in mine]
+        prompts = [tokenize_text_segment(ids_of(g), 0, K) for g in mine]
+    last = {}
 
     def step():
         # config 5: the context Segments' Mimi encode is part of every step (generation.py:108-125)
@@ -218,15 +242,23 @@ def main():
         if cfg["stream"]:
             from csm_mlx.generation import stream_generate_batch
             n = 0
+            chunks = [[] for _ in mine]
             for pcm, done in stream_generate_batch(model, pr, ms, temperature=cfg["temperature"],
                                                    top_k=cfg["top_k"], seeds=seeds):
                 n += int((~done).sum())
-            return n
-        out = generate_batch(model, pr, ms, temperature=cfg["temperature"], top_k=cfg["top_k"], seeds=seeds,
-                             decode=decode)
-        if decode:
-            return sum(len(w) // FRAME_SAMPLES for w in out)
-        return sum(len(c) for c in out)
+                for b in np.nonzero(~done)[0]:
+                    chunks[b].append(pcm[b])
+            codes = [c for c in model_codes(model, len(mine))]
+            pcm_l = [np.concatenate(c) if c else np.zeros((0,), np.float32) for c in chunks]
+        else:
+            out = generate_batch(model, pr, ms, temperature=cfg["temperature"], top_k=cfg["top_k"], seeds=seeds,
+                                 decode=decode, with_codes=decode)
+            codes, pcm_l = out if decode else (out, None)
+            n = sum(len(c) for c in codes)
+        if world > 1:   # result collection: one all-gather per kind (RCCL over xGMI / gloo)
+            codes, pcm_l = gather_results(codes, pcm_l, args.frames, FRAME_SAMPLES, dev)
+        last["codes"], last["pcm"] = codes, pcm_l
+        return n
 
     for _ in range(args.warmup):
         step()
@@ -259,6 +291,11 @@ def main():
         except Exception:  # noqa: BLE001
             pass
 
+    if rank == 0 and args.dump:
+        z = {f"codes_{i}": c for i, c in enumerate(last["codes"])}
+        if last["pcm"] is not None:
+            z.update({f"pcm_{i}": p for i, p in enumerate(last["pcm"])})
+        np.savez(args.dump, n=len(last["codes"]), **z)
     if rank == 0:
         line = {
             "metric": METRIC,

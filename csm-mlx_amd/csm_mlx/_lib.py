@@ -86,6 +86,8 @@ def lib():
             "csm_read_codes": ([P, P, P, P, ctypes.POINTER(I)], I),
             "csm_debug_read": ([P, ctypes.c_char_p, P, I64, ctypes.POINTER(I64)], I),
             "csm_codes_device_ptr": ([P, ctypes.POINTER(P)], I),
+            "csm_read_rows": ([P, ctypes.c_char_p, I, P, P], I),
+            "csm_linear": ([P, ctypes.c_char_p, I, P, P], I),
             "csm_synchronize": ([P], I),
             "csm_set_option": ([P, ctypes.c_char_p, I], I),
             "csm_bench_gemv": ([P, I, I, I, ctypes.POINTER(F), ctypes.POINTER(ctypes.c_double)], I),

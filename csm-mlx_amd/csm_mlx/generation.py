@@ -260,13 +260,17 @@ def generate(model: CSM, text, speaker: int, context: List[Segment], max_audio_l
 
 
 def generate_batch(model: CSM, prompts: Sequence[Tuple[np.ndarray, np.ndarray]], max_audio_length_ms: float = 10_000,
-                   *, temperature: float = 0.0, top_k: int = 0, sampler=None, seeds=None, decode: bool = True):
-    """Batched extension: B prompts (tokens, mask) -> list of waveforms (or codes if decode=False)."""
+                   *, temperature: float = 0.0, top_k: int = 0, sampler=None, seeds=None, decode: bool = True,
+                   with_codes: bool = False):
+    """Batched extension: B prompts (tokens, mask) -> list of waveforms (or codes if decode=False;
+    (codes, waveforms) with ``with_codes``)."""
     smp = _resolve_sampler(temperature, sampler, top_k)
     hist, n_frames, _ = generate_codes_batch(model, prompts, int(max_audio_length_ms / 80), sampler=smp, seeds=seeds)
+    codes = [hist[: n_frames[b], b] for b in range(len(prompts))]
     if not decode:
-        return [hist[: n_frames[b], b] for b in range(len(prompts))]
-    return _decode_batch(model, hist, n_frames)
+        return codes
+    pcm = _decode_batch(model, hist, n_frames)
+    return (codes, pcm) if with_codes else pcm
 
 
 def _overlapped_frames(cache: "FrameCache", codec, max_audio_frames: int):

@@ -172,11 +172,141 @@ class CSM:
         self.quantization = {"group_size": group_size, "bits": bits}
         return self
 
-    def embed_audio(self, codebook: int, tokens):
-        raise NotImplementedError("embeddings are gathered inside the HIP frame graph (models.py:79-80)")
+    # ------------------------------------------------------------------ module views (models.py:53-92)
+    def _rows(self, name: str, rows) -> np.ndarray:
+        rows = np.ascontiguousarray(np.asarray(rows, np.int32).reshape(-1))
+        width = self.n_backbone_embedding if "embeddings" in name else None
+        out = np.zeros((len(rows), width or _weight_width(self, name)), np.float32)
+        _lib.check(_lib.lib().csm_read_rows(self.engine, name.encode(), len(rows), _lib.ptr(rows), _lib.ptr(out)))
+        return out
 
-    def embed_tokens(self, tokens):
-        raise NotImplementedError("embeddings are gathered inside the HIP frame graph (models.py:82-92)")
+    def embed_audio(self, codebook: int, tokens) -> np.ndarray:
+        """models.py:79-80: audio_embeddings(tokens + codebook * n_audio_vocab), read from the GPU copy
+        (the frame graph gathers these rows itself; this is the module view)."""
+        t = np.asarray(tokens)
+        out = self._rows("audio_embeddings.weight", t + codebook * self.n_audio_vocab)
+        return out.reshape(t.shape + (out.shape[-1],))
+
+    def embed_tokens(self, tokens) -> np.ndarray:
+        """models.py:82-92: (..., K+1) ids -> (..., K+1, D): audio columns at code + V*k, the text
+        column from text_embeddings, concatenated in that order."""
+        t = np.asarray(tokens)
+        K, V = self.n_audio_codebooks, self.n_audio_vocab
+        text = self._rows("text_embeddings.weight", t[..., -1])
+        audio = self._rows("audio_embeddings.weight", t[..., :-1] + V * np.arange(K))
+        D = text.shape[-1]
+        return np.concatenate([audio.reshape(t.shape[:-1] + (K, D)), text.reshape(t.shape[:-1] + (1, D))], axis=-2)
+
+    @property
+    def projection(self) -> "_LinearView":
+        """models.py:59-61 (nn.Linear backbone_dim -> decoder_dim, no bias)."""
+        return _LinearView(self, "projection.weight")
+
+    @property
+    def codebook0_head(self) -> "_LinearView":
+        """models.py:62-64 (nn.Linear backbone_dim -> n_audio_vocab, no bias)."""
+        return _LinearView(self, "codebook0_head.weight")
+
+    @property
+    def audio_head(self) -> "_AudioHeadView":
+        """models.py:65-67: the raw (n_audio_codebooks - 1, decoder_dim, n_audio_vocab) array."""
+        return _AudioHeadView(self)
+
+
+def _weight_width(model: "CSM", name: str) -> int:
+    """Input width (K) of a stored Linear weight."""
+    if name in ("projection.weight", "codebook0_head.weight"):
+        return model.n_backbone_embedding
+    st = model.backbone.args if name.startswith("backbone.") else model.decoder.args
+    if name.endswith("o_proj.weight"):
+        return st.num_attention_heads * st.head_dim
+    if name.endswith("down_proj.weight"):
+        return st.intermediate_size
+    return st.hidden_size
+
+
+def _weight_rows(model: "CSM", name: str) -> int:
+    if name == "projection.weight":
+        return model.n_decoder_embedding
+    if name == "codebook0_head.weight":
+        return model.n_audio_vocab
+    if name == "text_embeddings.weight":
+        return model.n_text_vocab
+    if name == "audio_embeddings.weight":
+        return model.n_audio_vocab * model.n_audio_codebooks
+    st = model.backbone.args if name.startswith("backbone.") else model.decoder.args
+    if name.endswith(("q_proj.weight", "o_proj.weight", "down_proj.weight")):
+        return st.hidden_size if not name.endswith("q_proj.weight") else st.num_attention_heads * st.head_dim
+    if name.endswith(("k_proj.weight", "v_proj.weight")):
+        return st.num_key_value_heads * st.head_dim
+    return st.intermediate_size                                   # gate / up
+
+
+class _LinearView:
+    """A Linear of the engine: ``view(x)`` runs x W^T on the GPU (csm_linear, the GEMV's arithmetic);
+    ``view.weight`` reads the stored matrix back as fp32 (int4: dequantized)."""
+
+    def __init__(self, model: CSM, name: str):
+        self.model, self.name = model, name
+
+    @property
+    def weight(self) -> np.ndarray:
+        return self.model._rows(self.name, np.arange(_weight_rows(self.model, self.name)))
+
+    def __call__(self, x) -> np.ndarray:
+        x = np.asarray(x, np.float32)
+        lead, K = x.shape[:-1], x.shape[-1]
+        flat = np.ascontiguousarray(x.reshape(-1, K))
+        y = np.zeros((len(flat), _weight_rows(self.model, self.name)), np.float32)
+        _lib.check(_lib.lib().csm_linear(self.model.engine, self.name.encode(), len(flat), _lib.ptr(flat), _lib.ptr(y)))
+        return y.reshape(lead + (y.shape[-1],))
+
+
+class _AudioHeadView:
+    """``model.audio_head`` (K-1, Dd, V): ``np.asarray`` reads it back; ``audio_head[i]`` is a
+    (Dd, V) view whose ``x @ audio_head[i]`` runs on the GPU (generation.py:79)."""
+
+    def __init__(self, model: CSM):
+        self.model = model
+        self.shape = (model.n_audio_codebooks - 1, model.n_decoder_embedding, model.n_audio_vocab)
+
+    def __len__(self):
+        return self.shape[0]
+
+    def __array__(self, dtype=None, copy=None):
+        m = self.model
+        Km1, Dd, V = self.shape
+        Vp = (V + 7) // 8 * 8
+        f32 = m.dtype == "float32"
+        raw = np.zeros((Km1, Vp, Dd), np.float32 if f32 else np.uint16)
+        _lib.check(_lib.lib().csm_debug_read(m.engine, b"audio_head", _lib.ptr(raw), raw.nbytes, None))
+        if not f32:
+            raw = (raw.astype(np.uint32) << 16).view(np.float32)
+        a = np.ascontiguousarray(raw[:, :V, :].transpose(0, 2, 1))
+        return a if dtype is None else a.astype(dtype)
+
+    def __getitem__(self, i):
+        i = int(i) % self.shape[0]
+        return _AudioHeadSlice(self.model, i)
+
+
+class _AudioHeadSlice:
+    def __init__(self, model: CSM, i: int):
+        self.model, self.i = model, i
+        self.shape = (model.n_decoder_embedding, model.n_audio_vocab)
+
+    def __array__(self, dtype=None, copy=None):
+        a = np.asarray(_AudioHeadView(self.model))[self.i]
+        return a if dtype is None else a.astype(dtype)
+
+    def __rmatmul__(self, x) -> np.ndarray:
+        x = np.asarray(x, np.float32)
+        lead, K = x.shape[:-1], x.shape[-1]
+        flat = np.ascontiguousarray(x.reshape(-1, K))
+        y = np.zeros((len(flat), self.shape[1]), np.float32)
+        _lib.check(_lib.lib().csm_linear(self.model.engine, f"audio_head.{self.i}".encode(), len(flat),
+                                         _lib.ptr(flat), _lib.ptr(y)))
+        return y.reshape(lead + (y.shape[-1],))
 
 
 def _read_weight_file(path: str, only: Optional[str] = None):

@@ -1111,6 +1111,9 @@ int csm_debug_read(csm_engine* e, const char* what, void* host, int64_t nbytes, 
     else if (w == "ci_logits") { src = e->ci_logits; n = (e->K - 1) * B * Vp * 4; }
     else if (w == "codes") { src = e->codes; n = B * e->K * 4; }
     else if (w == "pos") { src = e->pos; n = B * 4; }
+    else if (w == "audio_head") {  // device layout [K-1][Vpad][Dd], f32 or bf16 bits
+      src = e->audio_head; n = (size_t)(e->K - 1) * Vp * e->Dd * (e->head_wdt == WDT_F32 ? 4 : 2);
+    }
     else if (w.rfind("weight:", 0) == 0) {  // a whole stored matrix in its device layout (not fused ones)
       Place pl;
       if (!weight_place(e, w.substr(7), pl) || pl.n != pl.Ntot) throw CsmError(CSM_ERR_ARG, "no whole matrix " + w);
@@ -1123,6 +1126,67 @@ int csm_debug_read(csm_engine* e, const char* what, void* host, int64_t nbytes, 
       if ((size_t)nbytes < n) throw CsmError(CSM_ERR_ARG, "debug buffer too small");
       HIPCHK(hipMemcpy(host, src, n, hipMemcpyDeviceToHost));
     }
+  }
+  CSM_CATCH
+}
+
+int csm_read_rows(csm_engine* e, const char* name, int n, const int32_t* rows, float* out) {
+  CSM_TRY {
+    if (!name || n < 0 || (n > 0 && (!rows || !out))) throw CsmError(CSM_ERR_ARG, "bad csm_read_rows arguments");
+    Place pl;
+    if (!weight_place(e, name, pl)) throw CsmError(CSM_ERR_ARG, std::string("not a Linear / Embedding weight: ") + name);
+    if (!e->loaded.count(name)) throw CsmError(CSM_ERR_STATE, std::string("weight not loaded: ") + name);
+    std::vector<int> idx(n);
+    for (int i = 0; i < n; ++i) {
+      if (rows[i] < 0 || rows[i] >= pl.n) throw CsmError(CSM_ERR_ARG, "row index out of range");
+      idx[i] = pl.row0 + rows[i] * pl.rstep;
+    }
+    if (n == 0) return CSM_OK;
+    HIPCHK(hipSetDevice(e->dev));
+    DevBuf di((size_t)n * 4), dout((size_t)n * pl.K * 4);
+    HIPCHK(hipMemcpyAsync(di.p, idx.data(), (size_t)n * 4, hipMemcpyHostToDevice, e->st));
+    launch_table_rows(pl.base, e->wdt, pl.Ntot, pl.K, (const int*)di.p, n, (float*)dout.p, e->st);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(out, dout.p, (size_t)n * pl.K * 4, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(hipStreamSynchronize(e->st));
+  }
+  CSM_CATCH
+}
+
+int csm_linear(csm_engine* e, const char* name, int M, const float* x, float* y) {
+  CSM_TRY {
+    if (!name || M <= 0 || !x || !y) throw CsmError(CSM_ERR_ARG, "bad csm_linear arguments");
+    const std::string nm(name);
+    const void* W = nullptr;
+    int wdt = e->wdt, N = 0, K = 0, row0 = 0, rstep = 1, n_out = 0;
+    if (nm.rfind("audio_head.", 0) == 0) {  // audio_head[i] (in, out): x @ audio_head[i] (generation.py:79)
+      char* end = nullptr;
+      const long i = strtol(nm.c_str() + 11, &end, 10);
+      if (!end || *end || i < 0 || i >= e->K - 1) throw CsmError(CSM_ERR_ARG, "audio_head index out of range");
+      if (!e->loaded.count("audio_head")) throw CsmError(CSM_ERR_STATE, "weight not loaded: audio_head");
+      wdt = e->head_wdt;
+      W = (const char*)e->audio_head + (size_t)i * e->Vpad * e->Dd * (wdt == WDT_F32 ? 4 : 2);
+      N = e->Vpad; K = e->Dd; n_out = e->V;
+    } else {
+      Place pl;
+      if (!weight_place(e, nm, pl) || nm.find("embeddings") != std::string::npos)
+        throw CsmError(CSM_ERR_ARG, "not a Linear weight: " + nm);
+      if (!e->loaded.count(nm)) throw CsmError(CSM_ERR_STATE, "weight not loaded: " + nm);
+      W = pl.base; N = pl.Ntot; K = pl.K; row0 = pl.row0; rstep = pl.rstep; n_out = pl.n;
+    }
+    HIPCHK(hipSetDevice(e->dev));
+    DevBuf dx((size_t)M * K * 4), dy((size_t)M * N * 4);
+    HIPCHK(hipMemcpyAsync(dx.p, x, (size_t)M * K * 4, hipMemcpyHostToDevice, e->st));
+    GemvParams g = gp(e);
+    g.W = W; g.N = N; g.K = K; g.x = (const float*)dx.p; g.xs = K; g.M = M; g.out = (float*)dy.p; g.os = N;
+    g.no_mfma = 1;  // the GEMV's fp32 arithmetic at any row count (no split-K scratch needed)
+    launch_gemv(g, wdt, EPI_STORE, 0, e->st, 2);
+    HIPCHK(hipGetLastError());
+    std::vector<float> full((size_t)M * N);
+    HIPCHK(hipMemcpyAsync(full.data(), dy.p, full.size() * 4, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(hipStreamSynchronize(e->st));
+    for (int m = 0; m < M; ++m)
+      for (int j = 0; j < n_out; ++j) y[(size_t)m * n_out + j] = full[(size_t)m * N + row0 + (size_t)j * rstep];
   }
   CSM_CATCH
 }

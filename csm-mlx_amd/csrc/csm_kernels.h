@@ -253,6 +253,8 @@ void launch_gemv(const GemvParams& p, int wdt, int epi, int norm, hipStream_t st
 int gemv_table_rows(int N, int K, int wdt, int tag);
 void launch_gemv_table(const GemvParams& p, int wdt, int epi, int norm, hipStream_t st, int tag);
 void launch_embed(const EmbedParams& p, int wdt, int M, hipStream_t st);
+// out[i] = stored row idx[i] of a [Ntot][K] matrix (f32 / bf16 / int4) as fp32 (K % 8 == 0)
+void launch_table_rows(const void* base, int wdt, int Ntot, int K, const int* idx, int n, float* out, hipStream_t st);
 // dst[i] = float(src[i]) for n elements (n % 8 == 0)
 void launch_to_f32(const void* src, int wdt, float* dst, size_t n, hipStream_t st);
 void launch_attn(const AttnParams& p, int hd, hipStream_t st);

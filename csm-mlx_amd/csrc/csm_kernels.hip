@@ -1414,3 +1414,27 @@ void launch_dec_attn_oproj(const GemvParams& p0, const AttnParams& a, int wdt, h
 #undef DA_R
 #undef DA_L
 }
+
+// ============================================================================ stored-row reads
+// out[i] = row idx[i] of a stored [Ntot][K] matrix as fp32 (int4: dequantized w = scale * q + bias,
+// the value every kernel computes with) -- the CSM.embed_tokens / embed_audio / weight views.
+template <typename WT>
+__global__ __launch_bounds__(256) void table_rows_kernel(const void* base, int Ntot, int K, const int* idx,
+                                                         float* out, int q4) {
+  const size_t r = (size_t)idx[blockIdx.x];
+  float* o = out + (size_t)blockIdx.x * K;
+  for (int k = threadIdx.x * 8; k < K; k += 256 * 8) {
+    float v[8];
+    if (q4) q4_load8((const uint8_t*)base, (size_t)Ntot, K, r, k, v);
+    else W8<WT>::load((const WT*)base + r * K + k, v);
+    *reinterpret_cast<float4*>(o + k) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(o + k + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  }
+}
+
+void launch_table_rows(const void* base, int wdt, int Ntot, int K, const int* idx, int n, float* out, hipStream_t st) {
+  if (n <= 0) return;
+  if (wdt == WDT_F32) hipLaunchKernelGGL(table_rows_kernel<float>, dim3(n), dim3(256), 0, st, base, Ntot, K, idx, out, 0);
+  else hipLaunchKernelGGL(table_rows_kernel<bf16_t>, dim3(n), dim3(256), 0, st, base, Ntot, K, idx, out,
+                          wdt == WDT_Q4 ? 1 : 0);
+}

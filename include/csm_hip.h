@@ -101,9 +101,17 @@ int csm_frame_forced(csm_engine* e, const int32_t* codes, float* c0_logits, floa
  * done[B].  Any pointer may be NULL. */
 int csm_read_codes(csm_engine* e, int32_t* hist, int32_t* n_frames, uint8_t* done, int* frames_run);
 /* Debug / parity taps: "h_last" [B][D], "c0_logits" [B][Vpad], "ci_logits" [K-1][B][Vpad], "codes" [B][K],
+ * "audio_head" [K-1][Vpad][Dd] (f32 or bf16 bits),
  * "weight:<MLX name>" a whole (unfused) Linear / Embedding matrix in its device layout (int4: nibbles
  * [N][K/2] then {scale, bias} bf16 pairs [N][K/64]). */
 int csm_debug_read(csm_engine* e, const char* what, void* host, int64_t nbytes, int64_t* needed);
+/* The module views of CSM (models.py:53-92): rows[n] of a stored Linear / Embedding weight (MLX key,
+ * e.g. "audio_embeddings.weight") as fp32 [n][in] (int4: the dequantized values the kernels use) --
+ * CSM.embed_tokens / embed_audio / <module>.weight -- and a Linear applied on the GPU: y [M][out] =
+ * x [M][in] . W^T (the GEMV's arithmetic) for a Linear key, or x [M][Dd] . audio_head[i] for
+ * "audio_head.<i>" (generation.py:79). */
+int csm_read_rows(csm_engine* e, const char* name, int n, const int32_t* rows, float* out);
+int csm_linear(csm_engine* e, const char* name, int M, const float* x, float* y);
 /* Device pointer of the code history [F][B][K] (for on-device Mimi decode) */
 int csm_codes_device_ptr(csm_engine* e, void** dev_ptr);
 int csm_synchronize(csm_engine* e);

@@ -78,8 +78,9 @@ def _batch_multiseg(args, seed=1):
 
 @pytest.mark.parametrize("per_sample,mismatch", [(False, False), (True, False), (False, True)])
 def test_compute_loss_multi_segment_matches_oracle(per_sample, mismatch):
-    """Text rows (and masked-speaker segments) after the first scored row: every utterance is scored
-    on its own, text rows appended to the backbone with their own masks."""
+    """Text rows (and masked-speaker segments) after the first scored row: utterance 0 is scored on
+    its own (text rows appended to the backbone with their own masks); utterance 1 (masked speaker
+    first, one scored segment last) takes the batched path -- both paths in one call."""
     from csm_mlx.models import CSM
     from csm_mlx.scoring import _split, compute_loss
     from oracle.csm_oracle import compute_loss_ref
@@ -88,7 +89,7 @@ def test_compute_loss_multi_segment_matches_oracle(per_sample, mismatch):
     model.load_weights(w)
     batch = _batch_multiseg(args)
     K = args.n_audio_codebooks
-    assert _split(batch["tokens"], batch["masks"], batch["loss_masks"], K)[1] == [False, False]
+    assert _split(batch["tokens"], batch["masks"], batch["loss_masks"], K)[1] == [False, True]
     got = compute_loss(model, batch, per_sample=per_sample, cause_mismatch=mismatch)
     ref = compute_loss_ref(oracle_for(args, w), batch, per_sample=per_sample, cause_mismatch=mismatch)
     assert np.all(np.isfinite(got)) and np.shape(got) == np.shape(ref)
