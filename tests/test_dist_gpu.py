@@ -1,9 +1,11 @@
 """The N-rank path of bench.py on the GPU: ``torch.distributed.run`` with 2
 ranks on this box's one GPU (``--dist-backend gloo``: device = LOCAL_RANK mod #GPUs), each rank
 generating its contiguous shard of the utterances through the real bench step (prefill, frames, Mimi
-decode) and all-gathering codes + PCM.  The gathered result must be byte-identical to one process
-generating every utterance itself.  (The 8-GPU RCCL run is the driver's; the collective is the
-same ``all_gather_into_tensor`` on device tensors.)"""
+decode) and all-gathering codes + PCM.  The gathered codes must be byte-identical to one process
+generating every utterance itself; the PCM agrees to float rounding (the Mimi decode's row count --
+2 vs 4 utterances per launch -- picks different kernel tilings; the transport itself is lossless,
+tests/test_dist_cpu.py).  (The 8-GPU RCCL run is the driver's; the collective is the same
+``all_gather_into_tensor`` on device tensors.)"""
 import os
 import socket
 import subprocess
@@ -45,5 +47,6 @@ def test_two_ranks_gathered_equal_single_process(tmp_path):
     assert len(codes2) == len(codes1) == 4
     for g in range(4):
         assert codes2[g].shape == codes1[g].shape and np.array_equal(codes2[g], codes1[g]), f"utterance {g} codes"
-        assert pcm2[g].tobytes() == pcm1[g].tobytes(), f"utterance {g} PCM"
-        assert len(pcm2[g]) == 1920 * len(codes2[g])
+        assert len(pcm2[g]) == len(pcm1[g]) == 1920 * len(codes2[g])
+        err = float(np.sqrt(np.mean((pcm2[g].astype(np.float64) - pcm1[g]) ** 2)))
+        assert err <= 1e-6, f"utterance {g} PCM RMS difference {err:.3e}"
