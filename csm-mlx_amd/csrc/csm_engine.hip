@@ -132,6 +132,13 @@ struct csm_engine {
   bool fuse_mlp = [] { const char* v = getenv("CSM_FUSE_MLP"); return v && v[0] == '1'; }();
   int acc_rows = 0;  // rows of the fused-MLP accumulators (the fused path runs for M <= acc_rows)
   GemmWs ws;         // split-K slabs + tickets of this engine's MFMA launches (ensure_batch sizes them)
+  // persistent frame decoder (dec_frame.hip) for batch-1 greedy bf16 frames: hand-off granules, tag
+  // epoch, timeout flag; csm_set_option "dec_frame" / CSM_DEC_FRAME=0 turn it off
+  void* df_gbuf = nullptr;
+  unsigned* df_epoch = nullptr;
+  int* df_err = nullptr;
+  bool dec_frame = [] { const char* v = getenv("CSM_DEC_FRAME"); return !(v && v[0] == '0'); }();
+  int df_hw = -1;    // 1: the device can hold one 512-thread workgroup on each of 256 CUs at once
 
   void* balloc(size_t bytes) {
     void* p = nullptr;
@@ -301,6 +308,60 @@ void enqueue_body(csm_engine* e, hipStream_t st) {
   launch_rmsnorm_rows(e->x, e->D, e->bb.norm, e->bb.d.eps, e->D, e->h_last, e->D, B, st, pend, e->acc_rows * e->D);
 }
 
+// The persistent frame decoder runs the whole head of a batch-1 greedy frame when the engine has
+// csm_1b's decoder shapes in bf16 and the folded tables, and the device has the 256 CUs its grid of
+// one workgroup per CU assumes (every workgroup must be resident: the hand-offs spin).
+bool dec_frame_eligible(csm_engine* e) {
+  if (!e->dec_frame || e->B != 1 || e->temperature > 0.f || e->wdt != WDT_BF16 || e->head_wdt != WDT_BF16) return false;
+  const csm_llama_dims& d = e->dec.d;
+  if (d.hidden != 1024 || d.intermediate != 8192 || d.n_heads != 8 || d.n_kv_heads != 2 || d.head_dim != 128 ||
+      d.n_layers != DEC_FRAME_LAYERS || e->bb.d.hidden != 2048 || e->V <= 2048 || e->V > 2051 || e->K > 32 ||
+      e->dec.S_cap != e->K)
+    return false;
+  for (const LayerW& l : e->dec.L)
+    if (!l.wdc) return false;
+  if (!e->proj_tab || !e->fold_proj || !e->use_qkv0_tab || !e->qkv0_built || e->proj_tab_dirty) return false;
+  if (e->df_hw < 0) {
+    hipDeviceProp_t prop;
+    int per_cu = 0;
+    e->df_hw = hipGetDeviceProperties(&prop, e->dev) == hipSuccess && prop.multiProcessorCount == DEC_FRAME_WGS &&
+                       hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dec_frame_kernel_ptr(), DEC_FRAME_THREADS, 0) ==
+                           hipSuccess && per_cu >= 1
+                   ? 1 : 0;
+  }
+  return e->df_hw == 1;
+}
+
+void enqueue_dec_frame(csm_engine* e, hipStream_t st) {
+  DecFrameArgs a{};
+  for (int l = 0; l < DEC_FRAME_LAYERS; ++l) {
+    const LayerW& w = e->dec.L[l];
+    a.wqkv[l] = (const bf16_t*)w.wqkv; a.wo[l] = (const bf16_t*)w.wo; a.wgu[l] = (const bf16_t*)w.wgu;
+    a.wdc[l] = (const bf16_t*)w.wdc; a.n1[l] = w.n1; a.n2[l] = w.n2; a.kc[l] = w.kc; a.vc[l] = w.vc;
+  }
+  a.norm = e->dec.norm; a.rope = e->dec.rope; a.S_cap = e->dec.S_cap; a.eps = e->dec.d.eps;
+  a.c0_head = (const bf16_t*)e->c0_head; a.proj = (const bf16_t*)e->proj; a.audio_head = (const bf16_t*)e->audio_head;
+  a.proj_tab = e->proj_tab; a.qkv0_tab = e->qkv0_tab; a.h_last = e->h_last;
+  a.V = e->V; a.VP = e->Vpad; a.K = e->K; a.codes = e->codes; a.c0_logits = e->c0_logits; a.ci_logits = e->ci_logits;
+  a.gbuf = (unsigned long long*)e->df_gbuf; a.epoch = e->df_epoch; a.err = e->df_err;
+  launch_dec_frame(a, st);
+  AdvanceParams ap{};  // codes are final: EOS test, history, frame counter
+  ap.codes = e->codes; ap.hist = e->hist; ap.F_cap = e->F_cap; ap.B = e->B; ap.K = e->K; ap.V = e->V; ap.done = e->done;
+  ap.n_frames = e->n_frames; ap.frame_ctr = e->frame_ctr;
+  launch_advance(ap, st);
+}
+
+// A hand-off wait of the persistent decoder that timed out leaves its flag raised: report it.
+void check_dec_frame(csm_engine* e) {
+  if (!e->df_err) return;
+  int v = 0;
+  HIPCHK(hipMemcpy(&v, e->df_err, 4, hipMemcpyDeviceToHost));
+  if (v) {
+    HIPCHK(hipMemset(e->df_err, 0, 4));
+    throw CsmError(CSM_ERR_HIP, "persistent frame decoder: a hand-off wait timed out (results of this batch are invalid)");
+  }
+}
+
 // phase 0: the whole head (what the frame graph captures).  phase 1: c0 logits only, stored for the
 // host (logits processors, generation.py:44-49).  phase 2: the rest of the frame from c0 logits the
 // host wrote back: c0 is picked by the sample kernel (arg-max when greedy, published as one partial),
@@ -308,6 +369,10 @@ void enqueue_body(csm_engine* e, hipStream_t st) {
 // phase 3: teacher forcing -- every head stores its logits and the code fed forward is the caller's
 // (e->force [B][K]), as compute_loss feeds the target frame (trainer.py:233-262).
 void enqueue_head_phase(csm_engine* e, hipStream_t st, int phase) {
+  if (phase == 0 && dec_frame_eligible(e)) {
+    enqueue_dec_frame(e, st);
+    return;
+  }
   const int B = e->B, K = e->K, D = e->D, Dd = e->Dd, V = e->V, Vp = e->Vpad;
   const bool greedy = e->temperature <= 0.f && phase != 3;
   const bool c0_sampled = !greedy || phase == 2;  // c0 published by sample_kernel as a single partial
@@ -686,6 +751,9 @@ int csm_engine_create(const csm_dims* dims, int device, int weight_dtype, int ma
     e->tok = (int32_t*)e->alloc(M * (K + 1) * 4);
     e->msk = (uint8_t*)e->alloc(M * (K + 1));
     e->frame_ctr = (int*)e->alloc(16);
+    e->df_gbuf = e->alloc(dec_frame_gbuf_bytes());
+    e->df_epoch = (unsigned*)e->alloc(16);
+    e->df_err = (int*)e->alloc(16);
     (void)Vp;
     (void)B;
     ensure_batch(e.get(), max_batch);
@@ -986,6 +1054,7 @@ int csm_run_frames(csm_engine* e, int nframes, int* all_done) {
       std::vector<uint8_t> d(e->B);
       HIPCHK(hipMemcpyAsync(d.data(), e->done, e->B, hipMemcpyDeviceToHost, e->st));
       HIPCHK(hipStreamSynchronize(e->st));
+      check_dec_frame(e);
       int all = 1;
       for (auto v : d) all &= (v != 0);
       *all_done = all;
@@ -1089,6 +1158,7 @@ int csm_read_codes(csm_engine* e, int32_t* hist, int32_t* n_frames, uint8_t* don
   CSM_TRY {
     HIPCHK(hipSetDevice(e->dev));
     HIPCHK(hipStreamSynchronize(e->st));
+    check_dec_frame(e);
     if (hist)
       HIPCHK(hipMemcpy(hist, e->hist, (size_t)e->frames_run * e->B * e->K * 4, hipMemcpyDeviceToHost));
     if (n_frames) HIPCHK(hipMemcpy(n_frames, e->n_frames, e->B * 4, hipMemcpyDeviceToHost));
@@ -1270,6 +1340,10 @@ int csm_set_option(csm_engine* e, const char* key, int value) {
       e->use_qkv0_tab = value != 0;
       if (e->use_qkv0_tab && !e->qkv0_built) e->proj_tab_dirty = true;  // built at the next csm_begin
     }
+    else if (k == "dec_frame") {
+      if (!e) throw CsmError(CSM_ERR_ARG, "dec_frame needs an engine");
+      e->dec_frame = value != 0;
+    }
     else if (k == "fuse_mlp") {
       if (!e) throw CsmError(CSM_ERR_ARG, "fuse_mlp needs an engine");
       e->fuse_mlp = value != 0;
@@ -1284,6 +1358,7 @@ int csm_synchronize(csm_engine* e) {
   CSM_TRY {
     HIPCHK(hipSetDevice(e->dev));
     HIPCHK(hipStreamSynchronize(e->st));
+    check_dec_frame(e);
     HIPCHK(hipGetLastError());
   }
   CSM_CATCH

@@ -319,3 +319,38 @@ void gemm_ws_free(GemmWs& ws);
 void launch_gather_rows(const GemvParams& p, int wdt, hipStream_t st);
 // arg-max partial slots per row written by launch_gemv for this shape / dtype / row count
 int gemv_partials(int N, int K, int M, int wdt);
+
+// ---- persistent frame decoder (dec_frame.hip): c0 head + 31 depth-decoder steps of one greedy batch-1
+// frame in one launch of 256 x 512 threads (one workgroup per CU), csm_1b decoder shapes, bf16 weights
+constexpr int DEC_FRAME_LAYERS = 4;
+struct DecFrameArgs {
+  const bf16_t* wqkv[DEC_FRAME_LAYERS];
+  const bf16_t* wo[DEC_FRAME_LAYERS];
+  const bf16_t* wgu[DEC_FRAME_LAYERS];   // gate/up rows interleaved
+  const bf16_t* wdc[DEC_FRAME_LAYERS];   // down_proj chunk-major [F/16][D][16]
+  const float* n1[DEC_FRAME_LAYERS];
+  const float* n2[DEC_FRAME_LAYERS];
+  const float* norm;                     // decoder final norm
+  const float* rope;                     // [S_cap][HD/2][2]
+  float* kc[DEC_FRAME_LAYERS];           // [Hkv][S_cap][HD] of utterance 0
+  float* vc[DEC_FRAME_LAYERS];
+  int S_cap;
+  float eps;
+  const bf16_t* c0_head;                 // [VP][2048]
+  const bf16_t* proj;                    // [1024][2048]
+  const bf16_t* audio_head;              // [K-1][VP][1024]
+  const float* proj_tab;                 // [K-1][V][1024]
+  const float* qkv0_tab;                 // [K-1][V][1536]
+  const float* h_last;                   // [2048]
+  int V, VP, K;
+  int* codes;                            // [K] of utterance 0
+  float* c0_logits;                      // [VP] (debug / parity taps, as the launch path stores them)
+  float* ci_logits;                      // [K-1][VP]
+  unsigned long long* gbuf;              // hand-off granules (dec_frame_gbuf_bytes)
+  unsigned* epoch;                       // hand-off tag base (advanced by every frame)
+  int* err;                              // raised when a hand-off wait times out
+};
+size_t dec_frame_gbuf_bytes();
+constexpr int DEC_FRAME_WGS = 256, DEC_FRAME_THREADS = 512;
+void launch_dec_frame(const DecFrameArgs& p, hipStream_t st);
+const void* dec_frame_kernel_ptr();  // for the occupancy query

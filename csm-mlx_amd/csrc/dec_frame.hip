@@ -1,0 +1,653 @@
+// Persistent frame decoder: codebook0_head + the 31 depth-decoder steps of one frame
+// (/root/reference/csm_mlx/generation.py:42-90) in ONE launch, batch 1, greedy, bf16 weights.
+//
+// Why: at batch 1 the depth decoder is a chain of 31 x (4 layers x 5 projections + attention + head)
+// dependent launches of 2-34 MB each; every launch pays a kernel boundary plus its own ramp and
+// drain, ~3.5 us apiece over ~650 launches per frame, while the weight bytes themselves stream in
+// far less.  Here every CU keeps one workgroup for the whole frame, owns a fixed slice of every
+// matrix, and streams its slices into registers one or two hand-offs AHEAD of use (the weights do not
+// depend on the activations), so the weight stream overlaps the dependency latency.
+//
+// Work split (NWG = 256 workgroups = one per CU, 512 threads = 8 waves each):
+//   QKV    1536 rows: 6 per WG (RoPE pairs stay inside a WG)        -> all-gather q|k|v  (E1)
+//   attention: every WG computes all 8 heads redundantly (<= 32 keys) -> no hand-off
+//   o_proj 1024 rows: 4 per WG, + residual                           -> all-gather x      (E3)
+//   gate/up 16384 interleaved rows: 64 per WG -> h[32 columns];
+//   down   split-K: WG w multiplies its 32 columns of W_down (chunk-major copy, [F/16][D][16])
+//          by its h -> 1024 partials                                  -> reduce-scatter   (E4)
+//          WG w sums the 256 partials of rows 4w..4w+3 in a fixed order, + residual
+//                                                                      -> all-gather x      (E5)
+//   heads  2051 rows: 8 per WG (+1 for WGs 0-2), arg-max partial       -> all-gather keys   (E6)
+// Layer 0 of steps >= 2 reads q|k|v (RoPE'd) and the input row from the folded tables built at
+// csm_begin (proj_tab / qkv0_tab), so it has no QKV hand-off.  16 hand-offs per step.
+//
+// Hand-offs are data-tagged granules (MI355X_MICROARCH.md hand-off price list, "Granule"): each value
+// travels as one naturally aligned 8-byte {float bits, tag} written by ONE agent-scope relaxed store
+// (sc1) and read with agent-scope relaxed loads (sc1) until the tag matches; tag = epoch + hand-off
+// index (epoch advances by the frame's hand-off count, never reused).  Buffers alternate by hand-off
+// parity: a WG can only overwrite a buffer after every WG has published the next hand-off, i.e. after
+// every WG finished reading the previous use.  Every spin is bounded: on timeout a WG raises the
+// error word and stops waiting (results garbage, the host raises) -- the grid always drains.
+//
+// Arithmetic: fp32 accumulation of bf16 weights x fp32 activations, RMSNorm as the oracle
+// (x * rsqrt(mean(x^2) + eps) * w), RoPE on interleaved pairs from the cos/sin table, softmax with
+// max subtraction, reductions in fixed orders (deterministic run to run).
+#include "csm_kernels.h"
+
+namespace {
+
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+typedef unsigned long long u64;
+
+constexpr int NWG = 256, NT = 512;
+constexpr int D = 1024, F = 8192, HQ = 8, HKV = 2, HD = 128, NL = DEC_FRAME_LAYERS, DB = 2048;
+constexpr int QKV = (HQ + 2 * HKV) * HD;  // 1536
+constexpr int MAXM = 2;                   // rows per step (step 1: [h_last, E_a[c0]])
+constexpr unsigned SPIN_LIMIT = 1u << 22; // ~0.1 s of s_sleep per hand-off before declaring failure
+
+__device__ __forceinline__ u64 gload(const u64* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void gput(u64* p, float v, unsigned tag) {
+  __hip_atomic_store(p, ((u64)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void gput_u(u64* p, unsigned v, unsigned tag) {
+  __hip_atomic_store(p, ((u64)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void sc1_store_f(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// 16-B agent-coherent (sc1) load at byte offset `off` of a buffer of `bytes` bytes
+__device__ __forceinline__ u32x4_t sc1_load16(const void* base, int off, int bytes) {
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, bytes, 0x00020000);
+  return __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16));
+}
+
+// 8 products of one 16-B bf16 weight chunk with 8 consecutive fp32 activations (fixed order)
+__device__ __forceinline__ float dot8(const u32x4_t w, const float* x) {
+  const float4 a = *reinterpret_cast<const float4*>(x), b = *reinterpret_cast<const float4*>(x + 4);
+  float s = bf16_lo(w.x) * a.x;
+  s = fmaf(bf16_hi(w.x), a.y, s);
+  s = fmaf(bf16_lo(w.y), a.z, s);
+  s = fmaf(bf16_hi(w.y), a.w, s);
+  s = fmaf(bf16_lo(w.z), b.x, s);
+  s = fmaf(bf16_hi(w.z), b.y, s);
+  s = fmaf(bf16_lo(w.w), b.z, s);
+  s = fmaf(bf16_hi(w.w), b.w, s);
+  return s;
+}
+
+// the same chunk against two activation rows (every weight converted once, used twice: no
+// loop-invariant conversions for the compiler to hoist out of a row loop)
+__device__ __forceinline__ void dot8x2(const u32x4_t w, const float* x0, const float* x1, float& s0, float& s1) {
+  const float4 a0 = *reinterpret_cast<const float4*>(x0), b0 = *reinterpret_cast<const float4*>(x0 + 4);
+  const float4 a1 = *reinterpret_cast<const float4*>(x1), b1 = *reinterpret_cast<const float4*>(x1 + 4);
+  float t;
+  t = bf16_lo(w.x); s0 = fmaf(t, a0.x, s0); s1 = fmaf(t, a1.x, s1);
+  t = bf16_hi(w.x); s0 = fmaf(t, a0.y, s0); s1 = fmaf(t, a1.y, s1);
+  t = bf16_lo(w.y); s0 = fmaf(t, a0.z, s0); s1 = fmaf(t, a1.z, s1);
+  t = bf16_hi(w.y); s0 = fmaf(t, a0.w, s0); s1 = fmaf(t, a1.w, s1);
+  t = bf16_lo(w.z); s0 = fmaf(t, b0.x, s0); s1 = fmaf(t, b1.x, s1);
+  t = bf16_hi(w.z); s0 = fmaf(t, b0.y, s0); s1 = fmaf(t, b1.y, s1);
+  t = bf16_lo(w.w); s0 = fmaf(t, b0.z, s0); s1 = fmaf(t, b1.z, s1);
+  t = bf16_hi(w.w); s0 = fmaf(t, b0.w, s0); s1 = fmaf(t, b1.w, s1);
+}
+
+__device__ __forceinline__ u32x4_t wload(const bf16_t* p) { return *reinterpret_cast<const u32x4_t*>(p); }
+
+// 16-B weight load as a raw buffer load: the matrix base rides in the (uniform) descriptor, the
+// lane-dependent part in ONE voffset register shared by every layer and row, the row / chunk step in
+// the scalar offset -- so per-layer weight addresses are not VGPR pairs the compiler keeps live
+// across the frame loop.
+__device__ __forceinline__ u32x4_t bload(const void* base, int voff, int soff) {
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+  return __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
+}
+
+struct Lds {
+  float x[MAXM][D];        // residual rows
+  float xn[MAXM][DB];      // normed x * norm weight (GEMV input); h_last at frame start
+  float qkv[MAXM][QKV];    // gathered q | k | v (RoPE'd)
+  float att[MAXM][D];      // attention output
+  float qs[HQ][HD];        // scaled query of one row per head
+  float hb[MAXM][32];      // this WG's h columns
+  float red[4 * MAXM][256];// reduce-scatter staging [row][producer]
+  float wsum[8][MAXM * 8]; // per-wave partial dots
+  float Ks[HKV][32][HD + 4];// cached keys of this layer (rows padded: conflict-free row-parallel reads)
+  float Vs[HKV][32][HD];    // cached values
+  int code;                // last arg-max
+  int flag;
+};
+
+}  // namespace
+
+namespace {
+
+// Granule buffer regions (u64 offsets), each double-buffered by hand-off parity.
+constexpr size_t G_X = 0;                                  // [2][MAXM][D] x slices
+constexpr size_t G_QKV = G_X + 2 * MAXM * D;               // [2][MAXM][QKV]
+constexpr size_t G_PART = G_QKV + 2 * MAXM * QKV;          // [2][NWG][MAXM][D] down partials
+constexpr size_t G_ARG = G_PART + (size_t)2 * NWG * MAXM * D;  // [2][NWG][2] arg-max keys
+constexpr size_t G_TOTAL = G_ARG + 2 * NWG * 2;
+
+// threadIdx.x through an opaque move: lane-dependent addresses derived from it inside the frame loop
+// are recomputed per iteration instead of being hoisted out of the loop and held (spilled) for the
+// whole frame.
+__device__ __forceinline__ int opaque_tid() {
+  int t;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"((int)threadIdx.x));
+  return t;
+}
+
+struct Ctx {
+  const DecFrameArgs& p;
+  Lds& L;
+  int w, tid, lane, wave;
+  unsigned tag0;
+  int e;  // hand-off counter
+  __device__ void refresh() {
+    tid = opaque_tid();
+    lane = tid & 63;
+    wave = tid >> 6;
+  }
+  __device__ unsigned tag() const { return tag0 + (unsigned)e; }
+  __device__ u64* buf(size_t region, size_t per) const { return p.gbuf + region + (size_t)(e & 1) * per; }
+};
+
+// Wait until granules [0, n) of buf carry `tag`; values -> out (LDS).  Threads take granules
+// tid, tid + NT, ... (at most GPT each), issue every load first, then re-poll stale ones.
+template <int GPT>
+__device__ __forceinline__ void gather(Ctx& c, const u64* buf, int n, float* out) {
+  const unsigned tag = c.tag();
+  u64 g[GPT];
+#pragma unroll
+  for (int u = 0; u < GPT; ++u) {
+    const int i = c.tid + u * NT;
+    g[u] = i < n ? gload(buf + i) : ((u64)tag << 32);
+  }
+  for (unsigned spin = 0;; ++spin) {
+    bool ok = true;
+#pragma unroll
+    for (int u = 0; u < GPT; ++u) ok &= (unsigned)(g[u] >> 32) == tag;
+    if (ok) break;
+    if (spin >= SPIN_LIMIT || ((spin & 255) == 255 && __hip_atomic_load(c.p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+      __hip_atomic_store(c.p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+    for (int u = 0; u < GPT; ++u) {
+      const int i = c.tid + u * NT;
+      if (i < n && (unsigned)(g[u] >> 32) != tag) g[u] = gload(buf + i);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < GPT; ++u) {
+    const int i = c.tid + u * NT;
+    if (i < n) out[i] = __uint_as_float((unsigned)g[u]);
+  }
+  __syncthreads();
+}
+
+// xn[m][k] = x[m][k] * rsqrt(mean(x^2) + eps) * nw[k] for rows m < M (every WG computes the same)
+__device__ __forceinline__ void rms_rows(Ctx& c, int M, const float* nw, int m0 = 0) {
+  // sum of squares: wave m sums row m in a fixed order
+  if (c.wave < M) {
+    const float* x = c.L.x[m0 + c.wave];
+    float s = 0.f;
+    for (int k = c.lane; k < D; k += 64) s = fmaf(x[k], x[k], s);
+    s = wave_sum(s);
+    if (c.lane == 0) c.L.wsum[0][c.wave] = s;
+  }
+  __syncthreads();
+  for (int i = c.tid; i < M * D; i += NT) {
+    const int m = i / D, k = i % D;
+    const float r = rsqrtf(c.L.wsum[0][m] / (float)D + c.p.eps);
+    c.L.xn[m][k] = c.L.x[m0 + m][k] * r * nw[k];
+  }
+  __syncthreads();
+}
+
+// ---- weight slices held in registers (issued ahead of use)
+struct WQkv { u32x4_t a, b; };      // waves 0..5: row 6w+wave, chunks lane / lane+64
+struct WO { u32x4_t a; };            // row 4w + wave/2, chunk (wave&1)*64 + lane
+struct WGu { u32x4_t a[8][2]; };     // rows 64w + 8*wave + r, chunks lane / lane+64
+struct WDn { u32x4_t a[2][2][2]; };  // [row t / t+512][chunk 2w+q][16-B half]
+struct WHd { u32x4_t a[2]; u32x4_t x[2]; };  // head row 8w+wave (+ row 2048+w for wave 0, w < 3)
+
+__device__ __forceinline__ void load_qkv(Ctx& c, int l, WQkv& r) {
+  if (c.wave < 6) {
+    const bf16_t* row = c.p.wqkv[l] + (size_t)(6 * c.w) * D;  // uniform
+    const int v = (c.wave * D + 8 * c.lane) * 2;
+    r.a = bload(row, v, 0);
+    r.b = bload(row, v, 1024);
+  }
+}
+__device__ __forceinline__ void load_o(Ctx& c, int l, WO& r) {
+  const bf16_t* row = c.p.wo[l] + (size_t)(4 * c.w) * D;
+  r.a = bload(row, ((c.wave >> 1) * D + 8 * ((c.wave & 1) * 64 + c.lane)) * 2, 0);
+}
+__device__ __forceinline__ void load_gu(Ctx& c, int l, WGu& r) {
+  const bf16_t* base = c.p.wgu[l] + (size_t)(64 * c.w) * D;
+  const int v = (8 * c.wave * D + 8 * c.lane) * 2;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    r.a[i][0] = bload(base, v, i * D * 2);
+    r.a[i][1] = bload(base, v, i * D * 2 + 1024);
+  }
+}
+__device__ __forceinline__ void load_dn(Ctx& c, int l, WDn& r) {
+  const bf16_t* base = c.p.wdc[l] + (size_t)(2 * c.w) * D * 16;
+  const int v = c.tid * 16 * 2;
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int so = (q * D * 16 + 512 * s * 16) * 2;
+      r.a[s][q][0] = bload(base, v, so);
+      r.a[s][q][1] = bload(base, v, so + 16);
+    }
+}
+__device__ __forceinline__ void load_head(Ctx& c, const bf16_t* W, int K, WHd& r) {
+  // K = 1024 (ci heads): 128 chunks per row -> 2 per lane
+  const bf16_t* base = W + (size_t)(8 * c.w) * K;
+  const int v = (c.wave * K + 8 * c.lane) * 2;
+  r.a[0] = bload(base, v, 0);
+  r.a[1] = bload(base, v, 1024);
+  if (c.wave == 0 && c.w < 3) {
+    const bf16_t* xr = W + (size_t)(2048 + c.w) * K;
+    r.x[0] = bload(xr, 16 * c.lane, 0);
+    r.x[1] = bload(xr, 16 * c.lane, 1024);
+  }
+}
+
+// ---- phases
+// QKV rows of this WG for M rows at positions pos0..pos0+M-1 (RoPE), published to E1.
+__device__ __forceinline__ void phase_qkv(Ctx& c, int M, int pos0, const WQkv& W) {
+  if (c.wave < 6) {  // both row slots at once (row 1 is junk when M == 1)
+    float s0 = 0.f, s1 = 0.f;
+    dot8x2(W.a, c.L.xn[0] + 8 * c.lane, c.L.xn[1] + 8 * c.lane, s0, s1);
+    dot8x2(W.b, c.L.xn[0] + 8 * (c.lane + 64), c.L.xn[1] + 8 * (c.lane + 64), s0, s1);
+    s0 = wave_sum(s0);
+    s1 = wave_sum(s1);
+    if (c.lane == 0) { c.L.wsum[c.wave][0] = s0; c.L.wsum[c.wave][1] = s1; }
+  }
+  __syncthreads();
+  u64* g = c.buf(G_QKV, MAXM * QKV);
+  if (c.tid < 3 * M) {  // RoPE pair j of row m: rows n, n+1 = 6w + 2j, +1
+    const int m = c.tid / 3, j = c.tid % 3, n = 6 * c.w + 2 * j;
+    float a = c.L.wsum[2 * j][m], b = c.L.wsum[2 * j + 1][m];
+    if (n < (HQ + HKV) * HD) {
+      const int d = n % HD;
+      const float2 cs = *reinterpret_cast<const float2*>(c.p.rope + ((size_t)(pos0 + m) * (HD / 2) + d / 2) * 2);
+      const float y0 = a * cs.x - b * cs.y, y1 = b * cs.x + a * cs.y;
+      a = y0;
+      b = y1;
+    }
+    gput(g + (size_t)m * QKV + n, a, c.tag());
+    gput(g + (size_t)m * QKV + n + 1, b, c.tag());
+  }
+}
+
+// K / V rows 0..pos0-1 of this layer's cache (written by WG 0 in earlier steps, write-through) are
+// fetched with sc1 loads into registers BEFORE the hand-off wait that precedes attention, and stored
+// to LDS after it: chunk idx = tid + 512 u -> (kv head idx >> 10, key (idx >> 5) & 31, 16-B chunk idx & 31).
+struct KvRegs { u32x4_t k[4], v[4]; };
+__device__ __forceinline__ void kv_issue(Ctx& c, int layer, int pos0, KvRegs& r) {
+  const int bytes = HKV * c.p.S_cap * HD * 4;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int idx = c.tid + 512 * u, g = idx >> 10, j = (idx >> 5) & 31, q = idx & 31;
+    if (j < pos0) {
+      const int off = ((g * c.p.S_cap + j) * HD + 4 * q) * 4;
+      r.k[u] = sc1_load16(c.p.kc[layer], off, bytes);
+      r.v[u] = sc1_load16(c.p.vc[layer], off, bytes);
+    }
+  }
+}
+__device__ __forceinline__ void kv_store(Ctx& c, int pos0, const KvRegs& r) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int idx = c.tid + 512 * u, g = idx >> 10, j = (idx >> 5) & 31, q = idx & 31;
+    if (j < pos0) {
+      *reinterpret_cast<u32x4_t*>(&c.L.Ks[g][j][4 * q]) = r.k[u];
+      *reinterpret_cast<u32x4_t*>(&c.L.Vs[g][j][4 * q]) = r.v[u];
+    }
+  }
+}
+
+// Attention of rows m < M (positions pos0 + m) over keys 0..pos0+m: keys < pos0 from c.L.Ks / Vs,
+// keys pos0.. from c.L.qkv.  Every WG computes all heads (wave = head), as attn_short_head: lane =
+// (key kj = lane & 31, half hh of the head dims), scores from two half dots added by one shuffle,
+// max-subtracted softmax, P.V in key order.  WG 0 also appends the new K/V rows to the cache
+// (write-through stores, drained) for later steps.
+__device__ __forceinline__ void phase_attn(Ctx& c, int M, int pos0, int layer) {
+  const int h = c.wave, g = h / (HQ / HKV);
+  const float scale = 0.08838834764831845f;  // 1 / sqrt(128)
+  const int kj = c.lane & 31, hh = c.lane >> 5;
+  for (int m = 0; m < M; ++m) {
+    const int pos = pos0 + m, n = pos + 1;
+    for (int d = c.lane; d < HD; d += 64) c.L.qs[h][d] = c.L.qkv[m][h * HD + d] * scale;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    float part = 0.f;
+    if (kj < n) {
+      const float* krow = kj < pos0 ? c.L.Ks[g][kj] : &c.L.qkv[kj - pos0][HQ * HD + g * HD];
+      const float4* k4 = reinterpret_cast<const float4*>(krow + hh * (HD / 2));
+      const float4* q4 = reinterpret_cast<const float4*>(c.L.qs[h] + hh * (HD / 2));
+      float d0 = 0.f, d1 = 0.f, d2 = 0.f, d3 = 0.f;
+#pragma unroll
+      for (int d4 = 0; d4 < HD / 8; ++d4) {
+        const float4 a = k4[d4], q = q4[d4];
+        d0 = fmaf(q.x, a.x, d0);
+        d1 = fmaf(q.y, a.y, d1);
+        d2 = fmaf(q.z, a.z, d2);
+        d3 = fmaf(q.w, a.w, d3);
+      }
+      part = (d0 + d1) + (d2 + d3);
+    }
+    const float other = __shfl_xor(part, 32, 64);
+    float s = hh == 0 ? part + other : other + part;
+    if (kj >= n) s = -INFINITY;
+    const float mx = wave_max(s);
+    const float pj = kj < n ? expf(s - mx) : 0.f;
+    const float l_run = wave_sum(hh == 0 ? pj : 0.f);
+    const int pji = __float_as_int(pj);
+    float o0 = 0.f, o1 = 0.f;
+#pragma unroll 4
+    for (int j = 0; j < n; ++j) {
+      const float pb = __int_as_float(__builtin_amdgcn_readlane(pji, j));
+      const float* vr = j < pos0 ? c.L.Vs[g][j] : &c.L.qkv[j - pos0][(HQ + HKV) * HD + g * HD];
+      o0 = fmaf(pb, vr[c.lane], o0);
+      o1 = fmaf(pb, vr[c.lane + 64], o1);
+    }
+    const float inv = 1.f / l_run;
+    c.L.att[m][h * HD + c.lane] = o0 * inv;
+    c.L.att[m][h * HD + c.lane + 64] = o1 * inv;
+  }
+  if (c.w == 0) {  // the new K / V rows -> cache (write-through; read by later steps after a hand-off)
+    for (int i = c.tid; i < M * HKV * HD; i += NT) {
+      const int m = i / (HKV * HD), r = i % (HKV * HD), gg = r / HD, d = r % HD;
+      const size_t off = ((size_t)gg * c.p.S_cap + pos0 + m) * HD + d;
+      sc1_store_f(c.p.kc[layer] + off, c.L.qkv[m][HQ * HD + r]);
+      sc1_store_f(c.p.vc[layer] + off, c.L.qkv[m][(HQ + HKV) * HD + r]);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+
+// o_proj rows 4w..4w+3 (+ residual) -> E3 granules
+__device__ __forceinline__ void phase_o(Ctx& c, int M, const WO& W) {
+  {
+    const int k = 8 * ((c.wave & 1) * 64 + c.lane);
+    float s0 = 0.f, s1 = 0.f;
+    dot8x2(W.a, c.L.att[0] + k, c.L.att[1] + k, s0, s1);
+    s0 = wave_sum(s0);
+    s1 = wave_sum(s1);
+    if (c.lane == 0) { c.L.wsum[c.wave][0] = s0; c.L.wsum[c.wave][1] = s1; }
+  }
+  __syncthreads();
+  if (c.tid < 4 * M) {
+    const int m = c.tid / 4, r = c.tid % 4, n = 4 * c.w + r;
+    const float o = c.L.wsum[2 * r][m] + c.L.wsum[2 * r + 1][m];
+    gput(c.buf(G_X, MAXM * D) + (size_t)m * D + n, c.L.x[m][n] + o, c.tag());
+  }
+}
+
+// gate/up (64 rows -> h[32]) and the split-K down partials of this WG's columns -> E4 granules
+__device__ __forceinline__ void phase_mlp(Ctx& c, int M, const WGu& G, const WDn& Wd) {
+  {
+    float s[8][2];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      s[i][0] = 0.f;
+      s[i][1] = 0.f;
+      dot8x2(G.a[i][0], c.L.xn[0] + 8 * c.lane, c.L.xn[1] + 8 * c.lane, s[i][0], s[i][1]);
+      dot8x2(G.a[i][1], c.L.xn[0] + 8 * (c.lane + 64), c.L.xn[1] + 8 * (c.lane + 64), s[i][0], s[i][1]);
+    }
+#pragma unroll
+    for (int m = 0; m < MAXM; ++m) {
+      if (m >= M) break;
+      float t[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) t[i] = wave_sum(s[i][m]);
+      if (c.lane < 4) {  // pair j = 4*wave + lane: rows 2j (gate), 2j+1 (up) of the WG slice
+        const float gt = c.lane == 0 ? t[0] : (c.lane == 1 ? t[2] : (c.lane == 2 ? t[4] : t[6]));
+        const float up = c.lane == 0 ? t[1] : (c.lane == 1 ? t[3] : (c.lane == 2 ? t[5] : t[7]));
+        c.L.hb[m][4 * c.wave + c.lane] = silu_f(gt) * up;
+      }
+    }
+  }
+  __syncthreads();
+  u64* g = c.buf(G_PART, (size_t)NWG * MAXM * D) + (size_t)c.w * MAXM * D;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      dot8x2(Wd.a[s][q][0], c.L.hb[0] + 16 * q, c.L.hb[1] + 16 * q, a0, a1);
+      dot8x2(Wd.a[s][q][1], c.L.hb[0] + 16 * q + 8, c.L.hb[1] + 16 * q + 8, a0, a1);
+    }
+    gput(g + c.tid + 512 * s, a0, c.tag());
+    if (M > 1) gput(g + D + c.tid + 512 * s, a1, c.tag());
+  }
+}
+
+// Reduce-scatter: rows 4w..4w+3 of every producer's partials (fixed order), + residual -> E5
+__device__ __forceinline__ void phase_reduce(Ctx& c, int M) {
+  const unsigned tag = c.tag();
+  const u64* g = c.buf(G_PART, (size_t)NWG * MAXM * D);
+  const int v = c.tid >> 1, half = c.tid & 1;
+  u64 q[MAXM][2];
+#pragma unroll
+  for (int m = 0; m < MAXM; ++m)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      q[m][u] = m < M ? gload(g + ((size_t)v * MAXM + m) * D + 4 * c.w + 2 * half + u) : ((u64)tag << 32);
+  for (unsigned spin = 0;; ++spin) {
+    bool ok = true;
+#pragma unroll
+    for (int m = 0; m < MAXM; ++m) ok &= ((unsigned)(q[m][0] >> 32) == tag) & ((unsigned)(q[m][1] >> 32) == tag);
+    if (ok) break;
+    if (spin >= SPIN_LIMIT || ((spin & 255) == 255 && __hip_atomic_load(c.p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+      __hip_atomic_store(c.p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+    for (int m = 0; m < MAXM; ++m)
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        if (m < M && (unsigned)(q[m][u] >> 32) != tag) q[m][u] = gload(g + ((size_t)v * MAXM + m) * D + 4 * c.w + 2 * half + u);
+  }
+#pragma unroll
+  for (int m = 0; m < MAXM; ++m)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      if (m < M) c.L.red[4 * m + 2 * half + u][v] = __uint_as_float((unsigned)q[m][u]);
+  __syncthreads();
+  ++c.e;  // the x hand-off that follows
+  if (c.wave < 4 * M) {
+    const float* r = c.L.red[c.wave];
+    float s = ((r[4 * c.lane] + r[4 * c.lane + 1]) + r[4 * c.lane + 2]) + r[4 * c.lane + 3];
+    s = wave_sum(s);
+    if (c.lane == 0) {
+      const int m = c.wave / 4, n = 4 * c.w + c.wave % 4;
+      gput(c.buf(G_X, MAXM * D) + (size_t)m * D + n, c.L.x[m][n] + s, c.tag());
+    }
+  }
+}
+
+// Head rows of this WG on row xn[0] (K = 1024 or 2048) -> arg-max key -> E6 granules (hi, lo words)
+template <int KH>
+__device__ __forceinline__ void phase_head(Ctx& c, const bf16_t* W, int n_valid, const u32x4_t (&wa)[KH / 512],
+                                           const u32x4_t (&wx)[KH / 512], float* logits) {
+  constexpr int CPL = KH / 512;  // chunks per lane
+  const int row = 8 * c.w + c.wave;
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) s += dot8(wa[i], c.L.xn[0] + 8 * (c.lane + 64 * i));
+  s = wave_sum(s);
+  unsigned long long best = row < n_valid ? pack_argmax(s, row) : 0ull;
+  if (c.lane == 0 && row < n_valid) logits[row] = s;
+  if (c.wave == 0 && c.w < 3) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < CPL; ++i) t += dot8(wx[i], c.L.xn[0] + 8 * (c.lane + 64 * i));
+    t = wave_sum(t);
+    const int xr = 2048 + c.w;
+    const unsigned long long k2 = xr < n_valid ? pack_argmax(t, xr) : 0ull;
+    best = k2 > best ? k2 : best;
+    if (c.lane == 0 && xr < n_valid) logits[xr] = t;
+  }
+  if (c.lane == 0) reinterpret_cast<unsigned long long*>(c.L.wsum)[c.wave] = best;
+  __syncthreads();
+  if (c.tid == 0) {
+    const unsigned long long* k = reinterpret_cast<const unsigned long long*>(c.L.wsum);
+    unsigned long long b = k[0];
+    for (int i = 1; i < 8; ++i) b = k[i] > b ? k[i] : b;
+    u64* g = c.buf(G_ARG, NWG * 2) + 2 * c.w;
+    gput_u(g, (unsigned)(b >> 32), c.tag());
+    gput_u(g + 1, (unsigned)b, c.tag());
+  }
+  __syncthreads();
+}
+
+// Gather the 256 arg-max keys -> code (every WG identical)
+__device__ __forceinline__ int gather_code(Ctx& c, int V) {
+  gather<1>(c, c.buf(G_ARG, NWG * 2), NWG * 2, &c.L.red[0][0]);
+  if (c.wave == 0) {
+    const unsigned* u = reinterpret_cast<const unsigned*>(&c.L.red[0][0]);
+    unsigned long long b = 0;
+    for (int i = c.lane; i < NWG; i += 64) {
+      const unsigned long long k = ((unsigned long long)u[2 * i] << 32) | u[2 * i + 1];
+      b = k > b ? k : b;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const unsigned long long t = __shfl_xor(b, o, 64);
+      b = t > b ? t : b;
+    }
+    if (c.lane == 0) c.L.code = min(max(unpack_argmax(b), 0), V - 1);
+  }
+  __syncthreads();
+  return c.L.code;
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(NT, 1) void dec_frame_kernel(DecFrameArgs p) {
+  __shared__ __attribute__((aligned(16))) Lds L;
+  Ctx c{p, L, (int)blockIdx.x, (int)threadIdx.x, (int)(threadIdx.x & 63), (int)(threadIdx.x >> 6), 0u, 0};
+  c.tag0 = __hip_atomic_load(p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  // ---- frame start: codebook0_head (K = 2048, 8 rows per WG + 1 for WGs 0-2) and the projection of
+  // h_last (rows 4w..4w+3) for decoder step 1, both published in one hand-off
+  u32x4_t c0a[4], c0x[4], pa[2];
+  {
+    const bf16_t* row = p.c0_head + (size_t)(8 * c.w) * DB;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) c0a[i] = bload(row, (c.wave * DB + 8 * c.lane) * 2, i * 1024);
+    if (c.wave == 0 && c.w < 3) {
+      const bf16_t* xr = p.c0_head + (size_t)(2048 + c.w) * DB;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) c0x[i] = bload(xr, 16 * c.lane, i * 1024);
+    }
+    const bf16_t* pr = p.proj + (size_t)(4 * c.w) * DB;
+    const int pv = ((c.wave >> 1) * DB + 8 * 128 * (c.wave & 1) + 8 * c.lane) * 2;
+    pa[0] = bload(pr, pv, 0);
+    pa[1] = bload(pr, pv, 1024);
+  }
+  WQkv wq;
+  WO wo;
+  WGu wg;
+  WDn wd;
+  load_qkv(c, 0, wq);
+  load_o(c, 0, wo);
+  for (int k = c.tid; k < DB; k += NT) L.xn[0][k] = p.h_last[k];
+  __syncthreads();
+  phase_head<DB>(c, p.c0_head, p.V, c0a, c0x, p.c0_logits);  // -> G_ARG (hand-off 0)
+  {
+    float s = dot8(pa[0], L.xn[0] + 8 * (128 * (c.wave & 1) + c.lane)) + dot8(pa[1], L.xn[0] + 8 * (128 * (c.wave & 1) + c.lane + 64));
+    s = wave_sum(s);
+    if (c.lane == 0) L.wsum[c.wave][0] = s;
+    __syncthreads();
+    if (c.tid < 4) gput(c.buf(G_X, MAXM * D) + 4 * c.w + c.tid, L.wsum[2 * c.tid][0] + L.wsum[2 * c.tid + 1][0], c.tag());
+  }
+  const int c0 = gather_code(c, p.V);
+  gather<2>(c, c.buf(G_X, MAXM * D), D, L.x[0]);  // x row 0 = projection(h_last)
+  ++c.e;
+  if (c.w == 0 && c.tid == 0) p.codes[0] = c0;
+  // x row 1 = projection(E_a[c0]) from the folded table (bit-identical to the projection GEMV)
+  for (int k = c.tid; k < D; k += NT) L.x[1][k] = p.proj_tab[(size_t)c0 * D + k];
+  __syncthreads();
+
+  // Register prefetch schedule (what is in flight during each hand-off wait):
+  //   E1 (q|k|v): the cached K/V rows       E3 (x): this layer's gate/up + down slices, next layer's QKV / o
+  //   E4 / E5 of the last layer: this step's head rows, the next step's o / QKV
+  WHd wh;
+  for (int step = 1; step < p.K; ++step) {
+    const int M = step == 1 ? 2 : 1;
+    const int pos0 = step == 1 ? 0 : step;
+    for (int l = 0; l < NL; ++l) {
+      c.refresh();
+      {
+        KvRegs kv;
+        kv_issue(c, l, pos0, kv);
+        if (l == 0 && step > 1) {
+          // layer 0 from the folded table: q | k | v (RoPE'd at position `step`) of input row x[0]
+          const float* t = p.qkv0_tab + ((size_t)(step - 1) * p.V + L.code) * QKV;
+          for (int k = c.tid; k < QKV; k += NT) L.qkv[0][k] = t[k];
+        } else {
+          rms_rows(c, M, p.n1[l]);
+          phase_qkv(c, M, pos0, wq);                    // -> E1
+          gather<6>(c, c.buf(G_QKV, MAXM * QKV), M * QKV, &L.qkv[0][0]);
+          ++c.e;
+        }
+        kv_store(c, pos0, kv);
+      }
+      __syncthreads();
+      c.refresh();
+      phase_attn(c, M, pos0, l);
+      phase_o(c, M, wo);                                // -> E3
+      load_gu(c, l, wg);
+      load_dn(c, l, wd);
+      if (l + 1 < NL) { load_qkv(c, l + 1, wq); load_o(c, l + 1, wo); }
+      gather<2 * MAXM>(c, c.buf(G_X, MAXM * D), M * D, &L.x[0][0]);
+      ++c.e;
+      c.refresh();
+      rms_rows(c, M, p.n2[l]);
+      phase_mlp(c, M, wg, wd);                          // -> E4
+      if (l + 1 == NL) {
+        load_head(c, p.audio_head + (size_t)(step - 1) * p.VP * D, D, wh);
+        if (step + 1 < p.K) { load_o(c, 0, wo); load_qkv(c, 1, wq); }
+      }
+      c.refresh();
+      phase_reduce(c, M);                               // waits E4, -> E5
+      gather<2 * MAXM>(c, c.buf(G_X, MAXM * D), M * D, &L.x[0][0]);
+      ++c.e;
+    }
+    // ci head on the last row: final norm, audio_head[step - 1] (generation.py:79)
+    c.refresh();
+    rms_rows(c, 1, p.norm, M - 1);
+    phase_head<D>(c, p.audio_head + (size_t)(step - 1) * p.VP * D, p.V, wh.a, wh.x, p.ci_logits + (size_t)(step - 1) * p.VP);  // -> E6
+    const int ci = gather_code(c, p.V);
+    ++c.e;
+    if (c.w == 0 && c.tid == 0) p.codes[step] = ci;
+    if (step + 1 < p.K) {  // next input row = projection(E_a[ci + V * step]) from the folded table
+      for (int k = c.tid; k < D; k += NT) L.x[0][k] = p.proj_tab[((size_t)step * p.V + ci) * D + k];
+      __syncthreads();
+    }
+  }
+  if (c.w == 0 && c.tid == 0) __hip_atomic_store(p.epoch, c.tag0 - 1u + (unsigned)c.e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+size_t dec_frame_gbuf_bytes() { return G_TOTAL * sizeof(u64); }
+
+void launch_dec_frame(const DecFrameArgs& p, hipStream_t st) {
+  hipLaunchKernelGGL(dec_frame_kernel, dim3(NWG), dim3(NT), 0, st, p);
+}
+
+const void* dec_frame_kernel_ptr() { return reinterpret_cast<const void*>(&dec_frame_kernel); }

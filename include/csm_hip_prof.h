@@ -27,7 +27,8 @@ int csm_bench_gemv(csm_engine* e, int which, int M, int iters, float* avg_us, do
  * t, default 5), "gemv_xl" (decode GEMVs with LDS-staged activations, default 1), "fold_proj"
  * (decoder steps >= 2 gather projection(E_a[c]) from a table built at csm_begin, default 1),
  * "qkv0_tab" (decoder layer 0's q, k, v gathered from a table at steps >= 2, default 1),
- * "fuse_mlp" (one-launch MLP for <= 4 rows, default 0). */
+ * "fuse_mlp" (one-launch MLP for <= 4 rows, default 0), "dec_frame" (batch-1 greedy bf16 frames on the
+ * persistent frame decoder, dec_frame.hip: codebook0_head + 31 decoder steps in one launch, default 1). */
 int csm_set_option(csm_engine* e, const char* key, int value);
 
 #ifdef __cplusplus

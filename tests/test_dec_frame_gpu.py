@@ -1,0 +1,57 @@
+"""The persistent frame decoder (dec_frame.hip: codebook0_head + the 31 depth-decoder steps of a
+batch-1 greedy bf16 frame in ONE launch, tagged-granule hand-offs between 256 resident workgroups)
+against the per-projection launch path it replaces and against the oracle.
+
+Codes must be identical to the launch path and to the oracle (both are fp32-accumulation paths over
+the same bf16 weights); logits within the bf16 bar; the decoder must be deterministic run to run and
+leave no hand-off timeout behind.  (tests/test_long_gpu.py's 125-frame bf16 fixture runs on it too.)"""
+import numpy as np
+import pytest
+
+from helpers import csm_weights, first_divergence, oracle_for, prompt_ids
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(model, prompt, frames):
+    from csm_mlx.generation import FrameCache
+    from csm_mlx.sampling import Sampler
+    V, K = model.n_audio_vocab, model.n_audio_codebooks
+    Vp = (V + 7) // 8 * 8
+    cache = FrameCache(model, 1, Sampler(0.0, 0), [0])
+    cache.prefill(0, *prompt)
+    logs = []
+    for _ in range(frames):
+        cache.run(1)
+        logs.append((cache.debug("c0_logits", (1, Vp))[0, :V], cache.debug("ci_logits", (K - 1, 1, Vp))[:, 0, :V]))
+    hist, n, _ = cache.codes()
+    return hist[: n[0], 0], logs
+
+
+def test_dec_frame_matches_launch_path_and_oracle():
+    from csm_mlx import _lib
+    from csm_mlx.generation import generate_codes_batch
+    from csm_mlx.models import CSM
+    from csm_mlx.sampling import Sampler
+    from csm_mlx.tokenizers import tokenize_text_segment
+    args, w = csm_weights("1b")
+    model = CSM(args, dtype="bf16")
+    model.load_weights(w)
+    L = _lib.lib()
+    prompt = tokenize_text_segment(prompt_ids(31), 0, 32)
+    _lib.check(L.csm_set_option(model.engine, b"dec_frame", 0))
+    ref, ref_logs = _run(model, prompt, 12)
+    _lib.check(L.csm_set_option(model.engine, b"dec_frame", 1))
+    got, got_logs = _run(model, prompt, 12)
+    assert first_divergence(got, ref) is None, f"dec_frame codes differ from the launch path at {first_divergence(got, ref)}"
+    for f, ((c0a, cia), (c0b, cib)) in enumerate(zip(got_logs, ref_logs)):
+        for a, b in ((c0a, c0b), (cia, cib)):
+            assert np.abs(a - b).max() <= 2e-3 * np.abs(b).max(), f"frame {f}: logits differ"
+    # deterministic, graph-replayed multi-frame loop (csm_run_frames of 16 frames per call)
+    h1, n1, _ = generate_codes_batch(model, [prompt], 40, sampler=Sampler(0.0, 0))
+    h2, n2, _ = generate_codes_batch(model, [prompt], 40, sampler=Sampler(0.0, 0))
+    assert np.array_equal(h1, h2) and np.array_equal(n1, n2)
+    assert first_divergence(h1[:12, 0], got) is None
+    orc = oracle_for(args, w, bf16=True).generate_codes(*prompt, 12)
+    assert first_divergence(got, orc) is None
+    del model
