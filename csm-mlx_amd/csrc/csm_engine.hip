@@ -139,6 +139,7 @@ struct csm_engine {
   int* df_err = nullptr;
   bool dec_frame = [] { const char* v = getenv("CSM_DEC_FRAME"); return !(v && v[0] == '0'); }();
   int df_hw = -1;    // 1: the device can hold one 512-thread workgroup on each of 256 CUs at once
+  unsigned long long* df_stamps = nullptr;  // csm_set_option "dec_frame_stamps": per-hand-off clock stamps
 
   void* balloc(size_t bytes) {
     void* p = nullptr;
@@ -343,7 +344,7 @@ void enqueue_dec_frame(csm_engine* e, hipStream_t st) {
   a.c0_head = (const bf16_t*)e->c0_head; a.proj = (const bf16_t*)e->proj; a.audio_head = (const bf16_t*)e->audio_head;
   a.proj_tab = e->proj_tab; a.qkv0_tab = e->qkv0_tab; a.h_last = e->h_last;
   a.V = e->V; a.VP = e->Vpad; a.K = e->K; a.codes = e->codes; a.c0_logits = e->c0_logits; a.ci_logits = e->ci_logits;
-  a.gbuf = (unsigned long long*)e->df_gbuf; a.epoch = e->df_epoch; a.err = e->df_err;
+  a.gbuf = (unsigned long long*)e->df_gbuf; a.epoch = e->df_epoch; a.err = e->df_err; a.stamps = e->df_stamps;
   launch_dec_frame(a, st);
   AdvanceParams ap{};  // codes are final: EOS test, history, frame counter
   ap.codes = e->codes; ap.hist = e->hist; ap.F_cap = e->F_cap; ap.B = e->B; ap.K = e->K; ap.V = e->V; ap.done = e->done;
@@ -1181,6 +1182,7 @@ int csm_debug_read(csm_engine* e, const char* what, void* host, int64_t nbytes, 
     else if (w == "ci_logits") { src = e->ci_logits; n = (e->K - 1) * B * Vp * 4; }
     else if (w == "codes") { src = e->codes; n = B * e->K * 4; }
     else if (w == "pos") { src = e->pos; n = B * 4; }
+    else if (w == "dec_frame_stamps" && e->df_stamps) { src = e->df_stamps; n = (size_t)DEC_FRAME_WGS * DEC_FRAME_STAMPS * 8; }
     else if (w == "audio_head") {  // device layout [K-1][Vpad][Dd], f32 or bf16 bits
       src = e->audio_head; n = (size_t)(e->K - 1) * Vp * e->Dd * (e->head_wdt == WDT_F32 ? 4 : 2);
     }
@@ -1339,6 +1341,11 @@ int csm_set_option(csm_engine* e, const char* key, int value) {
       if (!e) throw CsmError(CSM_ERR_ARG, "qkv0_tab needs an engine");
       e->use_qkv0_tab = value != 0;
       if (e->use_qkv0_tab && !e->qkv0_built) e->proj_tab_dirty = true;  // built at the next csm_begin
+    }
+    else if (k == "dec_frame_stamps") {
+      if (!e) throw CsmError(CSM_ERR_ARG, "dec_frame_stamps needs an engine");
+      if (value && !e->df_stamps) e->df_stamps = (unsigned long long*)e->alloc((size_t)DEC_FRAME_WGS * DEC_FRAME_STAMPS * 8);
+      if (!value && e->df_stamps) { e->release(e->df_stamps); e->df_stamps = nullptr; }
     }
     else if (k == "dec_frame") {
       if (!e) throw CsmError(CSM_ERR_ARG, "dec_frame needs an engine");

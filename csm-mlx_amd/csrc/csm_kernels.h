@@ -349,7 +349,9 @@ struct DecFrameArgs {
   unsigned long long* gbuf;              // hand-off granules (dec_frame_gbuf_bytes)
   unsigned* epoch;                       // hand-off tag base (advanced by every frame)
   int* err;                              // raised when a hand-off wait times out
+  unsigned long long* stamps;            // optional [NWG][DEC_FRAME_STAMPS] s_memrealtime per hand-off (profiling)
 };
+constexpr int DEC_FRAME_STAMPS = 1024;
 size_t dec_frame_gbuf_bytes();
 constexpr int DEC_FRAME_WGS = 256, DEC_FRAME_THREADS = 512;
 void launch_dec_frame(const DecFrameArgs& p, hipStream_t st);

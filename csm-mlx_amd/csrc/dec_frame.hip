@@ -146,6 +146,10 @@ struct Ctx {
   int w, tid, lane, wave;
   unsigned tag0;
   int e;  // hand-off counter
+  // profiling: the 100 MHz real-time clock when this WG's hand-off wait number e completed
+  __device__ void stamp() const {
+    if (p.stamps && tid == 0 && e < DEC_FRAME_STAMPS) p.stamps[(size_t)w * DEC_FRAME_STAMPS + e] = __builtin_amdgcn_s_memrealtime();
+  }
   __device__ void refresh() {
     tid = opaque_tid();
     lane = tid & 63;
@@ -182,6 +186,7 @@ __device__ __forceinline__ void gather(Ctx& c, const u64* buf, int n, float* out
       if (i < n && (unsigned)(g[u] >> 32) != tag) g[u] = gload(buf + i);
     }
   }
+  c.stamp();
 #pragma unroll
   for (int u = 0; u < GPT; ++u) {
     const int i = c.tid + u * NT;
@@ -367,14 +372,14 @@ __device__ __forceinline__ void phase_attn(Ctx& c, int M, int pos0, int layer) {
     c.L.att[m][h * HD + c.lane] = o0 * inv;
     c.L.att[m][h * HD + c.lane + 64] = o1 * inv;
   }
-  if (c.w == 0) {  // the new K / V rows -> cache (write-through; read by later steps after a hand-off)
-    for (int i = c.tid; i < M * HKV * HD; i += NT) {
-      const int m = i / (HKV * HD), r = i % (HKV * HD), gg = r / HD, d = r % HD;
-      const size_t off = ((size_t)gg * c.p.S_cap + pos0 + m) * HD + d;
-      sc1_store_f(c.p.kc[layer] + off, c.L.qkv[m][HQ * HD + r]);
-      sc1_store_f(c.p.vc[layer] + off, c.L.qkv[m][(HQ + HKV) * HD + r]);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // the new K / V rows -> cache, spread over the workgroups (WG w stores element w of each row:
+  // 2 heads x 128 = 256 elements), write-through; the storing threads drain them (vmcnt(0)) before
+  // this WG's next publish (phase_mlp), so a reader that saw that hand-off reads them coherently
+  if (c.tid < M) {
+    const int m = c.tid, r = c.w, gg = r / HD, d = r % HD;
+    const size_t off = ((size_t)gg * c.p.S_cap + pos0 + m) * HD + d;
+    sc1_store_f(c.p.kc[layer] + off, c.L.qkv[m][HQ * HD + r]);
+    sc1_store_f(c.p.vc[layer] + off, c.L.qkv[m][(HQ + HKV) * HD + r]);
   }
   __syncthreads();
 }
@@ -421,6 +426,7 @@ __device__ __forceinline__ void phase_mlp(Ctx& c, int M, const WGu& G, const WDn
       }
     }
   }
+  if (c.tid < MAXM) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this layer's K/V cache stores
   __syncthreads();
   u64* g = c.buf(G_PART, (size_t)NWG * MAXM * D) + (size_t)c.w * MAXM * D;
 #pragma unroll
@@ -463,6 +469,7 @@ __device__ __forceinline__ void phase_reduce(Ctx& c, int M) {
       for (int u = 0; u < 2; ++u)
         if (m < M && (unsigned)(q[m][u] >> 32) != tag) q[m][u] = gload(g + ((size_t)v * MAXM + m) * D + 4 * c.w + 2 * half + u);
   }
+  c.stamp();
 #pragma unroll
   for (int m = 0; m < MAXM; ++m)
 #pragma unroll
@@ -543,6 +550,7 @@ __global__ __launch_bounds__(NT, 1) void dec_frame_kernel(DecFrameArgs p) {
   __shared__ __attribute__((aligned(16))) Lds L;
   Ctx c{p, L, (int)blockIdx.x, (int)threadIdx.x, (int)(threadIdx.x & 63), (int)(threadIdx.x >> 6), 0u, 0};
   c.tag0 = __hip_atomic_load(p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  if (p.stamps && c.tid == 0) p.stamps[(size_t)c.w * DEC_FRAME_STAMPS + DEC_FRAME_STAMPS - 2] = __builtin_amdgcn_s_memrealtime();
   // ---- frame start: codebook0_head (K = 2048, 8 rows per WG + 1 for WGs 0-2) and the projection of
   // h_last (rows 4w..4w+3) for decoder step 1, both published in one hand-off
   u32x4_t c0a[4], c0x[4], pa[2];
@@ -587,25 +595,26 @@ __global__ __launch_bounds__(NT, 1) void dec_frame_kernel(DecFrameArgs p) {
   // Register prefetch schedule (what is in flight during each hand-off wait):
   //   E1 (q|k|v): the cached K/V rows       E3 (x): this layer's gate/up + down slices, next layer's QKV / o
   //   E4 / E5 of the last layer: this step's head rows, the next step's o / QKV
+  //   E6: the next step's layer-0 cached K/V rows
   WHd wh;
+  KvRegs kv0;  // layer 0's cached K/V rows of the next step, fetched during the head's hand-off
   for (int step = 1; step < p.K; ++step) {
     const int M = step == 1 ? 2 : 1;
     const int pos0 = step == 1 ? 0 : step;
     for (int l = 0; l < NL; ++l) {
       c.refresh();
-      {
+      if (l == 0 && step > 1) {
+        // layer 0 from the folded table: q | k | v (RoPE'd at position `step`) of input row x[0]
+        const float* t = p.qkv0_tab + ((size_t)(step - 1) * p.V + L.code) * QKV;
+        for (int k = c.tid; k < QKV; k += NT) L.qkv[0][k] = t[k];
+        kv_store(c, pos0, kv0);
+      } else {
         KvRegs kv;
         kv_issue(c, l, pos0, kv);
-        if (l == 0 && step > 1) {
-          // layer 0 from the folded table: q | k | v (RoPE'd at position `step`) of input row x[0]
-          const float* t = p.qkv0_tab + ((size_t)(step - 1) * p.V + L.code) * QKV;
-          for (int k = c.tid; k < QKV; k += NT) L.qkv[0][k] = t[k];
-        } else {
-          rms_rows(c, M, p.n1[l]);
-          phase_qkv(c, M, pos0, wq);                    // -> E1
-          gather<6>(c, c.buf(G_QKV, MAXM * QKV), M * QKV, &L.qkv[0][0]);
-          ++c.e;
-        }
+        rms_rows(c, M, p.n1[l]);
+        phase_qkv(c, M, pos0, wq);                      // -> E1
+        gather<6>(c, c.buf(G_QKV, MAXM * QKV), M * QKV, &L.qkv[0][0]);
+        ++c.e;
         kv_store(c, pos0, kv);
       }
       __syncthreads();
@@ -633,6 +642,7 @@ __global__ __launch_bounds__(NT, 1) void dec_frame_kernel(DecFrameArgs p) {
     c.refresh();
     rms_rows(c, 1, p.norm, M - 1);
     phase_head<D>(c, p.audio_head + (size_t)(step - 1) * p.VP * D, p.V, wh.a, wh.x, p.ci_logits + (size_t)(step - 1) * p.VP);  // -> E6
+    if (step + 1 < p.K) kv_issue(c, 0, step + 1, kv0);
     const int ci = gather_code(c, p.V);
     ++c.e;
     if (c.w == 0 && c.tid == 0) p.codes[step] = ci;
@@ -641,6 +651,7 @@ __global__ __launch_bounds__(NT, 1) void dec_frame_kernel(DecFrameArgs p) {
       __syncthreads();
     }
   }
+  if (p.stamps && c.tid == 0) p.stamps[(size_t)c.w * DEC_FRAME_STAMPS + DEC_FRAME_STAMPS - 1] = __builtin_amdgcn_s_memrealtime();
   if (c.w == 0 && c.tid == 0) __hip_atomic_store(p.epoch, c.tag0 - 1u + (unsigned)c.e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
