@@ -345,6 +345,9 @@ void enqueue_dec_frame(csm_engine* e, hipStream_t st) {
   a.proj_tab = e->proj_tab; a.qkv0_tab = e->qkv0_tab; a.h_last = e->h_last;
   a.V = e->V; a.VP = e->Vpad; a.K = e->K; a.codes = e->codes; a.c0_logits = e->c0_logits; a.ci_logits = e->ci_logits;
   a.gbuf = (unsigned long long*)e->df_gbuf; a.epoch = e->df_epoch; a.err = e->df_err; a.stamps = e->df_stamps;
+  static const int wnt = [] { const char* v = getenv("CSM_DF_WNT"); return v ? atoi(v) : 0; }();
+  static const int hnt = [] { const char* v = getenv("CSM_DF_HNT"); return v ? atoi(v) : 1; }();
+  a.wnt = wnt; a.hnt = hnt;
   launch_dec_frame(a, st);
   AdvanceParams ap{};  // codes are final: EOS test, history, frame counter
   ap.codes = e->codes; ap.hist = e->hist; ap.F_cap = e->F_cap; ap.B = e->B; ap.K = e->K; ap.V = e->V; ap.done = e->done;
@@ -1182,6 +1185,7 @@ int csm_debug_read(csm_engine* e, const char* what, void* host, int64_t nbytes, 
     else if (w == "ci_logits") { src = e->ci_logits; n = (e->K - 1) * B * Vp * 4; }
     else if (w == "codes") { src = e->codes; n = B * e->K * 4; }
     else if (w == "pos") { src = e->pos; n = B * 4; }
+    else if (w == "dec_frame_epoch") { src = e->df_epoch; n = 4; }  // advances by the hand-offs of every frame it ran
     else if (w == "dec_frame_stamps" && e->df_stamps) { src = e->df_stamps; n = (size_t)DEC_FRAME_WGS * DEC_FRAME_STAMPS * 8; }
     else if (w == "audio_head") {  // device layout [K-1][Vpad][Dd], f32 or bf16 bits
       src = e->audio_head; n = (size_t)(e->K - 1) * Vp * e->Dd * (e->head_wdt == WDT_F32 ? 4 : 2);

@@ -350,6 +350,7 @@ struct DecFrameArgs {
   unsigned* epoch;                       // hand-off tag base (advanced by every frame)
   int* err;                              // raised when a hand-off wait times out
   unsigned long long* stamps;            // optional [NWG][DEC_FRAME_STAMPS] s_memrealtime per hand-off (profiling)
+  int wnt, hnt;                          // non-temporal loads for the decoder weights / the heads
 };
 constexpr int DEC_FRAME_STAMPS = 1024;
 size_t dec_frame_gbuf_bytes();

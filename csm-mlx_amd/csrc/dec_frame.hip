@@ -100,8 +100,9 @@ __device__ __forceinline__ u32x4_t wload(const bf16_t* p) { return *reinterpret_
 // lane-dependent part in ONE voffset register shared by every layer and row, the row / chunk step in
 // the scalar offset -- so per-layer weight addresses are not VGPR pairs the compiler keeps live
 // across the frame loop.
-__device__ __forceinline__ u32x4_t bload(const void* base, int voff, int soff) {
+__device__ __forceinline__ u32x4_t bload(const void* base, int voff, int soff, int nt = 0) {
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+  if (nt) return __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 2));
   return __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
 }
 
@@ -146,6 +147,11 @@ struct Ctx {
   int w, tid, lane, wave;
   unsigned tag0;
   int e;  // hand-off counter
+  int ps = 0;  // phase-mark counter (profiling stamps 512..1007)
+  __device__ void mark() {
+    if (p.stamps && tid == 0 && ps < 496) p.stamps[(size_t)w * DEC_FRAME_STAMPS + 512 + ps] = __builtin_amdgcn_s_memrealtime();
+    ++ps;
+  }
   // profiling: the 100 MHz real-time clock when this WG's hand-off wait number e completed
   __device__ void stamp() const {
     if (p.stamps && tid == 0 && e < DEC_FRAME_STAMPS) p.stamps[(size_t)w * DEC_FRAME_STAMPS + e] = __builtin_amdgcn_s_memrealtime();
@@ -258,12 +264,12 @@ __device__ __forceinline__ void load_head(Ctx& c, const bf16_t* W, int K, WHd& r
   // K = 1024 (ci heads): 128 chunks per row -> 2 per lane
   const bf16_t* base = W + (size_t)(8 * c.w) * K;
   const int v = (c.wave * K + 8 * c.lane) * 2;
-  r.a[0] = bload(base, v, 0);
-  r.a[1] = bload(base, v, 1024);
+  r.a[0] = bload(base, v, 0, c.p.hnt);
+  r.a[1] = bload(base, v, 1024, c.p.hnt);
   if (c.wave == 0 && c.w < 3) {
     const bf16_t* xr = W + (size_t)(2048 + c.w) * K;
-    r.x[0] = bload(xr, 16 * c.lane, 0);
-    r.x[1] = bload(xr, 16 * c.lane, 1024);
+    r.x[0] = bload(xr, 16 * c.lane, 0, c.p.hnt);
+    r.x[1] = bload(xr, 16 * c.lane, 1024, c.p.hnt);
   }
 }
 
@@ -593,7 +599,8 @@ __global__ __launch_bounds__(NT, 1) void dec_frame_kernel(DecFrameArgs p) {
   __syncthreads();
 
   // Register prefetch schedule (what is in flight during each hand-off wait):
-  //   E1 (q|k|v): the cached K/V rows       E3 (x): this layer's gate/up + down slices, next layer's QKV / o
+  //   E1 (q|k|v): the cached K/V rows, this layer's down slices
+//   E3 (x): this layer's gate/up slices, next layer's QKV / o
   //   E4 / E5 of the last layer: this step's head rows, the next step's o / QKV
   //   E6: the next step's layer-0 cached K/V rows
   WHd wh;
@@ -606,11 +613,13 @@ __global__ __launch_bounds__(NT, 1) void dec_frame_kernel(DecFrameArgs p) {
       if (l == 0 && step > 1) {
         // layer 0 from the folded table: q | k | v (RoPE'd at position `step`) of input row x[0]
         const float* t = p.qkv0_tab + ((size_t)(step - 1) * p.V + L.code) * QKV;
+        load_dn(c, l, wd);
         for (int k = c.tid; k < QKV; k += NT) L.qkv[0][k] = t[k];
         kv_store(c, pos0, kv0);
       } else {
         KvRegs kv;
         kv_issue(c, l, pos0, kv);
+        load_dn(c, l, wd);
         rms_rows(c, M, p.n1[l]);
         phase_qkv(c, M, pos0, wq);                      // -> E1
         gather<6>(c, c.buf(G_QKV, MAXM * QKV), M * QKV, &L.qkv[0][0]);
@@ -619,16 +628,19 @@ __global__ __launch_bounds__(NT, 1) void dec_frame_kernel(DecFrameArgs p) {
       }
       __syncthreads();
       c.refresh();
+      c.mark();
       phase_attn(c, M, pos0, l);
+      c.mark();
       phase_o(c, M, wo);                                // -> E3
+      c.mark();
       load_gu(c, l, wg);
-      load_dn(c, l, wd);
       if (l + 1 < NL) { load_qkv(c, l + 1, wq); load_o(c, l + 1, wo); }
       gather<2 * MAXM>(c, c.buf(G_X, MAXM * D), M * D, &L.x[0][0]);
       ++c.e;
       c.refresh();
       rms_rows(c, M, p.n2[l]);
       phase_mlp(c, M, wg, wd);                          // -> E4
+      c.mark();
       if (l + 1 == NL) {
         load_head(c, p.audio_head + (size_t)(step - 1) * p.VP * D, D, wh);
         if (step + 1 < p.K) { load_o(c, 0, wo); load_qkv(c, 1, wq); }

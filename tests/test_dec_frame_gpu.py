@@ -42,7 +42,12 @@ def test_dec_frame_matches_launch_path_and_oracle():
     _lib.check(L.csm_set_option(model.engine, b"dec_frame", 0))
     ref, ref_logs = _run(model, prompt, 12)
     _lib.check(L.csm_set_option(model.engine, b"dec_frame", 1))
+    ep0 = np.zeros(1, np.uint32)
+    _lib.check(L.csm_debug_read(model.engine, b"dec_frame_epoch", _lib.ptr(ep0), 4, None))
     got, got_logs = _run(model, prompt, 12)
+    ep1 = np.zeros(1, np.uint32)
+    _lib.check(L.csm_debug_read(model.engine, b"dec_frame_epoch", _lib.ptr(ep1), 4, None))
+    assert int(ep1[0]) - int(ep0[0]) == 12 * 498, "the persistent frame decoder did not run every frame"
     assert first_divergence(got, ref) is None, f"dec_frame codes differ from the launch path at {first_divergence(got, ref)}"
     for f, ((c0a, cia), (c0b, cib)) in enumerate(zip(got_logs, ref_logs)):
         for a, b in ((c0a, c0b), (cia, cib)):

@@ -30,7 +30,7 @@ st = np.zeros((256, 1024), np.uint64)
 _lib.check(L.csm_debug_read(model.engine, b"dec_frame_stamps", _lib.ptr(st), st.nbytes, None))
 t0 = st[:, 1022].astype(np.int64)
 end = st[:, 1023].astype(np.int64)
-n = int((st[0, :1000] > 0).sum())
+n = int((st[0, :512] > 0).sum())
 rel = (st[:, :n].astype(np.int64) - t0.min()) / 100.0        # us since the first WG started
 print(f"hand-offs {n}; kernel span {(end.max() - t0.min()) / 100:.1f} us; start skew {(t0.max() - t0.min()) / 100:.2f} us")
 # kinds per step: L0 (E3, E4, E5), L1-3 (E1, E3, E4, E5) x3, E6; step 1 has E1 at L0; frame start A0
@@ -55,3 +55,31 @@ for k in sorted(gaps):
           f"WG completion spread {np.mean(spread[k]):.2f} us")
 step_t = [w0[kinds.index("E6", i)] for i in range(len(kinds)) if kinds[i] == "E6"]
 print("per step (us):", np.round(np.diff([0.0] + step_t), 1).tolist()[:8], "...")
+
+# phase marks (WG 0 and the mean over WGs): per layer [attn start, attn end, o published, mlp published]
+mk = (st[:, 512:1008].astype(np.int64) - t0.min()) / 100.0
+nm = 4 * 4 * 31
+mk = mk[:, :nm].reshape(256, 31, 4, 4)
+ho = {}
+e = 1
+for step in range(31):
+    for l in range(4):
+        if not (l == 0 and step > 0):
+            ho[(step, l, "E1")] = e; e += 1
+        ho[(step, l, "E3")] = e; e += 1
+        ho[(step, l, "E4")] = e; e += 1
+        ho[(step, l, "E5")] = e; e += 1
+    e += 1
+seg = collections.defaultdict(list)
+for step in range(1, 31):
+    for l in range(4):
+        a0, a1, oc, mp = [mk[:, step, l, i] for i in range(4)]
+        e3 = rel[:, ho[(step, l, "E3")]]
+        e4 = rel[:, ho[(step, l, "E4")]]
+        seg["attention"].append(np.mean(a1 - a0))
+        seg["o_proj+publish"].append(np.mean(oc - a1))
+        seg["E3 wait"].append(np.mean(e3 - oc))
+        seg["mlp compute+publish"].append(np.mean(mp - e3))
+        seg["E4 wait"].append(np.mean(e4 - mp))
+for k, v in seg.items():
+    print(f"  {k}: {np.mean(v):.2f} us (mean over WGs, steps 2-31)")
