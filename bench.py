@@ -12,9 +12,12 @@ shards over independent utterances, so there is no data-path collective; RCCL
 (torch.distributed "nccl") is used only for the barrier, the max-over-ranks
 timer and the frame count.  ``value`` = frames of all ranks / max rank time.
 
-Extra JSON fields: ``roofline`` for the dominant kernel (decoder gate/up GEMV,
-timed live with HIP events on the engine stream) and ``cpu_baseline`` (the
-numpy oracle, i.e. a CPU restatement -- NOT the MLX reference -- on this host).
+Extra JSON fields: ``roofline`` for the dominant kernel (the persistent frame
+decoder at batch 1, else the decoder gate/up projection the batch runs), timed
+live with HIP events on the engine stream; ``roofline_backbone`` (backbone
+gate/up); ``roofline_frame`` (the weights a frame step reads x frame steps/s);
+and ``cpu_baseline`` (the numpy oracle, i.e. a CPU restatement -- NOT the MLX
+reference -- on this host).
 """
 from __future__ import annotations
 
@@ -162,6 +165,79 @@ def context_prompts(mine, K: int = 32):
     return out
 
 
+def _wbytes(model, n: int, k: int) -> float:
+    """Storage bytes of an [n][k] Linear weight (common.h q4_bytes: nibbles + a 4-B affine pair per 64)."""
+    if model.dtype == "q4":
+        return n * k / 2 + n * (k // 64) * 4
+    return n * k * (4 if model.dtype == "float32" else 2)
+
+
+def frame_weight_bytes(model) -> float:
+    """Weight bytes one frame step reads, as the reference's generate_frame does (generation.py:34-92):
+    every backbone layer and codebook0_head once, then 31 x (projection + every decoder layer + one
+    audio_head slice).  audio_head stays in the float dtype under nn.quantize (a 3-D parameter)."""
+    def stack(la):
+        D, hd = la.hidden_size, la.head_dim
+        per = (_wbytes(model, (la.num_attention_heads + 2 * la.num_key_value_heads) * hd, D)
+               + _wbytes(model, D, la.num_attention_heads * hd) + _wbytes(model, 2 * la.intermediate_size, D)
+               + _wbytes(model, D, la.intermediate_size))
+        return per * la.num_hidden_layers
+    bb, dec = model.backbone.args, model.decoder.args
+    V, K = model.n_audio_vocab, model.n_audio_codebooks
+    head_b = 4 if model.dtype == "float32" else 2
+    return (stack(bb) + _wbytes(model, V, bb.hidden_size)
+            + (K - 1) * (stack(dec) + _wbytes(model, dec.hidden_size, bb.hidden_size) + V * dec.hidden_size * head_b))
+
+
+def _kernel_name(model, batch: int, stack: str) -> str:
+    if batch >= 8 and model.dtype in ("bf16", "q4"):
+        return (f"gemm_pipe_kernel<Q4={'true' if model.dtype == 'q4' else 'false'}> = {stack} RMSNorm + gate/up + "
+                f"SiLU*up as an exact-split MFMA GEMM over {batch} rows")
+    return f"gemv_xl_kernel<{model.dtype}> = {stack} RMSNorm + gate/up + SiLU*up GEMV over {batch} row(s)"
+
+
+def _traffic(key: str):
+    """HBM-side bytes per launch of `key` from the committed PMC pass that matches this exact run
+    configuration (profiles/pmc_traffic.json), with the pass it came from; (None, None) otherwise."""
+    f = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        tr = json.load(open(f))
+    except (OSError, ValueError):
+        return None, None
+    ent = tr.get("runs", {}).get(key)
+    return (ent["bytes"], ent["source"]) if ent else (None, None)
+
+
+def rooflines(model, batch: int):
+    """Live HIP-event rooflines on the engine stream.  ``dominant``: the persistent frame decoder
+    (dec_frame_kernel, one launch per frame) when it runs the frame's head -- batch 1 greedy bf16 --
+    else the decoder gate/up projection at this batch; ``backbone_gate_up`` beside it."""
+    from csm_mlx import _lib
+    L = _lib.lib()
+
+    def entry(us, nb, kernel, key):
+        ach = nb / (us * 1e-6) / 1e9
+        tb, src = _traffic(key)
+        return {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": tb, "traffic_source": src,
+                "avg_us": round(us, 3), "bytes_per_launch": int(nb), "kernel": kernel}
+
+    def gemv(which, stack):
+        us, nb = ctypes.c_float(0), ctypes.c_double(0)
+        _lib.check(L.csm_bench_gemv(model.engine, which, batch, 400, ctypes.byref(us), ctypes.byref(nb)))
+        return entry(us.value, nb.value, _kernel_name(model, batch, stack), f"{stack}_gate_up/{model.dtype}/B{batch}")
+
+    out = {"backbone_gate_up": gemv(0, "backbone")}
+    us, nb = ctypes.c_float(0), ctypes.c_double(0)
+    if batch == 1 and L.csm_bench_dec_frame(model.engine, 20, ctypes.byref(us), ctypes.byref(nb)) == 0:
+        out["dominant"] = entry(us.value, nb.value, "dec_frame_kernel = persistent frame decoder: codebook0_head + "
+                                "31 decoder steps (4 layers + audio_head slice each) of one greedy frame, one launch",
+                                f"dec_frame/{model.dtype}/B1")
+    else:
+        out["dominant"] = gemv(4, "decoder")
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -271,25 +347,15 @@ def main():
     dt = time.perf_counter() - t0
     total_frames, max_dt = aggregate(float(frames), dt, world, dev)
 
-    # roofline of the dominant kernel: decoder gate/up (+RMSNorm, SiLU*up) GEMV, 124 launches/frame
-    L = _lib.lib()
-    roof = {}
-    for key, which in (("decoder_gate_up", 4), ("backbone_gate_up", 0)):
-        us, nb = ctypes.c_float(0), ctypes.c_double(0)
-        _lib.check(L.csm_bench_gemv(model.engine, which, args.batch, 400, ctypes.byref(us), ctypes.byref(nb)))
-        ach = nb.value / (us.value * 1e-6) / 1e9
-        roof[key] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "avg_us": round(us.value, 3),
-                     "bytes_per_launch": int(nb.value)}
-    traffic_file = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(traffic_file):
-        try:
-            tr = json.load(open(traffic_file))
-            for k in roof:
-                if k in tr:
-                    roof[k]["traffic"] = tr[k]
-        except Exception:  # noqa: BLE001
-            pass
+    roof = rooflines(model, args.batch)
+    fb = frame_weight_bytes(model)
+    frame_steps_per_s = total_frames / max_dt / max(1, args.batch * world)   # engine frame steps / s per GPU
+    ach_f = fb * frame_steps_per_s / 1e9
+    roof_frame = {"bound": "hbm", "achieved": round(ach_f, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                  "frac": round(ach_f / HBM_PEAK_GBS, 4), "bytes_per_frame_step": int(fb),
+                  "note": "weights the reference reads per frame step (backbone + c0 head once; decoder, projection "
+                          "and one audio-head slice x31) in this engine's storage format, x frame steps/s per GPU; "
+                          "one frame step advances every utterance of the GPU's batch by one frame"}
 
     if rank == 0 and args.dump:
         z = {f"codes_{i}": c for i, c in enumerate(last["codes"])}
@@ -318,9 +384,9 @@ def main():
                        "model": "csm_1b (synthetic seed-0 weights)", "global_batch": args.batch * world,
                        "per_gpu_batch": args.batch, "frames": args.frames, "mimi_decode": decode,
                        "parallelism": f"dp{world}", "rtf": round(total_frames / max_dt / 12.5, 2)},
-            "roofline": dict(roof["decoder_gate_up"], kernel="gemv_xl_kernel<bf16,G=64,RPT=2,MT=1,TAG=1> = decoder "
-                             "RMSNorm+gate/up+SiLU*up GEMV, 33.5 MB bf16 weights per launch, 124 launches/frame"),
+            "roofline": roof["dominant"],
             "roofline_backbone": roof["backbone_gate_up"],
+            "roofline_frame": roof_frame,
         }
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.cpu_frames)

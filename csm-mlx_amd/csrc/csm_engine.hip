@@ -333,7 +333,7 @@ bool dec_frame_eligible(csm_engine* e) {
   return e->df_hw == 1;
 }
 
-void enqueue_dec_frame(csm_engine* e, hipStream_t st) {
+void enqueue_dec_frame_only(csm_engine* e, hipStream_t st) {
   DecFrameArgs a{};
   for (int l = 0; l < DEC_FRAME_LAYERS; ++l) {
     const LayerW& w = e->dec.L[l];
@@ -349,6 +349,10 @@ void enqueue_dec_frame(csm_engine* e, hipStream_t st) {
   static const int hnt = [] { const char* v = getenv("CSM_DF_HNT"); return v ? atoi(v) : 1; }();
   a.wnt = wnt; a.hnt = hnt;
   launch_dec_frame(a, st);
+}
+
+void enqueue_dec_frame(csm_engine* e, hipStream_t st) {
+  enqueue_dec_frame_only(e, st);
   AdvanceParams ap{};  // codes are final: EOS test, history, frame counter
   ap.codes = e->codes; ap.hist = e->hist; ap.F_cap = e->F_cap; ap.B = e->B; ap.K = e->K; ap.V = e->V; ap.done = e->done;
   ap.n_frames = e->n_frames; ap.frame_ctr = e->frame_ctr;
@@ -1324,6 +1328,45 @@ int csm_bench_gemv(csm_engine* e, int which, int M, int iters, float* avg_us, do
     (void)hipEventDestroy(b);
     if (avg_us) *avg_us = ms * 1000.f / iters;
     if (bytes) *bytes = (double)nbytes;
+  }
+  CSM_CATCH
+}
+
+int csm_bench_dec_frame(csm_engine* e, int iters, float* avg_us, double* bytes) {
+  CSM_TRY {
+    if (!e || iters <= 0) throw CsmError(CSM_ERR_ARG, "bad bench arguments");
+    if (!dec_frame_eligible(e)) throw CsmError(CSM_ERR_STATE, "the persistent frame decoder is not active on this engine");
+    if (e->prompt_len.empty() || e->prompt_len[0] < 0) throw CsmError(CSM_ERR_STATE, "csm_prefill first (the replay needs h_last)");
+    HIPCHK(hipSetDevice(e->dev));
+    // The replay recomputes the last frame's head from the same h_last: the same codes, logits and
+    // decoder K/V rows are written again (the advance launch is not replayed).
+    const size_t D = e->Dd, DB = e->D, V = e->V, F = e->dec.d.intermediate, QKV = e->dec.qkv_rows();
+    const size_t HKV = e->dec.d.n_kv_heads, HD = e->dec.d.head_dim;
+    double nb = (double)V * DB * 2 + DB * 4 + (double)D * DB * 2;    // codebook0_head, h_last, projection
+    for (int step = 1; step < e->K; ++step) {
+      const int rows = step == 1 ? 2 : 1, pos = step == 1 ? 1 : step;
+      for (int l = 0; l < DEC_FRAME_LAYERS; ++l) {
+        nb += (l == 0 && step > 1) ? (double)QKV * 4 : (double)QKV * D * 2;  // folded qkv0 table row / QKV
+        nb += (double)D * D * 2 + 2.0 * F * D * 2 + (double)F * D * 2;       // o, gate/up, down
+        nb += 2.0 * HKV * (pos + 1) * HD * 4 + 2.0 * HKV * rows * HD * 4;    // K/V history read + append
+      }
+      nb += (double)V * D * 2 + D * 4;                                      // audio_head[step-1], next x row
+    }
+    for (int i = 0; i < 2; ++i) enqueue_dec_frame_only(e, e->st);
+    hipEvent_t a, b;
+    HIPCHK(hipEventCreate(&a));
+    HIPCHK(hipEventCreate(&b));
+    HIPCHK(hipEventRecord(a, e->st));
+    for (int i = 0; i < iters; ++i) enqueue_dec_frame_only(e, e->st);
+    HIPCHK(hipEventRecord(b, e->st));
+    HIPCHK(hipEventSynchronize(b));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, a, b));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    check_dec_frame(e);
+    if (avg_us) *avg_us = ms * 1000.f / iters;
+    if (bytes) *bytes = nb;
   }
   CSM_CATCH
 }

@@ -223,6 +223,9 @@ __device__ __forceinline__ void rms_rows(Ctx& c, int M, const float* nw, int m0 
 // ---- weight slices held in registers (issued ahead of use)
 struct WQkv { u32x4_t a, b; };      // waves 0..5: row 6w+wave, chunks lane / lane+64
 struct WO { u32x4_t a; };            // row 4w + wave/2, chunk (wave&1)*64 + lane
+#ifndef GU_EARLY
+#define GU_EARLY 4  // gate/up rows per wave fetched before the attention (the rest after o_proj)
+#endif
 struct WGu { u32x4_t a[8][2]; };     // rows 64w + 8*wave + r, chunks lane / lane+64
 struct WDn { u32x4_t a[2][2][2]; };  // [row t / t+512][chunk 2w+q][16-B half]
 struct WHd { u32x4_t a[2]; u32x4_t x[2]; };  // head row 8w+wave (+ row 2048+w for wave 0, w < 3)
@@ -239,11 +242,12 @@ __device__ __forceinline__ void load_o(Ctx& c, int l, WO& r) {
   const bf16_t* row = c.p.wo[l] + (size_t)(4 * c.w) * D;
   r.a = bload(row, ((c.wave >> 1) * D + 8 * ((c.wave & 1) * 64 + c.lane)) * 2, 0);
 }
+template <int I0, int I1>
 __device__ __forceinline__ void load_gu(Ctx& c, int l, WGu& r) {
   const bf16_t* base = c.p.wgu[l] + (size_t)(64 * c.w) * D;
   const int v = (8 * c.wave * D + 8 * c.lane) * 2;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
+  for (int i = I0; i < I1; ++i) {
     r.a[i][0] = bload(base, v, i * D * 2);
     r.a[i][1] = bload(base, v, i * D * 2 + 1024);
   }
@@ -629,11 +633,12 @@ __global__ __launch_bounds__(NT, 1) void dec_frame_kernel(DecFrameArgs p) {
       __syncthreads();
       c.refresh();
       c.mark();
+      load_gu<0, GU_EARLY>(c, l, wg);
       phase_attn(c, M, pos0, l);
       c.mark();
       phase_o(c, M, wo);                                // -> E3
       c.mark();
-      load_gu(c, l, wg);
+      load_gu<GU_EARLY, 8>(c, l, wg);
       if (l + 1 < NL) { load_qkv(c, l + 1, wq); load_o(c, l + 1, wo); }
       gather<2 * MAXM>(c, c.buf(G_X, MAXM * D), M * D, &L.x[0][0]);
       ++c.e;

@@ -2,7 +2,7 @@
  * csm_hip_prof.h -- tuning and profiling hooks of libcsm_hip.so.
  *
  * NOT part of the reference-facing ABI (include/csm_hip.h): no reference interface corresponds to
- * these.  bench.py uses csm_bench_gemv for the live roofline of the dominant kernel; the parity
+ * these.  bench.py uses csm_bench_dec_frame / csm_bench_gemv for the live roofline of the dominant kernel; the parity
  * tests use csm_set_option to A/B the opt-in fused paths against the default launches.
  */
 #ifndef CSM_HIP_PROF_H
@@ -21,6 +21,13 @@ extern "C" {
  * *bytes = algorithmic bytes per launch (weights in their storage format + activations read and
  * written). */
 int csm_bench_gemv(csm_engine* e, int which, int M, int iters, float* avg_us, double* bytes);
+
+/* Replay the persistent frame decoder (dec_frame.hip: codebook0_head + 31 decoder steps of a batch-1
+ * greedy frame, one launch) `iters` times on the engine stream from the current h_last, timed with HIP
+ * events on that stream.  Needs an engine on which that kernel is active and a prefilled utterance.
+ * *bytes = algorithmic bytes per launch: every head and decoder weight the frame reads once in bf16,
+ * the folded-table rows, h_last, and the decoder K/V rows read and appended. */
+int csm_bench_dec_frame(csm_engine* e, int iters, float* avg_us, double* bytes);
 
 /* Tuning / debug switches (re-capture the frame graphs): "fuse_attn" (decoder attention recomputed
  * inside the o_proj launch, default 0), "nt_mask" (bit t: non-temporal weight loads for stack tag
