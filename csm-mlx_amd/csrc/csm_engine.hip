@@ -89,6 +89,9 @@ struct csm_engine {
   float* qkv0_tab = nullptr;
   bool use_qkv0_tab = [] { const char* v = getenv("CSM_QKV0_TAB"); return !(v && v[0] == '0'); }();  // csm_set_option "qkv0_tab"
   bool qkv0_built = false;
+  // fragment-tiled copies of the matrices the MFMA path reads (build_tiled; ws.tiled maps them)
+  std::vector<void*> tiled_bufs;
+  bool tiled_dirty = true;
   std::set<std::string> loaded;
   std::vector<std::string> required;
   // activations
@@ -125,6 +128,7 @@ struct csm_engine {
   // (6.1 + 5.3 us) plus the boundary it removes -- 205 vs 227 frames/s.
   bool fuse_attn = false;
   bool fold_proj = true;  // csm_set_option "fold_proj": decoder steps >= 2 read the folded table
+  bool linear_mfma = false;  // csm_set_option "linear_mfma": csm_linear on the MFMA GEMM (kernel tests)
   // csm_set_option "fuse_mlp" / CSM_FUSE_MLP=1: one-launch MLP (gate/up + SiLU*up + down, 64-bit
   // fixed-point atomics) for <= 4 rows.  Off: the atomics' memory-side serialization (512 blocks add
   // into the same D outputs) costs more than the launch it saves -- 197.9 vs 235.0 frames/s; with
@@ -145,6 +149,7 @@ struct csm_engine {
     void* p = nullptr;
     if (hipMalloc(&p, bytes) != hipSuccess) throw CsmError(CSM_ERR_HIP, "hipMalloc(" + std::to_string(bytes) + ") failed");
     (void)hipMemset(p, 0, bytes);
+    (void)hipDeviceSynchronize();  // the null-stream fill is not ordered with the engine's non-blocking stream
     batch_allocs.push_back(p);
     return p;
   }
@@ -152,6 +157,7 @@ struct csm_engine {
     void* p = nullptr;
     if (hipMalloc(&p, bytes) != hipSuccess) throw CsmError(CSM_ERR_HIP, "hipMalloc(" + std::to_string(bytes) + ") failed");
     (void)hipMemset(p, 0, bytes);
+    (void)hipDeviceSynchronize();  // the null-stream fill is not ordered with the engine's non-blocking stream
     allocs.push_back(p);
     return p;
   }
@@ -533,6 +539,42 @@ void ensure_batch(csm_engine* e, int B) {
   gemm_reserve(e->ws, (int)Vp, (int)Dd, (int)Bm);  // ci heads
 }
 
+// Fragment-tiled copies (launch_gemm_retile) of every matrix the batched MFMA path reads -- stack
+// projections, projection, codebook0_head, the bf16 audio_head slices -- rebuilt in place after any
+// weight change (csm_load_tensor, csm_quantize), at csm_begin, before graphs capture them.
+void build_tiled(csm_engine* e) {
+  // pass 0 allocates (alloc's zero fill runs on the null stream: drained before pass 1 writes the
+  // copies on the engine stream), pass 1 re-lays every matrix
+  for (int pass = 0; pass < 2; ++pass) {
+  size_t idx = 0;
+  auto one = [&](const void* W, int N, int K, int wdt) {
+    if (wdt != WDT_BF16 && wdt != WDT_Q4) return;
+    if (pass == 0) {
+      if (idx++ == e->tiled_bufs.size()) e->tiled_bufs.push_back(e->alloc(gemm_tiled_bytes(N, K, wdt)));
+      return;
+    }
+    void* T = e->tiled_bufs[idx++];
+    launch_gemm_retile(W, T, N, K, wdt, e->st);
+    e->ws.tiled[W] = T;
+  };
+  for (Stack* s : {&e->bb, &e->dec})
+    for (LayerW& l : s->L) {
+      const int D = s->d.hidden, F = s->d.intermediate;
+      one(l.wqkv, s->qkv_rows(), D, e->wdt);
+      one(l.wo, D, s->q_dim(), e->wdt);
+      one(l.wgu, 2 * F, D, e->wdt);
+      one(l.wd, D, F, e->wdt);
+    }
+  one(e->proj, e->Dd, e->D, e->wdt);
+  one(e->c0_head, e->Vpad, e->D, e->wdt);
+  if (e->head_wdt == WDT_BF16)
+    for (int cb = 0; cb < e->K - 1; ++cb) one((const char*)e->audio_head + (size_t)cb * e->Vpad * e->Dd * 2, e->Vpad, e->Dd, WDT_BF16);
+  HIPCHK(hipDeviceSynchronize());
+  }
+  HIPCHK(hipGetLastError());
+  e->tiled_dirty = false;
+}
+
 // proj_tab[cb] = projection(E_a rows of codebook cb), computed by the projection GEMV itself
 // (per-row arithmetic identical to the per-step launch it replaces).
 void build_proj_table(csm_engine* e) {
@@ -797,6 +839,7 @@ int csm_load_tensor(csm_engine* e, const char* cname, const void* host, int src_
       if (shp != std::vector<int64_t>(want)) throw CsmError(CSM_ERR_ARG, "shape mismatch for " + name);
     };
     if (name.rfind("decoder.layers.0.", 0) == 0) e->proj_tab_dirty = true;  // feeds the folded layer-0 QKV table
+    e->tiled_dirty = true;
     if (e->wdt == WDT_Q4 && load_q4(e, name, host, src_dtype, shp)) return CSM_OK;
     if (src_dtype == CSM_U32) throw CsmError(CSM_ERR_ARG, "packed int4 tensor " + name + " needs a CSM_Q4 engine");
     const size_t es = e->wsz;
@@ -947,6 +990,10 @@ int csm_quantize(csm_engine* e, int group_size, int bits) {
     e->head_wdt = old;
     e->wdt = WDT_Q4;
     e->proj_tab_dirty = true;
+    for (void* t : e->tiled_bufs) e->release(t);  // re-sized for int4 at the next csm_begin
+    e->tiled_bufs.clear();
+    e->ws.tiled.clear();
+    e->tiled_dirty = true;
     e->g_B = -1;
   }
   CSM_CATCH
@@ -959,6 +1006,7 @@ int csm_begin(csm_engine* e, int B, const uint64_t* seeds, float temperature, in
     if (temperature < 0.f) throw CsmError(CSM_ERR_ARG, "temperature must be >= 0");
     HIPCHK(hipSetDevice(e->dev));
     ensure_batch(e, B);
+    if (e->tiled_dirty) build_tiled(e);
     if (e->proj_tab_dirty) build_proj_table(e);
     e->pos_host.assign(B, -1);
     e->B = B;
@@ -1259,7 +1307,13 @@ int csm_linear(csm_engine* e, const char* name, int M, const float* x, float* y)
     HIPCHK(hipMemcpyAsync(dx.p, x, (size_t)M * K * 4, hipMemcpyHostToDevice, e->st));
     GemvParams g = gp(e);
     g.W = W; g.N = N; g.K = K; g.x = (const float*)dx.p; g.xs = K; g.M = M; g.out = (float*)dy.p; g.os = N;
-    g.no_mfma = 1;  // the GEMV's fp32 arithmetic at any row count (no split-K scratch needed)
+    // default: the GEMV's fp32 arithmetic at any row count; option "linear_mfma": the batched
+    // frame's MFMA GEMM where eligible (its split-K scratch reserved here: captured graphs re-capture)
+    g.no_mfma = !(e->linear_mfma && gemm_mfma_eligible(N, K, M, wdt));
+    if (!g.no_mfma) {
+      if (e->tiled_dirty) build_tiled(e);
+      if (gemm_reserve(e->ws, N, K, M)) e->g_B = -1;
+    }
     launch_gemv(g, wdt, EPI_STORE, 0, e->st, 2);
     HIPCHK(hipGetLastError());
     std::vector<float> full((size_t)M * N);
@@ -1280,6 +1334,7 @@ int csm_bench_gemv(csm_engine* e, int which, int M, int iters, float* avg_us, do
   CSM_TRY {
     if (M <= 0 || M > 2 * e->B_max || iters <= 0) throw CsmError(CSM_ERR_ARG, "bad bench arguments");
     HIPCHK(hipSetDevice(e->dev));
+    if (e->tiled_dirty) build_tiled(e);
     Stack& s = (which / 4 == 0) ? e->bb : e->dec;
     const int tag = (which / 4 == 0) ? 0 : 1;
     float* x = (which / 4 == 0) ? e->x : e->dx;
@@ -1380,7 +1435,10 @@ int csm_set_option(csm_engine* e, const char* key, int value) {
     }
     else if (k == "nt_mask") gemv_set_nt_mask(value);
     else if (k == "gemv_xl") gemv_set_xl(value);
-    else if (k == "fold_proj") {
+    else if (k == "linear_mfma") {
+      if (!e) throw CsmError(CSM_ERR_ARG, "linear_mfma needs an engine");
+      e->linear_mfma = value != 0;
+    } else if (k == "fold_proj") {
       if (!e) throw CsmError(CSM_ERR_ARG, "fold_proj needs an engine");
       e->fold_proj = value != 0;
     }

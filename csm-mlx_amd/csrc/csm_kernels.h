@@ -1,5 +1,7 @@
 // Kernel parameter blocks and launchers shared by the CSM engine and the Mimi codec.
 #pragma once
+#include <unordered_map>
+
 #include "common.h"
 
 enum { WDT_F32 = 0, WDT_BF16 = 1, WDT_Q4 = 2 };  // WDT_Q4: MLX affine int4, group 64 (common.h layout)
@@ -21,13 +23,15 @@ __device__ __forceinline__ long long acc_slots_sum(const long long* a, size_t ss
   return t;
 }
 
-// Split-K scratch of the MFMA path, owned by one engine (csm_engine::ws): slice partials and arrival
-// tickets, sized by gemm_reserve outside graph capture.
+// MFMA-path state owned by one engine (csm_engine::ws): split-K slice partials and arrival tickets,
+// sized by gemm_reserve outside graph capture, and the fragment-tiled copy of every weight matrix
+// the matrix cores read (row-major matrix -> its tiled copy, gemm_retile).
 struct GemmWs {
   float* kpart = nullptr;
   size_t bytes = 0;
   unsigned* tickets = nullptr;
   size_t n = 0;
+  std::unordered_map<const void*, const void*> tiled;
 };
 
 struct GemvParams {
@@ -71,6 +75,7 @@ struct GemvParams {
   int acc_ss;             // elements between accumulator slots
   // MFMA path split-K (set by launch_gemm_mfma from ws): slice partials [ksplit][M][N], sum-of-squares [ksplit][M]
   GemmWs* ws;            // the calling engine's scratch (host pointer; required for split launches)
+  const void* Wt;        // the weight's fragment-tiled copy (looked up in ws->tiled by launch_gemm_mfma)
   float* kpart;          // [tile][m chunk][slice][slab] split-K slice partials (+ sum x^2), written sc1
   unsigned* kticket;     // [tile][m chunk] arrival tickets (zero between launches)
   int ksplit;
@@ -310,10 +315,16 @@ bool gemv_q4_supported(int N, int K);
 // ---- batched projections on MFMA (gemm_kernels.hip)
 constexpr int GEMM_MFMA_MIN_M = 8;  // rows at which a bf16 projection leaves the GEMV for the matrix cores
 bool gemm_mfma_eligible(int N, int K, int M, int wdt);
-int gemm_blocks(int N);  // row-tile blocks (= arg-max partials per row)
+int gemm_tiles(int N, int K, int M, int wdt);  // row-tile blocks of an MFMA launch (= arg-max partials per row)
 void launch_gemm_mfma(const GemvParams& p, int wdt, bool nt, hipStream_t st);
 // pre-size ws for (N, K) at any row count <= M (outside graph capture); true if it reallocated
 bool gemm_reserve(GemmWs& ws, int N, int K, int M);
+// Fragment-tiled weight copy for the MFMA path: per 32-row tile and 64-K stage, the bytes each lane
+// of a wave loads for v_mfma_f32_32x32x16_bf16's B operand, contiguous (bf16: 4 KB = 4 steps x 64
+// lanes x 16 B; int4: 1 KB of nibbles, then a [tile][stage][32] block of scale|bias words); rows
+// past N are zero.
+size_t gemm_tiled_bytes(int N, int K, int wdt);
+void launch_gemm_retile(const void* W, void* T, int N, int K, int wdt, hipStream_t st);
 void gemm_ws_free(GemmWs& ws);
 // dense decoder-input rows from a table (codes resolved from arg-max partials), see gather_rows_kernel
 void launch_gather_rows(const GemvParams& p, int wdt, hipStream_t st);

@@ -1060,7 +1060,7 @@ static void launch_gemv_t(const GemvParams& p, hipStream_t st) {
 }
 
 int gemv_partials(int N, int K, int M, int wdt) {
-  if (gemm_mfma_eligible(N, K, M, wdt)) return gemm_blocks(N);
+  if (gemm_mfma_eligible(N, K, M, wdt)) return gemm_tiles(N, K, M, wdt);
   const int rpb = wdt == WDT_Q4 ? gemv_q4_rows_per_block(N, K, M) : gemv_rows_per_block(N, K, M);
   return (N + rpb - 1) / rpb;
 }

@@ -45,7 +45,7 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) unsigned int gu32;
 typedef __attribute__((address_space(1))) const f32x4_t gcf32x4;
 
-constexpr int GP_ROWS = 64, GP_KC = 64;  // weight rows per block, K per stage (= Q4_GROUP)
+constexpr int GP_KC = 64;  // K per stage (= Q4_GROUP)
 constexpr int GK_MAX_SLICES = 16;
 static_assert(GP_KC == Q4_GROUP, "one int4 group per stage");
 
@@ -67,19 +67,31 @@ __device__ __forceinline__ void split3_4(const float (&v)[4], u32x2_t& hi, u32x2
   lo = u32x2_t{l[0] | ((unsigned)l[1] << 16), l[2] | ((unsigned)l[3] << 16)};
 }
 
-// bf16 bits of the small integer n in [0, 15] (exact)
-__device__ __forceinline__ unsigned q_bits(unsigned n) { return __float_as_uint((float)n) >> 16; }
+// one uint32 of MLX int4 nibbles (k = 8s .. 8s+7, low nibble first) -> 8 exact bf16 (u32x4 of pairs):
+// bytes of the even / odd nibbles through v_cvt_f32_ubyte*, the floats' high halves paired by v_perm
+__device__ __forceinline__ u32x4_t q4_word_bf16(uint32_t u) {
+  const uint32_t a = u & 0x0F0F0F0Fu, b = (u >> 4) & 0x0F0F0F0Fu;
+  u32x4_t o;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t fa = __float_as_uint((float)((a >> (8 * i)) & 0xFFu));
+    const uint32_t fb = __float_as_uint((float)((b >> (8 * i)) & 0xFFu));
+    o[i] = __builtin_amdgcn_perm(fb, fa, 0x07060302u);  // {hi16(fa), hi16(fb)}
+  }
+  return o;
+}
 
 // Split-K combine (the last slice of a tile to arrive): every slice's partial is read with 16-B sc1
-// buffer loads, KS * U of them in flight per thread before the first add (one round trip per 4096
-// floats at U * KS = 16), and summed in slice order (deterministic).
+// buffer loads, KS * U of them in flight per thread before the first add, and summed in slice order
+// (deterministic).
 constexpr int GP_RSRC3 = 0x00020000;  // buffer descriptor word 3 (raw 32-bit format)
 constexpr int GP_SC1 = 16;            // cache policy: sc1 (agent-coherent, as __hip_atomic_load/store)
-template <int KS, int NB>
-__device__ __forceinline__ void gp_combine(__amdgpu_buffer_rsrc_t rs, float (*ct)[GP_ROWS + 1], float* ssb,
+constexpr int GP_NT = 2;              // cache policy: non-temporal
+template <int KS, int NB, int NBR>
+__device__ __forceinline__ void gp_combine(__amdgpu_buffer_rsrc_t rs, float (*ct)[NBR + 1], float* ssb,
                                            int mrows, bool norm, int slab_f, int tid) {
   constexpr int U = KS >= 16 ? 1 : 16 / KS;
-  const int nq = mrows * (GP_ROWS / 4);
+  const int nq = mrows * (NBR / 4);
   for (int q0 = tid; q0 < nq; q0 += 256 * U) {
     f32x4_t v[U][KS];
 #pragma unroll
@@ -95,7 +107,7 @@ __device__ __forceinline__ void gp_combine(__amdgpu_buffer_rsrc_t rs, float (*ct
         f32x4_t sum = v[u][0];
 #pragma unroll
         for (int s = 1; s < KS; ++s) sum += v[u][s];
-        const int ml = q / (GP_ROWS / 4), j = (q % (GP_ROWS / 4)) * 4;
+        const int ml = q / (NBR / 4), j = (q % (NBR / 4)) * 4;
         ct[ml][j] = sum.x;
         ct[ml][j + 1] = sum.y;
         ct[ml][j + 2] = sum.z;
@@ -107,7 +119,7 @@ __device__ __forceinline__ void gp_combine(__amdgpu_buffer_rsrc_t rs, float (*ct
     float v[KS];
 #pragma unroll
     for (int s = 0; s < KS; ++s)
-      v[s] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (NB * GP_ROWS + tid) * 4, s * slab_f * 4, GP_SC1));
+      v[s] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (NB * NBR + tid) * 4, s * slab_f * 4, GP_SC1));
     float sum = v[0];
 #pragma unroll
     for (int s = 1; s < KS; ++s) sum += v[s];
@@ -115,93 +127,96 @@ __device__ __forceinline__ void gp_combine(__amdgpu_buffer_rsrc_t rs, float (*ct
   }
 }
 
-template <bool Q4, int MT, bool NT, int PD>
-__global__ __launch_bounds__(256) void gemm_pipe_kernel(GemvParams p) {
+// Block = 4 waves over NBR weight rows x 32*MT batch rows x one K slice, stages of 64 K (one int4
+// group).  The activations are the MFMA A operand (rows = batch rows), the weights the B operand
+// (columns = weight rows): every lane's 16 accumulators then share ONE weight row, whose int4
+// scale / bias it loaded itself.  Weights go global -> registers in fragment order (no LDS): with
+// the K order permuted inside a stage (step s, half h <-> k = 32h + 8s + j, the same permutation on
+// both operands) lane (r, h) reads 64 contiguous bytes of weight row r per bf16 stage (16 for int4).
+// Activations go global -> registers -> (RMSNorm weight, sum of squares, hi/mid/lo split) -> LDS
+// once per stage and are shared by the block's NBR / 32 row tiles.  NBR = 256: 2 row tiles per
+// wave; 128: one; 64: two waves per row tile split each stage's steps (summed in a fixed order).
+template <bool Q4, int MT, int NBR, int PD, bool NT>
+__global__ __launch_bounds__(256) void gemm_wide_kernel(GemvParams p) {
   constexpr int NB = MT * 32;
-  constexpr int A_BYTES = 2 * 2 * 4 * 64 * 16;        // [buf][row tile][step][lane] x 16 B
-  constexpr int B_BYTES = 2 * 3 * MT * 4 * 64 * 16;   // [buf][hi/mid/lo][batch tile][step][lane] x 16 B
-  __shared__ __attribute__((aligned(16))) unsigned char smem[A_BYTES + B_BYTES];
-  __shared__ __attribute__((aligned(16))) uint32_t sbs[2][GP_ROWS];  // int4: {scale, bias} of the stage's group
-  __shared__ float xsum[2][NB];                                      // int4: sum of the stage's x per batch row
+  constexpr int KW = NBR == 64 ? 2 : 1;    // waves per row tile
+  constexpr int RTW = NBR == 256 ? 2 : 1;  // row tiles per wave
+  constexpr int NS = 4 / KW;               // k-steps per wave per stage
+  constexpr int SLOTS = 65;                // 16-B slots per (part, batch tile, step) block: lane l at l + l / 32
+  constexpr int XS_BYTES = 2 * 3 * MT * 4 * SLOTS * 16;
+  constexpr int CT_BYTES = NB * (NBR + 1) * 4;
+  constexpr int SM = XS_BYTES > CT_BYTES ? XS_BYTES : CT_BYTES;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SM];
+  __shared__ __attribute__((aligned(16))) float xsum[2][NB];  // int4: the stage's sum of x per batch row
   __shared__ float ssb[NB];
   __shared__ int last;
-  auto As = [&](int buf, int t, int s) { return reinterpret_cast<u32x4_t*>(smem) + ((buf * 2 + t) * 4 + s) * 64; };
-  auto Bs = [&](int buf, int part, int t, int s) {
-    return reinterpret_cast<u32x4_t*>(smem + A_BYTES) + (((buf * 3 + part) * MT + t) * 4 + s) * 64;
+  auto Xs = [&](int buf, int part, int t, int s) {
+    return reinterpret_cast<u32x4_t*>(smem) + (((buf * 3 + part) * MT + t) * 4 + s) * SLOTS;
   };
-  static_assert(NB * (GP_ROWS + 1) * 4 <= A_BYTES + B_BYTES, "C tile aliases the operand tiles");
-  float (*ct)[GP_ROWS + 1] = reinterpret_cast<float (*)[GP_ROWS + 1]>(smem);  // after the K loop
+  float (*ct)[NBR + 1] = reinterpret_cast<float (*)[NBR + 1]>(smem);  // after the K loop
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int r = lane & 31, h = lane >> 5;
-  const int wr = wave & 1, wc = wave >> 1;  // MT = 2: batch tile; MT = 1: K-step half
-  const int tile = blockIdx.x, n0 = tile * GP_ROWS;
+  const int r = lane & 31, h = lane >> 5, slot = lane + h;
+  const int tile = blockIdx.x, n0 = tile * NBR;
   const int mc = blockIdx.z, m0 = mc * NB, nchunks = gridDim.z;
   const int Kblk = p.K / p.ksplit, kslice = blockIdx.y * Kblk, nst = Kblk / GP_KC;
   const bool norm = p.nw != nullptr;
-  // staging maps
-  const int a_row = Q4 ? (tid >> 1) : (tid >> 2), a_seg = Q4 ? (tid & 1) : (tid & 3);
-  const bool a_on = !Q4 || tid < 128;
-  const size_t a_grow = (size_t)min(n0 + a_row, p.N - 1);
-  const uint8_t* Wq = (const uint8_t*)p.W;
-  const uint32_t* SB = Q4 ? reinterpret_cast<const uint32_t*>(Wq + q4_sb_offset(p.N, p.K)) : nullptr;
+  const int kh = KW == 2 ? (wave >> 1) : 0;
+  const int rt0 = KW == 2 ? (wave & 1) : wave * RTW;
+  // this lane's weight bytes in the fragment-tiled copy (gemm_retile): row tile T, stage kst at
+  // T * nks + kst blocks of 4 KB (bf16; + 1 KB per step) or 1 KB (int4; scale|bias words after)
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.Wt), 0, 0x7fffffff, GP_RSRC3);
+  const int nks = p.K / GP_KC, nt32 = (p.N + 31) / 32;
+  int wv[RTW], sv[RTW];
+#pragma unroll
+  for (int i = 0; i < RTW; ++i) {
+    const int T = min(n0 / 32 + rt0 + i, nt32 - 1);
+    wv[i] = Q4 ? T * nks * 1024 + 16 * lane : T * nks * 4096 + 16 * lane + 1024 * NS * kh;
+    sv[i] = nt32 * nks * 1024 + (T * nks * 32 + r) * 4;
+  }
+  // activation staging map: thread -> batch row x_c + 16 i, k x_k4 .. x_k4 + 3 of the stage
   const int x_c = tid >> 4, x_k4 = (tid & 15) * 4;
+  const int st_h = x_k4 >> 5, st_s = (x_k4 >> 3) & 3, st_j = (x_k4 >> 2) & 1;
   float ss[NB / 16];
 #pragma unroll
   for (int i = 0; i < NB / 16; ++i) ss[i] = 0.f;
-  // register ring: PD stages in flight while one is multiplied (nst % PD == 0, host-checked)
   struct Stage {
-    u32x4_t ar[2];
-    uint32_t asb;
+    u32x4_t w[RTW][Q4 ? 1 : NS];
+    uint32_t sb[RTW];
     f32x4_t xr[NB / 16];
     f32x4_t nwr;
   };
   Stage sg[PD];
-  // stage st >= nst is a placeholder: loads from the (L2-hot) activation row, nothing used
   const float* nwp = norm ? p.nw : p.x;
+  // Straight-line loads (no branch between a load and the waits that follow it, so the compiler's
+  // vmcnt counts stay exact): stages past the slice read through zero-sized buffer descriptors
+  // (out of range: zeros, no memory traffic).  Activations first: a wait for the next stage's
+  // activations (its LDS store) then leaves every younger weight load of the ring in flight
+  // (vmcnt retires in issue order).
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.x), 0, 0x7fffffff, GP_RSRC3);
+  const __amdgpu_buffer_rsrc_t nrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(nwp), 0, 0x7fffffff, GP_RSRC3);
+  const __amdgpu_buffer_rsrc_t zrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.Wt), 0, 0, GP_RSRC3);
+  int xv[NB / 16];
+#pragma unroll
+  for (int i = 0; i < NB / 16; ++i) xv[i] = (min(m0 + x_c + 16 * i, p.M - 1) * p.xs + x_k4) * 4;
   auto load = [&](int st, Stage& g) {
-    const bool junk = st >= nst;
-    const int kc = kslice + min(st, nst - 1) * GP_KC;
-    if (a_on) {
+    const bool live = st < nst;
+    const int kc = kslice + (live ? st : 0) * GP_KC;
+    const __amdgpu_buffer_rsrc_t xr = live ? xrs : zrs, nr = live ? nrs : zrs, wr = live ? wrs : zrs;
+#pragma unroll
+    for (int i = 0; i < NB / 16; ++i) g.xr[i] = __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(xr, xv[i], kc * 4, 0));
+    g.nwr = __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(nr, x_k4 * 4, kc * 4, 0));
+#pragma unroll
+    for (int i = 0; i < RTW; ++i) {
       if constexpr (Q4) {
-        const u32x4_t* src = junk ? reinterpret_cast<const u32x4_t*>(p.x)
-                                  : reinterpret_cast<const u32x4_t*>(Wq + a_grow * (p.K / 2) + (kc + 32 * a_seg) / 2);
-        g.ar[0] = NT ? __builtin_nontemporal_load(src) : *src;
-        const uint32_t* sbp = junk ? reinterpret_cast<const uint32_t*>(p.x) : SB + a_grow * (p.K / Q4_GROUP) + kc / Q4_GROUP;
-        g.asb = *sbp;
+        g.w[i][0] = __builtin_amdgcn_raw_buffer_load_b128(wr, wv[i], (kc / GP_KC) * 1024, NT ? GP_NT : 0);
+        g.sb[i] = __builtin_amdgcn_raw_buffer_load_b32(wr, sv[i], (kc / GP_KC) * 128, 0);
       } else {
-        const u32x4_t* src = junk ? reinterpret_cast<const u32x4_t*>(p.x)
-                                  : reinterpret_cast<const u32x4_t*>((const bf16_t*)p.W + a_grow * p.K + kc + 16 * a_seg);
-        g.ar[0] = NT ? __builtin_nontemporal_load(src) : src[0];
-        g.ar[1] = NT ? __builtin_nontemporal_load(src + 1) : src[1];
+#pragma unroll
+        for (int s = 0; s < NS; ++s) g.w[i][s] = __builtin_amdgcn_raw_buffer_load_b128(wr, wv[i], (kc / GP_KC) * 4096 + 1024 * s, NT ? GP_NT : 0);
       }
     }
-#pragma unroll
-    for (int i = 0; i < NB / 16; ++i) {
-      const int m = min(m0 + x_c + 16 * i, p.M - 1);
-      g.xr[i] = *(const gcf32x4*)(p.x + (size_t)m * p.xs + kc + x_k4);
-    }
-    g.nwr = *(const gcf32x4*)(nwp + kc + x_k4);
   };
   auto store = [&](const Stage& g, int buf, bool live) {
-    if (a_on) {
-      const int t = a_row >> 5, ln = a_row & 31;
-      if constexpr (Q4) {
-#pragma unroll
-        for (int w = 0; w < 4; ++w) {  // 8 consecutive k per word: step 2*seg + w/2, half w&1
-          const uint32_t u = g.ar[0][w];
-          unsigned b[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) b[j] = q_bits((u >> (4 * j)) & 15u);
-          const int s = 2 * a_seg + (w >> 1), hh = w & 1;
-          As(buf, t, s)[ln + 32 * hh] = u32x4_t{b[0] | (b[1] << 16), b[2] | (b[3] << 16), b[4] | (b[5] << 16), b[6] | (b[7] << 16)};
-        }
-        if (a_seg == 0) sbs[buf][a_row] = g.asb;
-      } else {
-        As(buf, t, a_seg)[ln] = g.ar[0];
-        As(buf, t, a_seg)[ln + 32] = g.ar[1];
-      }
-    }
-    const int s = x_k4 >> 4, hh = (x_k4 >> 3) & 1, j0 = x_k4 & 7;
 #pragma unroll
     for (int i = 0; i < NB / 16; ++i) {
       const int c = x_c + 16 * i;
@@ -222,49 +237,87 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemvParams p) {
       }
       u32x2_t hi, mid, lo;
       split3_4(v, hi, mid, lo);
-      const int ln = (c & 31) + 32 * hh;
-      *(reinterpret_cast<u32x2_t*>(&Bs(buf, 0, c >> 5, s)[ln]) + (j0 >> 2)) = hi;
-      *(reinterpret_cast<u32x2_t*>(&Bs(buf, 1, c >> 5, s)[ln]) + (j0 >> 2)) = mid;
-      *(reinterpret_cast<u32x2_t*>(&Bs(buf, 2, c >> 5, s)[ln]) + (j0 >> 2)) = lo;
+      const int sl = (c & 31) + 33 * st_h;
+      *(reinterpret_cast<u32x2_t*>(&Xs(buf, 0, c >> 5, st_s)[sl]) + st_j) = hi;
+      *(reinterpret_cast<u32x2_t*>(&Xs(buf, 1, c >> 5, st_s)[sl]) + st_j) = mid;
+      *(reinterpret_cast<u32x2_t*>(&Xs(buf, 2, c >> 5, st_s)[sl]) + st_j) = lo;
     }
   };
-  f32x16_t acc = f32x16_t{};
+  f32x16_t acc[MT][RTW];
+#pragma unroll
+  for (int t = 0; t < MT; ++t)
+#pragma unroll
+    for (int i = 0; i < RTW; ++i) acc[t][i] = f32x16_t{};
 #pragma unroll
   for (int d = 0; d < PD; ++d) load(d, sg[d]);
   store(sg[0], 0, true);
   __syncthreads();
-  const int s0 = MT == 2 ? 0 : 2 * wc, s1 = MT == 2 ? 4 : 2 * wc + 2;
-  const int bt = MT == 2 ? wc : 0;
   for (int it0 = 0; it0 < nst; it0 += PD) {
 #pragma unroll
     for (int d = 0; d < PD; ++d) {
       const int it = it0 + d, buf = it & 1;
-      load(it + PD, sg[d]);  // slot d's stage (it) is already in LDS
-      f32x16_t g = f32x16_t{};
+      const Stage& g = sg[d];
+      f32x16_t gq[MT][RTW];
+      if constexpr (Q4) {
 #pragma unroll
-      for (int s = s0; s < s1; ++s) {
-        const bf16x8_t a = __builtin_bit_cast(bf16x8_t, As(buf, wr, s)[lane]);
+        for (int t = 0; t < MT; ++t)
 #pragma unroll
-        for (int part = 0; part < 3; ++part) {
-          const bf16x8_t b = __builtin_bit_cast(bf16x8_t, Bs(buf, part, bt, s)[lane]);
-          if constexpr (Q4) g = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, g, 0, 0, 0);
-          else acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
-        }
+          for (int i = 0; i < RTW; ++i) gq[t][i] = f32x16_t{};
       }
-      if constexpr (Q4) {  // acc += scale * S_g + bias * X_g for this lane's 16 weight rows
-        const float xs = (MT == 2 || wc == 0) ? xsum[buf][32 * bt + r] : 0.f;
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const u32x4_t sb = *reinterpret_cast<const u32x4_t*>(&sbs[buf][32 * wr + 8 * q + 4 * h]);
+      for (int s = 0; s < NS; ++s) {
+        const int step = NS * kh + s;
+        bf16x8_t b[RTW];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int j = 4 * q + e;
-            acc[j] = fmaf(bf16_lo(sb[e]), g[j], acc[j]);
-            acc[j] = fmaf(bf16_hi(sb[e]), xs, acc[j]);
+        for (int i = 0; i < RTW; ++i) {
+          if constexpr (Q4) {  // (KW = 2: the wave's half of the 4 words, selected without indexing)
+            const uint32_t word = KW == 2 ? (kh ? g.w[i][0][NS + s] : g.w[i][0][s]) : g.w[i][0][s];
+            b[i] = __builtin_bit_cast(bf16x8_t, q4_word_bf16(word));
+          } else {
+            b[i] = __builtin_bit_cast(bf16x8_t, g.w[i][s]);
+          }
+        }
+#pragma unroll
+        for (int t = 0; t < MT; ++t)
+#pragma unroll
+          for (int part = 0; part < 3; ++part) {
+            const bf16x8_t a = __builtin_bit_cast(bf16x8_t, Xs(buf, part, t, step)[slot]);
+#pragma unroll
+            for (int i = 0; i < RTW; ++i) {
+              if constexpr (Q4) gq[t][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b[i], gq[t][i], 0, 0, 0);
+              else acc[t][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b[i], acc[t][i], 0, 0, 0);
+            }
+          }
+      }
+      if constexpr (Q4) {  // acc += scale * S_g + bias * X_g: this lane's weight row, 16 batch rows
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+          float xs[16];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const f32x4_t x4 = kh == 0 ? *reinterpret_cast<const f32x4_t*>(&xsum[buf][32 * t + 8 * q + 4 * h]) : f32x4_t{};
+            xs[4 * q] = x4.x; xs[4 * q + 1] = x4.y; xs[4 * q + 2] = x4.z; xs[4 * q + 3] = x4.w;
+          }
+#pragma unroll
+          for (int i = 0; i < RTW; ++i) {
+            const float sc = bf16_lo(g.sb[i]), bi = bf16_hi(g.sb[i]);
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+              acc[t][i][j] = fmaf(sc, gq[t][i][j], acc[t][i][j]);
+              acc[t][i][j] = fmaf(bi, xs[j], acc[t][i][j]);
+            }
           }
         }
       }
-      store(sg[(d + 1) % PD], buf ^ 1, it + 1 < nst);  // the last one stores a placeholder
+      if constexpr (PD == 1) {  // one slot (mostly one-stage slices): refill it first, nothing to protect
+        if (it + 1 < nst) {
+          load(it + 1, sg[0]);
+          store(sg[0], buf ^ 1, true);
+        }
+      } else {
+        store(sg[(d + 1) % PD], buf ^ 1, it + 1 < nst);  // past the slice: zeros into the idle buffer
+        load(it + PD, sg[d]);
+      }
       __syncthreads();
     }
   }
@@ -278,30 +331,39 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemvParams p) {
       if ((tid & 15) == 0) ssb[x_c + 16 * i] = v;
     }
   }
-  // accumulators -> C tile [batch row][weight row]
-  if (MT == 2 || wc == 0) {
+  // accumulators -> C tile [batch row][weight row]; lane (r, h) register j: batch row
+  // (j & 3) + 8 (j >> 2) + 4 h of tile t, weight row r of row tile rt0 + i
+  if (kh == 0) {
 #pragma unroll
-    for (int j = 0; j < 16; ++j) ct[32 * (MT == 2 ? wc : 0) + r][32 * wr + (j & 3) + 8 * (j >> 2) + 4 * h] = acc[j];
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+      for (int i = 0; i < RTW; ++i)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) ct[32 * t + (j & 3) + 8 * (j >> 2) + 4 * h][32 * (rt0 + i) + r] = acc[t][i][j];
   }
   __syncthreads();
-  if (MT == 1 && wc == 1) {  // second K-step half, added in a fixed order
+  if constexpr (KW == 2) {  // second half of the steps, added in a fixed order
+    if (kh == 1) {
 #pragma unroll
-    for (int j = 0; j < 16; ++j) ct[r][32 * wr + (j & 3) + 8 * (j >> 2) + 4 * h] += acc[j];
+      for (int t = 0; t < MT; ++t)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) ct[32 * t + (j & 3) + 8 * (j >> 2) + 4 * h][32 * rt0 + r] += acc[t][0][j];
+    }
+    __syncthreads();
   }
-  __syncthreads();
   const int mrows = min(NB, p.M - m0);
   if (p.ksplit > 1) {
-    // slice partial = [NB][64] tile values, then [NB] sums of squares; 16-B write-through stores
-    const int slab_f = NB * (GP_ROWS + 1);
+    // slice partial = [NB][NBR] tile values, then [NB] sums of squares; 16-B write-through stores
+    const int slab_f = NB * NBR + NB;
     float* slab = p.kpart + ((size_t)(tile * nchunks + mc) * p.ksplit) * slab_f;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(slab, 0, p.ksplit * slab_f * 4, GP_RSRC3);
     const int mine = blockIdx.y * slab_f * 4;
-    for (int q = tid; q < mrows * (GP_ROWS / 4); q += 256) {
-      const int ml = q / (GP_ROWS / 4), j = (q % (GP_ROWS / 4)) * 4;
+    for (int q = tid; q < mrows * (NBR / 4); q += 256) {
+      const int ml = q / (NBR / 4), j = (q % (NBR / 4)) * 4;
       const f32x4_t v = {ct[ml][j], ct[ml][j + 1], ct[ml][j + 2], ct[ml][j + 3]};
       __builtin_amdgcn_raw_buffer_store_b128(v, rs, q * 16, mine, GP_SC1);
     }
-    if (norm && tid < mrows) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ssb[tid]), rs, (NB * GP_ROWS + tid) * 4, mine, GP_SC1);
+    if (norm && tid < mrows) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(ssb[tid]), rs, (NB * NBR + tid) * 4, mine, GP_SC1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
@@ -313,15 +375,15 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemvParams p) {
     __syncthreads();
     if (!last) return;
     switch (p.ksplit) {
-      case 2: gp_combine<2, NB>(rs, ct, ssb, mrows, norm, slab_f, tid); break;
-      case 4: gp_combine<4, NB>(rs, ct, ssb, mrows, norm, slab_f, tid); break;
-      case 8: gp_combine<8, NB>(rs, ct, ssb, mrows, norm, slab_f, tid); break;
-      default: gp_combine<16, NB>(rs, ct, ssb, mrows, norm, slab_f, tid); break;
+      case 2: gp_combine<2, NB, NBR>(rs, ct, ssb, mrows, norm, slab_f, tid); break;
+      case 4: gp_combine<4, NB, NBR>(rs, ct, ssb, mrows, norm, slab_f, tid); break;
+      case 8: gp_combine<8, NB, NBR>(rs, ct, ssb, mrows, norm, slab_f, tid); break;
+      default: gp_combine<16, NB, NBR>(rs, ct, ssb, mrows, norm, slab_f, tid); break;
     }
     __syncthreads();
   }
-  for (int e = tid; e < mrows * (GP_ROWS / 2); e += 256) {
-    const int ml = e / (GP_ROWS / 2), rp = (e % (GP_ROWS / 2)) * 2;
+  for (int e = tid; e < mrows * (NBR / 2); e += 256) {
+    const int ml = e / (NBR / 2), rp = (e % (NBR / 2)) * 2;
     const int n = n0 + rp;
     float va = ct[ml][rp], vb = ct[ml][rp + 1];
     if (norm) {
@@ -339,7 +401,7 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemvParams p) {
     __syncthreads();
     if (tid < mrows) {
       unsigned long long best = 0;
-      for (int j = 0; j < GP_ROWS; ++j) {
+      for (int j = 0; j < NBR; ++j) {
         const int n = n0 + j;
         if (n < p.n_valid) {
           const unsigned long long key = pack_argmax(ct[tid][j], n);
@@ -352,23 +414,29 @@ __global__ __launch_bounds__(256) void gemm_pipe_kernel(GemvParams p) {
 }
 
 // ---------------------------------------------------------------------------- host side
-// K slices are added until the grid has this many blocks (measured best: 256 for <= 32 batch rows,
-// 512 above -- configs 4 / 5); CSM_PIPE_BLOCKS overrides (lab sweeps)
-static int g_pipe_target_env = [] { const char* e = getenv("CSM_PIPE_BLOCKS"); return e ? atoi(e) : 0; }();
-static int pipe_target(int M) { return g_pipe_target_env > 0 ? g_pipe_target_env : (M > 32 ? 512 : 256); }
-// deepest register prefetch ring (stages in flight, 1 / 2 / 4: 4 for <= 32 batch rows, 2 above, where
-// the 64-row stages cost twice the registers); CSM_PIPE_PD overrides
-static int g_pipe_pd_env = [] { const char* e = getenv("CSM_PIPE_PD"); return e ? atoi(e) : 0; }();
-static int pipe_pd_cap(int M) { return g_pipe_pd_env > 0 ? g_pipe_pd_env : (M > 32 ? 2 : 4); }
-
-// K slices: doubled while the grid has fewer than pipe_target(M) blocks and every slice keeps >= 2
-// stages; arg-max heads are split too (the last slice runs the arg-max epilogue).
-static int gemm_ksplit(int N, int K, int M) {
-  const int tiles = (N + GP_ROWS - 1) / GP_ROWS, chunks = (M + 63) / 64;
+// Shape of one launch: rows per block (NBR) and K slices, from csm_1b microbenchmarks
+// (tools/gemm_bench.py, profiles/r02_gemm_shapes.txt).  256-row blocks pay off only for the int4
+// backbone gate/up (the activation split shared by 8 row tiles outweighs the longer split-K combine);
+// 128 for the other wide int4 projections and the bf16 gate/up at 64 batch rows; 64 elsewhere.  K
+// slices are doubled until the grid has >= 256 blocks (every CU streaming) while each slice keeps
+// whole stages.  CSM_GEMM_NBR / CSM_GEMM_BLOCKS override (lab sweeps).
+static int g_nbr_env = [] { const char* e = getenv("CSM_GEMM_NBR"); return e ? atoi(e) : 0; }();
+static int g_blocks_env = [] { const char* e = getenv("CSM_GEMM_BLOCKS"); return e ? atoi(e) : 0; }();
+static int gemm_nbr(int N, int K, int M, bool q4) {
+  if (g_nbr_env == 64 || g_nbr_env == 128 || g_nbr_env == 256) return g_nbr_env;
+  if (q4) {
+    if (N >= 8192 && K >= 2048) return 256;
+    if (N >= 8192 || (N >= 2048 && (N >= 3072 || K >= 8192))) return 128;
+    return 64;
+  }
+  return (N >= 8192 && M > 32) ? 128 : 64;
+}
+static int gemm_ksplit(int N, int K, int M, bool q4) {
+  const int nbr = gemm_nbr(N, K, M, q4);
+  const int tiles = (N + nbr - 1) / nbr, chunks = (M + 63) / 64;
+  const int target = g_blocks_env > 0 ? g_blocks_env : 256;
   int ks = 1;
-  while (tiles * chunks * ks < pipe_target(M) && ks < GK_MAX_SLICES && K % (GP_KC * ks * 2) == 0 &&
-         K / (ks * 2) >= 2 * GP_KC)
-    ks *= 2;
+  while (tiles * chunks * ks < target && ks < GK_MAX_SLICES && K % (GP_KC * ks * 2) == 0) ks *= 2;
   return ks;
 }
 
@@ -376,24 +444,36 @@ bool gemm_mfma_eligible(int N, int K, int M, int wdt) {
   return M >= GEMM_MFMA_MIN_M && N % 2 == 0 && (wdt == WDT_BF16 || wdt == WDT_Q4) && K % GP_KC == 0;
 }
 
-int gemm_blocks(int N) { return (N + GP_ROWS - 1) / GP_ROWS; }
+int gemm_tiles(int N, int K, int M, int wdt) { const int nbr = gemm_nbr(N, K, M, wdt == WDT_Q4); return (N + nbr - 1) / nbr; }
 
 // split-K slab bytes and ticket count of one (N, K, M) launch
-static size_t gemm_need(int N, int K, int M, size_t& tk) {
-  const int ks = gemm_ksplit(N, K, M);
-  const int MT = M > 32 ? 2 : 1;
-  const size_t tiles = gemm_blocks(N), chunks = (M + MT * 32 - 1) / (MT * 32);
+static size_t gemm_need(int N, int K, int M, bool q4, size_t& tk) {
+  const int ks = gemm_ksplit(N, K, M, q4);
+  const int MT = M > 32 ? 2 : 1, nbr = gemm_nbr(N, K, M, q4);
+  const size_t tiles = (N + nbr - 1) / nbr, chunks = (M + MT * 32 - 1) / (MT * 32);
   tk = tiles * chunks;
-  return ks > 1 ? tiles * chunks * ks * (size_t)MT * 32 * (GP_ROWS + 1) * 4 : 0;
+  return ks > 1 ? tiles * chunks * ks * (size_t)MT * 32 * (nbr + 1) * 4 : 0;
 }
+
+static constexpr int gemm_pd_cap(bool q4, int mt, int nbr) { return nbr == 256 ? ((q4 && mt == 2) ? 2 : 4) : ((mt == 2 || q4) ? 4 : 8); }
 
 void launch_gemm_mfma(const GemvParams& p0, int wdt, bool nt, hipStream_t st) {
   GemvParams p = p0;
-  const int ks = gemm_ksplit(p.N, p.K, p.M);
+  const bool q4 = wdt == WDT_Q4;
+  p.Wt = nullptr;
+  if (p.ws) {
+    const auto ti = p.ws->tiled.find(p.W);
+    if (ti != p.ws->tiled.end()) p.Wt = ti->second;
+  }
+  if (!p.Wt) {  // built by the engine (launch_gemm_retile) outside graph capture
+    fprintf(stderr, "csm: no fragment-tiled copy of an N=%d K=%d weight for the MFMA path\n", p.N, p.K);
+    abort();
+  }
+  const int ks = gemm_ksplit(p.N, p.K, p.M, q4);
   p.ksplit = ks;
   if (ks > 1) {
     size_t tk = 0;
-    const size_t need = gemm_need(p.N, p.K, p.M, tk);
+    const size_t need = gemm_need(p.N, p.K, p.M, q4, tk);
     if (!p.ws || need > p.ws->bytes || tk > p.ws->n) {  // reserved by gemm_reserve outside graph capture
       fprintf(stderr, "csm: split-K scratch not reserved for N=%d K=%d M=%d\n", p.N, p.K, p.M);
       abort();
@@ -402,18 +482,65 @@ void launch_gemm_mfma(const GemvParams& p0, int wdt, bool nt, hipStream_t st) {
     p.kticket = p.ws->tickets;
   }
   // batch chunks of 64 (MT 2) or one chunk of 32 (MT 1) on grid.z
-  const int MT = p.M > 32 ? 2 : 1;
-  const dim3 g3(gemm_blocks(p.N), ks, (p.M + MT * 32 - 1) / (MT * 32));
+  const int MT = p.M > 32 ? 2 : 1, nbr = gemm_nbr(p.N, p.K, p.M, q4);
+  const dim3 g3((p.N + nbr - 1) / nbr, ks, (p.M + MT * 32 - 1) / (MT * 32));
   const int nst = p.K / ks / GP_KC;
-  const int cap = pipe_pd_cap(p.M);
-  const int pd = (nst % 4 == 0 && cap >= 4) ? 4 : ((nst % 2 == 0 && cap >= 2) ? 2 : 1);
-#define GP_K(Q_, MT_, PD_) do { if (nt) hipLaunchKernelGGL((gemm_pipe_kernel<Q_, MT_, true, PD_>), g3, dim3(256), 0, st, p); \
-                                else hipLaunchKernelGGL((gemm_pipe_kernel<Q_, MT_, false, PD_>), g3, dim3(256), 0, st, p); } while (0)
-#define GP_L(Q_, MT_) do { if (pd == 4) GP_K(Q_, MT_, 4); else if (pd == 2) GP_K(Q_, MT_, 2); else GP_K(Q_, MT_, 1); } while (0)
-  if (wdt == WDT_Q4) { if (MT == 2) GP_L(true, 2); else GP_L(true, 1); }
-  else { if (MT == 2) GP_L(false, 2); else GP_L(false, 1); }
-#undef GP_L
-#undef GP_K
+  // ring depth (stages of weights in flight per wave): 4 on 256-row blocks (32 KB a stage per
+  // block), 8 on the smaller ones at 32 batch rows, 4 at 64; 2 where 4 would spill (int4 at 64
+  // batch rows x 256 weight rows)
+  const int pd_cap = gemm_pd_cap(wdt == WDT_Q4, MT, nbr);
+  int pd = 1;  // the deepest ring within the cap that divides the stage count
+  while (pd * 2 <= pd_cap && nst % (pd * 2) == 0) pd *= 2;
+#define GW_K(Q_, MT_, NBR_, PD_) do { if (nt) hipLaunchKernelGGL((gemm_wide_kernel<Q_, MT_, NBR_, PD_, true>), g3, dim3(256), 0, st, p); \
+                                      else hipLaunchKernelGGL((gemm_wide_kernel<Q_, MT_, NBR_, PD_, false>), g3, dim3(256), 0, st, p); } while (0)
+#define GW_C(Q_, MT_, NBR_, PD_) (PD_ < gemm_pd_cap(Q_, MT_, NBR_) ? PD_ : gemm_pd_cap(Q_, MT_, NBR_))
+#define GW_P(Q_, MT_, NBR_) do { if (pd == 8) GW_K(Q_, MT_, NBR_, GW_C(Q_, MT_, NBR_, 8)); else if (pd == 4) GW_K(Q_, MT_, NBR_, GW_C(Q_, MT_, NBR_, 4)); \
+                                 else if (pd == 2) GW_K(Q_, MT_, NBR_, 2); else GW_K(Q_, MT_, NBR_, 1); } while (0)
+#define GW_N(Q_, MT_) do { if (nbr == 256) GW_P(Q_, MT_, 256); else if (nbr == 128) GW_P(Q_, MT_, 128); else GW_P(Q_, MT_, 64); } while (0)
+  if (wdt == WDT_Q4) { if (MT == 2) GW_N(true, 2); else GW_N(true, 1); }
+  else { if (MT == 2) GW_N(false, 2); else GW_N(false, 1); }
+#undef GW_N
+#undef GW_C
+#undef GW_P
+#undef GW_K
+}
+
+// ---------------------------------------------------------------------------- tiled weight copies
+size_t gemm_tiled_bytes(int N, int K, int wdt) {
+  const size_t rows = (size_t)(N + 31) / 32 * 32;
+  return wdt == WDT_Q4 ? rows * K / 2 + rows * (K / Q4_GROUP) * 4 : rows * K * 2;
+}
+
+// block = one (row tile, stage): 64 lanes; lane (r, h) copies row 32T + r, k 64 kst + 32h + 8s + 0..7
+// (bf16, step s) or the 32 nibbles at k 64 kst + 32h (int4) -- the B-fragment permutation of
+// gemm_wide_kernel -- and lanes < 32 the int4 scale|bias word of row 32T + lane
+template <bool Q4>
+__global__ __launch_bounds__(64) void gemm_retile_kernel(const uint8_t* W, uint8_t* T, int N, int K) {
+  const int nks = K / GP_KC, nt32 = (N + 31) / 32;
+  const int tile = blockIdx.x / nks, kst = blockIdx.x % nks, lane = threadIdx.x, r = lane & 31, h = lane >> 5;
+  const int row = 32 * tile + r;
+  const bool live = row < N;
+  if constexpr (Q4) {
+    const u32x4_t v = live ? *reinterpret_cast<const u32x4_t*>(W + (size_t)row * (K / 2) + (64 * kst + 32 * h) / 2) : u32x4_t{};
+    *reinterpret_cast<u32x4_t*>(T + ((size_t)blockIdx.x * 64 + lane) * 16) = v;
+    if (lane < 32) {
+      const uint32_t* SB = reinterpret_cast<const uint32_t*>(W + q4_sb_offset(N, K));
+      reinterpret_cast<uint32_t*>(T + (size_t)nt32 * 32 * K / 2)[(size_t)blockIdx.x * 32 + lane] =
+          live ? SB[(size_t)row * nks + kst] : 0u;
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const u32x4_t v = live ? *reinterpret_cast<const u32x4_t*>(W + ((size_t)row * K + 64 * kst + 32 * h + 8 * s) * 2) : u32x4_t{};
+      *reinterpret_cast<u32x4_t*>(T + (((size_t)blockIdx.x * 4 + s) * 64 + lane) * 16) = v;
+    }
+  }
+}
+
+void launch_gemm_retile(const void* W, void* T, int N, int K, int wdt, hipStream_t st) {
+  const int blocks = (N + 31) / 32 * (K / GP_KC);
+  if (wdt == WDT_Q4) hipLaunchKernelGGL(gemm_retile_kernel<true>, dim3(blocks), dim3(64), 0, st, (const uint8_t*)W, (uint8_t*)T, N, K);
+  else hipLaunchKernelGGL(gemm_retile_kernel<false>, dim3(blocks), dim3(64), 0, st, (const uint8_t*)W, (uint8_t*)T, N, K);
 }
 
 // Pre-size the engine's split-K slab and tickets for an (N, K) launched at any M <= Mmax (outside
@@ -421,9 +548,11 @@ void launch_gemm_mfma(const GemvParams& p0, int wdt, bool nt, hipStream_t st) {
 bool gemm_reserve(GemmWs& ws, int N, int K, int Mmax) {
   size_t slab = 0, tk = 0;
   for (int m = GEMM_MFMA_MIN_M; m <= Mmax; ++m) {  // cheap host loop (Mmax <= a few thousand)
-    size_t t = 0;
-    slab = std::max(slab, gemm_need(N, K, m, t));
-    tk = std::max(tk, t);
+    for (int q = 0; q < 2; ++q) {  // either weight format (an int4 engine keeps bf16 heads)
+      size_t t = 0;
+      slab = std::max(slab, gemm_need(N, K, m, q == 1, t));
+      tk = std::max(tk, t);
+    }
   }
   bool moved = false;
   if (slab > ws.bytes) {
@@ -437,7 +566,9 @@ bool gemm_reserve(GemmWs& ws, int N, int K, int Mmax) {
     if (ws.tickets) (void)hipFree(ws.tickets);
     ws.tickets = nullptr;
     ws.n = 0;
-    if (hipMalloc(&ws.tickets, tk * 4) == hipSuccess && hipMemset(ws.tickets, 0, tk * 4) == hipSuccess) ws.n = tk;
+    if (hipMalloc(&ws.tickets, tk * 4) == hipSuccess && hipMemset(ws.tickets, 0, tk * 4) == hipSuccess &&
+        hipDeviceSynchronize() == hipSuccess)  // (null-stream fill, drained before engine-stream use)
+      ws.n = tk;
     moved = true;
   }
   return moved;
@@ -446,7 +577,7 @@ bool gemm_reserve(GemmWs& ws, int N, int K, int Mmax) {
 void gemm_ws_free(GemmWs& ws) {
   if (ws.kpart) (void)hipFree(ws.kpart);
   if (ws.tickets) (void)hipFree(ws.tickets);
-  ws = GemmWs{};
+  ws = GemmWs{};  // (the tiled copies are engine allocations)
 }
 
 // ---------------------------------------------------------------------------- row gather

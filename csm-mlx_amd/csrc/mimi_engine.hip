@@ -95,6 +95,7 @@ struct mimi_codec {
     void* p = nullptr;
     if (hipMalloc(&p, bytes) != hipSuccess) throw CsmError(CSM_ERR_HIP, "hipMalloc(" + std::to_string(bytes) + ") failed");
     (void)hipMemset(p, 0, bytes);
+    (void)hipDeviceSynchronize();  // the null-stream fill is not ordered with the engine's non-blocking stream
     allocs.push_back(p);
     return p;
   }

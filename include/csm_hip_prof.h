@@ -35,7 +35,9 @@ int csm_bench_dec_frame(csm_engine* e, int iters, float* avg_us, double* bytes);
  * (decoder steps >= 2 gather projection(E_a[c]) from a table built at csm_begin, default 1),
  * "qkv0_tab" (decoder layer 0's q, k, v gathered from a table at steps >= 2, default 1),
  * "fuse_mlp" (one-launch MLP for <= 4 rows, default 0), "dec_frame" (batch-1 greedy bf16 frames on the
- * persistent frame decoder, dec_frame.hip: codebook0_head + 31 decoder steps in one launch, default 1). */
+ * persistent frame decoder, dec_frame.hip: codebook0_head + 31 decoder steps in one launch, default 1),
+ * "linear_mfma" (csm_linear runs the batched frame's MFMA GEMM at >= 8 rows instead of the GEMV,
+ * default 0: the GEMM's kernel tests). */
 int csm_set_option(csm_engine* e, const char* key, int value);
 
 #ifdef __cplusplus
