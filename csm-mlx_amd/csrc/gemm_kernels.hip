@@ -49,22 +49,34 @@ constexpr int GP_KC = 64;  // K per stage (= Q4_GROUP)
 constexpr int GK_MAX_SLICES = 16;
 static_assert(GP_KC == Q4_GROUP, "one int4 group per stage");
 
-__device__ __forceinline__ unsigned short bf16_bits_rne(float v) { return (unsigned short)st_cast<bf16_t>(v); }
 
-// x -> three bf16 parts holding all 24 significant bits (finite inputs; parts may be zero)
+// x -> three bf16 parts holding all 24 significant bits, by truncation: hi = x with its low 16
+// bits cleared (8 significant bits), r = x - hi (exact, <= 16 bits), mid = r truncated the same
+// way, lo = r - mid (exact, <= 8 bits: a bf16 value) -- x = hi + mid + lo exactly, and each part
+// times a bf16 weight is exact in fp32.  Pairs are packed by v_perm (the high halves of two floats).
 __device__ __forceinline__ void split3_4(const float (&v)[4], u32x2_t& hi, u32x2_t& mid, u32x2_t& lo) {
-  unsigned short h[4], m[4], l[4];
+  uint32_t h[4], m[4], l[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    h[q] = bf16_bits_rne(v[q]);
-    const float r1 = v[q] - __uint_as_float((unsigned)h[q] << 16);  // exact
-    m[q] = bf16_bits_rne(r1);
-    const float r2 = r1 - __uint_as_float((unsigned)m[q] << 16);    // exact, <= 8 significant bits
-    l[q] = bf16_bits_rne(r2);
+    const uint32_t u = __float_as_uint(v[q]);
+    h[q] = u & 0xFFFF0000u;
+    const float r = v[q] - __uint_as_float(h[q]);
+    m[q] = __float_as_uint(r) & 0xFFFF0000u;
+    l[q] = __float_as_uint(r - __uint_as_float(m[q]));
   }
-  hi = u32x2_t{h[0] | ((unsigned)h[1] << 16), h[2] | ((unsigned)h[3] << 16)};
-  mid = u32x2_t{m[0] | ((unsigned)m[1] << 16), m[2] | ((unsigned)m[3] << 16)};
-  lo = u32x2_t{l[0] | ((unsigned)l[1] << 16), l[2] | ((unsigned)l[3] << 16)};
+  hi = u32x2_t{__builtin_amdgcn_perm(h[1], h[0], 0x07060302u), __builtin_amdgcn_perm(h[3], h[2], 0x07060302u)};
+  mid = u32x2_t{__builtin_amdgcn_perm(m[1], m[0], 0x07060302u), __builtin_amdgcn_perm(m[3], m[2], 0x07060302u)};
+  lo = u32x2_t{__builtin_amdgcn_perm(l[1], l[0], 0x07060302u), __builtin_amdgcn_perm(l[3], l[2], 0x07060302u)};
+}
+
+// sum over each row of 16 lanes by DPP (row rotations by 8 and 4, then quad swaps): every lane of
+// the row gets the sum, in an order fixed by its position
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xF, 0xF, false));  // row_ror:8
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xF, 0xF, false));  // row_ror:4
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+  return v;
 }
 
 // one uint32 of MLX int4 nibbles (k = 8s .. 8s+7, low nibble first) -> 8 exact bf16 (u32x4 of pairs):
@@ -136,6 +148,16 @@ __device__ __forceinline__ void gp_combine(__amdgpu_buffer_rsrc_t rs, float (*ct
 // Activations go global -> registers -> (RMSNorm weight, sum of squares, hi/mid/lo split) -> LDS
 // once per stage and are shared by the block's NBR / 32 row tiles.  NBR = 256: 2 row tiles per
 // wave; 128: one; 64: two waves per row tile split each stage's steps (summed in a fixed order).
+#ifdef GEMM_STAMPS  // lab build only (tools/variant.sh ... -DGEMM_STAMPS): per-block phase clocks
+__device__ unsigned long long g_gemm_stamps[1024][6];
+#define GSTAMP(i) do { if (threadIdx.x == 0 && blin < 1024) g_gemm_stamps[blin][i] = __builtin_amdgcn_s_memrealtime(); } while (0)
+extern "C" int csm_gemm_stamps(unsigned long long* out, int n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_gemm_stamps), sizeof(unsigned long long) * 6 * (size_t)(n < 1024 ? n : 1024)) == hipSuccess ? 0 : 1;
+}
+#else
+#define GSTAMP(i) do {} while (0)
+#endif
+
 template <bool Q4, int MT, int NBR, int PD, bool NT>
 __global__ __launch_bounds__(256) void gemm_wide_kernel(GemvParams p) {
   constexpr int NB = MT * 32;
@@ -157,6 +179,9 @@ __global__ __launch_bounds__(256) void gemm_wide_kernel(GemvParams p) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = lane & 31, h = lane >> 5, slot = lane + h;
   const int tile = blockIdx.x, n0 = tile * NBR;
+  const int blin = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+  (void)blin;
+  GSTAMP(0);
   const int mc = blockIdx.z, m0 = mc * NB, nchunks = gridDim.z;
   const int Kblk = p.K / p.ksplit, kslice = blockIdx.y * Kblk, nst = Kblk / GP_KC;
   const bool norm = p.nw != nullptr;
@@ -230,9 +255,7 @@ __global__ __launch_bounds__(256) void gemm_wide_kernel(GemvParams p) {
         }
       }
       if constexpr (Q4) {  // sum of the group's 64 values of row c: 16 threads x 4, fixed order
-        float sum = (v[0] + v[1]) + (v[2] + v[3]);
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) sum += __shfl_xor(sum, o, 64);
+        const float sum = row16_sum((v[0] + v[1]) + (v[2] + v[3]));
         if ((tid & 15) == 0) xsum[buf][c] = sum;
       }
       u32x2_t hi, mid, lo;
@@ -252,6 +275,7 @@ __global__ __launch_bounds__(256) void gemm_wide_kernel(GemvParams p) {
   for (int d = 0; d < PD; ++d) load(d, sg[d]);
   store(sg[0], 0, true);
   __syncthreads();
+  GSTAMP(1);
   for (int it0 = 0; it0 < nst; it0 += PD) {
 #pragma unroll
     for (int d = 0; d < PD; ++d) {
@@ -321,13 +345,12 @@ __global__ __launch_bounds__(256) void gemm_wide_kernel(GemvParams p) {
       __syncthreads();
     }
   }
+  GSTAMP(2);
   // sum of squares per batch row: the 16 threads of a row share it
   if (norm) {
 #pragma unroll
     for (int i = 0; i < NB / 16; ++i) {
-      float v = ss[i];
-#pragma unroll
-      for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      const float v = row16_sum(ss[i]);
       if ((tid & 15) == 0) ssb[x_c + 16 * i] = v;
     }
   }
@@ -373,6 +396,7 @@ __global__ __launch_bounds__(256) void gemm_wide_kernel(GemvParams p) {
       if (last) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
     }
     __syncthreads();
+    GSTAMP(3);
     if (!last) return;
     switch (p.ksplit) {
       case 2: gp_combine<2, NB, NBR>(rs, ct, ssb, mrows, norm, slab_f, tid); break;
@@ -411,6 +435,7 @@ __global__ __launch_bounds__(256) void gemm_wide_kernel(GemvParams p) {
       p.part[(size_t)(m0 + tid) * p.part_stride + blockIdx.x] = best;
     }
   }
+  GSTAMP(4);
 }
 
 // ---------------------------------------------------------------------------- host side
