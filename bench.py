@@ -82,11 +82,16 @@ def build_codec(seed=0, device=None, model_name="csm_1b"):
     return codec
 
 
-def build_model(dtype: str, batch: int, seed=0, device=None, model_name="csm_1b"):
+def build_model(dtype: str, batch: int, seed=0, device=None, model_name="csm_1b", load=True):
+    """csm_1b (or the tiny test model) with seeded synthetic weights; load=False creates the engine
+    only (a rank that receives the weights by broadcast)."""
     from csm_mlx.models import CSM, csm_1b, csm_tiny
     from csm_mlx.weights import csm_param_specs, synthetic_csm_weights
     args = csm_1b() if model_name == "csm_1b" else csm_tiny()   # tiny: test rehearsals of the N-rank path only
     model = CSM(args, dtype=dtype, max_batch=batch, device=device)
+    if not load:
+        model.engine  # noqa: B018  (creates the engine and its weight buffers)
+        return model
     names = list(csm_param_specs(args))
     for i in range(0, len(names), 16):      # stream tensors in groups: bounded host memory
         model.load_weights(list(synthetic_csm_weights(args, seed, names[i:i + 16]).items()), strict=False)
@@ -191,8 +196,8 @@ def frame_weight_bytes(model) -> float:
 
 def _kernel_name(model, batch: int, stack: str) -> str:
     if batch >= 8 and model.dtype in ("bf16", "q4"):
-        return (f"gemm_pipe_kernel<Q4={'true' if model.dtype == 'q4' else 'false'}> = {stack} RMSNorm + gate/up + "
-                f"SiLU*up as an exact-split MFMA GEMM over {batch} rows")
+        return (f"gemm_wide_kernel<Q4={'true' if model.dtype == 'q4' else 'false'}> = {stack} RMSNorm + gate/up + "
+                f"SiLU*up as an exact-split MFMA GEMM over {batch} rows (fragment-tiled weights)")
     return f"gemv_xl_kernel<{model.dtype}> = {stack} RMSNorm + gate/up + SiLU*up GEMV over {batch} row(s)"
 
 
@@ -258,6 +263,9 @@ def main():
     ap.add_argument("--model", default="csm_1b", choices=["csm_1b", "tiny"],
                     help="tiny: the toy test model (multi-rank rehearsals in tests), never a bench line")
     ap.add_argument("--dump", default="", help="rank 0 writes the gathered codes / PCM of the last step (npz)")
+    ap.add_argument("--weights", default="bcast", choices=["bcast", "synthetic"],
+                    help="N ranks: rank 0 builds the weights and broadcasts the engine buffers device to device "
+                         "(bcast, default) or every rank generates them itself (synthetic)")
     args = ap.parse_args()
     cfg = dict(CONFIGS[args.config or 2])
     if args.config:
@@ -294,7 +302,23 @@ def main():
     from csm_mlx.generation import generate_batch
     from csm_mlx.tokenizers import tokenize_text_segment
 
-    model = build_model(args.dtype, args.batch, device=device, model_name=args.model)
+    bcast = world > 1 and args.weights == "bcast"
+    model = build_model(args.dtype, args.batch, device=device, model_name=args.model, load=not bcast or rank == 0)
+    weights_info = {"source": "synthetic seed 0, generated on every rank" if world > 1 else "synthetic seed 0"}
+    if bcast:
+        import torch
+        from csm_mlx.dist import broadcast_weights
+        tdev = dev if dev is not None else torch.device("cuda", device)
+        torch.cuda.set_device(tdev)
+        secs = broadcast_weights(model, 0, tdev)
+        n = ctypes.c_int(0)
+        L0 = _lib.lib()
+        _lib.check(L0.csm_weight_buffers(model.engine, None, None, 0, ctypes.byref(n)))
+        sizes = (ctypes.c_uint64 * n.value)()
+        _lib.check(L0.csm_weight_buffers(model.engine, None, sizes, n.value, ctypes.byref(n)))
+        weights_info = {"source": "synthetic seed 0 on rank 0",
+                        "distribution": f"{args.dist_backend} broadcast of the engine's {n.value} weight buffers",
+                        "bytes": int(sum(sizes)), "seconds_rank0": round(secs, 3)}
     K = model.n_audio_codebooks
     decode = not args.no_decode
     if decode or cfg["stream"] or cfg["context"]:
@@ -383,7 +407,8 @@ def main():
                        "context_segments": 3 if cfg["context"] else 0,
                        "model": "csm_1b (synthetic seed-0 weights)", "global_batch": args.batch * world,
                        "per_gpu_batch": args.batch, "frames": args.frames, "mimi_decode": decode,
-                       "parallelism": f"dp{world}", "rtf": round(total_frames / max_dt / 12.5, 2)},
+                       "parallelism": f"dp{world}", "rtf": round(total_frames / max_dt / 12.5, 2),
+                       "weights": weights_info},
             "roofline": roof["dominant"],
             "roofline_backbone": roof["backbone_gate_up"],
             "roofline_frame": roof_frame,

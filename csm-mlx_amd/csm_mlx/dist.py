@@ -1,4 +1,4 @@
-"""Data-parallel batch partition + result collection.
+"""Data-parallel batch partition, weight broadcast and result collection.
 
 Utterances are independent (no cross-utterance state), so N processes -- one per GPU, launched by
 ``torch.distributed.run`` -- each generate a contiguous shard of the global batch with no collective
@@ -10,6 +10,7 @@ extension, not a translation of anything there.
 """
 from __future__ import annotations
 
+import ctypes
 from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -21,6 +22,48 @@ def shard(global_batch: int, world: int, rank: int) -> List[int]:
         raise ValueError(f"global batch {global_batch} does not divide over {world} ranks")
     per = global_batch // world
     return list(range(rank * per, (rank + 1) * per))
+
+
+class _DeviceBytes:
+    """A raw device buffer seen by torch as a uint8 tensor (``__cuda_array_interface__``, no copy)."""
+
+    def __init__(self, ptr: int, nbytes: int):
+        self.__cuda_array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (ptr, False),
+                                         "version": 3, "strides": None}
+
+
+def broadcast_weights(model, src: int = 0, device=None) -> float:
+    """Weight distribution for N ranks: rank ``src`` has loaded the weights (a checkpoint or the
+    synthetic set); every other rank created the same model (dims, dtype, max batch) without loading.
+    The engine's resident buffers (kernel layout, storage dtype: csm_weight_buffers) are broadcast
+    device to device -- RCCL over xGMI on the "nccl" group, gloo otherwise -- and the receivers are
+    marked loaded (csm_weights_received).  Returns the seconds the broadcast took on this rank.
+    device: this rank's torch device (the GPU the engine runs on)."""
+    import time
+
+    import torch
+    import torch.distributed as dist
+
+    from . import _lib
+    L = _lib.lib()
+    n = ctypes.c_int(0)
+    _lib.check(L.csm_weight_buffers(model.engine, None, None, 0, ctypes.byref(n)))
+    ptrs = (ctypes.c_void_p * n.value)()
+    sizes = (ctypes.c_uint64 * n.value)()
+    _lib.check(L.csm_weight_buffers(model.engine, ptrs, sizes, n.value, ctypes.byref(n)))
+    dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    _lib.check(L.csm_synchronize(model.engine))
+    t0 = time.perf_counter()
+    with torch.cuda.device(dev):
+        for p, b in zip(ptrs, sizes):
+            t = torch.as_tensor(_DeviceBytes(int(p), int(b)), device=dev)
+            dist.broadcast(t, src)
+        torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    if dist.get_rank() != src:
+        _lib.check(L.csm_weights_received(model.engine))
+        model._loaded = set(model._loaded) | {"*broadcast*"}
+    return dt
 
 
 def _pack(items: Sequence[np.ndarray], width: int, dtype) -> Tuple[np.ndarray, np.ndarray]:

@@ -954,6 +954,56 @@ int csm_weights_ready(csm_engine* e) {
   CSM_CATCH
 }
 
+// resident weight buffers in a fixed order (identical across engines of the same dims / dtype)
+static std::vector<std::pair<void*, size_t>> weight_buffers(csm_engine* e) {
+  std::vector<std::pair<void*, size_t>> b;
+  for (Stack* s : {&e->bb, &e->dec}) {
+    const size_t D = s->d.hidden, F = s->d.intermediate;
+    b.emplace_back(s->norm, D * 4);
+    for (LayerW& l : s->L) {
+      b.emplace_back(l.wqkv, e->wbytes(s->qkv_rows(), D));
+      b.emplace_back(l.wo, e->wbytes(D, s->q_dim()));
+      b.emplace_back(l.wgu, e->wbytes(2 * F, D));
+      b.emplace_back(l.wd, e->wbytes(D, F));
+      if (l.wdc) b.emplace_back(l.wdc, D * F * 2);
+      b.emplace_back(l.n1, D * 4);
+      b.emplace_back(l.n2, D * 4);
+    }
+  }
+  const size_t D = e->D, Dd = e->Dd, V = e->V, K = e->K, Vp = e->Vpad;
+  b.emplace_back(e->text_emb, e->wbytes(e->dims.n_text_vocab, D));
+  b.emplace_back(e->audio_emb, e->wbytes(V * K, D));
+  b.emplace_back(e->proj, e->wbytes(Dd, D));
+  b.emplace_back(e->c0_head, e->wbytes(Vp, D));
+  b.emplace_back(e->audio_head, (K - 1) * Vp * Dd * (e->head_wdt == WDT_F32 ? 4 : 2));
+  return b;
+}
+
+int csm_weight_buffers(csm_engine* e, void** ptrs, uint64_t* bytes, int cap, int* n) {
+  CSM_TRY {
+    if (!e || !n || cap < 0) throw CsmError(CSM_ERR_ARG, "bad csm_weight_buffers arguments");
+    const auto b = weight_buffers(e);
+    *n = (int)b.size();
+    for (int i = 0; i < cap && i < (int)b.size(); ++i) {
+      if (ptrs) ptrs[i] = b[i].first;
+      if (bytes) bytes[i] = b[i].second;
+    }
+  }
+  CSM_CATCH
+}
+
+int csm_weights_received(csm_engine* e) {
+  CSM_TRY {
+    HIPCHK(hipSetDevice(e->dev));
+    HIPCHK(hipDeviceSynchronize());
+    for (const auto& nm : e->required) e->loaded.insert(nm);
+    e->tiled_dirty = true;
+    e->proj_tab_dirty = true;
+    e->g_B = -1;
+  }
+  CSM_CATCH
+}
+
 int csm_quantize(csm_engine* e, int group_size, int bits) {
   CSM_TRY {
     if (group_size != Q4_GROUP || bits != 4) throw CsmError(CSM_ERR_ARG, "only group_size=64, bits=4 is supported");

@@ -71,6 +71,14 @@ int csm_load_tensor(csm_engine* e, const char* name, const void* host, int src_d
 int csm_set_rope_table(csm_engine* e, int which, const float* table, int n_pos, int head_dim);
 /* returns CSM_ERR_STATE and names the first missing tensor when weights are incomplete */
 int csm_weights_ready(csm_engine* e);
+/* Multi-GPU weight distribution (no reference counterpart: the reference is single-device).  The
+ * engine's resident weight buffers -- every Linear / Embedding / norm / head matrix in kernel layout
+ * and storage dtype, in a fixed order -- so one rank's loaded buffers can be broadcast device to
+ * device (RCCL) into identically created engines.  *n = buffer count; up to cap (ptr, bytes) pairs
+ * are written.  csm_weights_received then marks a receiving engine's weights as loaded (derived
+ * tables and tiled copies rebuild at the next csm_begin). */
+int csm_weight_buffers(csm_engine* e, void** ptrs, uint64_t* bytes, int cap, int* n);
+int csm_weights_received(csm_engine* e);
 /* nn.quantize(model, group_size, bits) (run_streaming_csm_mlx.py:811-818; README.md:108-111): convert every
  * loaded Linear / Embedding weight to int4 in place (MLX affine rule, oracle/quant_oracle.py).  Only
  * group_size 64, bits 4.  audio_head and the norms keep their dtype. */

@@ -1,11 +1,13 @@
 """The N-rank path of bench.py on the GPU: ``torch.distributed.run`` with 2
 ranks on this box's one GPU (``--dist-backend gloo``: device = LOCAL_RANK mod #GPUs), each rank
 generating its contiguous shard of the utterances through the real bench step (prefill, frames, Mimi
-decode) and all-gathering codes + PCM.  The gathered codes must be byte-identical to one process
+decode) and all-gathering codes + PCM.  Rank 1 never loads weights: rank 0's engine buffers reach it
+by broadcast (csm_mlx.dist.broadcast_weights, the bench default for N ranks).  The gathered codes must be byte-identical to one process
 generating every utterance itself; the PCM agrees to float rounding (the Mimi decode's row count --
 2 vs 4 utterances per launch -- picks different kernel tilings; the transport itself is lossless,
 tests/test_dist_cpu.py).  (The 8-GPU RCCL run is the driver's; the collective is the same
 ``all_gather_into_tensor`` on device tensors.)"""
+import json
 import os
 import socket
 import subprocess
@@ -36,6 +38,9 @@ def _bench(tmp_path, nproc, batch_per_rank, frames, name, extra=()):
     env = dict(os.environ, OMP_NUM_THREADS="4")
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    if nproc > 1:
+        assert "broadcast" in line["config"]["weights"]["distribution"], line["config"]["weights"]
     z = np.load(out)
     n = int(z["n"])
     return [z[f"codes_{i}"] for i in range(n)], [z[f"pcm_{i}"] for i in range(n)]
