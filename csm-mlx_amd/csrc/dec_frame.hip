@@ -603,7 +603,7 @@ __global__ __launch_bounds__(NT, 1) void dec_frame_kernel(DecFrameArgs p) {
   __syncthreads();
 
   // Register prefetch schedule (what is in flight during each hand-off wait):
-  //   E1 (q|k|v): the cached K/V rows, this layer's down slices
+  //   E1 (q|k|v): the cached K/V rows, this layer's down slices (issued after the QKV publish)
 //   E3 (x): this layer's gate/up slices, next layer's QKV / o
   //   E4 / E5 of the last layer: this step's head rows, the next step's o / QKV
   //   E6: the next step's layer-0 cached K/V rows
@@ -622,10 +622,12 @@ __global__ __launch_bounds__(NT, 1) void dec_frame_kernel(DecFrameArgs p) {
         kv_store(c, pos0, kv0);
       } else {
         KvRegs kv;
-        kv_issue(c, l, pos0, kv);
-        load_dn(c, l, wd);
         rms_rows(c, M, p.n1[l]);
         phase_qkv(c, M, pos0, wq);                      // -> E1
+        // prefetches issued after the publish (its RoPE operand load would otherwise retire behind
+        // them in vmcnt order), still ahead of the hand-off wait they hide under
+        kv_issue(c, l, pos0, kv);
+        load_dn(c, l, wd);
         gather<6>(c, c.buf(G_QKV, MAXM * QKV), M * QKV, &L.qkv[0][0]);
         ++c.e;
         kv_store(c, pos0, kv);
