@@ -202,7 +202,11 @@ __device__ __forceinline__ void gather(Ctx& c, const u64* buf, int n, float* out
 }
 
 // xn[m][k] = x[m][k] * rsqrt(mean(x^2) + eps) * nw[k] for rows m < M (every WG computes the same)
-__device__ __forceinline__ void rms_rows(Ctx& c, int M, const float* nw, int m0 = 0) {
+// RMSNorm weight elements tid and tid + 512 (every element a thread scales), fetched a phase ahead
+__device__ __forceinline__ float2 nw_fetch(const Ctx& c, const float* nw) { return make_float2(nw[c.tid], nw[c.tid + NT]); }
+
+__device__ __forceinline__ void rms_rows(Ctx& c, int M, float2 nw, int m0 = 0) {
+  static_assert(D == 2 * NT, "a thread scales elements tid and tid + NT of each row");
   // sum of squares: wave m sums row m in a fixed order
   if (c.wave < M) {
     const float* x = c.L.x[m0 + c.wave];
@@ -212,10 +216,10 @@ __device__ __forceinline__ void rms_rows(Ctx& c, int M, const float* nw, int m0 
     if (c.lane == 0) c.L.wsum[0][c.wave] = s;
   }
   __syncthreads();
-  for (int i = c.tid; i < M * D; i += NT) {
-    const int m = i / D, k = i % D;
+  for (int m = 0; m < M; ++m) {
     const float r = rsqrtf(c.L.wsum[0][m] / (float)D + c.p.eps);
-    c.L.xn[m][k] = c.L.x[m0 + m][k] * r * nw[k];
+    c.L.xn[m][c.tid] = c.L.x[m0 + m][c.tid] * r * nw.x;
+    c.L.xn[m][c.tid + NT] = c.L.x[m0 + m][c.tid + NT] * r * nw.y;
   }
   __syncthreads();
 }
@@ -609,6 +613,7 @@ __global__ __launch_bounds__(NT, 1) void dec_frame_kernel(DecFrameArgs p) {
   //   E6: the next step's layer-0 cached K/V rows
   WHd wh;
   KvRegs kv0;  // layer 0's cached K/V rows of the next step, fetched during the head's hand-off
+  float2 nw1 = nw_fetch(c, p.n1[0]);  // RMSNorm weights, fetched a phase ahead of use
   for (int step = 1; step < p.K; ++step) {
     const int M = step == 1 ? 2 : 1;
     const int pos0 = step == 1 ? 0 : step;
@@ -617,12 +622,17 @@ __global__ __launch_bounds__(NT, 1) void dec_frame_kernel(DecFrameArgs p) {
       if (l == 0 && step > 1) {
         // layer 0 from the folded table: q | k | v (RoPE'd at position `step`) of input row x[0]
         const float* t = p.qkv0_tab + ((size_t)(step - 1) * p.V + L.code) * QKV;
+        float tv[(QKV + NT - 1) / NT];  // the row's loads first: the down prefetch retires after them
+#pragma unroll
+        for (int j = 0; j < (QKV + NT - 1) / NT; ++j) tv[j] = c.tid + j * NT < QKV ? t[c.tid + j * NT] : 0.f;
         load_dn(c, l, wd);
-        for (int k = c.tid; k < QKV; k += NT) L.qkv[0][k] = t[k];
+#pragma unroll
+        for (int j = 0; j < (QKV + NT - 1) / NT; ++j)
+          if (c.tid + j * NT < QKV) L.qkv[0][c.tid + j * NT] = tv[j];
         kv_store(c, pos0, kv0);
       } else {
         KvRegs kv;
-        rms_rows(c, M, p.n1[l]);
+        rms_rows(c, M, nw1);
         phase_qkv(c, M, pos0, wq);                      // -> E1
         // prefetches issued after the publish (its RoPE operand load would otherwise retire behind
         // them in vmcnt order), still ahead of the hand-off wait they hide under
@@ -635,6 +645,7 @@ __global__ __launch_bounds__(NT, 1) void dec_frame_kernel(DecFrameArgs p) {
       __syncthreads();
       c.refresh();
       c.mark();
+      const float2 nw2 = nw_fetch(c, p.n2[l]);
       load_gu<0, GU_EARLY>(c, l, wg);
       phase_attn(c, M, pos0, l);
       c.mark();
@@ -645,8 +656,9 @@ __global__ __launch_bounds__(NT, 1) void dec_frame_kernel(DecFrameArgs p) {
       gather<2 * MAXM>(c, c.buf(G_X, MAXM * D), M * D, &L.x[0][0]);
       ++c.e;
       c.refresh();
-      rms_rows(c, M, p.n2[l]);
+      rms_rows(c, M, nw2);
       phase_mlp(c, M, wg, wd);                          // -> E4
+      nw1 = nw_fetch(c, l + 1 < NL ? p.n1[l + 1] : p.norm);  // next layer's norm, or the final one
       c.mark();
       if (l + 1 == NL) {
         load_head(c, p.audio_head + (size_t)(step - 1) * p.VP * D, D, wh);
@@ -659,7 +671,7 @@ __global__ __launch_bounds__(NT, 1) void dec_frame_kernel(DecFrameArgs p) {
     }
     // ci head on the last row: final norm, audio_head[step - 1] (generation.py:79)
     c.refresh();
-    rms_rows(c, 1, p.norm, M - 1);
+    rms_rows(c, 1, nw1, M - 1);
     phase_head<D>(c, p.audio_head + (size_t)(step - 1) * p.VP * D, p.V, wh.a, wh.x, p.ci_logits + (size_t)(step - 1) * p.VP);  // -> E6
     if (step + 1 < p.K) kv_issue(c, 0, step + 1, kv0);
     const int ci = gather_code(c, p.V);
