@@ -82,6 +82,19 @@ class FrameCache:
         m = np.ascontiguousarray(mask, np.uint8)
         _lib.check(self.L.csm_prefill(self.model.engine, b, t.shape[0], _lib.ptr(t), _lib.ptr(m)))
 
+    def prefill_batch(self, items: Sequence[Tuple[int, np.ndarray, np.ndarray]]):
+        """prefill for several utterances in one pass per <= max_seq_len rows (csm_prefill_batch):
+        items = (b, tokens, mask) with distinct b."""
+        self._check()
+        if not items:
+            return
+        utts = np.array([b for b, _, _ in items], np.int32)
+        Ts = np.array([t.shape[0] for _, t, _ in items], np.int32)
+        toks = np.ascontiguousarray(np.concatenate([np.asarray(t, np.int32) for _, t, _ in items]), np.int32)
+        msks = np.ascontiguousarray(np.concatenate([np.asarray(m, np.uint8) for _, _, m in items]), np.uint8)
+        _lib.check(self.L.csm_prefill_batch(self.model.engine, len(items), _lib.ptr(utts), _lib.ptr(Ts),
+                                            _lib.ptr(toks), _lib.ptr(msks)))
+
     def run(self, nframes: int, sync: bool = True) -> bool:
         """Enqueue nframes frame graphs; with sync, wait and return whether every utterance is done
         (without, return False at once: the caller polls ``done()``, which waits for the frames)."""
@@ -206,8 +219,10 @@ def generate_codes_batch(model: CSM, prompts: Sequence[Tuple[np.ndarray, np.ndar
     for t, _ in prompts:
         _check_window(model, t.shape[0], max_audio_frames)
     cache = FrameCache(model, B, sampler, seeds)
-    for b, (t, m) in enumerate(prompts):
-        cache.prefill(b, t, m)
+    if B > 1:   # every prompt's rows through one pass of each projection (weights streamed once)
+        cache.prefill_batch([(b, t, m) for b, (t, m) in enumerate(prompts)])
+    else:
+        cache.prefill(0, *prompts[0])
     left = max_audio_frames
     if logits_processors:
         c0_history: list = []                                                    # generation.py:128
@@ -315,8 +330,7 @@ def stream_generate_batch(model: CSM, prompts: Sequence[Tuple[np.ndarray, np.nda
     B = len(prompts)
     codec = get_audio_tokenizer(model.n_audio_codebooks)
     cache = FrameCache(model, B, smp, seeds)
-    for b, (t, m) in enumerate(prompts):
-        cache.prefill(b, t, m)
+    cache.prefill_batch([(b, t, m) for b, (t, m) in enumerate(prompts)])
     codec.reset_state(B)
     try:
         yield from _overlapped_frames(cache, codec, max_audio_frames)

@@ -111,8 +111,12 @@ struct RowMap {
   int b_off;
   const int* pos_arr;
   int pos_const;
-  __device__ __forceinline__ int b(int m) const { return b_off + m / T; }
+  // ragged batched prefill: per-row utterance and position tables (device), overriding the above
+  const int* row_b = nullptr;
+  const int* row_pos = nullptr;
+  __device__ __forceinline__ int b(int m) const { return row_b ? row_b[m] : b_off + m / T; }
   __device__ __forceinline__ int pos(int m) const {
+    if (row_pos) return row_pos[m];
     const int bb = b(m);
     return (pos_arr ? pos_arr[bb] : 0) + pos_const + m % T;
   }

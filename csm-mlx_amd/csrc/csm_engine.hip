@@ -102,6 +102,7 @@ struct csm_engine {
   float *dx = nullptr, *din = nullptr, *dq = nullptr, *datt = nullptr, *dmlp = nullptr;
   int32_t* tok = nullptr;
   uint8_t* msk = nullptr;
+  int *row_b = nullptr, *row_pos = nullptr;  // [M_cap] batched-prefill row tables
   // per-batch state
   int *codes = nullptr, *hist = nullptr, *pos = nullptr, *n_frames = nullptr, *frame_ctr = nullptr;
   unsigned long long* part = nullptr;  // [K][B_max][part_stride] arg-max partials of the heads
@@ -800,6 +801,8 @@ int csm_engine_create(const csm_dims* dims, int device, int weight_dtype, int ma
       throw CsmError(CSM_ERR_ARG, "activation scratch too small for the projection table build");
     e->tok = (int32_t*)e->alloc(M * (K + 1) * 4);
     e->msk = (uint8_t*)e->alloc(M * (K + 1));
+    e->row_b = (int*)e->alloc(M * 4);
+    e->row_pos = (int*)e->alloc(M * 4);
     e->frame_ctr = (int*)e->alloc(16);
     e->df_gbuf = e->alloc(dec_frame_gbuf_bytes());
     e->df_epoch = (unsigned*)e->alloc(16);
@@ -1102,6 +1105,71 @@ int csm_prefill(csm_engine* e, int b, int T, const int32_t* tokens, const uint8_
     HIPCHK(hipStreamSynchronize(e->st));
     HIPCHK(hipGetLastError());
     e->prompt_len[b] = std::max(e->prompt_len[b], 0) + T;
+    e->need_body = false;
+  }
+  CSM_CATCH
+}
+
+int csm_prefill_batch(csm_engine* e, int n, const int32_t* utts, const int32_t* Ts, const int32_t* tokens,
+                      const uint8_t* masks) {
+  CSM_TRY {
+    if (n <= 0 || !utts || !Ts || !tokens || !masks) throw CsmError(CSM_ERR_ARG, "bad csm_prefill_batch arguments");
+    const int K = e->K;
+    std::vector<int> start(n);
+    std::vector<size_t> row0(n + 1, 0);
+    std::vector<char> seen(e->B, 0);
+    for (int i = 0; i < n; ++i) {
+      const int b = utts[i], T = Ts[i];
+      if (b < 0 || b >= e->B || seen[b]) throw CsmError(CSM_ERR_ARG, "utterance index out of range or repeated");
+      seen[b] = 1;
+      if (T <= 0 || T > e->M_cap) throw CsmError(CSM_ERR_ARG, "prompt length out of range");
+      start[i] = e->pos_host[b] + 1;
+      if (start[i] + T > e->dims.max_seq_len) throw CsmError(CSM_ERR_TOO_LONG, "rows exceed the 2048-position window");
+      row0[i + 1] = row0[i] + T;
+    }
+    HIPCHK(hipSetDevice(e->dev));
+    // utterances in groups of at most M_cap rows: one pass of every projection per group (the
+    // weights stream once for all of the group's rows), rows mapped to (utterance, position)
+    std::vector<int> rb, rp;
+    for (int i0 = 0; i0 < n;) {
+      int i1 = i0;
+      while (i1 < n && row0[i1 + 1] - row0[i0] <= (size_t)e->M_cap) ++i1;
+      const int R = (int)(row0[i1] - row0[i0]);
+      rb.assign(R, 0);
+      rp.assign(R, 0);
+      for (int i = i0; i < i1; ++i)
+        for (int t = 0; t < Ts[i]; ++t) {
+          rb[row0[i] - row0[i0] + t] = utts[i];
+          rp[row0[i] - row0[i0] + t] = start[i] + t;
+        }
+      HIPCHK(hipMemcpyAsync(e->tok, tokens + row0[i0] * (K + 1), (size_t)R * (K + 1) * 4, hipMemcpyHostToDevice, e->st));
+      HIPCHK(hipMemcpyAsync(e->msk, masks + row0[i0] * (K + 1), (size_t)R * (K + 1), hipMemcpyHostToDevice, e->st));
+      HIPCHK(hipMemcpyAsync(e->row_b, rb.data(), (size_t)R * 4, hipMemcpyHostToDevice, e->st));
+      HIPCHK(hipMemcpyAsync(e->row_pos, rp.data(), (size_t)R * 4, hipMemcpyHostToDevice, e->st));
+      EmbedParams ep{};
+      ep.tok = e->tok; ep.mask = e->msk; ep.text_emb = e->text_emb; ep.audio_emb = e->audio_emb; ep.V = e->V;
+      ep.K = K; ep.D = e->D; ep.out = e->x;
+      embed(e, ep, R, e->st);
+      RowMap rm{1, 0, nullptr, 0};
+      rm.row_b = e->row_b;
+      rm.row_pos = e->row_pos;
+      const long long* pend = run_stack(e, e->bb, e->x, R, e->q, e->att, e->mlp, rm, e->st);
+      for (int i = i0; i < i1; ++i) {  // h_last = norm(last row) of each utterance
+        const size_t last = row0[i + 1] - 1 - row0[i0];
+        launch_rmsnorm_rows(e->x + last * e->D, e->D, e->bb.norm, e->bb.d.eps, e->D, e->h_last + (size_t)utts[i] * e->D,
+                            e->D, 1, e->st, pend ? pend + last * e->D : nullptr, e->acc_rows * e->D);
+      }
+      HIPCHK(hipStreamSynchronize(e->st));  // the host row tables are reused by the next group
+      HIPCHK(hipGetLastError());
+      i0 = i1;
+    }
+    for (int i = 0; i < n; ++i) {
+      const int b = utts[i];
+      e->pos_host[b] = start[i] + Ts[i] - 1;
+      HIPCHK(hipMemcpyAsync(e->pos + b, &e->pos_host[b], 4, hipMemcpyHostToDevice, e->st));
+      e->prompt_len[b] = std::max(e->prompt_len[b], 0) + Ts[i];
+    }
+    HIPCHK(hipStreamSynchronize(e->st));
     e->need_body = false;
   }
   CSM_CATCH

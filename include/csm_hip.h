@@ -89,6 +89,13 @@ int csm_quantize(csm_engine* e, int group_size, int bits);
 int csm_begin(csm_engine* e, int B, const uint64_t* seeds, float temperature, int top_k);
 /* Prompt rows of utterance b: tokens/mask [T][K+1] (text id in the last column). */
 int csm_prefill(csm_engine* e, int b, int T, const int32_t* tokens, const uint8_t* mask);
+/* csm_prefill for several utterances at once (the rows of generate_batch's prompts): utts[i] gets
+ * Ts[i] rows, rows of all of them concatenated in tokens / masks.  Up to max_seq_len rows per pass
+ * run as ONE pass of every backbone projection (the weights stream once for all of them; each row
+ * keeps its own utterance's KV cache and positions), so the results are those of csm_prefill per
+ * utterance up to summation order.  No reference counterpart (the reference is batch-1). */
+int csm_prefill_batch(csm_engine* e, int n, const int32_t* utts, const int32_t* Ts, const int32_t* tokens,
+                      const uint8_t* masks);
 /* Generate up to nframes frames for the whole batch (one HIP graph replay per frame).
  * *all_done (optional) = 1 when every utterance hit EOS. */
 int csm_run_frames(csm_engine* e, int nframes, int* all_done);

@@ -93,3 +93,37 @@ def test_csm_1b_q4_batched_mfma(B):
     args, w = csm_weights("1b")
     id_sets = [prompt_ids(400 + b, 10 + b % 3) for b in range(B)]
     _batch_vs_oracle(args, w, id_sets, 4, 1e-3, dtype="q4", logits_of={0, B - 1})
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "q4"])
+def test_batched_prefill_matches_per_utterance(dtype):
+    """csm_prefill_batch (every prompt's rows in one pass per projection, ragged lengths) against
+    csm_prefill per utterance: identical greedy codes, logits within fp32 summation-order noise."""
+    from csm_mlx.generation import FrameCache
+    from csm_mlx.sampling import Sampler
+    from csm_mlx.tokenizers import tokenize_text_segment
+    args, w = csm_weights("tiny")
+    K, V = args.n_audio_codebooks, args.n_audio_vocab
+    Vp = (V + 7) // 8 * 8
+    B = 12
+    prompts = [tokenize_text_segment(tiny_prompt_ids(300 + b, 2 + (5 * b) % 11), 0, K) for b in range(B)]
+    out = []
+    for batched in (False, True):
+        model = _model(args, w, dtype, B)
+        cache = FrameCache(model, B, Sampler(0.0, 0), [0] * B)
+        if batched:
+            cache.prefill_batch([(b, t, m) for b, (t, m) in enumerate(prompts)])
+        else:
+            for b, (t, m) in enumerate(prompts):
+                cache.prefill(b, t, m)
+        logs = []
+        for _ in range(4):
+            cache.run(1)
+            logs.append(cache.debug("c0_logits", (B, Vp))[:, :V].copy())
+        hist, n, _ = cache.codes()
+        out.append((hist.copy(), n.copy(), logs))
+        del cache, model
+    (h0, n0, l0), (h1, n1, l1) = out
+    assert np.array_equal(n0, n1) and np.array_equal(h0, h1)
+    for a, b in zip(l0, l1):
+        assert np.abs(a - b).max() <= 1e-4 * np.abs(a).max()
