@@ -99,3 +99,18 @@ def test_encode_tiled_rvq_matches_per_row_kernel(monkeypatch):
     assert np.array_equal(tiled, ref_rows), f"first diff at {np.argwhere(tiled != ref_rows)[:3].tolist()}"
     ref = o.encode(pcm[[0, 23], None, :])
     assert np.array_equal(tiled[[0, 23]], ref)
+
+
+def test_codes_past_the_codebook_clamp():
+    """CSM can emit codes 2048-2050 (its audio vocabulary is 2051; Mimi's codebooks hold 2048): the
+    codec decodes them as 2047, on the GPU and in the oracle alike."""
+    m, codec, o = _pair("mimi_202407", "mlx")
+    rng = np.random.default_rng(9)
+    codes = rng.integers(0, m.bins, (2, m.n_q, 6)).astype(np.int32)
+    codes[0, 0, 1] = m.bins          # 2048
+    codes[1, 5, 3] = m.bins + 2      # 2050
+    codes[0, 31, 5] = m.bins + 1     # 2049
+    clamped = np.minimum(codes, m.bins - 1)
+    y, yc = codec.decode(codes), codec.decode(clamped)
+    assert np.array_equal(y, yc)
+    assert _rms(y, o.decode(codes)) <= 1e-4
