@@ -58,35 +58,6 @@ __device__ __forceinline__ void sc1_store_f(float* p, float v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Wave reductions without LDS round trips: each row of 16 lanes reduced by DPP (rotations by 8
-// and 4, then quad swaps), the four row results combined from lanes 0 / 16 / 32 / 48 by readlane in
-// a fixed order -- every lane returns the same value.
-__device__ __forceinline__ float dpp_f(float v, int ctrl_sel) {
-  switch (ctrl_sel) {
-    case 0: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xF, 0xF, false));
-    case 1: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xF, 0xF, false));
-    case 2: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
-    default: return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
-  }
-}
-__device__ __forceinline__ float rows4(float v, bool mx) {
-  const float a = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
-  const float b = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
-  const float c = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
-  const float d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
-  return mx ? fmaxf(fmaxf(a, b), fmaxf(c, d)) : (a + b) + (c + d);
-}
-__device__ __forceinline__ float wsum(float v) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) v += dpp_f(v, i);
-  return rows4(v, false);
-}
-__device__ __forceinline__ float wmax(float v) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) v = fmaxf(v, dpp_f(v, i));
-  return rows4(v, true);
-}
-
 // 16-B agent-coherent (sc1) load at byte offset `off` of a buffer of `bytes` bytes
 __device__ __forceinline__ u32x4_t sc1_load16(const void* base, int off, int bytes) {
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, bytes, 0x00020000);
@@ -241,7 +212,7 @@ __device__ __forceinline__ void rms_rows(Ctx& c, int M, float2 nw, int m0 = 0) {
     const float* x = c.L.x[m0 + c.wave];
     float s = 0.f;
     for (int k = c.lane; k < D; k += 64) s = fmaf(x[k], x[k], s);
-    s = wsum(s);
+    s = wave_sum(s);
     if (c.lane == 0) c.L.wsum[0][c.wave] = s;
   }
   __syncthreads();
@@ -317,8 +288,8 @@ __device__ __forceinline__ void phase_qkv(Ctx& c, int M, int pos0, const WQkv& W
     float s0 = 0.f, s1 = 0.f;
     dot8x2(W.a, c.L.xn[0] + 8 * c.lane, c.L.xn[1] + 8 * c.lane, s0, s1);
     dot8x2(W.b, c.L.xn[0] + 8 * (c.lane + 64), c.L.xn[1] + 8 * (c.lane + 64), s0, s1);
-    s0 = wsum(s0);
-    s1 = wsum(s1);
+    s0 = wave_sum(s0);
+    s1 = wave_sum(s1);
     if (c.lane == 0) { c.L.wsum[c.wave][0] = s0; c.L.wsum[c.wave][1] = s1; }
   }
   __syncthreads();
@@ -399,9 +370,9 @@ __device__ __forceinline__ void phase_attn(Ctx& c, int M, int pos0, int layer) {
     const float other = __shfl_xor(part, 32, 64);
     float s = hh == 0 ? part + other : other + part;
     if (kj >= n) s = -INFINITY;
-    const float mx = wmax(s);
+    const float mx = wave_max(s);
     const float pj = kj < n ? expf(s - mx) : 0.f;
-    const float l_run = wsum(hh == 0 ? pj : 0.f);
+    const float l_run = wave_sum(hh == 0 ? pj : 0.f);
     const int pji = __float_as_int(pj);
     float o0 = 0.f, o1 = 0.f;
 #pragma unroll 4
@@ -433,8 +404,8 @@ __device__ __forceinline__ void phase_o(Ctx& c, int M, const WO& W) {
     const int k = 8 * ((c.wave & 1) * 64 + c.lane);
     float s0 = 0.f, s1 = 0.f;
     dot8x2(W.a, c.L.att[0] + k, c.L.att[1] + k, s0, s1);
-    s0 = wsum(s0);
-    s1 = wsum(s1);
+    s0 = wave_sum(s0);
+    s1 = wave_sum(s1);
     if (c.lane == 0) { c.L.wsum[c.wave][0] = s0; c.L.wsum[c.wave][1] = s1; }
   }
   __syncthreads();
@@ -461,7 +432,7 @@ __device__ __forceinline__ void phase_mlp(Ctx& c, int M, const WGu& G, const WDn
       if (m >= M) break;
       float t[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) t[i] = wsum(s[i][m]);
+      for (int i = 0; i < 8; ++i) t[i] = wave_sum(s[i][m]);
       if (c.lane < 4) {  // pair j = 4*wave + lane: rows 2j (gate), 2j+1 (up) of the WG slice
         const float gt = c.lane == 0 ? t[0] : (c.lane == 1 ? t[2] : (c.lane == 2 ? t[4] : t[6]));
         const float up = c.lane == 0 ? t[1] : (c.lane == 1 ? t[3] : (c.lane == 2 ? t[5] : t[7]));
@@ -523,7 +494,7 @@ __device__ __forceinline__ void phase_reduce(Ctx& c, int M) {
   if (c.wave < 4 * M) {
     const float* r = c.L.red[c.wave];
     float s = ((r[4 * c.lane] + r[4 * c.lane + 1]) + r[4 * c.lane + 2]) + r[4 * c.lane + 3];
-    s = wsum(s);
+    s = wave_sum(s);
     if (c.lane == 0) {
       const int m = c.wave / 4, n = 4 * c.w + c.wave % 4;
       gput(c.buf(G_X, MAXM * D) + (size_t)m * D + n, c.L.x[m][n] + s, c.tag());
@@ -540,14 +511,14 @@ __device__ __forceinline__ void phase_head(Ctx& c, const bf16_t* W, int n_valid,
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < CPL; ++i) s += dot8(wa[i], c.L.xn[0] + 8 * (c.lane + 64 * i));
-  s = wsum(s);
+  s = wave_sum(s);
   unsigned long long best = row < n_valid ? pack_argmax(s, row) : 0ull;
   if (c.lane == 0 && row < n_valid) logits[row] = s;
   if (c.wave == 0 && c.w < 3) {
     float t = 0.f;
 #pragma unroll
     for (int i = 0; i < CPL; ++i) t += dot8(wx[i], c.L.xn[0] + 8 * (c.lane + 64 * i));
-    t = wsum(t);
+    t = wave_sum(t);
     const int xr = 2048 + c.w;
     const unsigned long long k2 = xr < n_valid ? pack_argmax(t, xr) : 0ull;
     best = k2 > best ? k2 : best;
@@ -622,7 +593,7 @@ __global__ __launch_bounds__(NT, 1) void dec_frame_kernel(DecFrameArgs p) {
   phase_head<DB>(c, p.c0_head, p.V, c0a, c0x, p.c0_logits);  // -> G_ARG (hand-off 0)
   {
     float s = dot8(pa[0], L.xn[0] + 8 * (128 * (c.wave & 1) + c.lane)) + dot8(pa[1], L.xn[0] + 8 * (128 * (c.wave & 1) + c.lane + 64));
-    s = wsum(s);
+    s = wave_sum(s);
     if (c.lane == 0) L.wsum[c.wave][0] = s;
     __syncthreads();
     if (c.tid < 4) gput(c.buf(G_X, MAXM * D) + 4 * c.w + c.tid, L.wsum[2 * c.tid][0] + L.wsum[2 * c.tid + 1][0], c.tag());
