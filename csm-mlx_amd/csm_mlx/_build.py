@@ -19,6 +19,10 @@ LIB = os.path.join(PKG, "libcsm_hip.so")
 ARCH = os.environ.get("CSM_HIP_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result"]
+# per-source flags: the persistent frame decoder holds weight prefetches in registers across hand-off
+# waits at 256 VGPRs; the AMDGPU scheduler's own register-pressure trackers keep it from spilling
+# them (55 -> 5 spilled VGPRs; a spill store waits for its load, draining the prefetch).
+SRC_FLAGS = {"dec_frame.hip": ["-mllvm", "-amdgpu-use-amdgpu-trackers=1"]}
 
 
 def _sources():
@@ -36,7 +40,7 @@ def _compile(src, hdr_mtime, verbose):
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), hdr_mtime):
         return obj
     lang = ["-x", "hip"] if src.endswith(".hip") else []
-    cmd = [HIPCC, *FLAGS, *lang, "-c", src, "-o", obj]
+    cmd = [HIPCC, *FLAGS, *SRC_FLAGS.get(os.path.basename(src), []), *lang, "-c", src, "-o", obj]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     r = subprocess.run(cmd, capture_output=True, text=True)

@@ -100,10 +100,11 @@ __device__ __forceinline__ u32x4_t wload(const bf16_t* p) { return *reinterpret_
 // lane-dependent part in ONE voffset register shared by every layer and row, the row / chunk step in
 // the scalar offset -- so per-layer weight addresses are not VGPR pairs the compiler keeps live
 // across the frame loop.
-__device__ __forceinline__ u32x4_t bload(const void* base, int voff, int soff, int nt = 0) {
+// AUX: cache policy (2 = nt), a compile-time constant so no load sits in a branch of its own.
+template <int AUX = 0>
+__device__ __forceinline__ u32x4_t bload(const void* base, int voff, int soff) {
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
-  if (nt) return __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 2));
-  return __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, 0));
+  return __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, AUX));
 }
 
 struct Lds {
@@ -269,15 +270,15 @@ __device__ __forceinline__ void load_dn(Ctx& c, int l, WDn& r) {
     }
 }
 __device__ __forceinline__ void load_head(Ctx& c, const bf16_t* W, int K, WHd& r) {
-  // K = 1024 (ci heads): 128 chunks per row -> 2 per lane
+  // K = 1024 (ci heads): 128 chunks per row -> 2 per lane; non-temporal (read once per frame)
   const bf16_t* base = W + (size_t)(8 * c.w) * K;
   const int v = (c.wave * K + 8 * c.lane) * 2;
-  r.a[0] = bload(base, v, 0, c.p.hnt);
-  r.a[1] = bload(base, v, 1024, c.p.hnt);
+  r.a[0] = bload<2>(base, v, 0);
+  r.a[1] = bload<2>(base, v, 1024);
   if (c.wave == 0 && c.w < 3) {
     const bf16_t* xr = W + (size_t)(2048 + c.w) * K;
-    r.x[0] = bload(xr, 16 * c.lane, 0, c.p.hnt);
-    r.x[1] = bload(xr, 16 * c.lane, 1024, c.p.hnt);
+    r.x[0] = bload<2>(xr, 16 * c.lane, 0);
+    r.x[1] = bload<2>(xr, 16 * c.lane, 1024);
   }
 }
 
@@ -558,6 +559,81 @@ __device__ __forceinline__ int gather_code(Ctx& c, int V) {
   return c.L.code;
 }
 
+
+// Registers carried between phases (prefetched weights, norm weights)
+struct Pre {
+  WQkv wq;
+  WO wo;
+  WGu wg;
+  WDn wd;
+  WHd wh;
+  float2 nw1;
+};
+
+// One decoder layer of step `step` (M rows at positions pos0..).  FIRST: layer 0, which at steps
+// >= 2 takes q | k | v (RoPE'd) from the folded qkv0 table and its input row from proj_tab (no QKV
+// hand-off).  LAST: the final layer, which also fetches this step's head rows and the next step's
+// layer-0 o / layer-1 QKV slices.
+template <bool FIRST, bool LAST>
+__device__ __forceinline__ void decoder_layer(Ctx& c, int l, int step, int M, int pos0, Pre& r) {
+  const DecFrameArgs& p = c.p;
+  Lds& L = c.L;
+  c.refresh();
+  if (FIRST && step > 1) {
+    // q | k | v of input row proj_tab[step - 1][code] at position `step`, and the row itself; both
+    // loads are in flight together, ahead of the down prefetch (vmcnt retires in issue order)
+    const float* t = p.qkv0_tab + ((size_t)(step - 1) * p.V + L.code) * QKV;
+    const float* xr = p.proj_tab + ((size_t)(step - 1) * p.V + L.code) * D;
+    float tv[(QKV + NT - 1) / NT], xv[D / NT];
+#pragma unroll
+    for (int j = 0; j < (QKV + NT - 1) / NT; ++j) tv[j] = c.tid + j * NT < QKV ? t[c.tid + j * NT] : 0.f;
+#pragma unroll
+    for (int j = 0; j < D / NT; ++j) xv[j] = xr[c.tid + j * NT];
+    load_dn(c, l, r.wd);
+#pragma unroll
+    for (int j = 0; j < (QKV + NT - 1) / NT; ++j)
+      if (c.tid + j * NT < QKV) L.qkv[0][c.tid + j * NT] = tv[j];
+#pragma unroll
+    for (int j = 0; j < D / NT; ++j) L.x[0][c.tid + j * NT] = xv[j];
+  } else {
+    KvRegs kv;
+    rms_rows(c, M, r.nw1);
+    phase_qkv(c, M, pos0, r.wq);                      // -> E1
+    // prefetches issued after the publish (its RoPE operand load would otherwise retire behind
+    // them in vmcnt order), still ahead of the hand-off wait they hide under
+    kv_issue(c, l, pos0, kv);
+    load_dn(c, l, r.wd);
+    gather<6>(c, c.buf(G_QKV, MAXM * QKV), M * QKV, &L.qkv[0][0]);
+    ++c.e;
+    kv_store(c, pos0, kv);
+  }
+  __syncthreads();
+  c.refresh();
+  c.mark();
+  const float2 nw2 = nw_fetch(c, p.n2[l]);
+  load_gu<0, GU_EARLY>(c, l, r.wg);
+  phase_attn(c, M, pos0, l);
+  c.mark();
+  phase_o(c, M, r.wo);                                // -> E3
+  c.mark();
+  load_gu<GU_EARLY, 8>(c, l, r.wg);
+  if (!LAST) { load_qkv(c, l + 1, r.wq); load_o(c, l + 1, r.wo); }
+  gather<2 * MAXM>(c, c.buf(G_X, MAXM * D), M * D, &L.x[0][0]);
+  ++c.e;
+  c.refresh();
+  rms_rows(c, M, nw2);
+  phase_mlp(c, M, r.wg, r.wd);                        // -> E4
+  r.nw1 = nw_fetch(c, LAST ? p.norm : p.n1[l + 1]);  // next layer's norm, or the final one
+  c.mark();
+  if (LAST) {
+    load_head(c, p.audio_head + (size_t)(step - 1) * p.VP * D, D, r.wh);
+    if (step + 1 < p.K) { load_o(c, 0, r.wo); load_qkv(c, 1, r.wq); }
+  }
+  c.refresh();
+  phase_reduce(c, M);                                 // waits E4, -> E5
+  gather<2 * MAXM>(c, c.buf(G_X, MAXM * D), M * D, &L.x[0][0]);
+  ++c.e;
+}
 }  // namespace
 
 __global__ __launch_bounds__(NT, 1) void dec_frame_kernel(DecFrameArgs p) {
@@ -582,12 +658,9 @@ __global__ __launch_bounds__(NT, 1) void dec_frame_kernel(DecFrameArgs p) {
     pa[0] = bload(pr, pv, 0);
     pa[1] = bload(pr, pv, 1024);
   }
-  WQkv wq;
-  WO wo;
-  WGu wg;
-  WDn wd;
-  load_qkv(c, 0, wq);
-  load_o(c, 0, wo);
+  Pre r;
+  load_qkv(c, 0, r.wq);
+  load_o(c, 0, r.wo);
   for (int k = c.tid; k < DB; k += NT) L.xn[0][k] = p.h_last[k];
   __syncthreads();
   phase_head<DB>(c, p.c0_head, p.V, c0a, c0x, p.c0_logits);  // -> G_ARG (hand-off 0)
@@ -608,79 +681,30 @@ __global__ __launch_bounds__(NT, 1) void dec_frame_kernel(DecFrameArgs p) {
 
   // Register prefetch schedule (what is in flight during each hand-off wait):
   //   E1 (q|k|v): the cached K/V rows, this layer's down slices (issued after the QKV publish)
-//   E3 (x): this layer's gate/up slices, next layer's QKV / o
+  //   E3 (x): this layer's gate/up slices, next layer's QKV / o
   //   E4 / E5 of the last layer: this step's head rows, the next step's o / QKV
   //   E6: the next step's layer-0 cached K/V rows
-  WHd wh;
-  KvRegs kv0;  // layer 0's cached K/V rows of the next step, fetched during the head's hand-off
-  float2 nw1 = nw_fetch(c, p.n1[0]);  // RMSNorm weights, fetched a phase ahead of use
+  // The first and last layers of a step are peeled out of the layer loop (decoder_layer<FIRST,
+  // LAST>): a prefetch that crosses a step boundary (layer-0 K/V rows, head rows) is then live only
+  // between its issue and its use, not around a loop back-edge, where it would hold its registers
+  // through every layer and spill.
+  r.nw1 = nw_fetch(c, p.n1[0]);  // RMSNorm weights, fetched a phase ahead of use
   for (int step = 1; step < p.K; ++step) {
     const int M = step == 1 ? 2 : 1;
     const int pos0 = step == 1 ? 0 : step;
-    for (int l = 0; l < NL; ++l) {
-      c.refresh();
-      if (l == 0 && step > 1) {
-        // layer 0 from the folded table: q | k | v (RoPE'd at position `step`) of input row x[0]
-        const float* t = p.qkv0_tab + ((size_t)(step - 1) * p.V + L.code) * QKV;
-        float tv[(QKV + NT - 1) / NT];  // the row's loads first: the down prefetch retires after them
-#pragma unroll
-        for (int j = 0; j < (QKV + NT - 1) / NT; ++j) tv[j] = c.tid + j * NT < QKV ? t[c.tid + j * NT] : 0.f;
-        load_dn(c, l, wd);
-#pragma unroll
-        for (int j = 0; j < (QKV + NT - 1) / NT; ++j)
-          if (c.tid + j * NT < QKV) L.qkv[0][c.tid + j * NT] = tv[j];
-        kv_store(c, pos0, kv0);
-      } else {
-        KvRegs kv;
-        rms_rows(c, M, nw1);
-        phase_qkv(c, M, pos0, wq);                      // -> E1
-        // prefetches issued after the publish (its RoPE operand load would otherwise retire behind
-        // them in vmcnt order), still ahead of the hand-off wait they hide under
-        kv_issue(c, l, pos0, kv);
-        load_dn(c, l, wd);
-        gather<6>(c, c.buf(G_QKV, MAXM * QKV), M * QKV, &L.qkv[0][0]);
-        ++c.e;
-        kv_store(c, pos0, kv);
-      }
-      __syncthreads();
-      c.refresh();
-      c.mark();
-      const float2 nw2 = nw_fetch(c, p.n2[l]);
-      load_gu<0, GU_EARLY>(c, l, wg);
-      phase_attn(c, M, pos0, l);
-      c.mark();
-      phase_o(c, M, wo);                                // -> E3
-      c.mark();
-      load_gu<GU_EARLY, 8>(c, l, wg);
-      if (l + 1 < NL) { load_qkv(c, l + 1, wq); load_o(c, l + 1, wo); }
-      gather<2 * MAXM>(c, c.buf(G_X, MAXM * D), M * D, &L.x[0][0]);
-      ++c.e;
-      c.refresh();
-      rms_rows(c, M, nw2);
-      phase_mlp(c, M, wg, wd);                          // -> E4
-      nw1 = nw_fetch(c, l + 1 < NL ? p.n1[l + 1] : p.norm);  // next layer's norm, or the final one
-      c.mark();
-      if (l + 1 == NL) {
-        load_head(c, p.audio_head + (size_t)(step - 1) * p.VP * D, D, wh);
-        if (step + 1 < p.K) { load_o(c, 0, wo); load_qkv(c, 1, wq); }
-      }
-      c.refresh();
-      phase_reduce(c, M);                               // waits E4, -> E5
-      gather<2 * MAXM>(c, c.buf(G_X, MAXM * D), M * D, &L.x[0][0]);
-      ++c.e;
-    }
+    decoder_layer<true, false>(c, 0, step, M, pos0, r);
+    for (int l = 1; l < NL - 1; ++l) decoder_layer<false, false>(c, l, step, M, pos0, r);
+    decoder_layer<false, true>(c, NL - 1, step, M, pos0, r);
     // ci head on the last row: final norm, audio_head[step - 1] (generation.py:79)
     c.refresh();
-    rms_rows(c, 1, nw1, M - 1);
-    phase_head<D>(c, p.audio_head + (size_t)(step - 1) * p.VP * D, p.V, wh.a, wh.x, p.ci_logits + (size_t)(step - 1) * p.VP);  // -> E6
+    rms_rows(c, 1, r.nw1, M - 1);
+    phase_head<D>(c, p.audio_head + (size_t)(step - 1) * p.VP * D, p.V, r.wh.a, r.wh.x, p.ci_logits + (size_t)(step - 1) * p.VP);  // -> E6
+    KvRegs kv0;  // layer 0's cached K/V rows of the next step: in flight during the head's hand-off,
     if (step + 1 < p.K) kv_issue(c, 0, step + 1, kv0);
     const int ci = gather_code(c, p.V);
     ++c.e;
     if (c.w == 0 && c.tid == 0) p.codes[step] = ci;
-    if (step + 1 < p.K) {  // next input row = projection(E_a[ci + V * step]) from the folded table
-      for (int k = c.tid; k < D; k += NT) L.x[0][k] = p.proj_tab[((size_t)step * p.V + ci) * D + k];
-      __syncthreads();
-    }
+    if (step + 1 < p.K) kv_store(c, step + 1, kv0);  // and in LDS before the loop back-edge
   }
   if (p.stamps && c.tid == 0) p.stamps[(size_t)c.w * DEC_FRAME_STAMPS + DEC_FRAME_STAMPS - 1] = __builtin_amdgcn_s_memrealtime();
   if (c.w == 0 && c.tid == 0) __hip_atomic_store(p.epoch, c.tag0 - 1u + (unsigned)c.e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

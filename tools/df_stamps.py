@@ -76,10 +76,23 @@ for step in range(1, 31):
         a0, a1, oc, mp = [mk[:, step, l, i] for i in range(4)]
         e3 = rel[:, ho[(step, l, "E3")]]
         e4 = rel[:, ho[(step, l, "E4")]]
-        seg["attention"].append(np.mean(a1 - a0))
-        seg["o_proj+publish"].append(np.mean(oc - a1))
-        seg["E3 wait"].append(np.mean(e3 - oc))
-        seg["mlp compute+publish"].append(np.mean(mp - e3))
-        seg["E4 wait"].append(np.mean(e4 - mp))
+        e5 = rel[:, ho[(step, l, "E5")]]
+        # previous hand-off completion: E5 of layer l-1, or E6 of the previous step for layer 0
+        prev = rel[:, ho[(step, l - 1, "E5")]] if l else rel[:, ho[(step - 1, 3, "E5")] + 1]
+        tag = "L0" if l == 0 else "L1-3"
+        if l:
+            e1 = rel[:, ho[(step, l, "E1")]]
+            seg[f"{tag} rms+qkv+publish+E1 wait"].append(np.mean(e1 - prev))
+            seg[f"{tag} kv_store -> attn start"].append(np.mean(a0 - e1))
+        else:
+            seg[f"{tag} table row+kv_store -> attn start"].append(np.mean(a0 - prev))
+        seg[f"{tag} attention"].append(np.mean(a1 - a0))
+        seg[f"{tag} o_proj+publish"].append(np.mean(oc - a1))
+        seg[f"{tag} E3 wait"].append(np.mean(e3 - oc))
+        seg[f"{tag} rms+mlp compute+publish"].append(np.mean(mp - e3))
+        seg[f"{tag} E4 wait"].append(np.mean(e4 - mp))
+        seg[f"{tag} reduce+publish+E5 wait"].append(np.mean(e5 - e4))
+    e6 = rel[:, ho[(step, 3, "E5")] + 1]
+    seg["head: rms+head+publish+E6 wait"].append(np.mean(e6 - rel[:, ho[(step, 3, "E5")]]))
 for k, v in seg.items():
     print(f"  {k}: {np.mean(v):.2f} us (mean over WGs, steps 2-31)")
