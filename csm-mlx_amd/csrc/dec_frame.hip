@@ -94,6 +94,24 @@ __device__ __forceinline__ void dot8x2(const u32x4_t w, const float* x0, const f
   t = bf16_hi(w.w); s0 = fmaf(t, b0.w, s0); s1 = fmaf(t, b1.w, s1);
 }
 
+// dot8x2 for the step's rows only: M == 1 runs row 0's chain alone (the same fmaf order)
+template <int M>
+__device__ __forceinline__ void dotm(const u32x4_t w, const float* x0, const float* x1, float& s0, float& s1) {
+  if constexpr (M == 2) {
+    dot8x2(w, x0, x1, s0, s1);
+  } else {
+    const float4 a0 = *reinterpret_cast<const float4*>(x0), b0 = *reinterpret_cast<const float4*>(x0 + 4);
+    s0 = fmaf(bf16_lo(w.x), a0.x, s0);
+    s0 = fmaf(bf16_hi(w.x), a0.y, s0);
+    s0 = fmaf(bf16_lo(w.y), a0.z, s0);
+    s0 = fmaf(bf16_hi(w.y), a0.w, s0);
+    s0 = fmaf(bf16_lo(w.z), b0.x, s0);
+    s0 = fmaf(bf16_hi(w.z), b0.y, s0);
+    s0 = fmaf(bf16_lo(w.w), b0.z, s0);
+    s0 = fmaf(bf16_hi(w.w), b0.w, s0);
+  }
+}
+
 __device__ __forceinline__ u32x4_t wload(const bf16_t* p) { return *reinterpret_cast<const u32x4_t*>(p); }
 
 // 16-B weight load as a raw buffer load: the matrix base rides in the (uniform) descriptor, the
@@ -113,6 +131,7 @@ struct Lds {
   float qkv[MAXM][QKV];    // gathered q | k | v (RoPE'd)
   float att[MAXM][D];      // attention output
   float qs[HQ][HD];        // scaled query of one row per head
+  float2 rope[MAXM][HD / 2];// (cos, sin) of this step's positions, staged once per step
   float hb[MAXM][32];      // this WG's h columns
   float red[4 * MAXM][256];// reduce-scatter staging [row][producer]
   float wsum[8][MAXM * 8]; // per-wave partial dots
@@ -206,7 +225,8 @@ __device__ __forceinline__ void gather(Ctx& c, const u64* buf, int n, float* out
 // RMSNorm weight elements tid and tid + 512 (every element a thread scales), fetched a phase ahead
 __device__ __forceinline__ float2 nw_fetch(const Ctx& c, const float* nw) { return make_float2(nw[c.tid], nw[c.tid + NT]); }
 
-__device__ __forceinline__ void rms_rows(Ctx& c, int M, float2 nw, int m0 = 0) {
+template <int M>
+__device__ __forceinline__ void rms_rows(Ctx& c, float2 nw, int m0 = 0) {
   static_assert(D == 2 * NT, "a thread scales elements tid and tid + NT of each row");
   // sum of squares: wave m sums row m in a fixed order
   if (c.wave < M) {
@@ -284,14 +304,15 @@ __device__ __forceinline__ void load_head(Ctx& c, const bf16_t* W, int K, WHd& r
 
 // ---- phases
 // QKV rows of this WG for M rows at positions pos0..pos0+M-1 (RoPE), published to E1.
-__device__ __forceinline__ void phase_qkv(Ctx& c, int M, int pos0, const WQkv& W) {
-  if (c.wave < 6) {  // both row slots at once (row 1 is junk when M == 1)
+template <int M>
+__device__ __forceinline__ void phase_qkv(Ctx& c, int pos0, const WQkv& W) {
+  if (c.wave < 6) {
     float s0 = 0.f, s1 = 0.f;
-    dot8x2(W.a, c.L.xn[0] + 8 * c.lane, c.L.xn[1] + 8 * c.lane, s0, s1);
-    dot8x2(W.b, c.L.xn[0] + 8 * (c.lane + 64), c.L.xn[1] + 8 * (c.lane + 64), s0, s1);
+    dotm<M>(W.a, c.L.xn[0] + 8 * c.lane, c.L.xn[1] + 8 * c.lane, s0, s1);
+    dotm<M>(W.b, c.L.xn[0] + 8 * (c.lane + 64), c.L.xn[1] + 8 * (c.lane + 64), s0, s1);
     s0 = wave_sum(s0);
-    s1 = wave_sum(s1);
-    if (c.lane == 0) { c.L.wsum[c.wave][0] = s0; c.L.wsum[c.wave][1] = s1; }
+    if constexpr (M == 2) s1 = wave_sum(s1);
+    if (c.lane == 0) { c.L.wsum[c.wave][0] = s0; if constexpr (M == 2) c.L.wsum[c.wave][1] = s1; }
   }
   __syncthreads();
   u64* g = c.buf(G_QKV, MAXM * QKV);
@@ -300,7 +321,7 @@ __device__ __forceinline__ void phase_qkv(Ctx& c, int M, int pos0, const WQkv& W
     float a = c.L.wsum[2 * j][m], b = c.L.wsum[2 * j + 1][m];
     if (n < (HQ + HKV) * HD) {
       const int d = n % HD;
-      const float2 cs = *reinterpret_cast<const float2*>(c.p.rope + ((size_t)(pos0 + m) * (HD / 2) + d / 2) * 2);
+      const float2 cs = c.L.rope[m][d / 2];
       const float y0 = a * cs.x - b * cs.y, y1 = b * cs.x + a * cs.y;
       a = y0;
       b = y1;
@@ -337,12 +358,25 @@ __device__ __forceinline__ void kv_store(Ctx& c, int pos0, const KvRegs& r) {
   }
 }
 
-// Attention of rows m < M (positions pos0 + m) over keys 0..pos0+m: keys < pos0 from c.L.Ks / Vs,
-// keys pos0.. from c.L.qkv.  Every WG computes all heads (wave = head), as attn_short_head: lane =
-// (key kj = lane & 31, half hh of the head dims), scores from two half dots added by one shuffle,
-// max-subtracted softmax, P.V in key order.  WG 0 also appends the new K/V rows to the cache
-// (write-through stores, drained) for later steps.
-__device__ __forceinline__ void phase_attn(Ctx& c, int M, int pos0, int layer) {
+// The step's new K / V rows (positions pos0 .. pos0+M-1, gathered in L.qkv) appended to the LDS
+// history, so the attention reads every key from one array.
+template <int M>
+__device__ __forceinline__ void kv_append(Ctx& c, int pos0) {
+  for (int idx = c.tid; idx < M * HKV * HD; idx += NT) {
+    const int m = idx / (HKV * HD), r = idx % (HKV * HD), g = r / HD, d = r % HD;
+    c.L.Ks[g][pos0 + m][d] = c.L.qkv[m][HQ * HD + r];
+    c.L.Vs[g][pos0 + m][d] = c.L.qkv[m][(HQ + HKV) * HD + r];
+  }
+}
+
+// Attention of rows m < M (positions pos0 + m) over keys 0..pos0+m, all in c.L.Ks / Vs (kv_store +
+// kv_append).  Every WG computes all heads (wave = head), as attn_short_head: lane = (key kj =
+// lane & 31, half hh of the head dims), scores from two half dots added by one shuffle,
+// max-subtracted softmax, P.V in key order with the V rows read 8 keys at a time (all in flight
+// together; rows past the last key are read but not used).  The new K/V rows go to the cache,
+// spread over the workgroups, for later steps.
+template <int M>
+__device__ __forceinline__ void phase_attn(Ctx& c, int pos0, int layer) {
   const int h = c.wave, g = h / (HQ / HKV);
   const float scale = 0.08838834764831845f;  // 1 / sqrt(128)
   const int kj = c.lane & 31, hh = c.lane >> 5;
@@ -353,9 +387,8 @@ __device__ __forceinline__ void phase_attn(Ctx& c, int M, int pos0, int layer) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     float part = 0.f;
-    if (kj < n) {
-      const float* krow = kj < pos0 ? c.L.Ks[g][kj] : &c.L.qkv[kj - pos0][HQ * HD + g * HD];
-      const float4* k4 = reinterpret_cast<const float4*>(krow + hh * (HD / 2));
+    {
+      const float4* k4 = reinterpret_cast<const float4*>(c.L.Ks[g][kj] + hh * (HD / 2));
       const float4* q4 = reinterpret_cast<const float4*>(c.L.qs[h] + hh * (HD / 2));
       float d0 = 0.f, d1 = 0.f, d2 = 0.f, d3 = 0.f;
 #pragma unroll
@@ -376,12 +409,24 @@ __device__ __forceinline__ void phase_attn(Ctx& c, int M, int pos0, int layer) {
     const float l_run = wave_sum(hh == 0 ? pj : 0.f);
     const int pji = __float_as_int(pj);
     float o0 = 0.f, o1 = 0.f;
-#pragma unroll 4
-    for (int j = 0; j < n; ++j) {
-      const float pb = __int_as_float(__builtin_amdgcn_readlane(pji, j));
-      const float* vr = j < pos0 ? c.L.Vs[g][j] : &c.L.qkv[j - pos0][(HQ + HKV) * HD + g * HD];
-      o0 = fmaf(pb, vr[c.lane], o0);
-      o1 = fmaf(pb, vr[c.lane + 64], o1);
+#pragma unroll
+    for (int j0 = 0; j0 < 32; j0 += 8) {
+      if (j0 < n) {
+        float va[8], vb[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          va[u] = c.L.Vs[g][j0 + u][c.lane];
+          vb[u] = c.L.Vs[g][j0 + u][c.lane + 64];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if (j0 + u < n) {
+            const float pb = __int_as_float(__builtin_amdgcn_readlane(pji, j0 + u));
+            o0 = fmaf(pb, va[u], o0);
+            o1 = fmaf(pb, vb[u], o1);
+          }
+        }
+      }
     }
     const float inv = 1.f / l_run;
     c.L.att[m][h * HD + c.lane] = o0 * inv;
@@ -400,14 +445,15 @@ __device__ __forceinline__ void phase_attn(Ctx& c, int M, int pos0, int layer) {
 }
 
 // o_proj rows 4w..4w+3 (+ residual) -> E3 granules
-__device__ __forceinline__ void phase_o(Ctx& c, int M, const WO& W) {
+template <int M>
+__device__ __forceinline__ void phase_o(Ctx& c, const WO& W) {
   {
     const int k = 8 * ((c.wave & 1) * 64 + c.lane);
     float s0 = 0.f, s1 = 0.f;
-    dot8x2(W.a, c.L.att[0] + k, c.L.att[1] + k, s0, s1);
+    dotm<M>(W.a, c.L.att[0] + k, c.L.att[1] + k, s0, s1);
     s0 = wave_sum(s0);
-    s1 = wave_sum(s1);
-    if (c.lane == 0) { c.L.wsum[c.wave][0] = s0; c.L.wsum[c.wave][1] = s1; }
+    if constexpr (M == 2) s1 = wave_sum(s1);
+    if (c.lane == 0) { c.L.wsum[c.wave][0] = s0; if constexpr (M == 2) c.L.wsum[c.wave][1] = s1; }
   }
   __syncthreads();
   if (c.tid < 4 * M) {
@@ -418,15 +464,16 @@ __device__ __forceinline__ void phase_o(Ctx& c, int M, const WO& W) {
 }
 
 // gate/up (64 rows -> h[32]) and the split-K down partials of this WG's columns -> E4 granules
-__device__ __forceinline__ void phase_mlp(Ctx& c, int M, const WGu& G, const WDn& Wd) {
+template <int M>
+__device__ __forceinline__ void phase_mlp(Ctx& c, const WGu& G, const WDn& Wd) {
   {
     float s[8][2];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       s[i][0] = 0.f;
       s[i][1] = 0.f;
-      dot8x2(G.a[i][0], c.L.xn[0] + 8 * c.lane, c.L.xn[1] + 8 * c.lane, s[i][0], s[i][1]);
-      dot8x2(G.a[i][1], c.L.xn[0] + 8 * (c.lane + 64), c.L.xn[1] + 8 * (c.lane + 64), s[i][0], s[i][1]);
+      dotm<M>(G.a[i][0], c.L.xn[0] + 8 * c.lane, c.L.xn[1] + 8 * c.lane, s[i][0], s[i][1]);
+      dotm<M>(G.a[i][1], c.L.xn[0] + 8 * (c.lane + 64), c.L.xn[1] + 8 * (c.lane + 64), s[i][0], s[i][1]);
     }
 #pragma unroll
     for (int m = 0; m < MAXM; ++m) {
@@ -449,8 +496,8 @@ __device__ __forceinline__ void phase_mlp(Ctx& c, int M, const WGu& G, const WDn
     float a0 = 0.f, a1 = 0.f;
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-      dot8x2(Wd.a[s][q][0], c.L.hb[0] + 16 * q, c.L.hb[1] + 16 * q, a0, a1);
-      dot8x2(Wd.a[s][q][1], c.L.hb[0] + 16 * q + 8, c.L.hb[1] + 16 * q + 8, a0, a1);
+      dotm<M>(Wd.a[s][q][0], c.L.hb[0] + 16 * q, c.L.hb[1] + 16 * q, a0, a1);
+      dotm<M>(Wd.a[s][q][1], c.L.hb[0] + 16 * q + 8, c.L.hb[1] + 16 * q + 8, a0, a1);
     }
     gput(g + c.tid + 512 * s, a0, c.tag());
     if (M > 1) gput(g + D + c.tid + 512 * s, a1, c.tag());
@@ -458,7 +505,8 @@ __device__ __forceinline__ void phase_mlp(Ctx& c, int M, const WGu& G, const WDn
 }
 
 // Reduce-scatter: rows 4w..4w+3 of every producer's partials (fixed order), + residual -> E5
-__device__ __forceinline__ void phase_reduce(Ctx& c, int M) {
+template <int M>
+__device__ __forceinline__ void phase_reduce(Ctx& c) {
   const unsigned tag = c.tag();
   const u64* g = c.buf(G_PART, (size_t)NWG * MAXM * D);
   const int v = c.tid >> 1, half = c.tid & 1;
@@ -574,11 +622,16 @@ struct Pre {
 // >= 2 takes q | k | v (RoPE'd) from the folded qkv0 table and its input row from proj_tab (no QKV
 // hand-off).  LAST: the final layer, which also fetches this step's head rows and the next step's
 // layer-0 o / layer-1 QKV slices.
-template <bool FIRST, bool LAST>
-__device__ __forceinline__ void decoder_layer(Ctx& c, int l, int step, int M, int pos0, Pre& r) {
+template <int M, bool FIRST, bool LAST>
+__device__ __forceinline__ void decoder_layer(Ctx& c, int l, int step, int pos0, Pre& r) {
   const DecFrameArgs& p = c.p;
   Lds& L = c.L;
   c.refresh();
+  // FIRST: RoPE (cos, sin) of this step's positions, loaded with the layer's first loads and staged
+  // in LDS for the QKV epilogues of every layer (no global round trip before a QKV publish)
+  float2 rp = make_float2(0.f, 0.f);
+  if (FIRST && c.tid < M * (HD / 2))
+    rp = reinterpret_cast<const float2*>(p.rope)[(size_t)pos0 * (HD / 2) + c.tid];
   if (FIRST && step > 1) {
     // q | k | v of input row proj_tab[step - 1][code] at position `step`, and the row itself; both
     // loads are in flight together, ahead of the down prefetch (vmcnt retires in issue order)
@@ -595,44 +648,72 @@ __device__ __forceinline__ void decoder_layer(Ctx& c, int l, int step, int M, in
       if (c.tid + j * NT < QKV) L.qkv[0][c.tid + j * NT] = tv[j];
 #pragma unroll
     for (int j = 0; j < D / NT; ++j) L.x[0][c.tid + j * NT] = xv[j];
+    if (c.tid < M * (HD / 2)) L.rope[c.tid / (HD / 2)][c.tid % (HD / 2)] = rp;
+    __syncthreads();  // L.qkv complete before kv_append reads it
+    kv_append<M>(c, pos0);
   } else {
     KvRegs kv;
-    rms_rows(c, M, r.nw1);
-    phase_qkv(c, M, pos0, r.wq);                      // -> E1
+    if (FIRST && c.tid < M * (HD / 2)) L.rope[c.tid / (HD / 2)][c.tid % (HD / 2)] = rp;
+    rms_rows<M>(c, r.nw1);  // (its barriers also publish the RoPE rows)
+    phase_qkv<M>(c, pos0, r.wq);                      // -> E1
     // prefetches issued after the publish (its RoPE operand load would otherwise retire behind
     // them in vmcnt order), still ahead of the hand-off wait they hide under
     kv_issue(c, l, pos0, kv);
     load_dn(c, l, r.wd);
-    gather<6>(c, c.buf(G_QKV, MAXM * QKV), M * QKV, &L.qkv[0][0]);
+    gather<(M * QKV + NT - 1) / NT>(c, c.buf(G_QKV, MAXM * QKV), M * QKV, &L.qkv[0][0]);
     ++c.e;
     kv_store(c, pos0, kv);
+    kv_append<M>(c, pos0);
   }
   __syncthreads();
   c.refresh();
   c.mark();
   const float2 nw2 = nw_fetch(c, p.n2[l]);
   load_gu<0, GU_EARLY>(c, l, r.wg);
-  phase_attn(c, M, pos0, l);
+  phase_attn<M>(c, pos0, l);
   c.mark();
-  phase_o(c, M, r.wo);                                // -> E3
+  phase_o<M>(c, r.wo);                                // -> E3
   c.mark();
   load_gu<GU_EARLY, 8>(c, l, r.wg);
   if (!LAST) { load_qkv(c, l + 1, r.wq); load_o(c, l + 1, r.wo); }
-  gather<2 * MAXM>(c, c.buf(G_X, MAXM * D), M * D, &L.x[0][0]);
+  gather<M * D / NT>(c, c.buf(G_X, MAXM * D), M * D, &L.x[0][0]);
   ++c.e;
   c.refresh();
-  rms_rows(c, M, nw2);
-  phase_mlp(c, M, r.wg, r.wd);                        // -> E4
+  rms_rows<M>(c, nw2);
+  phase_mlp<M>(c, r.wg, r.wd);                        // -> E4
   r.nw1 = nw_fetch(c, LAST ? p.norm : p.n1[l + 1]);  // next layer's norm, or the final one
   c.mark();
   if (LAST) {
     load_head(c, p.audio_head + (size_t)(step - 1) * p.VP * D, D, r.wh);
-    if (step + 1 < p.K) { load_o(c, 0, r.wo); load_qkv(c, 1, r.wq); }
+    if (step + 1 < p.K) {
+      load_o(c, 0, r.wo);
+      load_qkv(c, 1, r.wq);
+    }
   }
   c.refresh();
-  phase_reduce(c, M);                                 // waits E4, -> E5
-  gather<2 * MAXM>(c, c.buf(G_X, MAXM * D), M * D, &L.x[0][0]);
+  phase_reduce<M>(c);                                 // waits E4, -> E5
+  gather<M * D / NT>(c, c.buf(G_X, MAXM * D), M * D, &L.x[0][0]);
   ++c.e;
+}
+
+// One decoder step (generation.py:72-90): 4 layers over the step's M rows, the ci head, the arg-max.
+template <int M>
+__device__ __forceinline__ void run_step(Ctx& c, int step, Pre& r) {
+  const DecFrameArgs& p = c.p;
+  const int pos0 = M == 2 ? 0 : step;  // step 1: positions 0, 1
+  decoder_layer<M, true, false>(c, 0, step, pos0, r);
+  for (int l = 1; l < NL - 1; ++l) decoder_layer<M, false, false>(c, l, step, pos0, r);
+  decoder_layer<M, false, true>(c, NL - 1, step, pos0, r);
+  // ci head on the last row: final norm, audio_head[step - 1] (generation.py:79)
+  c.refresh();
+  rms_rows<1>(c, r.nw1, M - 1);
+  phase_head<D>(c, p.audio_head + (size_t)(step - 1) * p.VP * D, p.V, r.wh.a, r.wh.x, p.ci_logits + (size_t)(step - 1) * p.VP);  // -> E6
+  KvRegs kv0;  // layer 0's cached K/V rows of the next step: in flight during the head's hand-off,
+  if (step + 1 < p.K) kv_issue(c, 0, step + 1, kv0);
+  const int ci = gather_code(c, p.V);
+  ++c.e;
+  if (c.w == 0 && c.tid == 0) p.codes[step] = ci;
+  if (step + 1 < p.K) kv_store(c, step + 1, kv0);  // and in LDS before the loop back-edge
 }
 }  // namespace
 
@@ -689,23 +770,10 @@ __global__ __launch_bounds__(NT, 1) void dec_frame_kernel(DecFrameArgs p) {
   // between its issue and its use, not around a loop back-edge, where it would hold its registers
   // through every layer and spill.
   r.nw1 = nw_fetch(c, p.n1[0]);  // RMSNorm weights, fetched a phase ahead of use
-  for (int step = 1; step < p.K; ++step) {
-    const int M = step == 1 ? 2 : 1;
-    const int pos0 = step == 1 ? 0 : step;
-    decoder_layer<true, false>(c, 0, step, M, pos0, r);
-    for (int l = 1; l < NL - 1; ++l) decoder_layer<false, false>(c, l, step, M, pos0, r);
-    decoder_layer<false, true>(c, NL - 1, step, M, pos0, r);
-    // ci head on the last row: final norm, audio_head[step - 1] (generation.py:79)
-    c.refresh();
-    rms_rows(c, 1, r.nw1, M - 1);
-    phase_head<D>(c, p.audio_head + (size_t)(step - 1) * p.VP * D, p.V, r.wh.a, r.wh.x, p.ci_logits + (size_t)(step - 1) * p.VP);  // -> E6
-    KvRegs kv0;  // layer 0's cached K/V rows of the next step: in flight during the head's hand-off,
-    if (step + 1 < p.K) kv_issue(c, 0, step + 1, kv0);
-    const int ci = gather_code(c, p.V);
-    ++c.e;
-    if (c.w == 0 && c.tid == 0) p.codes[step] = ci;
-    if (step + 1 < p.K) kv_store(c, step + 1, kv0);  // and in LDS before the loop back-edge
-  }
+  // step 1 carries two rows ([h_last, E_a[c0]]), steps >= 2 one: each its own instantiation, so the
+  // one-row steps compute and read nothing for a second row
+  run_step<2>(c, 1, r);
+  for (int step = 2; step < p.K; ++step) run_step<1>(c, step, r);
   if (p.stamps && c.tid == 0) p.stamps[(size_t)c.w * DEC_FRAME_STAMPS + DEC_FRAME_STAMPS - 1] = __builtin_amdgcn_s_memrealtime();
   if (c.w == 0 && c.tid == 0) __hip_atomic_store(p.epoch, c.tag0 - 1u + (unsigned)c.e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
