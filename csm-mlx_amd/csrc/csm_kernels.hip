@@ -22,39 +22,47 @@
 // (generation.py:34-36).  Row pointers are resolved once into LDS; each thread then sums 8
 // consecutive dims with independent 16-B loads.
 template <typename WT>
-__global__ __launch_bounds__(256) void embed_rows_kernel(EmbedParams p) {
-  __shared__ const WT* rows[64];
-  const int m = blockIdx.x;
+__global__ __launch_bounds__(64) void embed_rows_kernel(EmbedParams p) {
+  // one wave per 512 columns of row m; every row's 16-B slice is loaded before any is summed (one
+  // memory round trip for all K + 1 rows), then added in column order j = 0..K as before
+  constexpr int CH = 33;
+  const int m = blockIdx.x, t = threadIdx.x;
   const int ncol = p.K + 1;
-  if (threadIdx.x < ncol) {
-    const int j = threadIdx.x;
-    const WT* r = nullptr;
-    if (p.codes) {  // decode: row = [codes, 0], mask = [1]*K + [0]  (generation.py:156-161)
-      if (j < p.K) r = (const WT*)p.audio_emb + ((size_t)p.codes[(size_t)m * p.K + j] + (size_t)p.V * j) * p.D;
-    } else if (p.mask[(size_t)m * ncol + j]) {
-      const int t = p.tok[(size_t)m * ncol + j];
-      r = (j < p.K) ? (const WT*)p.audio_emb + ((size_t)t + (size_t)p.V * j) * p.D
-                    : (const WT*)p.text_emb + (size_t)t * p.D;
+  if (p.pos_inc && blockIdx.y == 0 && t == 0) p.pos_inc[m] += 1;
+  const int d0 = (blockIdx.y * 64 + t) * 8;
+  if (d0 >= p.D) return;
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int j0 = 0; j0 < ncol; j0 += CH) {
+    Raw8<WT> raw[CH];
+    bool live[CH];
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+      const int j = j0 + u;
+      const WT* r = nullptr;
+      if (j < ncol) {
+        if (p.codes) {  // decode: row = [codes, 0], mask = [1]*K + [0]  (generation.py:156-161)
+          if (j < p.K) r = (const WT*)p.audio_emb + ((size_t)p.codes[(size_t)m * p.K + j] + (size_t)p.V * j) * p.D;
+        } else if (p.mask[(size_t)m * ncol + j]) {
+          const int tk = p.tok[(size_t)m * ncol + j];
+          r = (j < p.K) ? (const WT*)p.audio_emb + ((size_t)tk + (size_t)p.V * j) * p.D
+                        : (const WT*)p.text_emb + (size_t)tk * p.D;
+        }
+      }
+      live[u] = r != nullptr;
+      raw[u].template load<false>((r ? r : (const WT*)p.audio_emb) + d0);
     }
-    rows[j] = r;
-  }
-  __syncthreads();
-  if (p.pos_inc && threadIdx.x == 0) p.pos_inc[m] += 1;
-  float* out = p.out + (size_t)m * p.D;
-  for (int d0 = threadIdx.x * 8; d0 < p.D; d0 += blockDim.x * 8) {
-    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll 4
-    for (int j = 0; j < ncol; ++j) {
-      const WT* r = rows[j];
-      if (!r) continue;  // masked columns contribute exact zeros
+#pragma unroll
+    for (int u = 0; u < CH; ++u) {
+      if (!live[u]) continue;  // masked columns contribute exact zeros
       float w[8];
-      W8<WT>::load(r + d0, w);
+      raw[u].get(w);
 #pragma unroll
       for (int e = 0; e < 8; ++e) acc[e] += w[e];
     }
-    *reinterpret_cast<float4*>(out + d0) = make_float4(acc[0], acc[1], acc[2], acc[3]);
-    *reinterpret_cast<float4*>(out + d0 + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
   }
+  float* out = p.out + (size_t)m * p.D;
+  *reinterpret_cast<float4*>(out + d0) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+  *reinterpret_cast<float4*>(out + d0 + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
 }
 
 // ============================================================================ GEMV
@@ -1157,8 +1165,9 @@ void launch_to_f32(const void* src, int wdt, float* dst, size_t n, hipStream_t s
 }
 
 void launch_embed(const EmbedParams& p, int wdt, int M, hipStream_t st) {
-  if (wdt == WDT_BF16) hipLaunchKernelGGL(embed_rows_kernel<bf16_t>, dim3(M), dim3(256), 0, st, p);
-  else hipLaunchKernelGGL(embed_rows_kernel<float>, dim3(M), dim3(256), 0, st, p);
+  const dim3 grid(M, (p.D + 511) / 512);
+  if (wdt == WDT_BF16) hipLaunchKernelGGL(embed_rows_kernel<bf16_t>, grid, dim3(64), 0, st, p);
+  else hipLaunchKernelGGL(embed_rows_kernel<float>, grid, dim3(64), 0, st, p);
 }
 
 static bool g_attn_short = [] { const char* e = getenv("CSM_ATTN_SHORT"); return !(e && e[0] == '0'); }();
