@@ -13,6 +13,7 @@
 // Weights are streamed straight to VGPRs with 16-B loads (GEMV / M <= 16 regime: no LDS
 // round trip); x rows are tiny and served from L1/L2.
 #include "csm_kernels.h"
+#include "engine_util.h"
 
 #include <cstdlib>
 
@@ -23,12 +24,23 @@
 // consecutive dims with independent 16-B loads.
 template <typename WT>
 __global__ __launch_bounds__(64) void embed_rows_kernel(EmbedParams p) {
-  // one wave per 512 columns of row m; every row's 16-B slice is loaded before any is summed (one
-  // memory round trip for all K + 1 rows), then added in column order j = 0..K as before
+  // one wave per 512 columns of row m.  Lane j (< K + 1 <= 64) resolves column j's table row (one
+  // vector load of all codes / tokens / masks at once), then every row's 16-B slice is loaded
+  // before any is summed (one memory round trip for all K + 1 rows), added in column order j = 0..K.
   constexpr int CH = 33;
   const int m = blockIdx.x, t = threadIdx.x;
   const int ncol = p.K + 1;
   if (p.pos_inc && blockIdx.y == 0 && t == 0) p.pos_inc[m] += 1;
+  long long off = -1;  // element offset of column t's row in its table, -1 when masked
+  if (t < ncol) {
+    if (p.codes) {  // decode: row = [codes, 0], mask = [1]*K + [0]  (generation.py:156-161)
+      if (t < p.K) off = ((long long)p.codes[(size_t)m * p.K + t] + (long long)p.V * t) * p.D;
+    } else if (p.mask[(size_t)m * ncol + t]) {
+      const long long tk = p.tok[(size_t)m * ncol + t];
+      off = t < p.K ? (tk + (long long)p.V * t) * p.D : tk * p.D;
+    }
+  }
+  const int off_lo = (int)(unsigned long long)off, off_hi = (int)((unsigned long long)off >> 32);
   const int d0 = (blockIdx.y * 64 + t) * 8;
   if (d0 >= p.D) return;
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -38,18 +50,13 @@ __global__ __launch_bounds__(64) void embed_rows_kernel(EmbedParams p) {
 #pragma unroll
     for (int u = 0; u < CH; ++u) {
       const int j = j0 + u;
-      const WT* r = nullptr;
-      if (j < ncol) {
-        if (p.codes) {  // decode: row = [codes, 0], mask = [1]*K + [0]  (generation.py:156-161)
-          if (j < p.K) r = (const WT*)p.audio_emb + ((size_t)p.codes[(size_t)m * p.K + j] + (size_t)p.V * j) * p.D;
-        } else if (p.mask[(size_t)m * ncol + j]) {
-          const int tk = p.tok[(size_t)m * ncol + j];
-          r = (j < p.K) ? (const WT*)p.audio_emb + ((size_t)tk + (size_t)p.V * j) * p.D
-                        : (const WT*)p.text_emb + (size_t)tk * p.D;
-        }
-      }
-      live[u] = r != nullptr;
-      raw[u].template load<false>((r ? r : (const WT*)p.audio_emb) + d0);
+      long long o = -1;
+      if (j < ncol)
+        o = (long long)(((unsigned long long)(unsigned)__builtin_amdgcn_readlane(off_hi, j) << 32) |
+                        (unsigned)__builtin_amdgcn_readlane(off_lo, j));
+      live[u] = o >= 0;
+      const WT* base = (const WT*)(j < p.K ? p.audio_emb : p.text_emb);
+      raw[u].template load<false>(base + (o >= 0 ? o : 0) + d0);
     }
 #pragma unroll
     for (int u = 0; u < CH; ++u) {
@@ -996,18 +1003,21 @@ __global__ void advance_kernel(AdvanceParams p) {
     }
     __syncthreads();
   }
-  for (int b = threadIdx.x; b < p.B; b += blockDim.x) {
-    bool any = false;
-    for (int k = 0; k < p.K; ++k) {
-      const int c = p.codes[(size_t)b * p.K + k];
-      any |= (c != 0);
-      if (f < p.F_cap) p.hist[((size_t)f * p.B + b) * p.K + k] = c;
+  {  // one wave per utterance, lane k = codebook k (K <= 64): codes read once, history row written
+     // coalesced, the all-zero test by a wave vote
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int b = wave; b < p.B; b += nw) {
+      const int c = lane < p.K ? p.codes[(size_t)b * p.K + lane] : 0;
+      if (lane < p.K && f < p.F_cap) p.hist[((size_t)f * p.B + b) * p.K + lane] = c;
+      const bool any = __any(c != 0);
+      if (lane == 0) {
+        if (!any && !p.done[b]) {  // EOS: all-zero frame, not emitted (generation.py:151)
+          p.done[b] = 1;
+          p.n_frames[b] = f;
+        }
+        if (!p.done[b]) p.n_frames[b] = f + 1;
+      }
     }
-    if (!any && !p.done[b]) {  // EOS: all-zero frame, not emitted (generation.py:151)
-      p.done[b] = 1;
-      p.n_frames[b] = f;
-    }
-    if (!p.done[b]) p.n_frames[b] = f + 1;
   }
   __syncthreads();
   if (threadIdx.x == 0) p.frame_ctr[0] = f + 1;
@@ -1165,6 +1175,7 @@ void launch_to_f32(const void* src, int wdt, float* dst, size_t n, hipStream_t s
 }
 
 void launch_embed(const EmbedParams& p, int wdt, int M, hipStream_t st) {
+  if (p.K + 1 > 64) throw CsmError(CSM_ERR_ARG, "embedding gather: at most 63 codebooks");
   const dim3 grid(M, (p.D + 511) / 512);
   if (wdt == WDT_BF16) hipLaunchKernelGGL(embed_rows_kernel<bf16_t>, grid, dim3(64), 0, st, p);
   else hipLaunchKernelGGL(embed_rows_kernel<float>, grid, dim3(64), 0, st, p);
@@ -1394,6 +1405,7 @@ void launch_forced_ce(const float* c0, const float* ci, const int* forced, float
 }
 
 void launch_advance(const AdvanceParams& p, hipStream_t st) {
+  if (p.K > 64) throw CsmError(CSM_ERR_ARG, "advance: at most 64 codebooks");
   hipLaunchKernelGGL(advance_kernel, dim3(1), dim3(256), 0, st, p);
 }
 

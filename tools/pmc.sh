@@ -2,8 +2,8 @@
 # rocprofv3 PMC passes (one pass per counter group, each its own run) over one bench configuration,
 # eager launches (CSM_GRAPH=0: rocprofv3 cannot trace graph replays here), then a per-kernel summary.
 # A counter pass serializes every dispatch and prints nothing for minutes: a heartbeat file under
-# gpurun_out/ keeps the run visibly alive.  CSM_QKV0_TAB=0 skips the folded layer-0 table (~15k one-time build
-# launches, each serialized by the counters; the batched path does not read it).
+# gpurun_out/ keeps the run visibly alive.  (The folded layer-0 table stays on: the persistent frame
+# decoder needs it, and its build is one launch per codebook.)
 # usage: tools/pmc.sh <tag> <bench args...>      -> gpurun_out/pmc_<tag>/summary.txt
 set -o pipefail
 tag=$1; shift
@@ -16,7 +16,7 @@ trap 'kill $hb 2>/dev/null' EXIT
 i=0
 for pmc in "SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES GRBM_GUI_ACTIVE" "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
-  CSM_GRAPH=0 CSM_QKV0_TAB=0 timeout -s KILL 400 rocprofv3 --pmc $pmc --kernel-trace --output-format csv -d $out/p$i -o run -- \
+  CSM_GRAPH=0 timeout -s KILL 400 rocprofv3 --pmc $pmc --kernel-trace --output-format csv -d $out/p$i -o run -- \
     python3 bench.py --no-cpu-baseline "$@" > $out/p$i.json 2> $out/p$i.err || { echo "pass $i ($pmc) failed rc=$?"; tail -5 $out/p$i.err; exit 1; }
   echo "pass $i done: $pmc"
 done
