@@ -1,0 +1,442 @@
+// Persistent backbone step: the 16 Llama blocks of csm_1b's backbone for one decode row (batch 1,
+// bf16 weights) plus the final RMSNorm -> h_last, in ONE launch (/root/reference/csm_mlx/models.py:
+// 50-51 + generation.py:32-42: self.backbone(h, mask, cache) then norm(h[:, -1])).
+//
+// Why: at batch 1 the backbone is 16 x 5 dependent launches (QKV, attention, o_proj, gate/up, down);
+// each pays a kernel boundary plus its own ramp and drain around a 8-67 MB weight stream.  Here every
+// CU keeps one workgroup for the whole step, owns a fixed slice of every matrix and streams it into
+// registers ahead of the hand-off that releases its input (the same machinery as dec_frame.hip).
+//
+// Work split (NWG = 256 workgroups = one per CU, 512 threads = 8 waves each), per layer:
+//   QKV     3072 rows: 12 per WG (RoPE pairs stay inside a WG; k / v rows appended to the cache)
+//                                                              -> q | k | v granules      (E1)
+//   attention: WG a < 32 = query head a (group a / 4): gathers q_a, k_g, v_g (192 granules), keys
+//           < pos from the cache, key pos from the granules; 8 waves x 64-key blocks, online softmax,
+//           waves combined in fixed order                        -> att granules            (E2)
+//   o_proj  2048 rows: 8 per WG, + residual                      -> x granules              (E3)
+//   gate/up 16384 interleaved rows: 64 per WG (8 per wave) -> 32 SiLU*up columns
+//   down    split-K over those 32 columns (chunk-major copy [F/8][D][8]) -> 2048 partials     (E4)
+//           WG w sums rows 8w..8w+7 of every producer in a fixed order, + residual -> x       (E5)
+// Five hand-offs per layer; after the last layer every WG holds x, WG 0 writes h_last.
+//
+// Arithmetic: fp32 accumulation of bf16 weights x fp32 activations, RMSNorm as the oracle
+// (x * rsqrt(mean(x^2) + eps) * w), RoPE on interleaved pairs (attention.py:157-177, the engine's
+// EPI_QKV convention), softmax with max subtraction, every reduction in a fixed order
+// (deterministic run to run; summation order differs from the launch path's GEMVs).
+#include "csm_kernels.h"
+#include "handoff.h"
+
+namespace {
+
+using namespace handoff;
+
+constexpr int NWG = BB_STEP_WGS, NT = BB_STEP_THREADS;
+constexpr int D = 2048, F = 8192, HQ = 32, HKV = 8, HD = 64, NL = BB_STEP_LAYERS;
+constexpr int QKV = (HQ + 2 * HKV) * HD;  // 3072
+constexpr int NATT = HQ;                  // attention workgroups: one per query head
+constexpr unsigned SPIN_LIMIT = 1u << 22; // ~0.1 s of s_sleep per hand-off before declaring failure
+
+// granule regions (u64 offsets), double-buffered by hand-off parity
+constexpr size_t G_QKV = 0;                                   // [2][QKV]
+constexpr size_t G_ATT = G_QKV + 2 * QKV;                     // [2][D]
+constexpr size_t G_X = G_ATT + 2 * D;                         // [2][D]
+constexpr size_t G_PART = G_X + 2 * D;                        // [2][NWG][D]
+constexpr size_t G_TOTAL = G_PART + (size_t)2 * NWG * D;
+
+struct Lds {
+  float x[D];            // residual
+  float xn[D];           // normed projection input
+  float att[D];          // attention output (o_proj input)
+  float red[8][NWG];     // reduce-scatter staging [row][producer]
+  float wsum[8][8];      // per-wave partial dots
+  float hb[32];          // this WG's SiLU*up columns
+  float2 rope[HD / 2];   // (cos, sin) at the step's position
+  float q[HD], kn[HD], vn[HD];          // attention WGs: the head's q and the new k / v row
+  float am[8], al[8], ao[8][HD];        // attention WGs: per-wave online-softmax partials
+};
+
+struct Ctx {
+  const BbStepArgs& p;
+  Lds& L;
+  int w, tid, lane, wave;
+  unsigned tag0;
+  int e;  // hand-off counter
+  __device__ void refresh() {
+    tid = opaque_tid();
+    lane = tid & 63;
+    wave = tid >> 6;
+  }
+  __device__ unsigned tag() const { return tag0 + (unsigned)e; }
+  __device__ u64* buf(size_t region, size_t per) const { return p.gbuf + region + (size_t)(e & 1) * per; }
+};
+
+__device__ __forceinline__ bool spin_fail(Ctx& c, unsigned spin) {
+  if (spin >= SPIN_LIMIT || ((spin & 255) == 255 && __hip_atomic_load(c.p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+    __hip_atomic_store(c.p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+  }
+  return false;
+}
+
+// Wait until granules [0, n) of buf carry this hand-off's tag; values -> out (LDS).
+template <int GPT>
+__device__ __forceinline__ void gather(Ctx& c, const u64* buf, int n, float* out) {
+  const unsigned tag = c.tag();
+  u64 g[GPT];
+#pragma unroll
+  for (int u = 0; u < GPT; ++u) {
+    const int i = c.tid + u * NT;
+    g[u] = i < n ? gload(buf + i) : ((u64)tag << 32);
+  }
+  for (unsigned spin = 0;; ++spin) {
+    bool ok = true;
+#pragma unroll
+    for (int u = 0; u < GPT; ++u) ok &= (unsigned)(g[u] >> 32) == tag;
+    if (ok || spin_fail(c, spin)) break;
+    __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+    for (int u = 0; u < GPT; ++u) {
+      const int i = c.tid + u * NT;
+      if (i < n && (unsigned)(g[u] >> 32) != tag) g[u] = gload(buf + i);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < GPT; ++u) {
+    const int i = c.tid + u * NT;
+    if (i < n) out[i] = __uint_as_float((unsigned)g[u]);
+  }
+  __syncthreads();
+}
+
+// xn[k] = x[k] * rsqrt(mean(x^2) + eps) * nw[k]; nw elements tid + 512 j fetched a phase ahead
+struct Nw { float v[D / NT]; };
+__device__ __forceinline__ Nw nw_fetch(const Ctx& c, const float* nw) {
+  Nw r;
+#pragma unroll
+  for (int j = 0; j < D / NT; ++j) r.v[j] = nw[c.tid + j * NT];
+  return r;
+}
+__device__ __forceinline__ void rms(Ctx& c, const Nw& nw, float* out) {
+  if (c.wave == 0) {  // sum of squares in a fixed order
+    float s = 0.f;
+#pragma unroll 8
+    for (int k = c.lane; k < D; k += 64) s = fmaf(c.L.x[k], c.L.x[k], s);
+    s = wave_sum(s);
+    if (c.lane == 0) c.L.wsum[0][0] = s;
+  }
+  __syncthreads();
+  const float r = rsqrtf(c.L.wsum[0][0] / (float)D + c.p.eps);
+#pragma unroll
+  for (int j = 0; j < D / NT; ++j) out[c.tid + j * NT] = c.L.x[c.tid + j * NT] * r * nw.v[j];
+  __syncthreads();
+}
+
+// ---- weight slices held in registers
+// QKV / o_proj: thread (half h = tid >> 8, chunk c = tid & 255) holds chunk c of rows 6h+i / 4h+i
+struct WQ { u32x4_t a[6]; };
+struct WO { u32x4_t a[4]; };
+// gate/up: wave v holds rows 8v + r, chunks lane + 64 q (q < 4); split in halves r < 4 / r >= 4
+struct WGu { u32x4_t a[4][4]; };
+// down: thread t holds rows t + 512 k (k < 4) of the WG's 4 column chunks (8 columns each)
+struct WDn { u32x4_t a[4][4]; };
+
+__device__ __forceinline__ void load_q(Ctx& c, int l, WQ& r) {
+  const bf16_t* base = c.p.wqkv[l] + (size_t)(12 * c.w + 6 * (c.tid >> 8)) * D;
+  const int v = (c.tid & 255) * 16;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) r.a[i] = bload<2>(base, v, i * D * 2);
+}
+__device__ __forceinline__ void load_o(Ctx& c, int l, WO& r) {
+  const bf16_t* base = c.p.wo[l] + (size_t)(8 * c.w + 4 * (c.tid >> 8)) * D;
+  const int v = (c.tid & 255) * 16;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r.a[i] = bload<2>(base, v, i * D * 2);
+}
+template <int HALF>
+__device__ __forceinline__ void load_gu(Ctx& c, int l, WGu& r) {
+  const bf16_t* base = c.p.wgu[l] + (size_t)(64 * c.w + 8 * c.wave + 4 * HALF) * D;
+  const int v = c.lane * 16;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) r.a[i][q] = bload<2>(base, v, i * D * 2 + q * 64 * 16);
+}
+__device__ __forceinline__ void load_dn(Ctx& c, int l, WDn& r) {
+  // chunk 4w + q of [F/8][D][8]: row n at byte (n * 8) * 2
+  const bf16_t* base = c.p.wdc[l] + (size_t)(4 * c.w) * D * 8;
+  const int v = c.tid * 16;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) r.a[k][q] = bload<2>(base, v, (q * D * 8 + k * NT * 8) * 2);
+}
+
+// per-row partial sums of a (half, chunk)-split projection: wave partials -> wsum[wave][i]
+template <int R>
+__device__ __forceinline__ void rows_reduce(Ctx& c, float (&s)[R]) {
+#pragma unroll
+  for (int i = 0; i < R; ++i) s[i] = wave_sum(s[i]);
+  if (c.lane == 0) {
+#pragma unroll
+    for (int i = 0; i < R; ++i) c.L.wsum[c.wave][i] = s[i];
+  }
+  __syncthreads();
+}
+// row i of half h: waves 4h..4h+3 in order
+__device__ __forceinline__ float row_total(const Ctx& c, int h, int i) {
+  return ((c.L.wsum[4 * h][i] + c.L.wsum[4 * h + 1][i]) + c.L.wsum[4 * h + 2][i]) + c.L.wsum[4 * h + 3][i];
+}
+
+// QKV rows 12w.. (RoPE at pos), published to E1; k / v rows also appended to the cache at pos
+__device__ __forceinline__ void phase_qkv(Ctx& c, int l, int pos, const WQ& W) {
+  float s[6];
+  const float* xc = c.L.xn + 8 * (c.tid & 255);
+#pragma unroll
+  for (int i = 0; i < 6; ++i) s[i] = dot8(W.a[i], xc);
+  rows_reduce<6>(c, s);
+  if (c.tid < 6) {  // pair j: rows n, n + 1 of half h
+    const int h = c.tid / 3, i0 = 2 * (c.tid % 3), n = 12 * c.w + 6 * h + i0;
+    float a = row_total(c, h, i0), b = row_total(c, h, i0 + 1);
+    if (n < (HQ + HKV) * HD) {
+      const float2 cs = c.L.rope[(n % HD) / 2];
+      const float y0 = a * cs.x - b * cs.y, y1 = b * cs.x + a * cs.y;
+      a = y0;
+      b = y1;
+    }
+    u64* g = c.buf(G_QKV, QKV);
+    gput(g + n, a, c.tag());
+    gput(g + n + 1, b, c.tag());
+    if (n >= HQ * HD) {  // KVCache.update_and_fetch: the new row at pos (read by later launches)
+      const int nn = n < (HQ + HKV) * HD ? n - HQ * HD : n - (HQ + HKV) * HD;
+      float* cache = n < (HQ + HKV) * HD ? c.p.kc[l] : c.p.vc[l];
+      *reinterpret_cast<float2*>(cache + ((size_t)(nn / HD) * c.p.S_cap + pos) * HD + nn % HD) = make_float2(a, b);
+    }
+  }
+}
+
+// Attention of query head a (WG a < NATT) over keys 0..pos: keys < pos from the cache (written by
+// earlier launches), key pos from the E1 granules.  Wave v takes 64-key blocks v, v + 8, ...: lane j
+// scores key 64 b + j (q . k over 64 dims, four fixed FMA chains), online softmax per wave, P.V with
+// lane = head dim over the block's keys in order; waves combined in order 0..7 -> E2.
+__device__ __forceinline__ void phase_attn(Ctx& c, int l, int pos) {
+  const int a = c.w, g = a / (HQ / HKV);
+  {  // E1 (the hand-off before c.e): q_a, k_g, v_g
+    const u64* buf = c.p.gbuf + G_QKV + (size_t)((c.e - 1) & 1) * QKV;
+    const unsigned tag = c.tag() - 1u;
+    if (c.tid < 3 * HD) {
+      const int part = c.tid / HD, d = c.tid % HD;
+      const int idx = part == 0 ? a * HD + d : (part == 1 ? HQ * HD + g * HD + d : (HQ + HKV) * HD + g * HD + d);
+      u64 v = gload(buf + idx);
+      for (unsigned spin = 0; (unsigned)(v >> 32) != tag; ++spin) {
+        if (spin_fail(c, spin)) break;
+        __builtin_amdgcn_s_sleep(1);
+        v = gload(buf + idx);
+      }
+      const float f = __uint_as_float((unsigned)v);
+      if (part == 0) c.L.q[d] = f * 0.125f;  // 1 / sqrt(64)
+      else if (part == 1) c.L.kn[d] = f;
+      else c.L.vn[d] = f;
+    }
+    __syncthreads();
+  }
+  const float* K = c.p.kc[l] + (size_t)g * c.p.S_cap * HD;
+  const float* V = c.p.vc[l] + (size_t)g * c.p.S_cap * HD;
+  const int n = pos + 1;
+  float m_run = -INFINITY, l_run = 0.f, o = 0.f;
+  for (int b0 = 64 * c.wave; b0 < n; b0 += 64 * 8) {
+    const int j = b0 + c.lane;
+    // key row j: cache (j < pos) or the new row (j == pos); lanes past the range score -inf
+    float4 kr[HD / 4];
+    const float4* ksrc = reinterpret_cast<const float4*>(j < pos ? K + (size_t)j * HD : c.L.kn);
+#pragma unroll
+    for (int d4 = 0; d4 < HD / 4; ++d4) kr[d4] = j <= pos ? ksrc[d4] : make_float4(0.f, 0.f, 0.f, 0.f);
+    float vr[64];  // V[b0 + u][lane], u < 64
+#pragma unroll
+    for (int u = 0; u < 64; ++u) {
+      const int jj = b0 + u;
+      vr[u] = jj < pos ? V[(size_t)jj * HD + c.lane] : (jj == pos ? c.L.vn[c.lane] : 0.f);
+    }
+    const float4* q4 = reinterpret_cast<const float4*>(c.L.q);
+    float d0 = 0.f, d1 = 0.f, d2 = 0.f, d3 = 0.f;
+#pragma unroll
+    for (int d4 = 0; d4 < HD / 4; ++d4) {
+      const float4 qq = q4[d4];
+      d0 = fmaf(qq.x, kr[d4].x, d0);
+      d1 = fmaf(qq.y, kr[d4].y, d1);
+      d2 = fmaf(qq.z, kr[d4].z, d2);
+      d3 = fmaf(qq.w, kr[d4].w, d3);
+    }
+    const float sc = j <= pos ? (d0 + d1) + (d2 + d3) : -INFINITY;
+    const float m_new = fmaxf(m_run, wave_max(sc));
+    const float alpha = m_run == -INFINITY ? 0.f : expf(m_run - m_new);
+    const float pj = j <= pos ? expf(sc - m_new) : 0.f;
+    l_run = l_run * alpha + wave_sum(pj);
+    o *= alpha;
+    const int pji = __float_as_int(pj);
+#pragma unroll
+    for (int u = 0; u < 64; ++u)  // keys past pos: p = 0 and v = 0, an exact no-op
+      o = fmaf(__int_as_float(__builtin_amdgcn_readlane(pji, u)), vr[u], o);
+    m_run = m_new;
+  }
+  c.L.ao[c.wave][c.lane] = o;
+  if (c.lane == 0) { c.L.am[c.wave] = m_run; c.L.al[c.wave] = l_run; }
+  __syncthreads();
+  if (c.wave == 0) {
+    float M = -INFINITY;
+#pragma unroll
+    for (int v = 0; v < 8; ++v) M = fmaxf(M, c.L.am[v]);
+    float Ls = 0.f, O = 0.f;
+#pragma unroll
+    for (int v = 0; v < 8; ++v) {
+      const float wv = c.L.am[v] == -INFINITY ? 0.f : expf(c.L.am[v] - M);
+      Ls = fmaf(c.L.al[v], wv, Ls);
+      O = fmaf(c.L.ao[v][c.lane], wv, O);
+    }
+    gput(c.buf(G_ATT, D) + a * HD + c.lane, O / Ls, c.tag());  // E2
+  }
+}
+
+// o_proj rows 8w.. (+ residual) -> E3
+__device__ __forceinline__ void phase_o(Ctx& c, const WO& W) {
+  float s[4];
+  const float* xc = c.L.att + 8 * (c.tid & 255);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) s[i] = dot8(W.a[i], xc);
+  rows_reduce<4>(c, s);
+  if (c.tid < 8) {
+    const int h = c.tid / 4, i = c.tid % 4, n = 8 * c.w + c.tid;
+    gput(c.buf(G_X, D) + n, c.L.x[n] + row_total(c, h, i), c.tag());
+  }
+}
+
+// gate/up rows of one half (4 per wave) -> SiLU*up columns 4 * wave + 2 * HALF + {0, 1}
+template <int HALF>
+__device__ __forceinline__ void phase_gu(Ctx& c, const WGu& G) {
+  float t[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float s = dot8(G.a[i][0], c.L.xn + 8 * c.lane);
+#pragma unroll
+    for (int q = 1; q < 4; ++q) s += dot8(G.a[i][q], c.L.xn + 8 * (c.lane + 64 * q));
+    t[i] = wave_sum(s);
+  }
+  if (c.lane < 2) {  // pair k: rows 2k (gate), 2k + 1 (up)
+    const float gt = c.lane == 0 ? t[0] : t[2], up = c.lane == 0 ? t[1] : t[3];
+    c.L.hb[4 * c.wave + 2 * HALF + c.lane] = silu_f(gt) * up;
+  }
+}
+
+// down partials of this WG's 32 columns for every row -> E4
+__device__ __forceinline__ void phase_down(Ctx& c, const WDn& W) {
+  u64* g = c.buf(G_PART, (size_t)NWG * D) + (size_t)c.w * D;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    float s = dot8(W.a[k][0], c.L.hb);
+#pragma unroll
+    for (int q = 1; q < 4; ++q) s += dot8(W.a[k][q], c.L.hb + 8 * q);
+    gput(g + c.tid + NT * k, s, c.tag());
+  }
+}
+
+// Reduce-scatter: rows 8w..8w+7 of every producer's partials (fixed order), + residual -> E5
+__device__ __forceinline__ void phase_reduce(Ctx& c) {
+  const unsigned tag = c.tag();
+  const u64* g = c.buf(G_PART, (size_t)NWG * D);
+  const int v = c.tid >> 1, half = c.tid & 1;
+  const u64* src = g + (size_t)v * D + 8 * c.w + 4 * half;
+  u64 q[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) q[u] = gload(src + u);
+  for (unsigned spin = 0;; ++spin) {
+    bool ok = true;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) ok &= (unsigned)(q[u] >> 32) == tag;
+    if (ok || spin_fail(c, spin)) break;
+    __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if ((unsigned)(q[u] >> 32) != tag) q[u] = gload(src + u);
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u) c.L.red[4 * half + u][v] = __uint_as_float((unsigned)q[u]);
+  __syncthreads();
+  ++c.e;  // the x hand-off that follows
+  {
+    const float* r = c.L.red[c.wave];
+    float s = ((r[4 * c.lane] + r[4 * c.lane + 1]) + r[4 * c.lane + 2]) + r[4 * c.lane + 3];
+    s = wave_sum(s);
+    if (c.lane == 0) {
+      const int n = 8 * c.w + c.wave;
+      gput(c.buf(G_X, D) + n, c.L.x[n] + s, c.tag());
+    }
+  }
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(NT, 1) void bb_step_kernel(BbStepArgs p) {
+  __shared__ __attribute__((aligned(16))) Lds L;
+  Ctx c{p, L, (int)blockIdx.x, (int)threadIdx.x, (int)(threadIdx.x & 63), (int)(threadIdx.x >> 6), 0u, 0};
+  c.tag0 = __hip_atomic_load(p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  const int pos = p.pos[0];  // the new row's position (the embedding launch advanced it)
+  WQ wq;
+  WO wo;
+  WGu gu;
+  WDn wd;
+  load_q(c, 0, wq);
+  Nw nw1 = nw_fetch(c, p.n1[0]);
+  for (int k = c.tid; k < D; k += NT) L.x[k] = p.x[k];
+  if (c.tid < HD / 2) L.rope[c.tid] = reinterpret_cast<const float2*>(p.rope)[(size_t)pos * (HD / 2) + c.tid];
+  __syncthreads();
+  for (int l = 0; l < NL; ++l) {
+    c.refresh();
+    rms(c, nw1, L.xn);
+    phase_qkv(c, l, pos, wq);                         // -> E1
+    ++c.e;                                            // E1 is read by the attention workgroups only
+    const bool attn_wg = c.w < NATT;
+    if (!attn_wg) {  // stream the o_proj and down slices while the attention runs elsewhere
+      load_o(c, l, wo);
+      load_dn(c, l, wd);
+    }
+    const Nw nw2 = nw_fetch(c, p.n2[l]);
+    if (attn_wg) {
+      phase_attn(c, l, pos);                          // waits E1, -> E2
+      load_o(c, l, wo);
+      load_dn(c, l, wd);
+    }
+    load_gu<0>(c, l, gu);
+    gather<D / NT>(c, c.buf(G_ATT, D), D, L.att);     // E2
+    ++c.e;
+    c.refresh();
+    phase_o(c, wo);                                   // -> E3
+    if (l + 1 < NL) load_q(c, l + 1, wq);
+    gather<D / NT>(c, c.buf(G_X, D), D, L.x);         // E3
+    ++c.e;
+    c.refresh();
+    rms(c, nw2, L.xn);
+    phase_gu<0>(c, gu);
+    load_gu<1>(c, l, gu);
+    phase_gu<1>(c, gu);
+    __syncthreads();
+    phase_down(c, wd);                                // -> E4
+    nw1 = nw_fetch(c, l + 1 < NL ? p.n1[l + 1] : p.norm);
+    c.refresh();
+    phase_reduce(c);                                  // waits E4, -> E5
+    gather<D / NT>(c, c.buf(G_X, D), D, L.x);         // E5
+    ++c.e;
+  }
+  // final norm of the last row -> h_last (generation.py:42 reads norm(h[:, -1]))
+  c.refresh();
+  rms(c, nw1, L.xn);
+  if (c.w == 0)
+    for (int k = c.tid; k < D; k += NT) p.h_last[k] = L.xn[k];
+  if (c.w == 0 && c.tid == 0) __hip_atomic_store(p.epoch, c.tag0 - 1u + (unsigned)c.e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+size_t bb_step_gbuf_bytes() { return G_TOTAL * sizeof(u64); }
+
+void launch_bb_step(const BbStepArgs& p, hipStream_t st) {
+  hipLaunchKernelGGL(bb_step_kernel, dim3(NWG), dim3(NT), 0, st, p);
+}
+
+const void* bb_step_kernel_ptr() { return reinterpret_cast<const void*>(&bb_step_kernel); }

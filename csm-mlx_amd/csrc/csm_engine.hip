@@ -145,6 +145,13 @@ struct csm_engine {
   bool dec_frame = [] { const char* v = getenv("CSM_DEC_FRAME"); return !(v && v[0] == '0'); }();
   int df_hw = -1;    // 1: the device can hold one 512-thread workgroup on each of 256 CUs at once
   unsigned long long* df_stamps = nullptr;  // csm_set_option "dec_frame_stamps": per-hand-off clock stamps
+  // persistent backbone step (bb_step.hip) for batch-1 bf16 csm_1b decode rows; csm_set_option
+  // "bb_step" / CSM_BB_STEP=0 turn it off
+  void* bb_gbuf = nullptr;
+  unsigned* bb_epoch = nullptr;
+  int* bb_err = nullptr;
+  bool bb_step = [] { const char* v = getenv("CSM_BB_STEP"); return !(v && v[0] == '0'); }();
+  int bb_hw = -1;
 
   void* balloc(size_t bytes) {
     void* p = nullptr;
@@ -305,12 +312,51 @@ void embed(csm_engine* e, const EmbedParams& ep, int M, hipStream_t st) {
 // arg-max partial slots per row of a head launch (GEMV or MFMA path, dense or int4)
 int head_blocks(int N, int K, int M, int wdt) { return gemv_partials(N, K, M, wdt); }
 
+// The persistent backbone step runs the 16 blocks + final norm of a batch-1 decode row when the
+// engine has csm_1b's backbone shapes in bf16 (with the chunk-major down copies) and the device has
+// the 256 CUs its one-workgroup-per-CU grid assumes (every workgroup must be resident).
+bool bb_step_eligible(csm_engine* e) {
+  if (!e->bb_step || !e->bb_gbuf || e->B != 1 || e->wdt != WDT_BF16 || e->fuse_mlp) return false;
+  const csm_llama_dims& d = e->bb.d;
+  if (d.hidden != 2048 || d.intermediate != 8192 || d.n_heads != 32 || d.n_kv_heads != 8 || d.head_dim != 64 ||
+      d.n_layers != BB_STEP_LAYERS)
+    return false;
+  for (const LayerW& l : e->bb.L)
+    if (!l.wdc) return false;
+  if (e->bb_hw < 0) {
+    hipDeviceProp_t prop;
+    int per_cu = 0;
+    e->bb_hw = hipGetDeviceProperties(&prop, e->dev) == hipSuccess && prop.multiProcessorCount == BB_STEP_WGS &&
+                       hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bb_step_kernel_ptr(), BB_STEP_THREADS, 0) ==
+                           hipSuccess && per_cu >= 1
+                   ? 1 : 0;
+  }
+  return e->bb_hw == 1;
+}
+
+void enqueue_bb_step(csm_engine* e, hipStream_t st) {
+  BbStepArgs a{};
+  for (int l = 0; l < BB_STEP_LAYERS; ++l) {
+    const LayerW& w = e->bb.L[l];
+    a.wqkv[l] = (const bf16_t*)w.wqkv; a.wo[l] = (const bf16_t*)w.wo; a.wgu[l] = (const bf16_t*)w.wgu;
+    a.wdc[l] = (const bf16_t*)w.wdc; a.n1[l] = w.n1; a.n2[l] = w.n2; a.kc[l] = w.kc; a.vc[l] = w.vc;
+  }
+  a.norm = e->bb.norm; a.rope = e->bb.rope; a.S_cap = e->bb.S_cap; a.eps = e->bb.d.eps;
+  a.x = e->x; a.pos = e->pos; a.h_last = e->h_last;
+  a.gbuf = (unsigned long long*)e->bb_gbuf; a.epoch = e->bb_epoch; a.err = e->bb_err;
+  launch_bb_step(a, st);
+}
+
 void enqueue_body(csm_engine* e, hipStream_t st) {
   const int B = e->B;
   EmbedParams ep{};
   ep.codes = e->codes; ep.text_emb = e->text_emb; ep.audio_emb = e->audio_emb; ep.V = e->V; ep.K = e->K;
   ep.D = e->D; ep.out = e->x; ep.pos_inc = e->pos;
   embed(e, ep, B, st);
+  if (bb_step_eligible(e)) {
+    enqueue_bb_step(e, st);
+    return;
+  }
   RowMap rm{1, 0, e->pos, 0};
   const long long* pend = run_stack(e, e->bb, e->x, B, e->q, e->att, e->mlp, rm, st);
   launch_rmsnorm_rows(e->x, e->D, e->bb.norm, e->bb.d.eps, e->D, e->h_last, e->D, B, st, pend, e->acc_rows * e->D);
@@ -366,14 +412,17 @@ void enqueue_dec_frame(csm_engine* e, hipStream_t st) {
   launch_advance(ap, st);
 }
 
-// A hand-off wait of the persistent decoder that timed out leaves its flag raised: report it.
+// A hand-off wait of a persistent kernel that timed out leaves its flag raised: report it.
 void check_dec_frame(csm_engine* e) {
-  if (!e->df_err) return;
-  int v = 0;
-  HIPCHK(hipMemcpy(&v, e->df_err, 4, hipMemcpyDeviceToHost));
-  if (v) {
-    HIPCHK(hipMemset(e->df_err, 0, 4));
-    throw CsmError(CSM_ERR_HIP, "persistent frame decoder: a hand-off wait timed out (results of this batch are invalid)");
+  for (int* f : {e->df_err, e->bb_err}) {
+    if (!f) continue;
+    int v = 0;
+    HIPCHK(hipMemcpy(&v, f, 4, hipMemcpyDeviceToHost));
+    if (v) {
+      HIPCHK(hipMemset(f, 0, 4));
+      throw CsmError(CSM_ERR_HIP, std::string(f == e->df_err ? "persistent frame decoder" : "persistent backbone step") +
+                                      ": a hand-off wait timed out (results of this batch are invalid)");
+    }
   }
 }
 
@@ -807,6 +856,11 @@ int csm_engine_create(const csm_dims* dims, int device, int weight_dtype, int ma
     e->df_gbuf = e->alloc(dec_frame_gbuf_bytes());
     e->df_epoch = (unsigned*)e->alloc(16);
     e->df_err = (int*)e->alloc(16);
+    if (e->wdt == WDT_BF16 && b.hidden == 2048 && b.n_layers == BB_STEP_LAYERS) {
+      e->bb_gbuf = e->alloc(bb_step_gbuf_bytes());
+      e->bb_epoch = (unsigned*)e->alloc(16);
+      e->bb_err = (int*)e->alloc(16);
+    }
     (void)Vp;
     (void)B;
     ensure_batch(e.get(), max_batch);
@@ -1355,7 +1409,8 @@ int csm_debug_read(csm_engine* e, const char* what, void* host, int64_t nbytes, 
     else if (w == "ci_logits") { src = e->ci_logits; n = (e->K - 1) * B * Vp * 4; }
     else if (w == "codes") { src = e->codes; n = B * e->K * 4; }
     else if (w == "pos") { src = e->pos; n = B * 4; }
-    else if (w == "dec_frame_epoch") { src = e->df_epoch; n = 4; }  // advances by the hand-offs of every frame it ran
+    else if (w == "dec_frame_epoch") { src = e->df_epoch; n = 4; }
+    else if (w == "bb_step_epoch" && e->bb_epoch) { src = e->bb_epoch; n = 4; }  // advances by 80 per row it ran  // advances by the hand-offs of every frame it ran
     else if (w == "dec_frame_stamps" && e->df_stamps) { src = e->df_stamps; n = (size_t)DEC_FRAME_WGS * DEC_FRAME_STAMPS * 8; }
     else if (w == "audio_head") {  // device layout [K-1][Vpad][Dd], f32 or bf16 bits
       src = e->audio_head; n = (size_t)(e->K - 1) * Vp * e->Dd * (e->head_wdt == WDT_F32 ? 4 : 2);
@@ -1573,6 +1628,10 @@ int csm_set_option(csm_engine* e, const char* key, int value) {
     else if (k == "dec_frame") {
       if (!e) throw CsmError(CSM_ERR_ARG, "dec_frame needs an engine");
       e->dec_frame = value != 0;
+    }
+    else if (k == "bb_step") {
+      if (!e) throw CsmError(CSM_ERR_ARG, "bb_step needs an engine");
+      e->bb_step = value != 0;
     }
     else if (k == "fuse_mlp") {
       if (!e) throw CsmError(CSM_ERR_ARG, "fuse_mlp needs an engine");

@@ -333,6 +333,33 @@ int gemv_partials(int N, int K, int M, int wdt);
 
 // ---- persistent frame decoder (dec_frame.hip): c0 head + 31 depth-decoder steps of one greedy batch-1
 // frame in one launch of 256 x 512 threads (one workgroup per CU), csm_1b decoder shapes, bf16 weights
+// Persistent backbone step (bb_step.hip): the 16 backbone blocks of one batch-1 decode row (bf16,
+// csm_1b shapes) + the final norm in one launch.
+constexpr int BB_STEP_LAYERS = 16, BB_STEP_WGS = 256, BB_STEP_THREADS = 512;
+struct BbStepArgs {
+  const bf16_t* wqkv[BB_STEP_LAYERS];
+  const bf16_t* wo[BB_STEP_LAYERS];
+  const bf16_t* wgu[BB_STEP_LAYERS];     // gate/up rows interleaved
+  const bf16_t* wdc[BB_STEP_LAYERS];     // down_proj chunk-major [F/8][D][8]
+  const float* n1[BB_STEP_LAYERS];
+  const float* n2[BB_STEP_LAYERS];
+  float* kc[BB_STEP_LAYERS];             // [Hkv][S_cap][HD] of utterance 0
+  float* vc[BB_STEP_LAYERS];
+  const float* norm;                     // backbone final norm
+  const float* rope;                     // [S_cap][HD/2][2]
+  int S_cap;
+  float eps;
+  const float* x;                        // [D] the embedded row
+  const int* pos;                        // [1] its position (advanced by the embedding launch)
+  float* h_last;                         // [D] norm(h) of the row
+  unsigned long long* gbuf;              // hand-off granules (bb_step_gbuf_bytes)
+  unsigned* epoch;                       // hand-off tag base
+  int* err;                              // raised when a hand-off wait times out
+};
+size_t bb_step_gbuf_bytes();
+void launch_bb_step(const BbStepArgs& p, hipStream_t st);
+const void* bb_step_kernel_ptr();
+
 constexpr int DEC_FRAME_LAYERS = 4;
 struct DecFrameArgs {
   const bf16_t* wqkv[DEC_FRAME_LAYERS];

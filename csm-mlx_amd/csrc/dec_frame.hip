@@ -33,50 +33,17 @@
 // (x * rsqrt(mean(x^2) + eps) * w), RoPE on interleaved pairs from the cos/sin table, softmax with
 // max subtraction, reductions in fixed orders (deterministic run to run).
 #include "csm_kernels.h"
+#include "handoff.h"
 
 namespace {
 
-typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
-typedef unsigned long long u64;
+using namespace handoff;
 
 constexpr int NWG = 256, NT = 512;
 constexpr int D = 1024, F = 8192, HQ = 8, HKV = 2, HD = 128, NL = DEC_FRAME_LAYERS, DB = 2048;
 constexpr int QKV = (HQ + 2 * HKV) * HD;  // 1536
 constexpr int MAXM = 2;                   // rows per step (step 1: [h_last, E_a[c0]])
 constexpr unsigned SPIN_LIMIT = 1u << 22; // ~0.1 s of s_sleep per hand-off before declaring failure
-
-__device__ __forceinline__ u64 gload(const u64* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void gput(u64* p, float v, unsigned tag) {
-  __hip_atomic_store(p, ((u64)tag << 32) | __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void gput_u(u64* p, unsigned v, unsigned tag) {
-  __hip_atomic_store(p, ((u64)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void sc1_store_f(float* p, float v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// 16-B agent-coherent (sc1) load at byte offset `off` of a buffer of `bytes` bytes
-__device__ __forceinline__ u32x4_t sc1_load16(const void* base, int off, int bytes) {
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, bytes, 0x00020000);
-  return __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 16));
-}
-
-// 8 products of one 16-B bf16 weight chunk with 8 consecutive fp32 activations (fixed order)
-__device__ __forceinline__ float dot8(const u32x4_t w, const float* x) {
-  const float4 a = *reinterpret_cast<const float4*>(x), b = *reinterpret_cast<const float4*>(x + 4);
-  float s = bf16_lo(w.x) * a.x;
-  s = fmaf(bf16_hi(w.x), a.y, s);
-  s = fmaf(bf16_lo(w.y), a.z, s);
-  s = fmaf(bf16_hi(w.y), a.w, s);
-  s = fmaf(bf16_lo(w.z), b.x, s);
-  s = fmaf(bf16_hi(w.z), b.y, s);
-  s = fmaf(bf16_lo(w.w), b.z, s);
-  s = fmaf(bf16_hi(w.w), b.w, s);
-  return s;
-}
 
 // the same chunk against two activation rows (every weight converted once, used twice: no
 // loop-invariant conversions for the compiler to hoist out of a row loop)
@@ -114,17 +81,6 @@ __device__ __forceinline__ void dotm(const u32x4_t w, const float* x0, const flo
 
 __device__ __forceinline__ u32x4_t wload(const bf16_t* p) { return *reinterpret_cast<const u32x4_t*>(p); }
 
-// 16-B weight load as a raw buffer load: the matrix base rides in the (uniform) descriptor, the
-// lane-dependent part in ONE voffset register shared by every layer and row, the row / chunk step in
-// the scalar offset -- so per-layer weight addresses are not VGPR pairs the compiler keeps live
-// across the frame loop.
-// AUX: cache policy (2 = nt), a compile-time constant so no load sits in a branch of its own.
-template <int AUX = 0>
-__device__ __forceinline__ u32x4_t bload(const void* base, int voff, int soff) {
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
-  return __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, AUX));
-}
-
 struct Lds {
   float x[MAXM][D];        // residual rows
   float xn[MAXM][DB];      // normed x * norm weight (GEMV input); h_last at frame start
@@ -151,15 +107,6 @@ constexpr size_t G_QKV = G_X + 2 * MAXM * D;               // [2][MAXM][QKV]
 constexpr size_t G_PART = G_QKV + 2 * MAXM * QKV;          // [2][NWG][MAXM][D] down partials
 constexpr size_t G_ARG = G_PART + (size_t)2 * NWG * MAXM * D;  // [2][NWG][2] arg-max keys
 constexpr size_t G_TOTAL = G_ARG + 2 * NWG * 2;
-
-// threadIdx.x through an opaque move: lane-dependent addresses derived from it inside the frame loop
-// are recomputed per iteration instead of being hoisted out of the loop and held (spilled) for the
-// whole frame.
-__device__ __forceinline__ int opaque_tid() {
-  int t;
-  asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"((int)threadIdx.x));
-  return t;
-}
 
 struct Ctx {
   const DecFrameArgs& p;
