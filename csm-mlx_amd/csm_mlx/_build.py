@@ -19,10 +19,11 @@ LIB = os.path.join(PKG, "libcsm_hip.so")
 ARCH = os.environ.get("CSM_HIP_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-result"]
-# per-source flags: the persistent frame decoder holds weight prefetches in registers across hand-off
+# per-source flags: the persistent kernels hold weight prefetches in registers across hand-off
 # waits at 256 VGPRs; the AMDGPU scheduler's own register-pressure trackers keep it from spilling
 # them (55 -> 5 spilled VGPRs; a spill store waits for its load, draining the prefetch).
-SRC_FLAGS = {"dec_frame.hip": ["-mllvm", "-amdgpu-use-amdgpu-trackers=1"]}
+SRC_FLAGS = {"dec_frame.hip": ["-mllvm", "-amdgpu-use-amdgpu-trackers=1"],
+             "bb_step.hip": ["-mllvm", "-amdgpu-use-amdgpu-trackers=1"]}
 
 
 def _sources():

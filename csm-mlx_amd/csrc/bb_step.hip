@@ -53,6 +53,7 @@ struct Lds {
   float2 rope[HD / 2];   // (cos, sin) at the step's position
   float q[HD], kn[HD], vn[HD];          // attention WGs: the head's q and the new k / v row
   float am[8], al[8], ao[8][HD];        // attention WGs: per-wave online-softmax partials
+  float Ks[128][HD + 4], Vs[128][HD];   // attention WGs: one pass of 128 keys (K rows padded)
 };
 
 struct Ctx {
@@ -68,6 +69,10 @@ struct Ctx {
   }
   __device__ unsigned tag() const { return tag0 + (unsigned)e; }
   __device__ u64* buf(size_t region, size_t per) const { return p.gbuf + region + (size_t)(e & 1) * per; }
+  // profiling: the 100 MHz real-time clock when this WG passed hand-off e (slot e + 1; slot 0 = start)
+  __device__ void stamp(int slot) const {
+    if (p.stamps && tid == 0 && slot < BB_STEP_STAMPS) p.stamps[(size_t)w * BB_STEP_STAMPS + slot] = __builtin_amdgcn_s_memrealtime();
+  }
 };
 
 __device__ __forceinline__ bool spin_fail(Ctx& c, unsigned spin) {
@@ -100,6 +105,7 @@ __device__ __forceinline__ void gather(Ctx& c, const u64* buf, int n, float* out
       if (i < n && (unsigned)(g[u] >> 32) != tag) g[u] = gload(buf + i);
     }
   }
+  c.stamp(c.e + 1);
 #pragma unroll
   for (int u = 0; u < GPT; ++u) {
     const int i = c.tid + u * NT;
@@ -135,10 +141,16 @@ __device__ __forceinline__ void rms(Ctx& c, const Nw& nw, float* out) {
 // QKV / o_proj: thread (half h = tid >> 8, chunk c = tid & 255) holds chunk c of rows 6h+i / 4h+i
 struct WQ { u32x4_t a[6]; };
 struct WO { u32x4_t a[4]; };
-// gate/up: wave v holds rows 8v + r, chunks lane + 64 q (q < 4); split in halves r < 4 / r >= 4
-struct WGu { u32x4_t a[4][4]; };
-// down: thread t holds rows t + 512 k (k < 4) of the WG's 4 column chunks (8 columns each)
-struct WDn { u32x4_t a[4][4]; };
+// MLP quarter Q (of the WG's 64 gate/up rows and 4 down column chunks): wave v holds gate/up rows
+// 16Q + 2v, 16Q + 2v + 1 (one gate/up pair -> SiLU*up column 8Q + v), chunks lane + 64 j (j < 4);
+// thread t holds down rows t + 512 k (k < 4) of column chunk 4w + Q (8 columns)
+struct WMq { u32x4_t g[2][4]; u32x4_t d[4]; };
+#ifndef BB_PRE
+#define BB_PRE 2  // MLP quarters fetched right after the QKV publish (the rest while the MLP runs)
+#endif
+#ifndef BB_NEXT
+#define BB_NEXT 0  // 1: the next layer's o_proj rows + first quarter fetched after the down publish
+#endif
 
 __device__ __forceinline__ void load_q(Ctx& c, int l, WQ& r) {
   const bf16_t* base = c.p.wqkv[l] + (size_t)(12 * c.w + 6 * (c.tid >> 8)) * D;
@@ -152,23 +164,16 @@ __device__ __forceinline__ void load_o(Ctx& c, int l, WO& r) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) r.a[i] = bload<2>(base, v, i * D * 2);
 }
-template <int HALF>
-__device__ __forceinline__ void load_gu(Ctx& c, int l, WGu& r) {
-  const bf16_t* base = c.p.wgu[l] + (size_t)(64 * c.w + 8 * c.wave + 4 * HALF) * D;
-  const int v = c.lane * 16;
+__device__ __forceinline__ void load_mq(Ctx& c, int l, int Q, WMq& r) {
+  const bf16_t* g = c.p.wgu[l] + (size_t)(64 * c.w + 16 * Q + 2 * c.wave) * D;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) r.a[i][q] = bload<2>(base, v, i * D * 2 + q * 64 * 16);
-}
-__device__ __forceinline__ void load_dn(Ctx& c, int l, WDn& r) {
-  // chunk 4w + q of [F/8][D][8]: row n at byte (n * 8) * 2
-  const bf16_t* base = c.p.wdc[l] + (size_t)(4 * c.w) * D * 8;
-  const int v = c.tid * 16;
+    for (int j = 0; j < 4; ++j) r.g[i][j] = bload<2>(g, c.lane * 16, i * D * 2 + j * 64 * 16);
+  // chunk 4w + Q of [F/8][D][8]: row n at byte (n * 8) * 2
+  const bf16_t* d = c.p.wdc[l] + (size_t)(4 * c.w + Q) * D * 8;
 #pragma unroll
-  for (int k = 0; k < 4; ++k)
-#pragma unroll
-    for (int q = 0; q < 4; ++q) r.a[k][q] = bload<2>(base, v, (q * D * 8 + k * NT * 8) * 2);
+  for (int k = 0; k < 4; ++k) r.d[k] = bload<2>(d, c.tid * 16, k * NT * 8 * 2);
 }
 
 // per-row partial sums of a (half, chunk)-split projection: wave partials -> wsum[wave][i]
@@ -238,45 +243,62 @@ __device__ __forceinline__ void phase_attn(Ctx& c, int l, int pos) {
       else c.L.vn[d] = f;
     }
     __syncthreads();
+    c.stamp(c.e);  // E1 (index e - 1) passed
   }
   const float* K = c.p.kc[l] + (size_t)g * c.p.S_cap * HD;
   const float* V = c.p.vc[l] + (size_t)g * c.p.S_cap * HD;
   const int n = pos + 1;
   float m_run = -INFINITY, l_run = 0.f, o = 0.f;
-  for (int b0 = 64 * c.wave; b0 < n; b0 += 64 * 8) {
-    const int j = b0 + c.lane;
-    // key row j: cache (j < pos) or the new row (j == pos); lanes past the range score -inf
-    float4 kr[HD / 4];
-    const float4* ksrc = reinterpret_cast<const float4*>(j < pos ? K + (size_t)j * HD : c.L.kn);
+  // passes of 128 keys staged in LDS by all 512 threads (8 float4 each: few registers, so the
+  // weight prefetch can stay in flight through the attention); 64-key block b of the pass is wave
+  // (2 * pass + b) % 8's, so every wave still takes blocks v, v + 8, ... in increasing order
+  for (int k0 = 0; k0 < n; k0 += 128) {
+    float4 kv[4], vv[4];
 #pragma unroll
-    for (int d4 = 0; d4 < HD / 4; ++d4) kr[d4] = j <= pos ? ksrc[d4] : make_float4(0.f, 0.f, 0.f, 0.f);
-    float vr[64];  // V[b0 + u][lane], u < 64
-#pragma unroll
-    for (int u = 0; u < 64; ++u) {
-      const int jj = b0 + u;
-      vr[u] = jj < pos ? V[(size_t)jj * HD + c.lane] : (jj == pos ? c.L.vn[c.lane] : 0.f);
+    for (int u = 0; u < 4; ++u) {
+      const int idx = c.tid + NT * u, r = idx >> 4, c4 = idx & 15, j = k0 + r;
+      const float4* ks = reinterpret_cast<const float4*>(j < pos ? K + (size_t)j * HD : c.L.kn);
+      const float4* vs = reinterpret_cast<const float4*>(j < pos ? V + (size_t)j * HD : c.L.vn);
+      kv[u] = j <= pos ? ks[c4] : make_float4(0.f, 0.f, 0.f, 0.f);
+      vv[u] = j <= pos ? vs[c4] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-    const float4* q4 = reinterpret_cast<const float4*>(c.L.q);
-    float d0 = 0.f, d1 = 0.f, d2 = 0.f, d3 = 0.f;
+    __syncthreads();  // the previous pass is consumed
 #pragma unroll
-    for (int d4 = 0; d4 < HD / 4; ++d4) {
-      const float4 qq = q4[d4];
-      d0 = fmaf(qq.x, kr[d4].x, d0);
-      d1 = fmaf(qq.y, kr[d4].y, d1);
-      d2 = fmaf(qq.z, kr[d4].z, d2);
-      d3 = fmaf(qq.w, kr[d4].w, d3);
+    for (int u = 0; u < 4; ++u) {
+      const int idx = c.tid + NT * u, r = idx >> 4, c4 = idx & 15;
+      *reinterpret_cast<float4*>(&c.L.Ks[r][4 * c4]) = kv[u];
+      *reinterpret_cast<float4*>(&c.L.Vs[r][4 * c4]) = vv[u];
     }
-    const float sc = j <= pos ? (d0 + d1) + (d2 + d3) : -INFINITY;
-    const float m_new = fmaxf(m_run, wave_max(sc));
-    const float alpha = m_run == -INFINITY ? 0.f : expf(m_run - m_new);
-    const float pj = j <= pos ? expf(sc - m_new) : 0.f;
-    l_run = l_run * alpha + wave_sum(pj);
-    o *= alpha;
-    const int pji = __float_as_int(pj);
+    __syncthreads();
+    const int blk = c.wave - ((k0 >> 6) & 7);  // this wave's block within the pass (0 or 1), if any
+    if (blk == 0 || blk == 1) {
+      const int b0 = k0 + 64 * blk;
+      if (b0 < n) {
+        const int j = b0 + c.lane;
+        const float4* kr = reinterpret_cast<const float4*>(c.L.Ks[64 * blk + c.lane]);
+        const float4* q4 = reinterpret_cast<const float4*>(c.L.q);
+        float d0 = 0.f, d1 = 0.f, d2 = 0.f, d3 = 0.f;
 #pragma unroll
-    for (int u = 0; u < 64; ++u)  // keys past pos: p = 0 and v = 0, an exact no-op
-      o = fmaf(__int_as_float(__builtin_amdgcn_readlane(pji, u)), vr[u], o);
-    m_run = m_new;
+        for (int d4 = 0; d4 < HD / 4; ++d4) {
+          const float4 qq = q4[d4], kk = kr[d4];
+          d0 = fmaf(qq.x, kk.x, d0);
+          d1 = fmaf(qq.y, kk.y, d1);
+          d2 = fmaf(qq.z, kk.z, d2);
+          d3 = fmaf(qq.w, kk.w, d3);
+        }
+        const float sc = j <= pos ? (d0 + d1) + (d2 + d3) : -INFINITY;
+        const float m_new = fmaxf(m_run, wave_max(sc));
+        const float alpha = m_run == -INFINITY ? 0.f : expf(m_run - m_new);
+        const float pj = j <= pos ? expf(sc - m_new) : 0.f;
+        l_run = l_run * alpha + wave_sum(pj);
+        o *= alpha;
+        const int pji = __float_as_int(pj);
+#pragma unroll
+        for (int u = 0; u < 64; ++u)  // keys past pos: p = 0 and v = 0, an exact no-op
+          o = fmaf(__int_as_float(__builtin_amdgcn_readlane(pji, u)), c.L.Vs[64 * blk + u][c.lane], o);
+        m_run = m_new;
+      }
+    }
   }
   c.L.ao[c.wave][c.lane] = o;
   if (c.lane == 0) { c.L.am[c.wave] = m_run; c.L.al[c.wave] = l_run; }
@@ -309,32 +331,24 @@ __device__ __forceinline__ void phase_o(Ctx& c, const WO& W) {
   }
 }
 
-// gate/up rows of one half (4 per wave) -> SiLU*up columns 4 * wave + 2 * HALF + {0, 1}
-template <int HALF>
-__device__ __forceinline__ void phase_gu(Ctx& c, const WGu& G) {
-  float t[4];
+// MLP quarter Q: the wave's gate/up pair -> SiLU*up column 8Q + wave (LDS), then this quarter's 8
+// columns of the down split-K into the four row accumulators (column chunks added in order 0..3)
+template <int Q>
+__device__ __forceinline__ void phase_mq(Ctx& c, const WMq& m, float (&acc)[4]) {
+  float t[2];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    float s = dot8(G.a[i][0], c.L.xn + 8 * c.lane);
+  for (int i = 0; i < 2; ++i) {
+    float s = dot8(m.g[i][0], c.L.xn + 8 * c.lane);
 #pragma unroll
-    for (int q = 1; q < 4; ++q) s += dot8(G.a[i][q], c.L.xn + 8 * (c.lane + 64 * q));
+    for (int j = 1; j < 4; ++j) s += dot8(m.g[i][j], c.L.xn + 8 * (c.lane + 64 * j));
     t[i] = wave_sum(s);
   }
-  if (c.lane < 2) {  // pair k: rows 2k (gate), 2k + 1 (up)
-    const float gt = c.lane == 0 ? t[0] : t[2], up = c.lane == 0 ? t[1] : t[3];
-    c.L.hb[4 * c.wave + 2 * HALF + c.lane] = silu_f(gt) * up;
-  }
-}
-
-// down partials of this WG's 32 columns for every row -> E4
-__device__ __forceinline__ void phase_down(Ctx& c, const WDn& W) {
-  u64* g = c.buf(G_PART, (size_t)NWG * D) + (size_t)c.w * D;
+  if (c.lane == 0) c.L.hb[8 * Q + c.wave] = silu_f(t[0]) * t[1];
+  __syncthreads();
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    float s = dot8(W.a[k][0], c.L.hb);
-#pragma unroll
-    for (int q = 1; q < 4; ++q) s += dot8(W.a[k][q], c.L.hb + 8 * q);
-    gput(g + c.tid + NT * k, s, c.tag());
+    const float v = dot8(m.d[k], c.L.hb + 8 * Q);
+    acc[k] = Q == 0 ? v : acc[k] + v;
   }
 }
 
@@ -357,6 +371,7 @@ __device__ __forceinline__ void phase_reduce(Ctx& c) {
     for (int u = 0; u < 4; ++u)
       if ((unsigned)(q[u] >> 32) != tag) q[u] = gload(src + u);
   }
+  c.stamp(c.e + 1);
 #pragma unroll
   for (int u = 0; u < 4; ++u) c.L.red[4 * half + u][v] = __uint_as_float((unsigned)q[u]);
   __syncthreads();
@@ -378,15 +393,19 @@ __global__ __launch_bounds__(NT, 1) void bb_step_kernel(BbStepArgs p) {
   __shared__ __attribute__((aligned(16))) Lds L;
   Ctx c{p, L, (int)blockIdx.x, (int)threadIdx.x, (int)(threadIdx.x & 63), (int)(threadIdx.x >> 6), 0u, 0};
   c.tag0 = __hip_atomic_load(p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  c.stamp(0);
   const int pos = p.pos[0];  // the new row's position (the embedding launch advanced it)
   WQ wq;
   WO wo;
-  WGu gu;
-  WDn wd;
+  WMq mq[4];
   load_q(c, 0, wq);
   Nw nw1 = nw_fetch(c, p.n1[0]);
   for (int k = c.tid; k < D; k += NT) L.x[k] = p.x[k];
   if (c.tid < HD / 2) L.rope[c.tid] = reinterpret_cast<const float2*>(p.rope)[(size_t)pos * (HD / 2) + c.tid];
+#if BB_NEXT
+  load_o(c, 0, wo);
+  load_mq(c, 0, 0, mq[0]);
+#endif
   __syncthreads();
   for (int l = 0; l < NL; ++l) {
     c.refresh();
@@ -394,17 +413,15 @@ __global__ __launch_bounds__(NT, 1) void bb_step_kernel(BbStepArgs p) {
     phase_qkv(c, l, pos, wq);                         // -> E1
     ++c.e;                                            // E1 is read by the attention workgroups only
     const bool attn_wg = c.w < NATT;
-    if (!attn_wg) {  // stream the o_proj and down slices while the attention runs elsewhere
-      load_o(c, l, wo);
-      load_dn(c, l, wd);
-    }
+    // weights for the o_proj and the first MLP quarters stream while the attention runs
+#if !BB_NEXT
+    load_o(c, l, wo);
+    load_mq(c, l, 0, mq[0]);
+#endif
+    if (BB_PRE > 1) load_mq(c, l, 1, mq[1]);
+    if (BB_PRE > 2) load_mq(c, l, 2, mq[2]);
     const Nw nw2 = nw_fetch(c, p.n2[l]);
-    if (attn_wg) {
-      phase_attn(c, l, pos);                          // waits E1, -> E2
-      load_o(c, l, wo);
-      load_dn(c, l, wd);
-    }
-    load_gu<0>(c, l, gu);
+    if (attn_wg) phase_attn(c, l, pos);               // waits E1, -> E2
     gather<D / NT>(c, c.buf(G_ATT, D), D, L.att);     // E2
     ++c.e;
     c.refresh();
@@ -414,11 +431,24 @@ __global__ __launch_bounds__(NT, 1) void bb_step_kernel(BbStepArgs p) {
     ++c.e;
     c.refresh();
     rms(c, nw2, L.xn);
-    phase_gu<0>(c, gu);
-    load_gu<1>(c, l, gu);
-    phase_gu<1>(c, gu);
-    __syncthreads();
-    phase_down(c, wd);                                // -> E4
+    float acc[4];
+    phase_mq<0>(c, mq[0], acc);
+    if (BB_PRE <= 2) load_mq(c, l, 2, mq[2]);
+    phase_mq<1>(c, mq[1], acc);
+    load_mq(c, l, 3, mq[3]);
+    phase_mq<2>(c, mq[2], acc);
+    phase_mq<3>(c, mq[3], acc);
+    {
+      u64* g = c.buf(G_PART, (size_t)NWG * D) + (size_t)c.w * D;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) gput(g + c.tid + NT * k, acc[k], c.tag());   // -> E4
+    }
+#if BB_NEXT
+    if (l + 1 < NL) {
+      load_o(c, l + 1, wo);
+      load_mq(c, l + 1, 0, mq[0]);
+    }
+#endif
     nw1 = nw_fetch(c, l + 1 < NL ? p.n1[l + 1] : p.norm);
     c.refresh();
     phase_reduce(c);                                  // waits E4, -> E5
@@ -430,6 +460,7 @@ __global__ __launch_bounds__(NT, 1) void bb_step_kernel(BbStepArgs p) {
   rms(c, nw1, L.xn);
   if (c.w == 0)
     for (int k = c.tid; k < D; k += NT) p.h_last[k] = L.xn[k];
+  c.stamp(BB_STEP_STAMPS - 1);
   if (c.w == 0 && c.tid == 0) __hip_atomic_store(p.epoch, c.tag0 - 1u + (unsigned)c.e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 

@@ -152,6 +152,7 @@ struct csm_engine {
   int* bb_err = nullptr;
   bool bb_step = [] { const char* v = getenv("CSM_BB_STEP"); return !(v && v[0] == '0'); }();
   int bb_hw = -1;
+  unsigned long long* bb_stamps = nullptr;  // csm_set_option "bb_step_stamps": per-hand-off clock stamps
 
   void* balloc(size_t bytes) {
     void* p = nullptr;
@@ -343,7 +344,7 @@ void enqueue_bb_step(csm_engine* e, hipStream_t st) {
   }
   a.norm = e->bb.norm; a.rope = e->bb.rope; a.S_cap = e->bb.S_cap; a.eps = e->bb.d.eps;
   a.x = e->x; a.pos = e->pos; a.h_last = e->h_last;
-  a.gbuf = (unsigned long long*)e->bb_gbuf; a.epoch = e->bb_epoch; a.err = e->bb_err;
+  a.gbuf = (unsigned long long*)e->bb_gbuf; a.epoch = e->bb_epoch; a.err = e->bb_err; a.stamps = e->bb_stamps;
   launch_bb_step(a, st);
 }
 
@@ -1410,7 +1411,8 @@ int csm_debug_read(csm_engine* e, const char* what, void* host, int64_t nbytes, 
     else if (w == "codes") { src = e->codes; n = B * e->K * 4; }
     else if (w == "pos") { src = e->pos; n = B * 4; }
     else if (w == "dec_frame_epoch") { src = e->df_epoch; n = 4; }
-    else if (w == "bb_step_epoch" && e->bb_epoch) { src = e->bb_epoch; n = 4; }  // advances by 80 per row it ran  // advances by the hand-offs of every frame it ran
+    else if (w == "bb_step_epoch" && e->bb_epoch) { src = e->bb_epoch; n = 4; }  // advances by 80 per row it ran
+    else if (w == "bb_step_stamps" && e->bb_stamps) { src = e->bb_stamps; n = (size_t)BB_STEP_WGS * BB_STEP_STAMPS * 8; }  // advances by the hand-offs of every frame it ran
     else if (w == "dec_frame_stamps" && e->df_stamps) { src = e->df_stamps; n = (size_t)DEC_FRAME_WGS * DEC_FRAME_STAMPS * 8; }
     else if (w == "audio_head") {  // device layout [K-1][Vpad][Dd], f32 or bf16 bits
       src = e->audio_head; n = (size_t)(e->K - 1) * Vp * e->Dd * (e->head_wdt == WDT_F32 ? 4 : 2);
@@ -1628,6 +1630,11 @@ int csm_set_option(csm_engine* e, const char* key, int value) {
     else if (k == "dec_frame") {
       if (!e) throw CsmError(CSM_ERR_ARG, "dec_frame needs an engine");
       e->dec_frame = value != 0;
+    }
+    else if (k == "bb_step_stamps") {
+      if (!e) throw CsmError(CSM_ERR_ARG, "bb_step_stamps needs an engine");
+      if (value && !e->bb_stamps) e->bb_stamps = (unsigned long long*)e->alloc((size_t)BB_STEP_WGS * BB_STEP_STAMPS * 8);
+      if (!value && e->bb_stamps) { e->release(e->bb_stamps); e->bb_stamps = nullptr; }
     }
     else if (k == "bb_step") {
       if (!e) throw CsmError(CSM_ERR_ARG, "bb_step needs an engine");

@@ -355,7 +355,9 @@ struct BbStepArgs {
   unsigned long long* gbuf;              // hand-off granules (bb_step_gbuf_bytes)
   unsigned* epoch;                       // hand-off tag base
   int* err;                              // raised when a hand-off wait times out
+  unsigned long long* stamps;            // optional [NWG][BB_STEP_STAMPS] s_memrealtime per hand-off (profiling)
 };
+constexpr int BB_STEP_STAMPS = 128;
 size_t bb_step_gbuf_bytes();
 void launch_bb_step(const BbStepArgs& p, hipStream_t st);
 const void* bb_step_kernel_ptr();
