@@ -216,7 +216,9 @@ def _traffic(key: str):
 def rooflines(model, batch: int):
     """Live HIP-event rooflines on the engine stream.  ``dominant``: the persistent frame decoder
     (dec_frame_kernel, one launch per frame) when it runs the frame's head -- batch 1 greedy bf16 --
-    else the decoder gate/up projection at this batch; ``backbone_gate_up`` beside it."""
+    else the decoder gate/up projection at this batch; ``backbone_gate_up`` beside it: the persistent
+    backbone step (bb_step_kernel) when it runs the batch-1 backbone, else the backbone gate/up
+    projection at this batch."""
     from csm_mlx import _lib
     L = _lib.lib()
 
@@ -232,7 +234,13 @@ def rooflines(model, batch: int):
         _lib.check(L.csm_bench_gemv(model.engine, which, batch, 400, ctypes.byref(us), ctypes.byref(nb)))
         return entry(us.value, nb.value, _kernel_name(model, batch, stack), f"{stack}_gate_up/{model.dtype}/B{batch}")
 
-    out = {"backbone_gate_up": gemv(0, "backbone")}
+    us, nb = ctypes.c_float(0), ctypes.c_double(0)
+    if batch == 1 and L.csm_bench_bb_step(model.engine, 20, ctypes.byref(us), ctypes.byref(nb)) == 0:
+        out = {"backbone_gate_up": entry(us.value, nb.value, "bb_step_kernel = persistent backbone step: the 16 "
+                                         "backbone blocks + final norm of one decode row, one launch",
+                                         f"bb_step/{model.dtype}/B1")}
+    else:
+        out = {"backbone_gate_up": gemv(0, "backbone")}
     us, nb = ctypes.c_float(0), ctypes.c_double(0)
     if batch == 1 and L.csm_bench_dec_frame(model.engine, 20, ctypes.byref(us), ctypes.byref(nb)) == 0:
         out["dominant"] = entry(us.value, nb.value, "dec_frame_kernel = persistent frame decoder: codebook0_head + "

@@ -93,6 +93,7 @@ def lib():
             "csm_set_option": ([P, ctypes.c_char_p, I], I),
             "csm_bench_gemv": ([P, I, I, I, ctypes.POINTER(F), ctypes.POINTER(ctypes.c_double)], I),
             "csm_bench_dec_frame": ([P, I, ctypes.POINTER(F), ctypes.POINTER(ctypes.c_double)], I),
+            "csm_bench_bb_step": ([P, I, ctypes.POINTER(F), ctypes.POINTER(ctypes.c_double)], I),
             "csm_weight_buffers": ([P, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint64), I,
                                     ctypes.POINTER(I)], I),
             "csm_weights_received": ([P], I),

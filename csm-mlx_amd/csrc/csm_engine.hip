@@ -1601,6 +1601,42 @@ int csm_bench_dec_frame(csm_engine* e, int iters, float* avg_us, double* bytes) 
   CSM_CATCH
 }
 
+int csm_bench_bb_step(csm_engine* e, int iters, float* avg_us, double* bytes) {
+  CSM_TRY {
+    if (!e || iters <= 0) throw CsmError(CSM_ERR_ARG, "bad bench arguments");
+    if (!bb_step_eligible(e)) throw CsmError(CSM_ERR_STATE, "the persistent backbone step is not active on this engine");
+    if (e->frames_run < 2) throw CsmError(CSM_ERR_STATE, "run two frames first (the replay needs an embedded decode row)");
+    HIPCHK(hipSetDevice(e->dev));
+    // The replay recomputes the last backbone row from the same embedded x at the same position: the
+    // same K/V rows and h_last are written again.
+    int pos = 0;
+    HIPCHK(hipMemcpy(&pos, e->pos, 4, hipMemcpyDeviceToHost));
+    const csm_llama_dims& d = e->bb.d;
+    const double D = d.hidden, F = d.intermediate, QKV = e->bb.qkv_rows(), HKV = d.n_kv_heads, HD = d.head_dim;
+    double nb = D * 4 * 2;                                                     // x in, h_last out
+    for (int l = 0; l < d.n_layers; ++l) {
+      nb += (QKV * D + D * D + 2 * F * D + D * F) * 2 + 2 * D * 4;              // weights, norm weights
+      nb += 2 * HKV * (double)pos * HD * 4 + 2 * HKV * HD * 4;                  // K/V history read + append
+    }
+    for (int i = 0; i < 2; ++i) enqueue_bb_step(e, e->st);
+    hipEvent_t a, b;
+    HIPCHK(hipEventCreate(&a));
+    HIPCHK(hipEventCreate(&b));
+    HIPCHK(hipEventRecord(a, e->st));
+    for (int i = 0; i < iters; ++i) enqueue_bb_step(e, e->st);
+    HIPCHK(hipEventRecord(b, e->st));
+    HIPCHK(hipEventSynchronize(b));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, a, b));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    check_dec_frame(e);
+    if (avg_us) *avg_us = ms * 1000.f / iters;
+    if (bytes) *bytes = nb;
+  }
+  CSM_CATCH
+}
+
 int csm_set_option(csm_engine* e, const char* key, int value) {
   CSM_TRY {
     const std::string k(key ? key : "");

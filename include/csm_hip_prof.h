@@ -28,6 +28,11 @@ int csm_bench_gemv(csm_engine* e, int which, int M, int iters, float* avg_us, do
  * *bytes = algorithmic bytes per launch: every head and decoder weight the frame reads once in bf16,
  * the folded-table rows, h_last, and the decoder K/V rows read and appended. */
 int csm_bench_dec_frame(csm_engine* e, int iters, float* avg_us, double* bytes);
+/* The persistent backbone step (bb_step.hip) replayed `iters` times for the last decoded row (same x,
+ * same position; idempotent): average launch time (HIP events, engine stream) and the algorithmic
+ * bytes one launch moves (every backbone weight in bf16 + the K/V rows).  CSM_ERR_STATE when the
+ * engine does not run it (not batch-1 bf16 csm_1b shapes, or no frame run yet). */
+int csm_bench_bb_step(csm_engine* e, int iters, float* avg_us, double* bytes);
 
 /* Tuning / debug switches (re-capture the frame graphs): "fuse_attn" (decoder attention recomputed
  * inside the o_proj launch, default 0), "nt_mask" (bit t: non-temporal weight loads for stack tag
