@@ -312,6 +312,13 @@ def main():
 
     bcast = world > 1 and args.weights == "bcast"
     model = build_model(args.dtype, args.batch, device=device, model_name=args.model, load=not bcast or rank == 0)
+    if world > 1:
+        import torch
+        if world > max(1, torch.cuda.device_count()):
+            # rehearsal with several ranks on one GPU: the persistent kernels need every CU of the
+            # device for one launch (their workgroups wait on each other), so they stay off here
+            for opt in (b"dec_frame", b"bb_step"):
+                _lib.check(_lib.lib().csm_set_option(model.engine, opt, 0))
     weights_info = {"source": "synthetic seed 0, generated on every rank" if world > 1 else "synthetic seed 0"}
     if bcast:
         import torch

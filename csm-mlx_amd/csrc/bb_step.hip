@@ -148,6 +148,12 @@ struct WMq { u32x4_t g[2][4]; u32x4_t d[4]; };
 #ifndef BB_PRE
 #define BB_PRE 2  // MLP quarters fetched right after the QKV publish (the rest while the MLP runs)
 #endif
+#ifndef BB_ATT_LIGHT
+#define BB_ATT_LIGHT 1  // 1: attention workgroups fetch MLP quarter 1 after the attention (2: quarters 0-1)
+#endif
+#ifndef BB_Q2_EARLY
+#define BB_Q2_EARLY 0  // 1: MLP quarter 2 fetched after the E2 gather (streams during E3)
+#endif
 #ifndef BB_NEXT
 #define BB_NEXT 0  // 1: the next layer's o_proj rows + first quarter fetched after the down publish
 #endif
@@ -413,17 +419,24 @@ __global__ __launch_bounds__(NT, 1) void bb_step_kernel(BbStepArgs p) {
     phase_qkv(c, l, pos, wq);                         // -> E1
     ++c.e;                                            // E1 is read by the attention workgroups only
     const bool attn_wg = c.w < NATT;
-    // weights for the o_proj and the first MLP quarters stream while the attention runs
+    // weights for the o_proj and the first MLP quarters stream while the attention runs; the
+    // attention workgroups fetch less ahead of their E1 poll (it queues behind the prefetch in
+    // vmcnt order and E2 waits on them) and the second quarter after the attention
 #if !BB_NEXT
     load_o(c, l, wo);
-    load_mq(c, l, 0, mq[0]);
+    if (BB_ATT_LIGHT < 2 || !attn_wg) load_mq(c, l, 0, mq[0]);
 #endif
-    if (BB_PRE > 1) load_mq(c, l, 1, mq[1]);
+    if (BB_PRE > 1 && (!BB_ATT_LIGHT || !attn_wg)) load_mq(c, l, 1, mq[1]);
     if (BB_PRE > 2) load_mq(c, l, 2, mq[2]);
     const Nw nw2 = nw_fetch(c, p.n2[l]);
-    if (attn_wg) phase_attn(c, l, pos);               // waits E1, -> E2
+    if (attn_wg) {
+      phase_attn(c, l, pos);                          // waits E1, -> E2
+      if (BB_ATT_LIGHT >= 2) load_mq(c, l, 0, mq[0]);
+      if (BB_PRE > 1 && BB_ATT_LIGHT) load_mq(c, l, 1, mq[1]);
+    }
     gather<D / NT>(c, c.buf(G_ATT, D), D, L.att);     // E2
     ++c.e;
+    if (BB_Q2_EARLY && BB_PRE <= 2) load_mq(c, l, 2, mq[2]);  // the third quarter streams during E3
     c.refresh();
     phase_o(c, wo);                                   // -> E3
     if (l + 1 < NL) load_q(c, l + 1, wq);
@@ -433,7 +446,7 @@ __global__ __launch_bounds__(NT, 1) void bb_step_kernel(BbStepArgs p) {
     rms(c, nw2, L.xn);
     float acc[4];
     phase_mq<0>(c, mq[0], acc);
-    if (BB_PRE <= 2) load_mq(c, l, 2, mq[2]);
+    if (!BB_Q2_EARLY && BB_PRE <= 2) load_mq(c, l, 2, mq[2]);
     phase_mq<1>(c, mq[1], acc);
     load_mq(c, l, 3, mq[3]);
     phase_mq<2>(c, mq[2], acc);
