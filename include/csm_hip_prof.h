@@ -41,7 +41,9 @@ int csm_bench_bb_step(csm_engine* e, int iters, float* avg_us, double* bytes);
  * "qkv0_tab" (decoder layer 0's q, k, v gathered from a table at steps >= 2, default 1),
  * "fuse_mlp" (one-launch MLP for <= 4 rows, default 0), "dec_frame" (batch-1 greedy bf16 frames on the
  * persistent frame decoder, dec_frame.hip: codebook0_head + 31 decoder steps in one launch, default 1),
- * "linear_mfma" (csm_linear runs the batched frame's MFMA GEMM at >= 8 rows instead of the GEMV,
+ * "bb_step" (batch-1 bf16 backbone rows on the persistent backbone step, bb_step.hip: 16 blocks + the
+ * final norm in one launch, default 1), "dec_frame_stamps" / "bb_step_stamps" (per-hand-off clock
+ * stamps of the persistent kernels, read back with csm_debug_read, default 0), "linear_mfma" (csm_linear runs the batched frame's MFMA GEMM at >= 8 rows instead of the GEMV,
  * default 0: the GEMM's kernel tests). */
 int csm_set_option(csm_engine* e, const char* key, int value);
 
