@@ -145,18 +145,6 @@ struct WO { u32x4_t a[4]; };
 // 16Q + 2v, 16Q + 2v + 1 (one gate/up pair -> SiLU*up column 8Q + v), chunks lane + 64 j (j < 4);
 // thread t holds down rows t + 512 k (k < 4) of column chunk 4w + Q (8 columns)
 struct WMq { u32x4_t g[2][4]; u32x4_t d[4]; };
-#ifndef BB_PRE
-#define BB_PRE 2  // MLP quarters fetched right after the QKV publish (the rest while the MLP runs)
-#endif
-#ifndef BB_ATT_LIGHT
-#define BB_ATT_LIGHT 1  // 1: attention workgroups fetch MLP quarter 1 after the attention (2: quarters 0-1)
-#endif
-#ifndef BB_Q2_EARLY
-#define BB_Q2_EARLY 0  // 1: MLP quarter 2 fetched after the E2 gather (streams during E3)
-#endif
-#ifndef BB_NEXT
-#define BB_NEXT 0  // 1: the next layer's o_proj rows + first quarter fetched after the down publish
-#endif
 
 __device__ __forceinline__ void load_q(Ctx& c, int l, WQ& r) {
   const bf16_t* base = c.p.wqkv[l] + (size_t)(12 * c.w + 6 * (c.tid >> 8)) * D;
@@ -408,10 +396,6 @@ __global__ __launch_bounds__(NT, 1) void bb_step_kernel(BbStepArgs p) {
   Nw nw1 = nw_fetch(c, p.n1[0]);
   for (int k = c.tid; k < D; k += NT) L.x[k] = p.x[k];
   if (c.tid < HD / 2) L.rope[c.tid] = reinterpret_cast<const float2*>(p.rope)[(size_t)pos * (HD / 2) + c.tid];
-#if BB_NEXT
-  load_o(c, 0, wo);
-  load_mq(c, 0, 0, mq[0]);
-#endif
   __syncthreads();
   for (int l = 0; l < NL; ++l) {
     c.refresh();
@@ -419,24 +403,21 @@ __global__ __launch_bounds__(NT, 1) void bb_step_kernel(BbStepArgs p) {
     phase_qkv(c, l, pos, wq);                         // -> E1
     ++c.e;                                            // E1 is read by the attention workgroups only
     const bool attn_wg = c.w < NATT;
-    // weights for the o_proj and the first MLP quarters stream while the attention runs; the
-    // attention workgroups fetch less ahead of their E1 poll (it queues behind the prefetch in
-    // vmcnt order and E2 waits on them) and the second quarter after the attention
-#if !BB_NEXT
+    // the o_proj rows and the first two MLP quarters stream while the attention runs; the attention
+    // workgroups fetch their second quarter after it (their E1 poll would queue behind it in the
+    // CU's memory pipeline, and E2 waits on them).  Measured alternatives: both
+    // quarters after the attention, the third quarter during E3, the next layer's first quarter
+    // during E4 / E5 -- none faster.
     load_o(c, l, wo);
-    if (BB_ATT_LIGHT < 2 || !attn_wg) load_mq(c, l, 0, mq[0]);
-#endif
-    if (BB_PRE > 1 && (!BB_ATT_LIGHT || !attn_wg)) load_mq(c, l, 1, mq[1]);
-    if (BB_PRE > 2) load_mq(c, l, 2, mq[2]);
+    load_mq(c, l, 0, mq[0]);
+    if (!attn_wg) load_mq(c, l, 1, mq[1]);
     const Nw nw2 = nw_fetch(c, p.n2[l]);
     if (attn_wg) {
       phase_attn(c, l, pos);                          // waits E1, -> E2
-      if (BB_ATT_LIGHT >= 2) load_mq(c, l, 0, mq[0]);
-      if (BB_PRE > 1 && BB_ATT_LIGHT) load_mq(c, l, 1, mq[1]);
+      load_mq(c, l, 1, mq[1]);
     }
     gather<D / NT>(c, c.buf(G_ATT, D), D, L.att);     // E2
     ++c.e;
-    if (BB_Q2_EARLY && BB_PRE <= 2) load_mq(c, l, 2, mq[2]);  // the third quarter streams during E3
     c.refresh();
     phase_o(c, wo);                                   // -> E3
     if (l + 1 < NL) load_q(c, l + 1, wq);
@@ -446,7 +427,7 @@ __global__ __launch_bounds__(NT, 1) void bb_step_kernel(BbStepArgs p) {
     rms(c, nw2, L.xn);
     float acc[4];
     phase_mq<0>(c, mq[0], acc);
-    if (!BB_Q2_EARLY && BB_PRE <= 2) load_mq(c, l, 2, mq[2]);
+    load_mq(c, l, 2, mq[2]);
     phase_mq<1>(c, mq[1], acc);
     load_mq(c, l, 3, mq[3]);
     phase_mq<2>(c, mq[2], acc);
@@ -456,12 +437,6 @@ __global__ __launch_bounds__(NT, 1) void bb_step_kernel(BbStepArgs p) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) gput(g + c.tid + NT * k, acc[k], c.tag());   // -> E4
     }
-#if BB_NEXT
-    if (l + 1 < NL) {
-      load_o(c, l + 1, wo);
-      load_mq(c, l + 1, 0, mq[0]);
-    }
-#endif
     nw1 = nw_fetch(c, l + 1 < NL ? p.n1[l + 1] : p.norm);
     c.refresh();
     phase_reduce(c);                                  // waits E4, -> E5
