@@ -461,7 +461,9 @@ static int gemm_nbr(int N, int K, int M, bool q4) {
 static int gemm_ksplit(int N, int K, int M, bool q4) {
   const int nbr = gemm_nbr(N, K, M, q4);
   const int tiles = (N + nbr - 1) / nbr, chunks = (M + 63) / 64;
-  const int target = g_blocks_env > 0 ? g_blocks_env : 256;
+  // the depth decoder's 1-3 MB QKV / o_proj (bf16): half the slices, fewer partials to combine
+  // (tools/gemm_bench.py at 32 rows: 11.1 -> 10.0 and 9.4 -> 8.4 us; every other shape is slower so)
+  const int target = g_blocks_env > 0 ? g_blocks_env : ((!q4 && (size_t)N * K <= (size_t)1536 * 1024) ? 128 : 256);
   int ks = 1;
   while (tiles * chunks * ks < target && ks < GK_MAX_SLICES && K % (GP_KC * ks * 2) == 0) ks *= 2;
   return ks;
