@@ -461,9 +461,12 @@ static int gemm_nbr(int N, int K, int M, bool q4) {
 static int gemm_ksplit(int N, int K, int M, bool q4) {
   const int nbr = gemm_nbr(N, K, M, q4);
   const int tiles = (N + nbr - 1) / nbr, chunks = (M + 63) / 64;
-  // the depth decoder's 1-3 MB QKV / o_proj (bf16): half the slices, fewer partials to combine
-  // (tools/gemm_bench.py at 32 rows: 11.1 -> 10.0 and 9.4 -> 8.4 us; every other shape is slower so)
-  const int target = g_blocks_env > 0 ? g_blocks_env : ((!q4 && (size_t)N * K <= (size_t)1536 * 1024) ? 128 : 256);
+  // half the slices (fewer partials to combine) where it measured faster (tools/gemm_bench.py): the
+  // depth decoder's QKV / o_proj (bf16 at 32 rows 11.1 -> 10.0 and 9.4 -> 8.4 us; int4 at 64 rows
+  // 16.2 -> 15.4 and 12.7 -> 12.2) and the int4 backbone QKV (30.5 -> 25.2 us); every other
+  // csm_1b shape is slower so
+  const bool half = (size_t)N * K <= (size_t)1536 * 1024 || (q4 && N == 3072 && K == 2048);
+  const int target = g_blocks_env > 0 ? g_blocks_env : (half ? 128 : 256);
   int ks = 1;
   while (tiles * chunks * ks < target && ks < GK_MAX_SLICES && K % (GP_KC * ks * 2) == 0) ks *= 2;
   return ks;
