@@ -100,25 +100,33 @@ def build_model(dtype: str, batch: int, seed=0, device=None, model_name="csm_1b"
 
 
 def cpu_baseline(frames: int = 2):
-    """The numpy oracle (CPU restatement of generation.py) on this host, csm_1b fp32, B=1."""
+    """The numpy oracles (CPU restatements of generation.py and of Mimi) on this host, csm_1b fp32,
+    B=1: prompt prefill + ``frames`` frames + the Mimi decode of those frames to PCM -- the same work
+    per frame as the GPU line (generation.py:139-174), on a bounded sample of the 125-frame job."""
     from threadpoolctl import threadpool_info, threadpool_limits
-    from csm_mlx.config import BACKBONE_CONFIGURATION as BB, DECODER_CONFIGURATION as DC
+    from csm_mlx.config import BACKBONE_CONFIGURATION as BB, DECODER_CONFIGURATION as DC, MIMI_CONFIGURATION
     from csm_mlx.models import csm_1b
-    from csm_mlx.weights import synthetic_csm_weights
+    from csm_mlx.weights import synthetic_csm_weights, synthetic_mimi_weights
     from oracle.csm_oracle import OracleCSM, text_frame
+    from oracle.mimi_oracle import OracleMimi
     cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     with threadpool_limits(limits=cores):
         args = csm_1b()
         o = OracleCSM(args, synthetic_csm_weights(args, 0), BB["1b"], DC["100m"])
+        mc = MIMI_CONFIGURATION["mimi_202407"]
+        om = OracleMimi(mc, synthetic_mimi_weights(mc, 0))
         t, m = text_frame(prompt_ids(0), 32)
-        o.generate_codes(t, m, 1)                 # warm (page in weights)
+        om.decode(o.generate_codes(t, m, 1).T[None].astype(np.int32))   # warm (page in weights)
         t0 = time.perf_counter()
-        o.generate_codes(t, m, frames)
+        codes = o.generate_codes(t, m, frames)
+        t1 = time.perf_counter()
+        pcm = om.decode(np.ascontiguousarray(codes.T[None]).astype(np.int32))
         dt = time.perf_counter() - t0
         threads = max((i.get("num_threads", 1) for i in threadpool_info()), default=1)
     return {"value": frames / dt, "unit": "audio frames/s", "cores": int(threads), "kind": "port",
-            "sample": f"numpy fp32 oracle (CPU restatement, not MLX), csm_1b B=1 greedy, prompt prefill + "
-                      f"{frames} frames, codes only, {dt:.1f} s"}
+            "sample": f"numpy fp32 oracles (CPU restatements, not MLX), csm_1b B=1 greedy: prompt prefill + "
+                      f"{frames} frames ({t1 - t0:.1f} s) + Mimi decode of them to {pcm.shape[-1]} PCM samples "
+                      f"({dt - (t1 - t0):.1f} s), {dt:.1f} s in all -- the GPU line's per-frame work"}
 
 
 CONFIGS = {
@@ -131,6 +139,12 @@ CONFIGS = {
             workload="configs[3]: csm_1b greedy, 256 utterances over 8 GPUs = 32 per GPU, 10 s + Mimi decode"),
     5: dict(batch=64, dtype="q4", temperature=0.0, top_k=0, stream=False, context=True,
             workload="configs[4]: csm_1b int4 g64 (nn.quantize), 3-Segment context (Mimi encode), B=64 + decode"),
+    # configs[1]'s utterance with sampling instead of greedy (not a BASELINE config: extra lines)
+    6: dict(batch=1, dtype="bf16", temperature=0.8, top_k=50, stream=False, context=False,
+            workload="configs[1] sampled: csm_1b temperature 0.8, top_k 50 generate(), B=1, 10 s + Mimi decode"),
+    7: dict(batch=1, dtype="bf16", temperature=0.8, top_k=0, stream=False, context=False,
+            workload="configs[1] with the reference's default sampler (generate(temperature=0.8), "
+                     "generation.py:102), B=1, 10 s + Mimi decode"),
 }
 
 
@@ -215,7 +229,7 @@ def _traffic(key: str):
 
 def rooflines(model, batch: int):
     """Live HIP-event rooflines on the engine stream.  ``dominant``: the persistent frame decoder
-    (dec_frame_kernel, one launch per frame) when it runs the frame's head -- batch 1 greedy bf16 --
+    (dec_frame_kernel, one launch per frame) when it runs the frame's head -- batch 1 bf16 --
     else the decoder gate/up projection at this batch; ``backbone_gate_up`` beside it: the persistent
     backbone step (bb_step_kernel) when it runs the batch-1 backbone, else the backbone gate/up
     projection at this batch."""
@@ -244,7 +258,7 @@ def rooflines(model, batch: int):
     us, nb = ctypes.c_float(0), ctypes.c_double(0)
     if batch == 1 and L.csm_bench_dec_frame(model.engine, 20, ctypes.byref(us), ctypes.byref(nb)) == 0:
         out["dominant"] = entry(us.value, nb.value, "dec_frame_kernel = persistent frame decoder: codebook0_head + "
-                                "31 decoder steps (4 layers + audio_head slice each) of one greedy frame, one launch",
+                                "31 decoder steps (4 layers + audio_head slice each) of one frame, one launch",
                                 f"dec_frame/{model.dtype}/B1")
     else:
         out["dominant"] = gemv(4, "decoder")
@@ -263,7 +277,7 @@ def main():
     ap.add_argument("--no-decode", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=96, help="oracle frames timed for cpu_baseline (~10 s on 16 cores)")
-    ap.add_argument("--config", type=int, default=0, choices=[0, 2, 3, 4, 5],
+    ap.add_argument("--config", type=int, default=0, choices=[0, 2, 3, 4, 5, 6, 7],
                     help="run BASELINE.json configs[N-1] (batch, dtype, sampling, streaming, context) instead of "
                          "the default configs[1] line; the metric stays audio frames/s")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],

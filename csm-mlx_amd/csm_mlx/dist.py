@@ -32,6 +32,27 @@ class _DeviceBytes:
                                          "version": 3, "strides": None}
 
 
+def check_buffer_layout(sizes: Sequence[int], device=None) -> None:
+    """Every rank must hold the same weight-buffer list (count and byte sizes) before the per-buffer
+    broadcasts: engines created differently (e.g. a bf16 engine later ``nn.quantize``'d on rank 0 vs
+    ``dtype='q4'`` receivers) would otherwise put the collectives out of step.  All-gathers a
+    fingerprint (count, total bytes, order-sensitive hash of the sizes) and raises on a mismatch."""
+    import torch
+    import torch.distributed as dist
+    h = 1469598103934665603
+    for s in sizes:                                    # FNV-1a over the sizes, order-sensitive
+        h = ((h ^ int(s)) * 1099511628211) & ((1 << 62) - 1)
+    fp = torch.tensor([len(sizes), int(sum(sizes)), h], dtype=torch.int64,
+                      device=device if device is not None else "cpu")
+    allfp = [torch.zeros_like(fp) for _ in range(dist.get_world_size())]
+    dist.all_gather(allfp, fp)
+    rows = [tuple(int(v) for v in t.cpu().tolist()) for t in allfp]
+    if any(r != rows[0] for r in rows):
+        raise RuntimeError("broadcast_weights: ranks hold different weight-buffer layouts "
+                           f"(count, bytes, hash per rank: {rows}); create every rank's model with the same "
+                           "dims, dtype and quantization before broadcasting")
+
+
 def broadcast_weights(model, src: int = 0, device=None) -> float:
     """Weight distribution for N ranks: rank ``src`` has loaded the weights (a checkpoint or the
     synthetic set); every other rank created the same model (dims, dtype, max batch) without loading.
@@ -52,6 +73,7 @@ def broadcast_weights(model, src: int = 0, device=None) -> float:
     sizes = (ctypes.c_uint64 * n.value)()
     _lib.check(L.csm_weight_buffers(model.engine, ptrs, sizes, n.value, ctypes.byref(n)))
     dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    check_buffer_layout([int(s) for s in sizes], dev if dist.get_backend() == "nccl" else None)
     _lib.check(L.csm_synchronize(model.engine))
     t0 = time.perf_counter()
     with torch.cuda.device(dev):

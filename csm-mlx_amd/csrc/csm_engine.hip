@@ -136,6 +136,9 @@ struct csm_engine {
   // the atomics removed (invalid results) the one-launch MLP ran at 264 frames/s.
   bool fuse_mlp = [] { const char* v = getenv("CSM_FUSE_MLP"); return v && v[0] == '1'; }();
   int acc_rows = 0;  // rows of the fused-MLP accumulators (the fused path runs for M <= acc_rows)
+  // csm_set_option "prefill_rows": row cap of one csm_prefill_batch group (0 = M_cap); lowering it makes
+  // small test batches take the multi-group path that config 5's 64 x 248-row contexts take
+  int prefill_rows = 0;
   GemmWs ws;         // split-K slabs + tickets of this engine's MFMA launches (ensure_batch sizes them)
   // persistent frame decoder (dec_frame.hip) for batch-1 greedy bf16 frames: hand-off granules, tag
   // epoch, timeout flag; csm_set_option "dec_frame" / CSM_DEC_FRAME=0 turn it off
@@ -363,11 +366,12 @@ void enqueue_body(csm_engine* e, hipStream_t st) {
   launch_rmsnorm_rows(e->x, e->D, e->bb.norm, e->bb.d.eps, e->D, e->h_last, e->D, B, st, pend, e->acc_rows * e->D);
 }
 
-// The persistent frame decoder runs the whole head of a batch-1 greedy frame when the engine has
+// The persistent frame decoder runs the whole head of a batch-1 frame (greedy, or sampled: its heads
+// then hand every logit to every workgroup, which runs the sampler's top-k + Gumbel-max) when the engine has
 // csm_1b's decoder shapes in bf16 and the folded tables, and the device has the 256 CUs its grid of
 // one workgroup per CU assumes (every workgroup must be resident: the hand-offs spin).
 bool dec_frame_eligible(csm_engine* e) {
-  if (!e->dec_frame || e->B != 1 || e->temperature > 0.f || e->wdt != WDT_BF16 || e->head_wdt != WDT_BF16) return false;
+  if (!e->dec_frame || e->B != 1 || e->wdt != WDT_BF16 || e->head_wdt != WDT_BF16) return false;
   const csm_llama_dims& d = e->dec.d;
   if (d.hidden != 1024 || d.intermediate != 8192 || d.n_heads != 8 || d.n_kv_heads != 2 || d.head_dim != 128 ||
       d.n_layers != DEC_FRAME_LAYERS || e->bb.d.hidden != 2048 || e->V <= 2048 || e->V > 2051 || e->K > 32 ||
@@ -402,6 +406,7 @@ void enqueue_dec_frame_only(csm_engine* e, hipStream_t st) {
   static const int wnt = [] { const char* v = getenv("CSM_DF_WNT"); return v ? atoi(v) : 0; }();
   static const int hnt = [] { const char* v = getenv("CSM_DF_HNT"); return v ? atoi(v) : 1; }();
   a.wnt = wnt; a.hnt = hnt;
+  a.temperature = e->temperature; a.top_k = e->top_k; a.seeds = e->seeds; a.frame_ctr = e->frame_ctr;
   launch_dec_frame(a, st);
 }
 
@@ -414,17 +419,19 @@ void enqueue_dec_frame(csm_engine* e, hipStream_t st) {
 }
 
 // A hand-off wait of a persistent kernel that timed out leaves its flag raised: report it.
+// Every raised flag is cleared and named in the one error.
 void check_dec_frame(csm_engine* e) {
+  std::string who;
   for (int* f : {e->df_err, e->bb_err}) {
     if (!f) continue;
     int v = 0;
     HIPCHK(hipMemcpy(&v, f, 4, hipMemcpyDeviceToHost));
     if (v) {
       HIPCHK(hipMemset(f, 0, 4));
-      throw CsmError(CSM_ERR_HIP, std::string(f == e->df_err ? "persistent frame decoder" : "persistent backbone step") +
-                                      ": a hand-off wait timed out (results of this batch are invalid)");
+      who += std::string(who.empty() ? "" : " and ") + (f == e->df_err ? "persistent frame decoder" : "persistent backbone step");
     }
   }
+  if (!who.empty()) throw CsmError(CSM_ERR_HIP, who + ": a hand-off wait timed out (results of this batch are invalid)");
 }
 
 // phase 0: the whole head (what the frame graph captures).  phase 1: c0 logits only, stored for the
@@ -1086,6 +1093,11 @@ int csm_quantize(csm_engine* e, int group_size, int bits) {
     mats.emplace_back(&e->c0_head, e->Vpad, e->D);
     for (auto& [pp, N, Kd] : mats)
       if (!gemv_q4_supported(N, Kd)) throw CsmError(CSM_ERR_ARG, "int4 GEMV does not support this shape");
+    // the bf16 chunk-major down_proj copies serve only the bf16 persistent kernels: freed, so an
+    // nn.quantize'd engine lists the same weight buffers as one created as CSM_Q4 (csm_weight_buffers)
+    for (Stack* s : {&e->bb, &e->dec})
+      for (LayerW& l : s->L)
+        if (l.wdc) { e->release(l.wdc); l.wdc = nullptr; }
     for (auto& [pp, N, Kd] : mats) {
       void* q = e->alloc(q4_bytes(N, Kd));
       launch_q4_quantize(*pp, old, N, Kd, q, N, 0, 1, e->st);
@@ -1183,12 +1195,14 @@ int csm_prefill_batch(csm_engine* e, int n, const int32_t* utts, const int32_t* 
       row0[i + 1] = row0[i] + T;
     }
     HIPCHK(hipSetDevice(e->dev));
+    const size_t cap = e->prefill_rows > 0 ? std::min(e->prefill_rows, e->M_cap) : e->M_cap;
     // utterances in groups of at most M_cap rows: one pass of every projection per group (the
     // weights stream once for all of the group's rows), rows mapped to (utterance, position)
     std::vector<int> rb, rp;
     for (int i0 = 0; i0 < n;) {
       int i1 = i0;
-      while (i1 < n && row0[i1 + 1] - row0[i0] <= (size_t)e->M_cap) ++i1;
+      while (i1 < n && row0[i1 + 1] - row0[i0] <= cap) ++i1;
+      if (i1 == i0) i1 = i0 + 1;  // one utterance longer than a lowered cap: a group of its own (T <= M_cap)
       const int R = (int)(row0[i1] - row0[i0]);
       rb.assign(R, 0);
       rp.assign(R, 0);
@@ -1292,6 +1306,21 @@ int csm_run_frames(csm_engine* e, int nframes, int* all_done) {
   CSM_CATCH
 }
 
+int csm_frame_step(csm_engine* e, int32_t* out_codes, uint8_t* done) {
+  if (!e) { csm_set_error("null engine"); return CSM_ERR_ARG; }
+  if (e->frames_run >= e->F_cap) { csm_set_error("frame capacity reached"); return CSM_ERR_STATE; }
+  const int rc = csm_run_frames(e, 1, nullptr);
+  if (rc != CSM_OK) return rc;
+  CSM_TRY {
+    if (out_codes)
+      HIPCHK(hipMemcpyAsync(out_codes, e->codes, (size_t)e->B * e->K * 4, hipMemcpyDeviceToHost, e->st));
+    if (done) HIPCHK(hipMemcpyAsync(done, e->done, e->B, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(hipStreamSynchronize(e->st));
+    check_dec_frame(e);
+  }
+  CSM_CATCH
+}
+
 // One frame in two halves around a host hook on the c0 logits (generation.py:42-49): eager launches
 // of the same kernels the frame graph holds.
 int csm_frame_c0_logits(csm_engine* e, float* logits) {
@@ -1316,6 +1345,7 @@ int csm_frame_c0_logits(csm_engine* e, float* logits) {
     HIPCHK(hipMemcpy2DAsync(logits, (size_t)e->V * 4, e->c0_logits, (size_t)e->Vpad * 4, (size_t)e->V * 4, e->B,
                             hipMemcpyDeviceToHost, e->st));
     HIPCHK(hipStreamSynchronize(e->st));
+    check_dec_frame(e);  // the backbone row may have run on the persistent step
     e->c0_pending = true;
   }
   CSM_CATCH
@@ -1343,6 +1373,7 @@ int csm_frame_finish(csm_engine* e, const float* logits, int* all_done) {
     } else {
       HIPCHK(hipStreamSynchronize(e->st));  // the host logits buffer may be released on return
     }
+    check_dec_frame(e);
   }
   CSM_CATCH
 }
@@ -1379,6 +1410,7 @@ int csm_frame_forced(csm_engine* e, const int32_t* codes, float* c0_logits, floa
                               hipMemcpyDeviceToHost, e->st));
     if (ce) HIPCHK(hipMemcpyAsync(ce, e->force_ce, B * e->K * 4, hipMemcpyDeviceToHost, e->st));
     HIPCHK(hipStreamSynchronize(e->st));
+    check_dec_frame(e);  // the backbone row may have run on the persistent step
   }
   CSM_CATCH
 }
@@ -1675,6 +1707,16 @@ int csm_set_option(csm_engine* e, const char* key, int value) {
     else if (k == "bb_step") {
       if (!e) throw CsmError(CSM_ERR_ARG, "bb_step needs an engine");
       e->bb_step = value != 0;
+    }
+    else if (k == "prefill_rows") {
+      if (!e || value < 0) throw CsmError(CSM_ERR_ARG, "prefill_rows needs an engine and a row count >= 0");
+      e->prefill_rows = value;
+    }
+    else if (k == "inject_handoff_error") {  // test hook: raise the persistent kernels' timeout flags
+      if (!e) throw CsmError(CSM_ERR_ARG, "inject_handoff_error needs an engine");
+      const int one = 1;
+      for (int* f : {e->df_err, e->bb_err})
+        if (f && value) HIPCHK(hipMemcpy(f, &one, 4, hipMemcpyHostToDevice));
     }
     else if (k == "fuse_mlp") {
       if (!e) throw CsmError(CSM_ERR_ARG, "fuse_mlp needs an engine");

@@ -83,6 +83,26 @@ struct GemvParams {
   int row_chunk;         // gemv_xl_kernel: blockIdx.y takes rows [y*row_chunk, +row_chunk) (table builds)
 };
 
+// order-preserving float <-> uint32 keys (radix select of the top-k threshold)
+__device__ __forceinline__ uint32_t f2key(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float key2f(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+// The sampler's counter-based Gumbel-max (restated in oracle/csm_oracle.py gumbel_u): one key per
+// (utterance seed, frame * K + codebook), one uniform per vocabulary entry, perturbed logit in double.
+// Shared by sample_kernel and the persistent frame decoder so both pick identical codes.
+__device__ __forceinline__ uint64_t gumbel_key(uint64_t seed, int step) {
+  return splitmix64(splitmix64(seed) ^ (uint64_t)step);
+}
+__device__ __forceinline__ double gumbel_perturbed(float logit, float inv_t, uint64_t key, int v) {
+  const uint64_t h = splitmix64(key ^ (uint64_t)v);
+  const double u = ((double)(h >> 11) + 0.5) * 1.1102230246251565e-16;  // 2^-53
+  return (double)(logit * inv_t) + (-log(-log(u)));
+}
+
 __device__ __forceinline__ unsigned long long pack_argmax(float v, int idx) {
   const uint32_t u = __float_as_uint(v);
   const uint32_t key = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
@@ -391,6 +411,12 @@ struct DecFrameArgs {
   int* err;                              // raised when a hand-off wait times out
   unsigned long long* stamps;            // optional [NWG][DEC_FRAME_STAMPS] s_memrealtime per hand-off (profiling)
   int wnt, hnt;                          // non-temporal loads for the decoder weights / the heads
+  // sampling (temperature > 0): every head's logits are handed to every workgroup, which picks the
+  // code by the sampler's top-k threshold + Gumbel-max (gumbel_perturbed) redundantly
+  float temperature;
+  int top_k;
+  const uint64_t* seeds;                 // [1] utterance 0's sampling seed
+  const int* frame_ctr;                  // frame index (the sampler's counter)
 };
 constexpr int DEC_FRAME_STAMPS = 1024;
 size_t dec_frame_gbuf_bytes();

@@ -846,13 +846,6 @@ __global__ __launch_bounds__(256) void rmsnorm_rows_kernel(const float* x, int x
 }
 
 // ============================================================================ sampling
-__device__ __forceinline__ uint32_t f2key(float f) {
-  const uint32_t u = __float_as_uint(f);
-  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-}
-__device__ __forceinline__ float key2f(uint32_t k) {
-  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
-}
 
 // (value, index) arg-max with the first-max tie rule of mx.argmax
 template <typename T>
@@ -964,8 +957,7 @@ __global__ __launch_bounds__(256) void sample_kernel(SampleParams p) {
       }
       thr = key2f(prefix);
     }
-    const int step = p.frame_ctr[0] * p.K + p.cb;
-    const uint64_t key = splitmix64(splitmix64(p.seeds[b]) ^ (uint64_t)step);
+    const uint64_t key = gumbel_key(p.seeds[b], p.frame_ctr[0] * p.K + p.cb);
     const float inv_t = 1.0f / p.temperature;
     double best = -INFINITY;
     int bi = 0x7fffffff;
@@ -974,9 +966,7 @@ __global__ __launch_bounds__(256) void sample_kernel(SampleParams p) {
       const int v = tid + 256 * i;
       const float l = lv[i];
       if (v >= V || !(l >= thr)) continue;
-      const uint64_t h = splitmix64(key ^ (uint64_t)v);
-      const double u = ((double)(h >> 11) + 0.5) * 1.1102230246251565e-16;  // 2^-53
-      const double val = (double)(l * inv_t) + (-log(-log(u)));
+      const double val = gumbel_perturbed(l, inv_t, key, v);
       if (val > best) {
         best = val;
         bi = v;

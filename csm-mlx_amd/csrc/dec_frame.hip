@@ -44,6 +44,7 @@ constexpr int D = 1024, F = 8192, HQ = 8, HKV = 2, HD = 128, NL = DEC_FRAME_LAYE
 constexpr int QKV = (HQ + 2 * HKV) * HD;  // 1536
 constexpr int MAXM = 2;                   // rows per step (step 1: [h_last, E_a[c0]])
 constexpr unsigned SPIN_LIMIT = 1u << 22; // ~0.1 s of s_sleep per hand-off before declaring failure
+constexpr int VMAX = 2056;                // padded audio vocabulary (V <= 2051, checked by the engine)
 
 // the same chunk against two activation rows (every weight converted once, used twice: no
 // loop-invariant conversions for the compiler to hoist out of a row loop)
@@ -93,6 +94,7 @@ struct Lds {
   float wsum[8][MAXM * 8]; // per-wave partial dots
   float Ks[HKV][32][HD + 4];// cached keys of this layer (rows padded: conflict-free row-parallel reads)
   float Vs[HKV][32][HD];    // cached values
+  float lg[VMAX];          // sampling: the head's logits, gathered from every workgroup
   int code;                // last arg-max
   int flag;
 };
@@ -106,7 +108,8 @@ constexpr size_t G_X = 0;                                  // [2][MAXM][D] x sli
 constexpr size_t G_QKV = G_X + 2 * MAXM * D;               // [2][MAXM][QKV]
 constexpr size_t G_PART = G_QKV + 2 * MAXM * QKV;          // [2][NWG][MAXM][D] down partials
 constexpr size_t G_ARG = G_PART + (size_t)2 * NWG * MAXM * D;  // [2][NWG][2] arg-max keys
-constexpr size_t G_TOTAL = G_ARG + 2 * NWG * 2;
+constexpr size_t G_LOG = G_ARG + 2 * NWG * 2;              // [2][VMAX] logits (sampling)
+constexpr size_t G_TOTAL = G_LOG + 2 * VMAX;
 
 struct Ctx {
   const DecFrameArgs& p;
@@ -510,15 +513,22 @@ __device__ __forceinline__ void phase_head(Ctx& c, const bf16_t* W, int n_valid,
   s = wave_sum(s);
   unsigned long long best = row < n_valid ? pack_argmax(s, row) : 0ull;
   if (c.lane == 0 && row < n_valid) logits[row] = s;
+  const int xr = 2048 + c.w;
+  float t = 0.f;
   if (c.wave == 0 && c.w < 3) {
-    float t = 0.f;
 #pragma unroll
     for (int i = 0; i < CPL; ++i) t += dot8(wx[i], c.L.xn[0] + 8 * (c.lane + 64 * i));
     t = wave_sum(t);
-    const int xr = 2048 + c.w;
     const unsigned long long k2 = xr < n_valid ? pack_argmax(t, xr) : 0ull;
     best = k2 > best ? k2 : best;
     if (c.lane == 0 && xr < n_valid) logits[xr] = t;
+  }
+  if (c.p.temperature > 0.f) {  // sampling: every logit to every workgroup (sample_code)
+    u64* g = c.buf(G_LOG, VMAX);
+    if (c.lane == 0 && row < n_valid) gput(g + row, s, c.tag());
+    if (c.lane == 0 && c.wave == 0 && c.w < 3 && xr < n_valid) gput(g + xr, t, c.tag());
+    __syncthreads();
+    return;
   }
   if (c.lane == 0) reinterpret_cast<unsigned long long*>(c.L.wsum)[c.wave] = best;
   __syncthreads();
@@ -554,6 +564,102 @@ __device__ __forceinline__ int gather_code(Ctx& c, int V) {
   return c.L.code;
 }
 
+// Sampling (temperature > 0): gather the head's V logits, then -- identically in every workgroup --
+// the sampler of sample_kernel (csm_kernels.hip): the top_k-th largest logit by radix select (keys
+// >= it kept, ties included), then the Gumbel-max over logits * (1/temp) of the kept entries with
+// the first-max tie rule.  cb: codebook index of the sampler's counter (frame * K + cb).
+__device__ __forceinline__ int sample_code(Ctx& c, int V, int cb) {
+  constexpr int NPT = (VMAX + NT - 1) / NT;  // logits per thread
+  gather<NPT>(c, c.buf(G_LOG, VMAX), V, c.L.lg);
+  const DecFrameArgs& p = c.p;
+  float thr = -INFINITY;
+  if (p.top_k > 0 && p.top_k < V) {
+    // radix select, 8 bits per pass; threads 0..255 hold digit 255 - tid for the suffix count
+    uint32_t* hist = reinterpret_cast<uint32_t*>(&c.L.red[0][0]);
+    uint32_t* wsum = hist + 256;
+    uint32_t* sh = hist + 264;  // [prefix, remain]
+    uint32_t prefix = 0, maskbits = 0, rem = (uint32_t)p.top_k;
+    for (int shift = 24; shift >= 0; shift -= 8) {
+      if (c.tid < 256) hist[c.tid] = 0;
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < NPT; ++i) {
+        const int v = c.tid + NT * i;
+        if (v < V) {
+          const uint32_t key = f2key(c.L.lg[v]);
+          if ((key & maskbits) == prefix) atomicAdd(&hist[(key >> shift) & 255u], 1u);
+        }
+      }
+      __syncthreads();
+      uint32_t h = 0, cnt = 0;
+      if (c.tid < 256) {
+        h = hist[255 - c.tid];
+        cnt = h;  // inclusive prefix over t = count of keys with digit >= 255 - t
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t u = __shfl_up(cnt, o, 64);
+          if (c.lane >= o) cnt += u;
+        }
+        if (c.lane == 63) wsum[c.wave] = cnt;
+      }
+      __syncthreads();
+      if (c.tid < 256) {
+        for (int w = 0; w < c.wave; ++w) cnt += wsum[w];
+        const uint32_t above = cnt - h;
+        if (h > 0 && above < rem && rem <= cnt) {  // exactly one digit
+          sh[0] = prefix | ((uint32_t)(255 - c.tid) << shift);
+          sh[1] = rem - above;
+        }
+      }
+      __syncthreads();
+      prefix = sh[0];
+      rem = sh[1];
+      maskbits |= 255u << shift;
+      __syncthreads();  // sh / hist reused by the next pass
+    }
+    thr = key2f(prefix);
+  }
+  const uint64_t key = gumbel_key(p.seeds[0], p.frame_ctr[0] * p.K + cb);
+  const float inv_t = 1.0f / p.temperature;
+  double best = -INFINITY;
+  int bi = 0x7fffffff;
+#pragma unroll
+  for (int i = 0; i < NPT; ++i) {
+    const int v = c.tid + NT * i;
+    if (v >= V) continue;
+    const float l = c.L.lg[v];
+    if (!(l >= thr)) continue;
+    const double val = gumbel_perturbed(l, inv_t, key, v);
+    if (val > best) {  // increasing v per thread: first max kept
+      best = val;
+      bi = v;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double ov = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+  }
+  double* sv = reinterpret_cast<double*>(&c.L.wsum[0][0]);
+  int* si = reinterpret_cast<int*>(sv + 8);
+  if (c.lane == 0) { sv[c.wave] = best; si[c.wave] = bi; }
+  __syncthreads();
+  if (c.tid == 0) {
+    double bv = sv[0];
+    int b = si[0];
+    for (int w2 = 1; w2 < NT / 64; ++w2)
+      if (sv[w2] > bv || (sv[w2] == bv && si[w2] < b)) { bv = sv[w2]; b = si[w2]; }
+    c.L.code = min(max(b, 0), V - 1);  // NaN logits leave no winner: clamp (as sample_kernel)
+  }
+  __syncthreads();
+  return c.L.code;
+}
+
+// the code of a head: greedy arg-max of the published keys, or the sampler over the logits
+__device__ __forceinline__ int head_code(Ctx& c, int V, int cb) {
+  return c.p.temperature > 0.f ? sample_code(c, V, cb) : gather_code(c, V);
+}
 
 // Registers carried between phases (prefetched weights, norm weights)
 struct Pre {
@@ -657,7 +763,7 @@ __device__ __forceinline__ void run_step(Ctx& c, int step, Pre& r) {
   phase_head<D>(c, p.audio_head + (size_t)(step - 1) * p.VP * D, p.V, r.wh.a, r.wh.x, p.ci_logits + (size_t)(step - 1) * p.VP);  // -> E6
   KvRegs kv0;  // layer 0's cached K/V rows of the next step: in flight during the head's hand-off,
   if (step + 1 < p.K) kv_issue(c, 0, step + 1, kv0);
-  const int ci = gather_code(c, p.V);
+  const int ci = head_code(c, p.V, step);
   ++c.e;
   if (c.w == 0 && c.tid == 0) p.codes[step] = ci;
   if (step + 1 < p.K) kv_store(c, step + 1, kv0);  // and in LDS before the loop back-edge
@@ -699,7 +805,7 @@ __global__ __launch_bounds__(NT, 1) void dec_frame_kernel(DecFrameArgs p) {
     __syncthreads();
     if (c.tid < 4) gput(c.buf(G_X, MAXM * D) + 4 * c.w + c.tid, L.wsum[2 * c.tid][0] + L.wsum[2 * c.tid + 1][0], c.tag());
   }
-  const int c0 = gather_code(c, p.V);
+  const int c0 = head_code(c, p.V, 0);
   gather<2>(c, c.buf(G_X, MAXM * D), D, L.x[0]);  // x row 0 = projection(h_last)
   ++c.e;
   if (c.w == 0 && c.tid == 0) p.codes[0] = c0;

@@ -99,6 +99,11 @@ int csm_prefill_batch(csm_engine* e, int n, const int32_t* utts, const int32_t* 
 /* Generate up to nframes frames for the whole batch (one HIP graph replay per frame).
  * *all_done (optional) = 1 when every utterance hit EOS. */
 int csm_run_frames(csm_engine* e, int nframes, int* all_done);
+/* One frame (generation.py:21-92 + the EOS test :151) with its result handed back: out_codes [B][K]
+ * int32 = the frame's codes (the `sample` generate_frame returns), done [B] = utterances past EOS.
+ * Either pointer may be NULL.  Equivalent to csm_run_frames(e, 1, NULL) followed by a read of the
+ * frame's codes; CSM_ERR_STATE when the engine's frame capacity is exhausted. */
+int csm_frame_step(csm_engine* e, int32_t* out_codes, uint8_t* done);
 /* One frame split around a host hook on the c0 logits (logits_processors, generation.py:42-49):
  * csm_frame_c0_logits runs the backbone step + codebook0_head and copies logits [B][V] out;
  * csm_frame_finish takes the (processed) logits [B][V] back, picks c0 (arg-max when greedy, else the

@@ -84,3 +84,34 @@ def test_bb_step_long_context(model_1b):
     ids = [int(t) for t in rng.integers(1000, 120000, 600)]  # 600 text rows: keys span two passes
     prompt = tokenize_text_segment(ids, 0, 32)
     _compare(model, prompt, 4)
+
+
+def test_handoff_timeout_reported_by_every_frame_entry(model_1b):
+    """A raised hand-off timeout flag of the persistent kernels surfaces as an error from the
+    teacher-forced frame and from both halves of the processor-split frame (not only from a later
+    generate): csm_frame_forced / csm_frame_c0_logits / csm_frame_finish check it."""
+    from csm_mlx import _lib
+    from csm_mlx.generation import FrameCache
+    from csm_mlx.sampling import Sampler
+    from csm_mlx.tokenizers import tokenize_text_segment
+    args, w, model = model_1b
+    L = _lib.lib()
+    K, V = args.n_audio_codebooks, args.n_audio_vocab
+    prompt = tokenize_text_segment(prompt_ids(31), 0, K)
+    codes = np.ones((1, K), np.int32)
+    logits = np.zeros((1, V), np.float32)
+    for entry in ("forced", "c0", "finish"):
+        cache = FrameCache(model, 1, Sampler(0.0, 0), [0])
+        cache.prefill(0, *prompt)
+        cache.run(1)                                      # the next frame starts with a backbone step
+        if entry == "finish":
+            _lib.check(L.csm_frame_c0_logits(model.engine, _lib.ptr(logits)))
+        _lib.check(L.csm_set_option(model.engine, b"inject_handoff_error", 1))
+        with pytest.raises(_lib.CsmHipError, match="hand-off wait timed out"):
+            if entry == "forced":
+                _lib.check(L.csm_frame_forced(model.engine, _lib.ptr(codes), None, None, None))
+            elif entry == "c0":
+                _lib.check(L.csm_frame_c0_logits(model.engine, _lib.ptr(logits)))
+            else:
+                _lib.check(L.csm_frame_finish(model.engine, _lib.ptr(logits), None))
+        _lib.check(L.csm_synchronize(model.engine))       # the flag was consumed by the report

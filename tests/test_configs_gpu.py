@@ -98,3 +98,61 @@ def test_config4_q4_context_segments():
     ref = oracle_batch(oracle_for(args, w, q4=True), prompts, frames)
     for b in range(B):
         assert n[b] == frames and first_divergence(hist[:frames, b], ref[b][0]) is None, f"utterance {b}"
+
+
+def test_config5_multi_group_prefill():
+    """configs[4] at its real prefill shape: B = 9 prompts of 248 Mimi-encoded context rows = 2,232
+    rows, more than one csm_prefill_batch group holds (<= 2,048 rows: groups of 8 + 1), and again with
+    the group cap lowered to 500 rows (5 groups of <= 2 utterances) -- the per-group h_last and row
+    tables bench.py --config 5 runs (B = 64: 8 groups).  Both against csm_prefill per utterance
+    (h_last within the int4 bar, the first 2 frames' codes identical) and against the oracle on the
+    dequantized weights for utterances 0, 7 (last of group 1) and 8 (group 2 alone)."""
+    import ctypes
+    from csm_mlx import _lib
+    from csm_mlx.generation import FrameCache
+    from csm_mlx.models import CSM
+    from csm_mlx.sampling import Sampler
+    from csm_mlx.segment import Segment
+    from csm_mlx.tokenizers import tokenize_segments_batch, tokenize_text_segment
+    import bench
+    B, frames = 9, 2
+    args, w = csm_weights("1b")
+    model = CSM(args, dtype="q4", max_batch=B)
+    model.load_weights(w)
+    _codec(3 * B)
+    segs = [Segment(s % 2, prompt_ids(10_000 + 10 * g + s), bench.context_audio(g, s)) for g in range(B) for s in range(3)]
+    enc = tokenize_segments_batch(segs, n_audio_codebooks=32)
+    prompts = []
+    for g in range(B):
+        parts = enc[3 * g:3 * g + 3] + [tokenize_text_segment(prompt_ids(g), 0, 32)]
+        prompts.append((np.concatenate([t for t, _ in parts]), np.concatenate([m for _, m in parts])))
+    assert sum(t.shape[0] for t, _ in prompts) > 2048
+    L = _lib.lib()
+    D = model.backbone.args.hidden_size
+
+    def run(mode):
+        _lib.check(L.csm_set_option(model.engine, b"prefill_rows", 500 if mode == "cap500" else 0))
+        cache = FrameCache(model, B, Sampler(0.0, 0), [0] * B)
+        if mode == "single":
+            for b, (t, m) in enumerate(prompts):
+                cache.prefill(b, t, m)
+        else:
+            cache.prefill_batch([(b, t, m) for b, (t, m) in enumerate(prompts)])
+        h = cache.debug("h_last", (B, D))
+        cache.run(frames)
+        hist, n, _ = cache.codes()
+        return h, hist[:frames], n
+
+    h1, c1, n1 = run("single")
+    h2, c2, n2 = run("default")
+    h3, c3, n3 = run("cap500")
+    _lib.check(L.csm_set_option(model.engine, b"prefill_rows", 0))
+    del model
+    for h, c, n, tag in ((h2, c2, n2, "2 groups"), (h3, c3, n3, "5 groups")):
+        err = np.abs(h - h1).max(axis=1) / np.abs(h1).max(axis=1)
+        assert err.max() <= 1e-3, f"{tag}: h_last differs from per-utterance prefill ({err.max():.2e})"
+        assert np.array_equal(c, c1) and np.array_equal(n, n1), f"{tag}: codes differ from per-utterance prefill"
+    sel = [0, 7, 8]
+    ref = oracle_batch(oracle_for(args, w, q4=True), [prompts[b] for b in sel], frames)
+    for j, b in enumerate(sel):
+        assert n1[b] == frames and first_divergence(c2[:, b], ref[j][0]) is None, f"utterance {b} vs oracle"

@@ -60,3 +60,42 @@ def test_dec_frame_matches_launch_path_and_oracle():
     orc = oracle_for(args, w, bf16=True).generate_codes(*prompt, 12)
     assert first_divergence(got, orc) is None
     del model
+
+
+@pytest.mark.parametrize("top_k", [0, 50])
+def test_dec_frame_sampled_matches_launch_path_and_oracle(top_k):
+    """The reference's default sampler (temperature 0.8, generation.py:102, :51-54; top_k 0) and
+    config 3's top-k 50 at batch 1 on the persistent frame decoder: every head hands all its logits
+    to every workgroup, which runs sample_kernel's top-k radix select + Gumbel-max.  12 frames: codes
+    identical to the launch path (sample_kernel) and to the oracle's restatement of the counter-based
+    RNG; the decoder ran every frame (same 498 hand-offs as greedy)."""
+    from csm_mlx import _lib
+    from csm_mlx.generation import FrameCache, generate_codes_batch
+    from csm_mlx.models import CSM
+    from csm_mlx.sampling import Sampler
+    from csm_mlx.tokenizers import tokenize_text_segment
+    args, w = csm_weights("1b")
+    model = CSM(args, dtype="bf16")
+    model.load_weights(w)
+    L = _lib.lib()
+    prompt = tokenize_text_segment(prompt_ids(33), 0, 32)
+    smp, seed, frames = Sampler(0.8, top_k), 4242, 12
+
+    def run():
+        h, n, _ = generate_codes_batch(model, [prompt], frames, sampler=smp, seeds=[seed])
+        return h[: n[0], 0].copy()
+    _lib.check(L.csm_set_option(model.engine, b"dec_frame", 0))
+    ref = run()
+    _lib.check(L.csm_set_option(model.engine, b"dec_frame", 1))
+    ep0 = np.zeros(1, np.uint32)
+    _lib.check(L.csm_debug_read(model.engine, b"dec_frame_epoch", _lib.ptr(ep0), 4, None))
+    got = run()
+    ep1 = np.zeros(1, np.uint32)
+    _lib.check(L.csm_debug_read(model.engine, b"dec_frame_epoch", _lib.ptr(ep1), 4, None))
+    assert int(ep1[0]) - int(ep0[0]) == frames * 498, "the persistent frame decoder did not run every sampled frame"
+    assert len(got) == frames and first_divergence(got, ref) is None, \
+        f"sampled dec_frame codes differ from the launch path at {first_divergence(got, ref)}"
+    assert np.array_equal(run(), got)                                     # deterministic per seed
+    orc = oracle_for(args, w, bf16=True).generate_codes(*prompt, frames, temperature=0.8, top_k=top_k, seed=seed)
+    assert first_divergence(got, orc) is None
+    del model

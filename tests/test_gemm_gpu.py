@@ -127,3 +127,40 @@ def test_batched_prefill_matches_per_utterance(dtype):
     assert np.array_equal(n0, n1) and np.array_equal(h0, h1)
     for a, b in zip(l0, l1):
         assert np.abs(a - b).max() <= 1e-4 * np.abs(a).max()
+
+
+def test_csm_1b_bf16_batch_composition_invariance():
+    """An utterance's greedy codes do not depend on which other prompts share its batch: the same
+    csm_1b bf16 prompt alone (B = 1: persistent backbone step + frame decoder, fp32 GEMV sums) and
+    as utterance 5 of a B = 32 batch prefilled in one csm_prefill_batch pass (matrix-core GEMMs whose
+    split-K slice count follows the batch's total row count) -- 6 frames, codes identical, c0 logits
+    within the bf16 bar.  (Summation order differs between the two; greedy codes are the bar.)"""
+    from csm_mlx.generation import FrameCache
+    from csm_mlx.sampling import Sampler
+    from csm_mlx.tokenizers import tokenize_text_segment
+    args, w = csm_weights("1b")
+    K, V = args.n_audio_codebooks, args.n_audio_vocab
+    Vp = (V + 7) // 8 * 8
+    B, frames, j = 32, 6, 5
+    prompts = [tokenize_text_segment(prompt_ids(700 + b, 8 + b % 5), 0, K) for b in range(B)]
+    model = _model(args, w, "bf16", B)
+    out = []
+    for batch in ([prompts[j]], prompts):
+        cache = FrameCache(model, len(batch), Sampler(0.0, 0), [0] * len(batch))
+        if len(batch) > 1:
+            cache.prefill_batch([(b, t, m) for b, (t, m) in enumerate(batch)])
+        else:
+            cache.prefill(0, *batch[0])
+        logs = []
+        for _ in range(frames):
+            cache.run(1)
+            logs.append(cache.debug("c0_logits", (len(batch), Vp))[:, :V].copy())
+        hist, n, _ = cache.codes()
+        b = 0 if len(batch) == 1 else j
+        out.append((hist[: n[b], b].copy(), [l[b] for l in logs]))
+        del cache
+    del model
+    (c1, l1), (c32, l32) = out
+    assert len(c1) == frames and first_divergence(c1, c32) is None, "codes depend on the batch composition"
+    for a, b in zip(l1, l32):
+        assert np.abs(a - b).max() <= 2e-3 * np.abs(a).max()

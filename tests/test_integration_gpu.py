@@ -21,8 +21,9 @@ def _stub_source():
 
 def test_stub_text_exposes_reference_calls():
     src = _stub_source()
-    for fn in ("csm_begin", "csm_prefill", "csm_run_frames", "csm_debug_read"):
+    for fn in ("csm_begin", "csm_prefill", "csm_frame_step"):
         assert fn in src
+    assert "csm_debug_read" not in src          # the result channel is csm_frame_step, not a debug tap
 
 
 def test_integration_stub_runs_verbatim(monkeypatch):
