@@ -78,6 +78,7 @@ def lib():
             "csm_weights_ready": ([P], I),
             "csm_quantize": ([P, I, I], I),
             "csm_begin": ([P, I, P, F, I], I),
+            "csm_set_sampler_filters": ([P, ctypes.c_double, ctypes.c_double, I], I),
             "csm_prefill": ([P, I, I, P, P], I),
             "csm_prefill_batch": ([P, I, P, P, P, P], I),
             "csm_run_frames": ([P, I, ctypes.POINTER(I)], I),

@@ -67,6 +67,9 @@ class FrameCache:
         self.seeds = _seed_list(seeds, batch_size)
         self.L = _lib.lib()
         _lib.check(self.L.csm_begin(model.engine, batch_size, _lib.ptr(self.seeds), sampler.temp, sampler.top_k))
+        if not sampler.greedy and sampler.filtered:
+            _lib.check(self.L.csm_set_sampler_filters(model.engine, sampler.top_p, sampler.min_p,
+                                                      sampler.min_tokens_to_keep))
         model._generation = getattr(model, "_generation", 0) + 1
         self._gen = model._generation
         self.frames = 0
@@ -174,10 +177,9 @@ def generate_frame(model: CSM, tokens, *, temperature: float = 0.8, token_mask=N
         # the sampler is fixed when the cache starts its batch (csm_begin); the reference applies the
         # temperature of every call (generation.py:51-54), so a different one cannot be honoured
         want = _resolve_sampler(temperature, sampler)
-        if (want.temp, want.top_k) != (cache.sampler.temp, cache.sampler.top_k):
-            raise ValueError(f"generate_frame(temperature={want.temp}, top_k={want.top_k}) differs from the "
-                             f"cache's sampler (temperature={cache.sampler.temp}, top_k={cache.sampler.top_k}); "
-                             f"create the cache with make_frame_cache(model, temperature=...)")
+        if want != cache.sampler:
+            raise ValueError(f"generate_frame's sampler {want} differs from the cache's {cache.sampler}; "
+                             f"create the cache with make_frame_cache(model, temperature=..., sampler=...)")
     for b in range(B):
         cache.prefill(b, tokens[b], mask[b])
     if logits_processors:

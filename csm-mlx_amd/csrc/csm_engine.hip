@@ -112,6 +112,10 @@ struct csm_engine {
   int B = 0;
   float temperature = 0.f;
   int top_k = 0;
+  // mlx_lm filter chain beyond top-k (csm_set_sampler_filters; reset by csm_begin)
+  int use_top_p = 0, use_min_p = 0, min_keep = 1;
+  float top_p_cut = 0.f, log_min_p = 0.f;
+  int filters_id = 0, g_filters = -1;  // graphs capture the filter parameters by value
   int frames_run = 0;
   bool need_body = false;
   std::vector<int> prompt_len;
@@ -372,6 +376,7 @@ void enqueue_body(csm_engine* e, hipStream_t st) {
 // one workgroup per CU assumes (every workgroup must be resident: the hand-offs spin).
 bool dec_frame_eligible(csm_engine* e) {
   if (!e->dec_frame || e->B != 1 || e->wdt != WDT_BF16 || e->head_wdt != WDT_BF16) return false;
+  if (e->temperature > 0.f && (e->use_top_p || e->use_min_p)) return false;  // filters: sample_filtered_kernel
   const csm_llama_dims& d = e->dec.d;
   if (d.hidden != 1024 || d.intermediate != 8192 || d.n_heads != 8 || d.n_kv_heads != 2 || d.head_dim != 128 ||
       d.n_layers != DEC_FRAME_LAYERS || e->bb.d.hidden != 2048 || e->V <= 2048 || e->V > 2051 || e->K > 32 ||
@@ -454,6 +459,8 @@ void enqueue_head_phase(csm_engine* e, hipStream_t st, int phase) {
   SampleParams sp{};
   sp.ls = Vp; sp.V = V; sp.temperature = e->temperature; sp.top_k = e->top_k; sp.seeds = e->seeds;
   sp.frame_ctr = e->frame_ctr; sp.K = K; sp.codes = e->codes; sp.part_stride = e->part_stride;
+  sp.use_top_p = e->use_top_p; sp.use_min_p = e->use_min_p; sp.min_keep = e->min_keep;
+  sp.top_p_cut = e->top_p_cut; sp.log_min_p = e->log_min_p;
   sp.forced = phase == 3 ? e->force : nullptr;
   // c0 = codebook0_head(h_last) (generation.py:42); greedy arg-max fused into the GEMV epilogue
   GemvParams g = gp(e);
@@ -1132,6 +1139,10 @@ int csm_begin(csm_engine* e, int B, const uint64_t* seeds, float temperature, in
     e->B = B;
     e->temperature = temperature;
     e->top_k = top_k;
+    e->use_top_p = e->use_min_p = 0;
+    e->min_keep = 1;
+    e->top_p_cut = e->log_min_p = 0.f;
+    ++e->filters_id;
     e->frames_run = 0;
     e->need_body = false;
     e->prompt_len.assign(B, -1);
@@ -1143,6 +1154,24 @@ int csm_begin(csm_engine* e, int B, const uint64_t* seeds, float temperature, in
     HIPCHK(hipMemsetAsync(e->frame_ctr, 0, 16, e->st));
     HIPCHK(hipMemsetAsync(e->codes, 0, (size_t)B * e->K * 4, e->st));
     HIPCHK(hipStreamSynchronize(e->st));
+  }
+  CSM_CATCH
+}
+
+int csm_set_sampler_filters(csm_engine* e, double top_p, double min_p, int min_tokens_to_keep) {
+  CSM_TRY {
+    if (!e) throw CsmError(CSM_ERR_ARG, "null engine");
+    if (e->frames_run > 0 || e->c0_pending) throw CsmError(CSM_ERR_STATE, "set the sampler filters before the first frame");
+    if (!(top_p >= 0.0 && top_p <= 1.0) || !(min_p >= 0.0 && min_p <= 1.0) || min_tokens_to_keep < 1)
+      throw CsmError(CSM_ERR_ARG, "top_p and min_p must lie in [0, 1], min_tokens_to_keep >= 1");
+    // mlx_lm make_sampler: top_p active in (0, 1), min_p when != 0; the cuts are the float32 values
+    // its comparisons use: 1 - top_p and log(min_p) evaluated in double, then rounded
+    e->use_top_p = top_p > 0.0 && top_p < 1.0;
+    e->use_min_p = min_p != 0.0;
+    e->top_p_cut = (float)(1.0 - top_p);
+    e->log_min_p = e->use_min_p ? (float)std::log(min_p) : 0.f;
+    e->min_keep = min_tokens_to_keep;
+    ++e->filters_id;
   }
   CSM_CATCH
 }
@@ -1275,7 +1304,8 @@ int csm_run_frames(csm_engine* e, int nframes, int* all_done) {
       HIPCHK(hipGetLastError());
       nframes = 0;
     }
-    if (use_graph && (e->g_B != e->B || e->g_temp != e->temperature || e->g_topk != e->top_k || !e->g_head)) {
+    if (use_graph && (e->g_B != e->B || e->g_temp != e->temperature || e->g_topk != e->top_k ||
+                      e->g_filters != e->filters_id || !e->g_head)) {
       if (e->g_body) (void)hipGraphExecDestroy(e->g_body);
       if (e->g_head) (void)hipGraphExecDestroy(e->g_head);
       e->g_body = capture(e, enqueue_body);
@@ -1283,6 +1313,7 @@ int csm_run_frames(csm_engine* e, int nframes, int* all_done) {
       e->g_B = e->B;
       e->g_temp = e->temperature;
       e->g_topk = e->top_k;
+      e->g_filters = e->filters_id;
     }
     for (int f = 0; f < nframes; ++f) {
       if (e->need_body) {

@@ -97,10 +97,13 @@ __device__ __forceinline__ float key2f(uint32_t k) {
 __device__ __forceinline__ uint64_t gumbel_key(uint64_t seed, int step) {
   return splitmix64(splitmix64(seed) ^ (uint64_t)step);
 }
-__device__ __forceinline__ double gumbel_perturbed(float logit, float inv_t, uint64_t key, int v) {
+__device__ __forceinline__ double gumbel_noise(uint64_t key, int v) {
   const uint64_t h = splitmix64(key ^ (uint64_t)v);
   const double u = ((double)(h >> 11) + 0.5) * 1.1102230246251565e-16;  // 2^-53
-  return (double)(logit * inv_t) + (-log(-log(u)));
+  return -log(-log(u));
+}
+__device__ __forceinline__ double gumbel_perturbed(float logit, float inv_t, uint64_t key, int v) {
+  return (double)(logit * inv_t) + gumbel_noise(key, v);
 }
 
 __device__ __forceinline__ unsigned long long pack_argmax(float v, int idx) {
@@ -260,6 +263,11 @@ struct SampleParams {
   unsigned long long* part;  // optional: publish the code as partial [b * part_stride]
   int part_stride;
   const int* forced;    // optional [B][K]: teacher forcing -- the code is forced[b][cb], logits untouched
+  // mlx_lm filter chain beyond top-k (sample_filtered_kernel): top_p keeps entries whose ascending
+  // cumulative probability > top_p_cut = float32(1 - top_p); min_p keeps lp >= best + log_min_p
+  // (float32(log(min_p))) and the first min_keep ranks
+  int use_top_p, use_min_p, min_keep;
+  float top_p_cut, log_min_p;
 };
 
 struct AdvanceParams {

@@ -880,11 +880,52 @@ __device__ __forceinline__ int block_argmax(T v, int i, T* sv, int* si) {
 // make_sampler(temp, top_k) semantics with the build's counter-based RNG.  The chosen code's
 // audio embedding (embed_audio, models.py:79-80) is gathered into the next decoder input row.
 constexpr int SAMPLE_NPT = 16;  // logits per thread: V <= 4096 (checked at launch)
+// The top_k-th largest of a 256-thread block's logits (lv[i] = logit tid + 256 i, i < SAMPLE_NPT):
+// radix select of its order-preserving key, 8 bits per pass; the digit is found by a parallel suffix
+// count over the 256 bins (thread t holds digit 255 - t), not a serial scan.  Every logit >= the
+// result is in the top-k set (ties at the k-th value kept).
+__device__ float topk_threshold_256(const float (&lv)[SAMPLE_NPT], int V, int k, uint32_t* hist, uint32_t* wsum,
+                                    uint32_t* sh) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  uint32_t prefix = 0, maskbits = 0, rem = (uint32_t)k;
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    hist[tid] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < SAMPLE_NPT; ++i) {
+      const uint32_t key = f2key(lv[i]);
+      if (tid + 256 * i < V && (key & maskbits) == prefix) atomicAdd(&hist[(key >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    const uint32_t h = hist[255 - tid];
+    uint32_t c = h;  // inclusive prefix over t = count of keys with digit >= 255 - t
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = __shfl_up(c, o, 64);
+      if (lane >= o) c += u;
+    }
+    if (lane == 63) wsum[wave] = c;
+    __syncthreads();
+    for (int w = 0; w < wave; ++w) c += wsum[w];
+    const uint32_t above = c - h;
+    if (h > 0 && above < rem && rem <= c) {  // exactly one digit
+      sh[0] = prefix | ((uint32_t)(255 - tid) << shift);
+      sh[1] = rem - above;
+    }
+    __syncthreads();
+    prefix = sh[0];
+    rem = sh[1];
+    maskbits |= 255u << shift;
+    __syncthreads();  // hist / sh reused by the next pass
+  }
+  return key2f(prefix);
+}
+
 template <typename WT>
 __global__ __launch_bounds__(256) void sample_kernel(SampleParams p) {
   __shared__ uint32_t hist[256];
   __shared__ uint32_t wsum[4];
-  __shared__ uint32_t sh_prefix, sh_remain;
+  __shared__ uint32_t sh[2];
   __shared__ double sdv[4];
   __shared__ float sfv[4];
   __shared__ int si[4];
@@ -920,43 +961,7 @@ __global__ __launch_bounds__(256) void sample_kernel(SampleParams p) {
       const int v = tid + 256 * i;
       lv[i] = v < V ? lg[v] : 0.f;
     }
-    float thr = -INFINITY;
-    if (p.top_k > 0 && p.top_k < V) {
-      // radix select of the top_k-th largest key, 8 bits per pass; the digit is found by a parallel
-      // suffix count over the 256 bins (thread t holds digit 255 - t), not a serial scan
-      uint32_t prefix = 0, maskbits = 0, rem = (uint32_t)p.top_k;
-      const int lane = tid & 63, wave = tid >> 6;
-      for (int shift = 24; shift >= 0; shift -= 8) {
-        hist[tid] = 0;
-        __syncthreads();
-#pragma unroll
-        for (int i = 0; i < SAMPLE_NPT; ++i) {
-          const uint32_t key = f2key(lv[i]);
-          if (tid + 256 * i < V && (key & maskbits) == prefix) atomicAdd(&hist[(key >> shift) & 255u], 1u);
-        }
-        __syncthreads();
-        const uint32_t h = hist[255 - tid];
-        uint32_t c = h;  // inclusive prefix over t = count of keys with digit >= 255 - t
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-          const uint32_t u = __shfl_up(c, o, 64);
-          if (lane >= o) c += u;
-        }
-        if (lane == 63) wsum[wave] = c;
-        __syncthreads();
-        for (int w = 0; w < wave; ++w) c += wsum[w];
-        const uint32_t above = c - h;
-        if (h > 0 && above < rem && rem <= c) {  // exactly one digit
-          sh_prefix = prefix | ((uint32_t)(255 - tid) << shift);
-          sh_remain = rem - above;
-        }
-        __syncthreads();
-        prefix = sh_prefix;
-        rem = sh_remain;
-        maskbits |= 255u << shift;
-      }
-      thr = key2f(prefix);
-    }
+    const float thr = (p.top_k > 0 && p.top_k < V) ? topk_threshold_256(lv, V, p.top_k, hist, wsum, sh) : -INFINITY;
     const uint64_t key = gumbel_key(p.seeds[b], p.frame_ctr[0] * p.K + p.cb);
     const float inv_t = 1.0f / p.temperature;
     double best = -INFINITY;
@@ -979,6 +984,152 @@ __global__ __launch_bounds__(256) void sample_kernel(SampleParams p) {
   if (tid == 0) {
     p.codes[(size_t)b * p.K + p.cb] = code;
     if (p.part) p.part[(size_t)b * p.part_stride] = pack_argmax(0.f, code);  // consumed as a 1-entry partial
+  }
+}
+
+// Sampling with mlx_lm's filter chain beyond top-k (make_sampler(temp, top_p, min_p,
+// min_tokens_to_keep, top_k): apply_top_k -> apply_top_p -> apply_min_p -> categorical), restated in
+// oracle/csm_oracle.py filter_keep on the log-probabilities lp = logits - logsumexp(logits).  One
+// block per utterance: the top-k threshold (radix select), lse (fixed-order block sums), a bitonic
+// sort of (lp desc, index asc) in LDS, the ascending cumulative probability of the kept entries as
+// suffix sums of that order (top_p), the min_p cut against the best kept lp with the first
+// min_keep ranks always kept, then the Gumbel-max of sample_kernel over the survivors.
+constexpr int SORT_N = 256 * SAMPLE_NPT;  // 4096 >= V
+__global__ __launch_bounds__(256) void sample_filtered_kernel(SampleParams p) {
+  __shared__ unsigned long long srt[SORT_N];  // (key(l) << 32) | ~index, sorted descending
+  __shared__ float lgs[SORT_N];               // the row's logits by index
+  __shared__ uint8_t keep[SORT_N];
+  __shared__ uint32_t hist[256];
+  __shared__ uint32_t wsum[4];
+  __shared__ uint32_t sh[2];
+  __shared__ float fred[8];
+  __shared__ double sdv[4];
+  __shared__ int si[4];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const float* lg = p.logits + (size_t)b * p.ls;
+  const int V = p.V;
+  float lv[SAMPLE_NPT];
+#pragma unroll
+  for (int i = 0; i < SAMPLE_NPT; ++i) {
+    const int v = tid + 256 * i;
+    lv[i] = v < V ? lg[v] : -INFINITY;
+    lgs[v] = lv[i];
+    keep[v] = 0;
+  }
+  const float thr = (p.top_k > 0 && p.top_k < V) ? topk_threshold_256(lv, V, p.top_k, hist, wsum, sh) : -INFINITY;
+  // lse = max + log(sum exp(l - max)) over the valid logits (per-thread sums in i order, waves by
+  // DPP reductions, the 4 waves in order)
+  float mx = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < SAMPLE_NPT; ++i) mx = fmaxf(mx, lv[i]);
+  mx = wave_max(mx);
+  if (lane == 0) fred[wave] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(fred[0], fred[1]), fmaxf(fred[2], fred[3]));
+  float se = 0.f;
+#pragma unroll
+  for (int i = 0; i < SAMPLE_NPT; ++i)
+    if (tid + 256 * i < V) se += expf(lv[i] - mx);
+  se = wave_sum(se);
+  __syncthreads();
+  if (lane == 0) fred[4 + wave] = se;
+  __syncthreads();
+  const float lse = mx + logf(((fred[4] + fred[5]) + fred[6]) + fred[7]);
+  // sort entries by (lp desc, index asc), lp = l - lse in fp32 (rounding can tie distinct logits)
+#pragma unroll
+  for (int i = 0; i < SAMPLE_NPT; ++i) {
+    const int v = tid + 256 * i;
+    srt[v] = v < V ? (((unsigned long long)f2key(lv[i] - lse) << 32) | (0xFFFFFFFFu - (uint32_t)v)) : 0ull;
+  }
+  __syncthreads();
+  for (int k = 2; k <= SORT_N; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+#pragma unroll 4
+      for (int t = tid; t < SORT_N / 2; t += 256) {
+        const int i = 2 * t - (t & (j - 1)), ixj = i + j;
+        const unsigned long long a = srt[i], c = srt[ixj];
+        if (((i & k) == 0) ? (a < c) : (a > c)) { srt[i] = c; srt[ixj] = a; }
+      }
+      __syncthreads();
+    }
+  // thread t owns sorted positions 16t .. 16t+15
+  int idx[SAMPLE_NPT];
+  bool kp[SAMPLE_NPT];
+  float lpv[SAMPLE_NPT];
+#pragma unroll
+  for (int r = 0; r < SAMPLE_NPT; ++r) {
+    const unsigned long long e = srt[SAMPLE_NPT * tid + r];
+    idx[r] = (int)(0xFFFFFFFFu - (uint32_t)e);
+    const bool valid = e != 0ull && idx[r] < V;
+    const float l = valid ? lgs[idx[r]] : -INFINITY;
+    lpv[r] = l - lse;
+    kp[r] = valid && l >= thr;
+  }
+  if (p.use_top_p) {
+    // cum_asc at sorted position r = sum of exp(lp) of kept entries at positions >= r
+    float suf[SAMPLE_NPT];
+    float acc = 0.f;
+#pragma unroll
+    for (int r = SAMPLE_NPT - 1; r >= 0; --r) {
+      acc += kp[r] ? expf(lpv[r]) : 0.f;
+      suf[r] = acc;
+    }
+    // exclusive suffix of the thread totals over threads > tid: reverse inclusive scan in each
+    // wave, then the later waves' totals
+    float c = acc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const float u = __shfl_down(c, o, 64);
+      if (lane + o < 64) c += u;
+    }
+    __syncthreads();
+    if (lane == 0) fred[wave] = c;  // wave total
+    __syncthreads();
+    float later = c - acc;          // threads after tid in this wave
+    for (int w2 = 3; w2 > wave; --w2) later += fred[w2];
+#pragma unroll
+    for (int r = 0; r < SAMPLE_NPT; ++r) kp[r] = kp[r] && (suf[r] + later > p.top_p_cut);
+  }
+  if (p.use_min_p) {
+    // the best kept lp (kept entries are a prefix of the sorted order: position 0 if any)
+    __syncthreads();
+    if (tid == 0) fred[0] = kp[0] ? lpv[0] : -INFINITY;
+    __syncthreads();
+    const float tmin = fred[0] + p.log_min_p;
+#pragma unroll
+    for (int r = 0; r < SAMPLE_NPT; ++r) kp[r] = kp[r] && (!(lpv[r] < tmin) || SAMPLE_NPT * tid + r < p.min_keep);
+  }
+#pragma unroll
+  for (int r = 0; r < SAMPLE_NPT; ++r)
+    if (kp[r]) keep[idx[r]] = 1;
+  __syncthreads();
+  const uint64_t key = gumbel_key(p.seeds[b], p.frame_ctr[0] * p.K + p.cb);
+  const float inv_t = 1.0f / p.temperature;
+  double best = -INFINITY;
+  int bi = 0x7fffffff;
+  float bl = -INFINITY;
+  int bli = 0x7fffffff;
+#pragma unroll
+  for (int i = 0; i < SAMPLE_NPT; ++i) {
+    const int v = tid + 256 * i;
+    if (v >= V) continue;
+    if (lv[i] > bl) { bl = lv[i]; bli = v; }  // fallback: the arg-max when nothing survives
+    if (!keep[v]) continue;
+    const double val = gumbel_perturbed(lv[i], inv_t, key, v);
+    if (val > best) {
+      best = val;
+      bi = v;
+    }
+  }
+  int code = block_argmax<double>(best, bi, sdv, si);
+  if (code == 0x7fffffff) {
+    __syncthreads();
+    code = block_argmax<float>(bl, bli, fred, si);
+  }
+  code = min(max(code, 0), V - 1);
+  if (tid == 0) {
+    p.codes[(size_t)b * p.K + p.cb] = code;
+    if (p.part) p.part[(size_t)b * p.part_stride] = pack_argmax(0.f, code);
   }
 }
 
@@ -1358,6 +1509,10 @@ void launch_sample(const SampleParams& p, int wdt, int B, hipStream_t st) {
   if (p.V > 256 * SAMPLE_NPT) {
     fprintf(stderr, "csm: sampler supports V <= %d (got %d)\n", 256 * SAMPLE_NPT, p.V);
     abort();
+  }
+  if (!p.forced && p.temperature > 0.f && (p.use_top_p || p.use_min_p)) {
+    hipLaunchKernelGGL(sample_filtered_kernel, dim3(B), dim3(256), 0, st, p);
+    return;
   }
   if (wdt == WDT_BF16) hipLaunchKernelGGL(sample_kernel<bf16_t>, dim3(B), dim3(256), 0, st, p);
   else hipLaunchKernelGGL(sample_kernel<float>, dim3(B), dim3(256), 0, st, p);

@@ -570,8 +570,16 @@ __device__ __forceinline__ int gather_code(Ctx& c, int V) {
 // the first-max tie rule.  cb: codebook index of the sampler's counter (frame * K + cb).
 __device__ __forceinline__ int sample_code(Ctx& c, int V, int cb) {
   constexpr int NPT = (VMAX + NT - 1) / NT;  // logits per thread
-  gather<NPT>(c, c.buf(G_LOG, VMAX), V, c.L.lg);
   const DecFrameArgs& p = c.p;
+  // the Gumbel noise does not depend on the logits: drawn before the hand-off wait (overlaps it)
+  const uint64_t key = gumbel_key(p.seeds[0], p.frame_ctr[0] * p.K + cb);
+  double gn[NPT];
+#pragma unroll
+  for (int i = 0; i < NPT; ++i) {
+    const int v = c.tid + NT * i;
+    gn[i] = v < V ? gumbel_noise(key, v) : 0.0;
+  }
+  gather<NPT>(c, c.buf(G_LOG, VMAX), V, c.L.lg);
   float thr = -INFINITY;
   if (p.top_k > 0 && p.top_k < V) {
     // radix select, 8 bits per pass; threads 0..255 hold digit 255 - tid for the suffix count
@@ -619,7 +627,6 @@ __device__ __forceinline__ int sample_code(Ctx& c, int V, int cb) {
     }
     thr = key2f(prefix);
   }
-  const uint64_t key = gumbel_key(p.seeds[0], p.frame_ctr[0] * p.K + cb);
   const float inv_t = 1.0f / p.temperature;
   double best = -INFINITY;
   int bi = 0x7fffffff;
@@ -629,7 +636,7 @@ __device__ __forceinline__ int sample_code(Ctx& c, int V, int cb) {
     if (v >= V) continue;
     const float l = c.L.lg[v];
     if (!(l >= thr)) continue;
-    const double val = gumbel_perturbed(l, inv_t, key, v);
+    const double val = (double)(l * inv_t) + gn[i];  // = gumbel_perturbed(l, inv_t, key, v)
     if (val > best) {  // increasing v per thread: first max kept
       best = val;
       bi = v;

@@ -87,6 +87,11 @@ int csm_quantize(csm_engine* e, int group_size, int bits);
 /* Start a batch of B utterances.  temperature 0 = greedy (generation.py:51); top_k 0 = off.
  * seeds[B]: per-utterance sampling seeds (build's counter-based Gumbel sampler). */
 int csm_begin(csm_engine* e, int B, const uint64_t* seeds, float temperature, int top_k);
+/* mlx_lm make_sampler's filters beyond top_k (README.md:49, cli/generate.py:168-174: temp, top_p, min_p,
+ * min_tokens_to_keep, top_k), applied in its order top_k -> top_p -> min_p to the log-probabilities
+ * before the Gumbel-max draw (oracle/csm_oracle.py filter_keep).  top_p in (0, 1) and min_p != 0 are
+ * active; call after csm_begin, before the first frame (csm_begin resets them to off). */
+int csm_set_sampler_filters(csm_engine* e, double top_p, double min_p, int min_tokens_to_keep);
 /* Prompt rows of utterance b: tokens/mask [T][K+1] (text id in the last column). */
 int csm_prefill(csm_engine* e, int b, int T, const int32_t* tokens, const uint8_t* mask);
 /* csm_prefill for several utterances at once (the rows of generate_batch's prompts): utts[i] gets

@@ -225,16 +225,58 @@ def topk_threshold(logits: np.ndarray, k: int) -> float:
     return float(np.sort(logits)[::-1][k - 1])
 
 
-def sample_one(logits: np.ndarray, temperature: float, top_k: int, seed: int, step: int) -> int:
-    """Greedy = first max (mx.argmax); else Gumbel-max of logits*(1/temp) over the top-k set."""
+def filter_keep(logits: np.ndarray, top_k: int, top_p: float, min_p: float, min_keep: int) -> np.ndarray:
+    """The kept set of mlx_lm ``make_sampler``'s filter chain (sample_utils: apply_top_k, then
+    apply_top_p, then apply_min_p, then categorical_sampling), restated on the log-probabilities
+    ``lp = logits - logsumexp(logits)`` that mlx_lm's generate hands its sampler:
+
+      * top_k: keep lp >= the k-th largest (ties at the k-th value kept; mlx argpartition breaks them
+        arbitrarily);
+      * top_p: probs = exp(lp) (0 where masked, not renormalised), cumulative sum in ascending
+        order; keep where it exceeds float32(1 - top_p);
+      * min_p: keep lp >= max(kept lp) + float32(log(min_p)), and always the first min_keep entries
+        of the descending order (if still kept).
+    Order for the sorts: lp descending, equal values by index ascending (ascending = its reverse).
+    Sums are float32 (np.cumsum order); the GPU sums the same values in a parallel order, so a
+    top_p boundary within float32 rounding of 1 - top_p may fall differently (never seen in tests).
+    If every entry is removed the arg-max is kept (mlx would sample from an all -inf row)."""
+    l = logits.astype(F32)
+    n = l.shape[-1]
+    keep = l >= topk_threshold(l, top_k)
+    if (0.0 < top_p < 1.0) or min_p != 0.0:
+        mx_ = l.max()
+        lse = F32(mx_ + F32(np.log(np.sum(np.exp(l - mx_, dtype=F32), dtype=F32))))
+        lp = (l - lse).astype(F32)
+        order = np.lexsort((np.arange(n), -lp.astype(np.float64)))        # lp desc, index asc
+        if 0.0 < top_p < 1.0:
+            p_desc = np.where(keep[order], np.exp(lp[order]), F32(0)).astype(F32)
+            cum_asc = np.cumsum(p_desc[::-1], dtype=F32)[::-1]           # ascending cumsum, back in desc order
+            kp = np.zeros(n, bool)
+            kp[order] = cum_asc > F32(1.0 - top_p)
+            keep &= kp
+        if min_p != 0.0 and keep.any():
+            top = lp[keep].max()
+            tmin = F32(top + F32(math.log(min_p)))
+            rank = np.empty(n, np.int64)
+            rank[order] = np.arange(n)
+            keep &= ~(lp < tmin) | (rank < min_keep)
+    if not keep.any():
+        keep[int(np.argmax(l))] = True
+    return keep
+
+
+def sample_one(logits: np.ndarray, temperature: float, top_k: int, seed: int, step: int,
+               top_p: float = 0.0, min_p: float = 0.0, min_keep: int = 1) -> int:
+    """Greedy = first max (mx.argmax); else Gumbel-max of logits*(1/temp) over the kept set
+    (top-k; with top_p / min_p the mlx_lm filter chain, ``filter_keep``)."""
     logits = logits.astype(F32)
     if temperature == 0:
         return int(np.argmax(logits))
-    thr = topk_threshold(logits, top_k)
+    keep = filter_keep(logits, top_k, top_p, min_p, min_keep)
     scaled = (logits * (F32(1.0) / F32(temperature))).astype(F32).astype(np.float64)
     u = gumbel_u(seed, step, logits.shape[-1])
     g = -np.log(-np.log(u))
-    val = np.where(logits >= thr, scaled + g, -np.inf)
+    val = np.where(keep, scaled + g, -np.inf)
     return int(np.argmax(val))
 
 
@@ -270,7 +312,7 @@ class OracleCSM:
         return np.concatenate([audio, text], axis=-2)
 
     def frame(self, tokens, mask, cache, temperature=0.0, top_k=0, seeds=None, frame_idx=0,
-              processors=None, c0_history=None):
+              processors=None, c0_history=None, top_p=0.0, min_p=0.0, min_keep=1):
         """generation.py:21-92.  tokens/mask (B,T,33).  Returns codes (B,K) int32.
         processors: logits processors on c0 (:44-49), called with (stack(c0_history) or zeros((0,)),
         logits); c0 (B,1) is appended to c0_history when it is a list (:60-61)."""
@@ -288,7 +330,8 @@ class OracleCSM:
         self.debug["c0_logits"] = c0_logits
         self.debug["h_last"] = h_last
         seeds = seeds if seeds is not None else [0] * B
-        c0 = np.array([sample_one(c0_logits[b], temperature, top_k, seeds[b], frame_idx * self.K)
+        flt = dict(top_p=top_p, min_p=min_p, min_keep=min_keep)
+        c0 = np.array([sample_one(c0_logits[b], temperature, top_k, seeds[b], frame_idx * self.K, **flt)
                        for b in range(B)], dtype=np.int64)                        # :51-54
         out = np.zeros((B, self.K), np.int32)
         out[:, 0] = c0
@@ -302,7 +345,7 @@ class OracleCSM:
                              dcache)                                               # :74-77
             logits = np.matmul(z[:, -1, :], self.w["audio_head"][i - 1]).astype(F32)   # :79 (in,out) layout
             ci_logits_all.append(logits)
-            ci = np.array([sample_one(logits[b], temperature, top_k, seeds[b], frame_idx * self.K + i)
+            ci = np.array([sample_one(logits[b], temperature, top_k, seeds[b], frame_idx * self.K + i, **flt)
                            for b in range(B)], dtype=np.int64)
             out[:, i] = ci
             dec_in = self.embed_audio(i, ci)[:, None, :]                          # :87-89
@@ -311,7 +354,7 @@ class OracleCSM:
 
     def generate_codes(self, prompt_tokens: np.ndarray, prompt_mask: np.ndarray, max_frames: int,
                        temperature=0.0, top_k=0, seed=0, max_seq_len=2048, collect_logits=False,
-                       processors=None):
+                       processors=None, top_p=0.0, min_p=0.0, min_keep=1):
         """generation.py:95-178 up to (not including) decode_audio.  prompt (L,33).
 
         Returns (codes (F,K) int32 up to EOS, logits list if requested)."""
@@ -323,7 +366,8 @@ class OracleCSM:
         inp, msk = prompt_tokens[None].astype(np.int64), prompt_mask[None].astype(bool)
         samples, logs, c0_history = [], [], []                                     # :128
         for f in range(max_frames):                                                # :139
-            s = self.frame(inp, msk, cache, temperature, top_k, [seed], f, processors, c0_history)
+            s = self.frame(inp, msk, cache, temperature, top_k, [seed], f, processors, c0_history,
+                           top_p=top_p, min_p=min_p, min_keep=min_keep)
             if collect_logits:
                 logs.append((self.debug["c0_logits"][0].copy(), self.debug["ci_logits"][0].copy()))
             if not s.any():                                                        # :151 EOS

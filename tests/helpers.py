@@ -94,7 +94,7 @@ def write_adapter_dir(path, config, tensors):
     return path
 
 
-def oracle_batch(o, prompts, frames, collect_logits=False, temperature=0.0, top_k=0, seeds=None):
+def oracle_batch(o, prompts, frames, collect_logits=False, temperature=0.0, top_k=0, seeds=None, **flt):
     """Greedy oracle frames for many utterances at once: prompts (tokens, mask) of equal length run as
     one (B, L, 33) batch through OracleCSM.frame (the reference's generate_frame is batch-agnostic,
     generation.py:21-92).  Returns per utterance (codes (F_b, K), [(c0, ci) per frame] or None);
@@ -112,7 +112,7 @@ def oracle_batch(o, prompts, frames, collect_logits=False, temperature=0.0, top_
         cache = o.new_backbone_cache()
         codes, logs = [], []
         for f in range(frames):
-            s = o.frame(toks, msk, cache, temperature, top_k, [seeds[i] for i in idx], f)
+            s = o.frame(toks, msk, cache, temperature, top_k, [seeds[i] for i in idx], f, **flt)
             codes.append(s)
             if collect_logits:
                 logs.append((o.debug["c0_logits"].copy(), o.debug["ci_logits"].copy()))
@@ -122,7 +122,7 @@ def oracle_batch(o, prompts, frames, collect_logits=False, temperature=0.0, top_
         for j, i in enumerate(idx):
             if not codes[j].any(-1).all():                            # EOS inside the window: run alone
                 res = o.generate_codes(prompts[i][0], prompts[i][1], frames, temperature, top_k, seeds[i],
-                                       collect_logits=collect_logits)
+                                       collect_logits=collect_logits, **flt)
                 out[i] = res if collect_logits else (res, None)
             else:
                 out[i] = (codes[j], [(c0[j], ci[j]) for c0, ci in logs] if collect_logits else None)

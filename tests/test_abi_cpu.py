@@ -47,8 +47,32 @@ def test_sampler_descriptor():
     s = make_sampler(0.8, top_k=50)
     assert s.temp == 0.8 and s.top_k == 50 and not s.greedy
     assert make_sampler(0.0).greedy
+    f = make_sampler(0.8, top_p=0.9, min_p=0.05, min_tokens_to_keep=3, top_k=40)
+    assert (f.top_p, f.min_p, f.min_tokens_to_keep, f.top_k) == (0.9, 0.05, 3, 40) and f.filtered
+    assert not make_sampler(0.8, top_p=1.0).filtered                     # mlx_lm: top_p active in (0, 1)
     with pytest.raises(NotImplementedError):
-        make_sampler(0.8, top_p=0.9)
+        make_sampler(0.8, xtc_probability=0.1)
+    with pytest.raises(ValueError):
+        make_sampler(0.8, top_p=1.5)
+
+
+def test_filter_chain_restatement():
+    """oracle filter_keep (mlx_lm apply_top_k -> apply_top_p -> apply_min_p) on hand-worked rows."""
+    from oracle.csm_oracle import filter_keep
+    lp = np.log(np.array([0.5, 0.2, 0.15, 0.1, 0.05], np.float64)).astype(np.float32)
+    # top_p 0.6: ascending cumsum 0.05 .15 .25 .45 1.0 (in value order) > 0.4 keeps {0.5, 0.2}
+    assert filter_keep(lp, 0, 0.6, 0.0, 1).tolist() == [True, True, False, False, False]
+    # top_p 0.75 keeps the 0.15 entry too (its ascending cumsum 0.3 ... > 0.25)
+    assert filter_keep(lp, 0, 0.75, 0.0, 1).tolist() == [True, True, True, False, False]
+    # min_p 0.25: keep p >= 0.125 -> {0.5, 0.2, 0.15}; min_tokens_to_keep 4 adds the 0.1
+    assert filter_keep(lp, 0, 0.0, 0.25, 1).tolist() == [True, True, True, False, False]
+    assert filter_keep(lp, 0, 0.0, 0.25, 4).tolist() == [True, True, True, True, False]
+    # top_k 2 first: probs not renormalised, cumsum 0.2, 0.7 > 1 - 0.5 keeps only the top one
+    assert filter_keep(lp, 2, 0.5, 0.0, 1).tolist() == [True, False, False, False, False]
+    # shift invariance: raw logits (unnormalised) give the same sets
+    assert filter_keep(lp + 3.0, 0, 0.75, 0.25, 1).tolist() == filter_keep(lp, 0, 0.75, 0.25, 1).tolist()
+    # nothing survives (top_k 1 mass 0.5 < 1 - 0.4): the arg-max is kept
+    assert filter_keep(lp, 1, 0.4, 0.0, 1).tolist() == [True, False, False, False, False]
 
 
 def test_param_inventory_counts():
