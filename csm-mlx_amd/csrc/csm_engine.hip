@@ -143,6 +143,9 @@ struct csm_engine {
   // csm_set_option "prefill_rows": row cap of one csm_prefill_batch group (0 = M_cap); lowering it makes
   // small test batches take the multi-group path that config 5's 64 x 248-row contexts take
   int prefill_rows = 0;
+  // csm_set_option "qkv0_tab_batched" 0: batched (matrix-core) frames run layer 0's QKV projection
+  // instead of gathering it from the folded table (A/B and parity checks)
+  bool no_tab_batched = false;
   GemmWs ws;         // split-K slabs + tickets of this engine's MFMA launches (ensure_batch sizes them)
   // persistent frame decoder (dec_frame.hip) for batch-1 greedy bf16 frames: hand-off granules, tag
   // epoch, timeout flag; csm_set_option "dec_frame" / CSM_DEC_FRAME=0 turn it off
@@ -486,7 +489,8 @@ void enqueue_head_phase(csm_engine* e, hipStream_t st, int phase) {
     g0.xtab = e->proj_tab; g0.xtab_f32 = 1; g0.xtab_q4_rows = 0;
     RowMap rm = (i == 1) ? RowMap{2, 0, nullptr, 0} : RowMap{1, 0, nullptr, i};
     const long long* pend = nullptr;  // fused-MLP output of the last decoder layer, read by the head
-    if (gemm_mfma_eligible(Dd, D, M, e->wdt) || gemm_mfma_eligible(e->dec.qkv_rows(), Dd, M, e->wdt)) {
+    const bool use_tab = folded && e->use_qkv0_tab && e->qkv0_built && !e->no_tab_batched;
+    if (!use_tab && (gemm_mfma_eligible(Dd, D, M, e->wdt) || gemm_mfma_eligible(e->dec.qkv_rows(), Dd, M, e->wdt))) {
       // batched: materialise the gathered rows densely, then every projection runs on the matrix cores
       if (!folded) {
         GemvParams gr = g;
@@ -501,7 +505,9 @@ void enqueue_head_phase(csm_engine* e, hipStream_t st, int phase) {
         launch_gather_rows(gr, e->wdt, st);
       }
       pend = run_stack(e, e->dec, e->dx, M, e->dq, e->datt, e->dmlp, rm, st, nullptr);
-    } else if (folded && e->use_qkv0_tab && e->qkv0_built) {
+    } else if (use_tab) {
+      // layer 0's q | k | v and input row gathered from the folded tables by the attention (no layer-0
+      // QKV projection); at >= 8 rows the other projections run on the matrix cores
       AttnParams a0{};
       a0.g_tab = e->qkv0_tab + (size_t)(i - 1) * V * e->dec.qkv_rows(); a0.g_row = e->dec.qkv_rows();
       a0.g_part = g.xpart; a0.g_part_stride = g.xpart_stride; a0.g_part_n = g.xpart_n; a0.g_V = V;
@@ -1738,6 +1744,10 @@ int csm_set_option(csm_engine* e, const char* key, int value) {
     else if (k == "bb_step") {
       if (!e) throw CsmError(CSM_ERR_ARG, "bb_step needs an engine");
       e->bb_step = value != 0;
+    }
+    else if (k == "qkv0_tab_batched") {
+      if (!e) throw CsmError(CSM_ERR_ARG, "qkv0_tab_batched needs an engine");
+      e->no_tab_batched = value == 0;
     }
     else if (k == "prefill_rows") {
       if (!e || value < 0) throw CsmError(CSM_ERR_ARG, "prefill_rows needs an engine and a row count >= 0");

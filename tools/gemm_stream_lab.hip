@@ -24,7 +24,7 @@ constexpr int KC = 64;  // K per stage
 // A fragments: [mtile][kst][part 3][s 4][lane 64] x 16 B;  W fragments: [tile32][kst][s 4][lane 64] x 16 B
 // Block: WAVES waves over one K slice (split evenly), RTW 32-row weight tiles per wave (the same tiles for
 // every wave), MT batch tiles.  Waves' partial sums are added in a fixed order through LDS.
-template <int RTW, int MT, int WAVES>
+template <int RTW, int MT, int WAVES, int PD>
 __global__ __launch_bounds__(64 * WAVES) void gemm_stream(const u32x4_t* __restrict__ W, const u32x4_t* __restrict__ A,
                                                           float* __restrict__ out, int N, int K, int ks) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -50,21 +50,29 @@ __global__ __launch_bounds__(64 * WAVES) void gemm_stream(const u32x4_t* __restr
 #pragma unroll
         for (int s = 0; s < 4; ++s) g.a[t][p][s] = A[((((size_t)t * nks + st) * 3 + p) * 4 + s) * 64 + lane];
   };
-  St g[2];
-  load(ws0, g[0]);
-  for (int j = 0; j < wst; ++j) {
-    if (j + 1 < wst) load(ws0 + j + 1, g[(j + 1) & 1]);
-    const St& c = g[j & 1];
+  // ring of PD stages, loads straight-line (a clamped stage index past the end re-reads the last
+  // stage: no branch around a load, so the compiler's vmcnt counts stay exact)
+  St g[PD];
 #pragma unroll
-    for (int s = 0; s < 4; ++s)
+  for (int d = 0; d < PD; ++d) load(ws0 + min(d, wst - 1), g[d]);
+  asm volatile("" ::: "memory");  // keep the ring's loads where they are issued (no sinking to their use)
+  for (int j0 = 0; j0 < wst; j0 += PD) {
 #pragma unroll
-      for (int p = 0; p < 3; ++p)
+    for (int d = 0; d < PD; ++d) {
+      const St& c = g[d];
 #pragma unroll
-        for (int t = 0; t < MT; ++t)
+      for (int s = 0; s < 4; ++s)
 #pragma unroll
-          for (int i = 0; i < RTW; ++i)
-            acc[t][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, c.a[t][p][s]),
-                                                                 __builtin_bit_cast(bf16x8_t, c.w[i][s]), acc[t][i], 0, 0, 0);
+        for (int p = 0; p < 3; ++p)
+#pragma unroll
+          for (int t = 0; t < MT; ++t)
+#pragma unroll
+            for (int i = 0; i < RTW; ++i)
+              acc[t][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, c.a[t][p][s]),
+                                                                   __builtin_bit_cast(bf16x8_t, c.w[i][s]), acc[t][i], 0, 0, 0);
+      load(ws0 + min(j0 + d + PD, wst - 1), g[d]);
+      asm volatile("" ::: "memory");
+    }
   }
   // fixed-order cross-wave sum through LDS: [wave][t][i][j][lane]
   __shared__ float red[WAVES > 1 ? (WAVES - 1) : 1][MT * RTW * 16][64];
@@ -117,7 +125,7 @@ __global__ void ref_kernel(const unsigned short* W, const unsigned short* A, flo
   out[(size_t)m * N + n] = s;
 }
 
-template <int RTW, int MT, int WAVES>
+template <int RTW, int MT, int WAVES, int PD = 2>
 void run(const char* name, int N, int K, int ks, int nlay) {
   const int M = 32 * MT;
   const size_t wbytes = (size_t)N * K * 2, abytes = (size_t)M * K * 6;
@@ -136,7 +144,7 @@ void run(const char* name, int N, int K, int ks, int nlay) {
   CK(hipMalloc(&ref, (size_t)M * N * 4));
   const dim3 grid(N / (32 * RTW), ks);
   for (int i = 0; i < 3; ++i)
-    hipLaunchKernelGGL((gemm_stream<RTW, MT, WAVES>), grid, dim3(64 * WAVES), 0, 0, (const u32x4_t*)Ws[i % nlay], (const u32x4_t*)A, out, N, K, ks);
+    hipLaunchKernelGGL((gemm_stream<RTW, MT, WAVES, PD>), grid, dim3(64 * WAVES), 0, 0, (const u32x4_t*)Ws[i % nlay], (const u32x4_t*)A, out, N, K, ks);
   CK(hipDeviceSynchronize());
   // check
   hipLaunchKernelGGL(ref_kernel, dim3((N + 255) / 256, M), dim3(256), 0, 0, (const unsigned short*)Ws[2 % nlay], (const unsigned short*)A, ref, N, K, M);
@@ -157,7 +165,7 @@ void run(const char* name, int N, int K, int ks, int nlay) {
   const int iters = 200;
   CK(hipEventRecord(a, 0));
   for (int i = 0; i < iters; ++i)
-    hipLaunchKernelGGL((gemm_stream<RTW, MT, WAVES>), grid, dim3(64 * WAVES), 0, 0, (const u32x4_t*)Ws[i % nlay], (const u32x4_t*)A, out, N, K, ks);
+    hipLaunchKernelGGL((gemm_stream<RTW, MT, WAVES, PD>), grid, dim3(64 * WAVES), 0, 0, (const u32x4_t*)Ws[i % nlay], (const u32x4_t*)A, out, N, K, ks);
   CK(hipEventRecord(b, 0));
   CK(hipEventSynchronize(b));
   float ms;
@@ -172,25 +180,18 @@ void run(const char* name, int N, int K, int ks, int nlay) {
 }
 
 int main() {
-  // decoder shapes, 4 layers' weights rotated (the frame's working set)
-  run<2, 1, 4>("gate_up", 16384, 1024, 1, 4);
-  run<2, 1, 4>("gate_up", 16384, 1024, 2, 4);
-  run<4, 1, 4>("gate_up", 16384, 1024, 2, 4);
-  run<2, 1, 8>("gate_up", 16384, 1024, 1, 4);
-  run<2, 1, 4>("down", 1024, 8192, 16, 4);
-  run<2, 1, 8>("down", 1024, 8192, 16, 4);
-  run<1, 1, 4>("down", 1024, 8192, 8, 4);
-  run<1, 1, 8>("down", 1024, 8192, 8, 4);
-  run<2, 1, 4>("qkv", 1536, 1024, 4, 4);
-  run<1, 1, 4>("qkv", 1536, 1024, 4, 4);
-  run<1, 1, 4>("qkv", 1536, 1024, 2, 4);
-  run<1, 1, 4>("o", 1024, 1024, 4, 4);
-  run<1, 1, 2>("o", 1024, 1024, 8, 4);
-  run<2, 2, 4>("gate_up", 16384, 1024, 1, 4);
-  run<2, 2, 4>("down", 1024, 8192, 16, 4);
-  run<1, 2, 4>("qkv", 1536, 1024, 4, 4);
-  // backbone shapes (16 layers rotated = 1 GB working set: HBM)
-  run<2, 1, 4>("bb_gu", 16384, 2048, 2, 16);
-  run<2, 1, 4>("bb_down", 2048, 8192, 8, 16);
+  // (wst must be a multiple of PD: stages per wave = K / 64 / ks / WAVES)
+  run<2, 1, 4, 1>("gate_up", 16384, 1024, 1, 4);
+  run<2, 1, 4, 2>("gate_up", 16384, 1024, 1, 4);
+  run<2, 1, 4, 4>("gate_up", 16384, 1024, 1, 4);
+  run<2, 1, 2, 4>("gate_up", 16384, 1024, 1, 4);
+  run<2, 1, 2, 8>("gate_up", 16384, 1024, 1, 4);
+  run<2, 1, 1, 8>("gate_up", 16384, 1024, 1, 4);
+  run<4, 1, 4, 2>("gate_up", 16384, 1024, 2, 4);
+  run<2, 1, 4, 2>("down", 1024, 8192, 16, 4);
+  run<2, 1, 2, 4>("down", 1024, 8192, 16, 4);
+  run<2, 1, 1, 8>("down", 1024, 8192, 16, 4);
+  run<1, 1, 4, 1>("qkv", 1536, 1024, 4, 4);
+  run<1, 1, 2, 1>("o", 1024, 1024, 8, 4);
   return 0;
 }
