@@ -280,6 +280,9 @@ def main():
     ap.add_argument("--config", type=int, default=0, choices=[0, 2, 3, 4, 5, 6, 7],
                     help="run BASELINE.json configs[N-1] (batch, dtype, sampling, streaming, context) instead of "
                          "the default configs[1] line; the metric stays audio frames/s")
+    ap.add_argument("--phases", action="store_true",
+                    help="add phases_s_per_step: wall seconds of Mimi encode / prefill / frames / Mimi decode per "
+                         "step (the engine is synchronized at each boundary)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (RCCL over xGMI) for real runs; gloo rehearses N ranks on fewer GPUs")
     ap.add_argument("--model", default="csm_1b", choices=["csm_1b", "tiny"],
@@ -365,9 +368,14 @@ def main():
         prompts = [tokenize_text_segment(ids_of(g), 0, K) for g in mine]
     last = {}
 
+    phases = {} if args.phases else None
+
     def step():
         # config 5: the context Segments' Mimi encode is part of every step (generation.py:108-125)
+        t_enc = time.perf_counter()
         pr = context_prompts(mine) if cfg["context"] else prompts
+        if phases is not None and cfg["context"]:
+            phases["mimi_encode"] = phases.get("mimi_encode", 0.0) + time.perf_counter() - t_enc
         if cfg["stream"]:
             from csm_mlx.generation import stream_generate_batch
             n = 0
@@ -381,7 +389,7 @@ def main():
             pcm_l = [np.concatenate(c) if c else np.zeros((0,), np.float32) for c in chunks]
         else:
             out = generate_batch(model, pr, ms, temperature=cfg["temperature"], top_k=cfg["top_k"], seeds=seeds,
-                                 decode=decode, with_codes=decode)
+                                 decode=decode, with_codes=decode, timings=phases)
             codes, pcm_l = out if decode else (out, None)
             n = sum(len(c) for c in codes)
         if world > 1:   # result collection: one all-gather per kind (RCCL over xGMI / gloo)
@@ -391,6 +399,8 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    if phases is not None:
+        phases.clear()
     barrier_sync()
     t0 = time.perf_counter()
     frames = 0
@@ -442,6 +452,8 @@ def main():
             "roofline_backbone": roof["backbone_gate_up"],
             "roofline_frame": roof_frame,
         }
+        if phases is not None:  # per-phase wall seconds of one step (synchronized boundaries: lab option)
+            line["phases_s_per_step"] = {k: round(v / args.steps, 4) for k, v in phases.items()}
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.cpu_frames)
         print(json.dumps(line), flush=True)

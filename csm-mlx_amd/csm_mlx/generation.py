@@ -212,19 +212,36 @@ def _check_window(model: CSM, L: int, max_audio_frames: int):
         raise ValueError(f"Inputs too long ({L}), must be below max_seq_len - max_audio_frames: {max_seq_len}")
 
 
+def _mark(timings: Optional[dict], key: str, t0: float, model: Optional[CSM] = None) -> float:
+    """Phase timer (bench.py --phases): wait for the engine, add the elapsed wall time to timings[key]."""
+    import time
+    if timings is None:
+        return t0
+    if model is not None:
+        _lib.check(_lib.lib().csm_synchronize(model.engine))
+    t = time.perf_counter()
+    timings[key] = timings.get(key, 0.0) + (t - t0)
+    return t
+
+
 def generate_codes_batch(model: CSM, prompts: Sequence[Tuple[np.ndarray, np.ndarray]], max_audio_frames: int, *,
                          sampler: Sampler, seeds=None, chunk: int = 16,
-                         logits_processors: Optional[List[Callable]] = None):
+                         logits_processors: Optional[List[Callable]] = None, timings: Optional[dict] = None):
     """Run the frame loop for B prompts.  Returns (hist [F,B,K], n_frames [B], cache).  With
-    ``logits_processors`` every frame pauses after codebook0_head for them (generation.py:44-49)."""
+    ``logits_processors`` every frame pauses after codebook0_head for them (generation.py:44-49).
+    ``timings`` (optional dict): wall seconds of the prompt prefill and of the frames are added to
+    its "prefill" / "frames" entries (the engine is synchronized at each boundary)."""
+    import time
     B = len(prompts)
     for t, _ in prompts:
         _check_window(model, t.shape[0], max_audio_frames)
+    t0 = time.perf_counter()
     cache = FrameCache(model, B, sampler, seeds)
     if B > 1:   # every prompt's rows through one pass of each projection (weights streamed once)
         cache.prefill_batch([(b, t, m) for b, (t, m) in enumerate(prompts)])
     else:
         cache.prefill(0, *prompts[0])
+    t0 = _mark(timings, "prefill", t0, model)
     left = max_audio_frames
     if logits_processors:
         c0_history: list = []                                                    # generation.py:128
@@ -239,6 +256,7 @@ def generate_codes_batch(model: CSM, prompts: Sequence[Tuple[np.ndarray, np.ndar
         if all_done:
             break
     hist, n_frames, _ = cache.codes()
+    _mark(timings, "frames", t0, model)
     return hist, n_frames, cache
 
 
@@ -278,15 +296,20 @@ def generate(model: CSM, text, speaker: int, context: List[Segment], max_audio_l
 
 def generate_batch(model: CSM, prompts: Sequence[Tuple[np.ndarray, np.ndarray]], max_audio_length_ms: float = 10_000,
                    *, temperature: float = 0.0, top_k: int = 0, sampler=None, seeds=None, decode: bool = True,
-                   with_codes: bool = False):
+                   with_codes: bool = False, timings: Optional[dict] = None):
     """Batched extension: B prompts (tokens, mask) -> list of waveforms (or codes if decode=False;
-    (codes, waveforms) with ``with_codes``)."""
+    (codes, waveforms) with ``with_codes``).  ``timings``: per-phase wall seconds (prefill, frames,
+    decode) added to the dict."""
+    import time
     smp = _resolve_sampler(temperature, sampler, top_k)
-    hist, n_frames, _ = generate_codes_batch(model, prompts, int(max_audio_length_ms / 80), sampler=smp, seeds=seeds)
+    hist, n_frames, _ = generate_codes_batch(model, prompts, int(max_audio_length_ms / 80), sampler=smp, seeds=seeds,
+                                             timings=timings)
     codes = [hist[: n_frames[b], b] for b in range(len(prompts))]
     if not decode:
         return codes
+    t0 = time.perf_counter()
     pcm = _decode_batch(model, hist, n_frames)
+    _mark(timings, "decode", t0)
     return (codes, pcm) if with_codes else pcm
 
 

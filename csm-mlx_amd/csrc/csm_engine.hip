@@ -25,6 +25,7 @@
 #include "../../include/csm_hip_prof.h"
 #include "csm_kernels.h"
 #include "engine_util.h"
+#include "xs.h"
 
 namespace {
 
@@ -146,6 +147,13 @@ struct csm_engine {
   // csm_set_option "qkv0_tab_batched" 0: batched (matrix-core) frames run layer 0's QKV projection
   // instead of gathering it from the folded table (A/B and parity checks)
   bool no_tab_batched = false;
+  // batched depth decoder (8..64 utterances, bf16, codebook steps >= 2) on the streaming matrix-core
+  // GEMM over pre-split activations (gemm_xs.hip): split rows x * norm [64][Dd], attention output,
+  // SiLU*up rows [64][F] (xs.h layout), per-row partial sums of squares [64 tiles][64 rows].
+  // csm_set_option "gemm_xs" / CSM_GEMM_XS=0 turn it off.
+  bool xs_on = [] { const char* v = getenv("CSM_GEMM_XS"); return v && v[0] == '1'; }();  // default off until measured
+  void *xs_D = nullptr, *xs_A = nullptr, *xs_F = nullptr;
+  float* xs_ss = nullptr;
   GemmWs ws;         // split-K slabs + tickets of this engine's MFMA launches (ensure_batch sizes them)
   // persistent frame decoder (dec_frame.hip) for batch-1 greedy bf16 frames: hand-off granules, tag
   // epoch, timeout flag; csm_set_option "dec_frame" / CSM_DEC_FRAME=0 turn it off
@@ -315,6 +323,121 @@ long long* run_stack(csm_engine* e, Stack& s, float* x, int M, float* q, float* 
   return fused ? s.acc[(d.n_layers - 1) & 1] : nullptr;
 }
 
+// The batched depth decoder at codebook steps >= 2 (generation.py:72-89 at batch M) on the streaming
+// matrix-core GEMM (gemm_xs.hip): layer 0's q | k | v and input row come from the folded tables (attn0),
+// and every projection's epilogue writes the split activations of the next one (xs.h) -- o_proj:
+// the new residual x * n2 (+ per-row sums of squares), gate/up: SiLU*up, down: the new residual x *
+// (next layer's n1, or the final norm for the head) -- so no launch re-normalises or re-splits rows.
+bool dec_xs_eligible(csm_engine* e, int M) {
+  const Stack& s = e->dec;
+  const int Dd = s.d.hidden, F = s.d.intermediate;
+  return e->xs_on && e->xs_D && M >= GEMM_MFMA_MIN_M && M <= GEMM_XS_MAX_M && e->wdt == WDT_BF16 &&
+         e->head_wdt == WDT_BF16 && !e->fuse_mlp && s.d.head_dim == 128 && s.S_cap <= 32 &&
+         gemm_xs_eligible(s.qkv_rows(), Dd, M, e->wdt) && gemm_xs_eligible(Dd, s.q_dim(), M, e->wdt) &&
+         gemm_xs_eligible(2 * F, Dd, M, e->wdt) && gemm_xs_eligible(Dd, F, M, e->wdt) &&
+         gemm_xs_eligible(e->Vpad, Dd, M, e->head_wdt) && gemm_xs_tiles(Dd, F, M) <= 64 &&
+         gemm_xs_tiles(Dd, s.q_dim(), M) <= 64;
+}
+
+void run_dec_xs(csm_engine* e, int M, const RowMap& rm, hipStream_t st, const AttnParams& attn0) {
+  Stack& s = e->dec;
+  const csm_llama_dims& d = s.d;
+  const int D = d.hidden, F = d.intermediate;
+  const int ss_o = gemm_xs_tiles(D, s.q_dim(), M), ss_d = gemm_xs_tiles(D, F, M);
+  for (int i = 0; i < d.n_layers; ++i) {
+    LayerW& l = s.L[i];
+    if (i > 0) {  // norm1 + QKV + RoPE + KV append from the split rows the previous down wrote
+      GemvParams g = gp(e);
+      g.W = l.wqkv; g.N = s.qkv_rows(); g.K = D; g.M = M; g.nw = l.n1; g.eps = d.eps;
+      g.out = e->dq; g.os = s.q_dim(); g.Hq = d.n_heads; g.Hkv = d.n_kv_heads; g.hd = d.head_dim;
+      g.S_cap = s.S_cap; g.rope = s.rope; g.kc = l.kc; g.vc = l.vc; g.rm = rm;
+      g.xs_in = e->xs_D; g.ss_in = e->xs_ss; g.ss_n = ss_d; g.ss_stride = GEMM_XS_MAX_M;
+      launch_gemm_xs(g, EPI_QKV, st);
+    }
+    AttnParams a = i == 0 ? attn0 : AttnParams{};
+    a.q = e->dq; a.qs = s.q_dim(); a.M = M; a.kc = l.kc; a.vc = l.vc; a.Hq = d.n_heads; a.Hkv = d.n_kv_heads;
+    a.S_cap = s.S_cap; a.scale = 1.0f / sqrtf((float)d.head_dim); a.mode = ATTN_CAUSAL; a.window = 0; a.rm = rm;
+    a.out = e->datt; a.os = s.q_dim(); a.xs_out = e->xs_A; a.xs_K = s.q_dim();
+    launch_attn(a, d.head_dim, st);
+    {  // o_proj + residual -> x; split (x * n2) + sums of squares for gate/up
+      GemvParams g = gp(e);
+      g.W = l.wo; g.N = D; g.K = s.q_dim(); g.M = M; g.out = e->dx; g.os = D; g.xs_in = e->xs_A;
+      g.xs_out = e->xs_D; g.xs_nw = l.n2; g.ss_out = e->xs_ss; g.ss_stride = GEMM_XS_MAX_M; g.xs_K = D;
+      launch_gemm_xs(g, EPI_ADD, st);
+    }
+    {  // norm2 + gate/up + SiLU*up -> split h
+      GemvParams g = gp(e);
+      g.W = l.wgu; g.N = 2 * F; g.K = D; g.M = M; g.nw = l.n2; g.eps = d.eps; g.out = nullptr; g.os = F;
+      g.xs_in = e->xs_D; g.ss_in = e->xs_ss; g.ss_n = ss_o; g.ss_stride = GEMM_XS_MAX_M;
+      g.xs_out = e->xs_F; g.xs_K = F;
+      launch_gemm_xs(g, EPI_SILU_MUL, st);
+    }
+    {  // down + residual -> x; split (x * next norm) + sums of squares
+      GemvParams g = gp(e);
+      g.W = l.wd; g.N = D; g.K = F; g.M = M; g.out = e->dx; g.os = D; g.xs_in = e->xs_F;
+      g.xs_out = e->xs_D; g.xs_nw = i + 1 < d.n_layers ? s.L[i + 1].n1 : s.norm; g.ss_out = e->xs_ss;
+      g.ss_stride = GEMM_XS_MAX_M; g.xs_K = D;
+      launch_gemm_xs(g, EPI_ADD, st);
+    }
+  }
+}
+
+// The batched backbone step (generation.py:39 at batch M, one decode row per utterance) on the same
+// streaming path: the embedding gather writes split rows (x * n1[0]) + per-512-column sums of squares,
+// then every projection's epilogue (and the attention) writes the next projection's operand.
+bool bb_xs_eligible(csm_engine* e, int M) {
+  const Stack& s = e->bb;
+  const int D = s.d.hidden, F = s.d.intermediate;
+  return e->xs_on && e->xs_D && M >= GEMM_MFMA_MIN_M && M <= GEMM_XS_MAX_M && e->wdt == WDT_BF16 &&
+         !e->fuse_mlp && D % 512 == 0 && D / 512 <= 64 && gemm_xs_eligible(s.qkv_rows(), D, M, e->wdt) &&
+         gemm_xs_eligible(D, s.q_dim(), M, e->wdt) && gemm_xs_eligible(2 * F, D, M, e->wdt) &&
+         gemm_xs_eligible(D, F, M, e->wdt) && gemm_xs_tiles(D, F, M) <= 64 && gemm_xs_tiles(D, s.q_dim(), M) <= 64;
+}
+
+void run_bb_xs(csm_engine* e, int M, const RowMap& rm, hipStream_t st) {
+  Stack& s = e->bb;
+  const csm_llama_dims& d = s.d;
+  const int D = d.hidden, F = d.intermediate;
+  const int ss_o = gemm_xs_tiles(D, s.q_dim(), M), ss_d = gemm_xs_tiles(D, F, M);
+  for (int i = 0; i < d.n_layers; ++i) {
+    LayerW& l = s.L[i];
+    {  // norm1 + QKV + RoPE + KV append
+      GemvParams g = gp(e);
+      g.W = l.wqkv; g.N = s.qkv_rows(); g.K = D; g.M = M; g.nw = l.n1; g.eps = d.eps;
+      g.out = e->q; g.os = s.q_dim(); g.Hq = d.n_heads; g.Hkv = d.n_kv_heads; g.hd = d.head_dim;
+      g.S_cap = s.S_cap; g.rope = s.rope; g.kc = l.kc; g.vc = l.vc; g.rm = rm;
+      g.xs_in = e->xs_D; g.ss_in = e->xs_ss; g.ss_n = i == 0 ? D / 512 : ss_d; g.ss_stride = GEMM_XS_MAX_M;
+      launch_gemm_xs(g, EPI_QKV, st, gemv_nt(0));
+    }
+    AttnParams a{};
+    a.q = e->q; a.qs = s.q_dim(); a.M = M; a.kc = l.kc; a.vc = l.vc; a.Hq = d.n_heads; a.Hkv = d.n_kv_heads;
+    a.S_cap = s.S_cap; a.scale = 1.0f / sqrtf((float)d.head_dim); a.mode = ATTN_CAUSAL; a.window = 0; a.rm = rm;
+    a.out = e->att; a.os = s.q_dim(); a.xs_out = e->xs_A; a.xs_K = s.q_dim();
+    launch_attn(a, d.head_dim, st);
+    {  // o_proj + residual
+      GemvParams g = gp(e);
+      g.W = l.wo; g.N = D; g.K = s.q_dim(); g.M = M; g.out = e->x; g.os = D; g.xs_in = e->xs_A;
+      g.xs_out = e->xs_D; g.xs_nw = l.n2; g.ss_out = e->xs_ss; g.ss_stride = GEMM_XS_MAX_M; g.xs_K = D;
+      launch_gemm_xs(g, EPI_ADD, st, gemv_nt(0));
+    }
+    {  // norm2 + gate/up + SiLU*up
+      GemvParams g = gp(e);
+      g.W = l.wgu; g.N = 2 * F; g.K = D; g.M = M; g.nw = l.n2; g.eps = d.eps; g.out = nullptr; g.os = F;
+      g.xs_in = e->xs_D; g.ss_in = e->xs_ss; g.ss_n = ss_o; g.ss_stride = GEMM_XS_MAX_M;
+      g.xs_out = e->xs_F; g.xs_K = F;
+      launch_gemm_xs(g, EPI_SILU_MUL, st, gemv_nt(0));
+    }
+    {  // down + residual (the last layer's rows go to the final norm in fp32 only)
+      GemvParams g = gp(e);
+      g.W = l.wd; g.N = D; g.K = F; g.M = M; g.out = e->x; g.os = D; g.xs_in = e->xs_F;
+      if (i + 1 < d.n_layers) {
+        g.xs_out = e->xs_D; g.xs_nw = s.L[i + 1].n1; g.ss_out = e->xs_ss; g.ss_stride = GEMM_XS_MAX_M; g.xs_K = D;
+      }
+      launch_gemm_xs(g, EPI_ADD, st, gemv_nt(0));
+    }
+  }
+}
+
 void embed(csm_engine* e, const EmbedParams& ep, int M, hipStream_t st) {
   if (e->wdt == WDT_Q4) launch_embed_q4(ep, e->dims.n_text_vocab, M, st);
   else launch_embed(ep, e->wdt, M, st);
@@ -363,12 +486,21 @@ void enqueue_body(csm_engine* e, hipStream_t st) {
   EmbedParams ep{};
   ep.codes = e->codes; ep.text_emb = e->text_emb; ep.audio_emb = e->audio_emb; ep.V = e->V; ep.K = e->K;
   ep.D = e->D; ep.out = e->x; ep.pos_inc = e->pos;
+  const bool bb_xs = !bb_step_eligible(e) && bb_xs_eligible(e, B);
+  if (bb_xs) {
+    ep.xs_out = e->xs_D; ep.xs_nw = e->bb.L[0].n1; ep.ss_out = e->xs_ss; ep.ss_stride = GEMM_XS_MAX_M;
+  }
   embed(e, ep, B, st);
   if (bb_step_eligible(e)) {
     enqueue_bb_step(e, st);
     return;
   }
   RowMap rm{1, 0, e->pos, 0};
+  if (bb_xs) {
+    run_bb_xs(e, B, rm, st);
+    launch_rmsnorm_rows(e->x, e->D, e->bb.norm, e->bb.d.eps, e->D, e->h_last, e->D, B, st, nullptr, 0);
+    return;
+  }
   const long long* pend = run_stack(e, e->bb, e->x, B, e->q, e->att, e->mlp, rm, st);
   launch_rmsnorm_rows(e->x, e->D, e->bb.norm, e->bb.d.eps, e->D, e->h_last, e->D, B, st, pend, e->acc_rows * e->D);
 }
@@ -490,6 +622,7 @@ void enqueue_head_phase(csm_engine* e, hipStream_t st, int phase) {
     RowMap rm = (i == 1) ? RowMap{2, 0, nullptr, 0} : RowMap{1, 0, nullptr, i};
     const long long* pend = nullptr;  // fused-MLP output of the last decoder layer, read by the head
     const bool use_tab = folded && e->use_qkv0_tab && e->qkv0_built && !e->no_tab_batched;
+    const bool xs_dec = use_tab && dec_xs_eligible(e, M);  // streaming matrix-core decoder + head
     if (!use_tab && (gemm_mfma_eligible(Dd, D, M, e->wdt) || gemm_mfma_eligible(e->dec.qkv_rows(), Dd, M, e->wdt))) {
       // batched: materialise the gathered rows densely, then every projection runs on the matrix cores
       if (!folded) {
@@ -513,7 +646,8 @@ void enqueue_head_phase(csm_engine* e, hipStream_t st, int phase) {
       a0.g_part = g.xpart; a0.g_part_stride = g.xpart_stride; a0.g_part_n = g.xpart_n; a0.g_V = V;
       a0.g_codes = e->codes; a0.g_codes_K = K; a0.g_cb = i - 1;
       a0.g_xtab = e->proj_tab + (size_t)(i - 1) * V * Dd; a0.g_xout = e->dx; a0.g_D = Dd;
-      pend = run_stack(e, e->dec, e->dx, M, e->dq, e->datt, e->dmlp, rm, st, nullptr, &a0);
+      if (xs_dec) run_dec_xs(e, M, rm, st, a0);
+      else pend = run_stack(e, e->dec, e->dx, M, e->dq, e->datt, e->dmlp, rm, st, nullptr, &a0);
     } else {
       if (!folded) launch_gemv(g, e->wdt, EPI_STORE, 0, st);
       pend = run_stack(e, e->dec, e->dx, M, e->dq, e->datt, e->dmlp, rm, st, folded ? &g0 : nullptr);
@@ -528,7 +662,13 @@ void enqueue_head_phase(csm_engine* e, hipStream_t st, int phase) {
       g.xacc = pend + (i == 1 ? Dd : 0);
       g.acc_ss = e->acc_rows * Dd;
     }
-    if (!(ablate() & 64)) launch_gemv(g, e->head_wdt, greedy ? EPI_ARGMAX : EPI_STORE, 1, st);
+    if (xs_dec) {  // the head reads the split rows (x * final norm) the last down wrote
+      g.xs_in = e->xs_D; g.ss_in = e->xs_ss; g.ss_n = gemm_xs_tiles(Dd, e->dec.d.intermediate, M);
+      g.ss_stride = GEMM_XS_MAX_M;
+      launch_gemm_xs(g, greedy ? EPI_ARGMAX : EPI_STORE, st);
+    } else if (!(ablate() & 64)) {
+      launch_gemv(g, e->head_wdt, greedy ? EPI_ARGMAX : EPI_STORE, 1, st);
+    }
     if (!greedy) {
       sp.logits = e->ci_logits + (size_t)(i - 1) * B * Vp; sp.cb = i; sp.part = part(i);
       launch_sample(sp, e->wdt, B, st);
@@ -608,6 +748,27 @@ void ensure_batch(csm_engine* e, int B) {
   gemm_reserve(e->ws, (int)Dd, (int)D, 2 * (int)Bm);
   gemm_reserve(e->ws, (int)Vp, (int)D, (int)Bm);   // c0 head
   gemm_reserve(e->ws, (int)Vp, (int)Dd, (int)Bm);  // ci heads
+  // the streaming decoder path (gemm_xs): split-row buffers for up to GEMM_XS_MAX_M rows + its scratch
+  {
+    // (shared by the backbone and the decoder: their launches never overlap)
+    const int xm = GEMM_XS_MAX_M, rows = std::min((int)Bm, xm);
+    size_t bD = 0, bA = 0, bF = 0;
+    for (Stack* s : {&e->bb, &e->dec}) {
+      const int Dm = s->d.hidden, F = s->d.intermediate;
+      bD = std::max(bD, xs::bytes(xm, Dm));
+      bA = std::max(bA, xs::bytes(xm, s->q_dim()));
+      bF = std::max(bF, xs::bytes(xm, F));
+      gemm_xs_reserve(e->ws, s->qkv_rows(), Dm, rows);
+      gemm_xs_reserve(e->ws, Dm, s->q_dim(), rows);
+      gemm_xs_reserve(e->ws, 2 * F, Dm, rows);
+      gemm_xs_reserve(e->ws, Dm, F, rows);
+    }
+    gemm_xs_reserve(e->ws, (int)Vp, (int)Dd, rows);
+    e->xs_D = e->balloc(bD);
+    e->xs_A = e->balloc(bA);
+    e->xs_F = e->balloc(bF);
+    e->xs_ss = (float*)e->balloc((size_t)64 * xm * 4);
+  }
 }
 
 // Fragment-tiled copies (launch_gemm_retile) of every matrix the batched MFMA path reads -- stack
@@ -1744,6 +1905,10 @@ int csm_set_option(csm_engine* e, const char* key, int value) {
     else if (k == "bb_step") {
       if (!e) throw CsmError(CSM_ERR_ARG, "bb_step needs an engine");
       e->bb_step = value != 0;
+    }
+    else if (k == "gemm_xs") {
+      if (!e) throw CsmError(CSM_ERR_ARG, "gemm_xs needs an engine");
+      e->xs_on = value != 0;
     }
     else if (k == "qkv0_tab_batched") {
       if (!e) throw CsmError(CSM_ERR_ARG, "qkv0_tab_batched needs an engine");

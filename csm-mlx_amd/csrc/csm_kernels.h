@@ -81,6 +81,20 @@ struct GemvParams {
   int ksplit;
   int no_mfma;           // keep the GEMV's per-row arithmetic at any M (folded-table builds)
   int row_chunk;         // gemv_xl_kernel: blockIdx.y takes rows [y*row_chunk, +row_chunk) (table builds)
+  // Streaming matrix-core path (gemm_xs.hip; the batched depth decoder): the A operand arrives
+  // pre-split (xs.h) instead of as fp32 rows x.  With nw set, the RMSNorm scale of row m is
+  // rsqrt(sum_t ss_in[t * ss_stride + m] / K + eps) (ss_n producer partials, summed in order).
+  const void* xs_in;
+  const float* ss_in;
+  int ss_n, ss_stride;
+  // Producer side (gemm_xs epilogue, attention, row gathers): the rows this launch produces (EPI_ADD:
+  // the new residual, EPI_STORE: the stored rows, EPI_SILU_MUL: silu(gate) * up) are also written
+  // split into xs_out (xs_K columns, times xs_nw -- the consuming projection's RMSNorm weight -- when
+  // set), with per-row partial sums of squares of the un-normed values in ss_out[tile * ss_stride + m].
+  void* xs_out;
+  const float* xs_nw;
+  float* ss_out;
+  int xs_K;
 };
 
 // order-preserving float <-> uint32 keys (radix select of the top-k threshold)
@@ -222,6 +236,12 @@ struct EmbedParams {
   int V, K, D;
   float* out;            // [M][D]
   int* pos_inc;          // decode mode: pos[m] += 1 (position of the new backbone row)
+  // streaming backbone (gemm_xs): rows also written split (x * xs_nw, xs.h, K = D) with per-row sums of
+  // squares per 512-column block in ss_out[blockIdx.y * ss_stride + m]
+  void* xs_out;
+  const float* xs_nw;
+  float* ss_out;
+  int ss_stride;
 };
 
 struct AttnParams {
@@ -249,6 +269,9 @@ struct AttnParams {
   const float* g_xtab;
   float* g_xout;
   int g_D;
+  // streaming matrix-core path: the attention output also written split (xs.h) for the o_proj GEMM
+  void* xs_out;
+  int xs_K;
 };
 
 struct SampleParams {
@@ -347,6 +370,12 @@ int gemm_tiles(int N, int K, int M, int wdt);  // row-tile blocks of an MFMA lau
 void launch_gemm_mfma(const GemvParams& p, int wdt, bool nt, hipStream_t st);
 // pre-size ws for (N, K) at any row count <= M (outside graph capture); true if it reallocated
 bool gemm_reserve(GemmWs& ws, int N, int K, int M);
+// Streaming matrix-core GEMM over pre-split activations (gemm_xs.hip): bf16 weights, <= 64 rows
+constexpr int GEMM_XS_MAX_M = 64;
+bool gemm_xs_eligible(int N, int K, int M, int wdt);
+int gemm_xs_tiles(int N, int K, int M);       // column tiles of a launch (ss / arg-max partials per row)
+void launch_gemm_xs(const GemvParams& p, int epi, hipStream_t st, bool nt = false);
+bool gemm_xs_reserve(GemmWs& ws, int N, int K, int M);
 // Fragment-tiled weight copy for the MFMA path: per 32-row tile and 64-K stage, the bytes each lane
 // of a wave loads for v_mfma_f32_32x32x16_bf16's B operand, contiguous (bf16: 4 KB = 4 steps x 64
 // lanes x 16 B; int4: 1 KB of nibbles, then a [tile][stage][32] block of scale|bias words); rows

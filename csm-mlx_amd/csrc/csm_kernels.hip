@@ -14,6 +14,7 @@
 // round trip); x rows are tiny and served from L1/L2.
 #include "csm_kernels.h"
 #include "engine_util.h"
+#include "xs.h"
 
 #include <cstdlib>
 
@@ -70,6 +71,20 @@ __global__ __launch_bounds__(64) void embed_rows_kernel(EmbedParams p) {
   float* out = p.out + (size_t)m * p.D;
   *reinterpret_cast<float4*>(out + d0) = make_float4(acc[0], acc[1], acc[2], acc[3]);
   *reinterpret_cast<float4*>(out + d0 + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
+  if (p.xs_out) {  // the streaming backbone QKV's operand: split (x * n1), + this block's sum of squares
+    float s = 0.f;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s = fmaf(acc[e], acc[e], s);
+    s = wave_sum(s);
+    if (t == 0) p.ss_out[(size_t)blockIdx.y * p.ss_stride + m] = s;
+#pragma unroll
+    for (int hf = 0; hf < 2; ++hf) {
+      float v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = acc[4 * hf + u] * p.xs_nw[d0 + 4 * hf + u];
+      xs::store4(p.xs_out, p.D, m, d0 + 4 * hf, v);
+    }
+  }
 }
 
 // ============================================================================ GEMV
@@ -592,6 +607,7 @@ __device__ __forceinline__ void attn_block(const AttnParams& p, int m, int kvh, 
 #pragma unroll
   for (int i = 0; i < NO; ++i) {
     out[lane + 64 * i] = o[i] * inv;
+    if (p.xs_out) xs::store1(p.xs_out, p.xs_K, m, h * HD + lane + 64 * i, o[i] * inv);  // streaming o_proj
   }
 }
 
@@ -715,6 +731,9 @@ __global__ __launch_bounds__(64) void attn_short_kernel(AttnParams p) {
   float* out = p.out + (size_t)m * p.os + h * HD;
 #pragma unroll
   for (int i = 0; i < HD / 64; ++i) out[threadIdx.x + 64 * i] = o[i];
+  if (p.xs_out)  // split for the streaming o_proj GEMM (gemm_xs.hip)
+#pragma unroll
+    for (int i = 0; i < HD / 64; ++i) xs::store1(p.xs_out, p.xs_K, m, h * HD + threadIdx.x + 64 * i, o[i]);
 }
 
 template <int HD>
@@ -1325,7 +1344,11 @@ void launch_embed(const EmbedParams& p, int wdt, int M, hipStream_t st) {
 static bool g_attn_short = [] { const char* e = getenv("CSM_ATTN_SHORT"); return !(e && e[0] == '0'); }();
 
 void launch_attn(const AttnParams& p, int hd, hipStream_t st) {
-  if (g_attn_short && hd == 128 && p.mode == ATTN_CAUSAL && p.S_cap <= 32) {  // depth decoder
+  if (p.xs_out && p.g_tab && !(hd == 128 && p.mode == ATTN_CAUSAL && p.S_cap <= 32)) {
+    fprintf(stderr, "csm: table-gathered attention with split output only on the depth decoder's short attention\n");
+    abort();
+  }
+  if ((g_attn_short || (p.xs_out && p.g_tab)) && hd == 128 && p.mode == ATTN_CAUSAL && p.S_cap <= 32) {  // depth decoder
     hipLaunchKernelGGL((attn_short_kernel<128, 32>), dim3(p.M * p.Hq), dim3(64), 0, st, p);
     return;
   }

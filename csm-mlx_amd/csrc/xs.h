@@ -1,0 +1,65 @@
+// Split activations ("XS"): the A operand of the streaming matrix-core GEMM (gemm_xs.hip) for the
+// batched depth decoder, written once by whichever kernel produces a row block and read by every
+// block of the consuming projection straight into MFMA registers (no LDS staging, no per-block split).
+//
+// An fp32 activation x is held as three bf16 parts x = hi + mid + lo (all 24 significant bits;
+// each part times a bf16 weight is exact in fp32, so three v_mfma_f32_32x32x16_bf16 per K-step give
+// the fp32 product exactly -- the arithmetic of gemm_wide_kernel, gemm_kernels.hip).  For a matrix of
+// K columns and rows padded to 32, element (m, k) lives at
+//   [m / 32][k / 64][part][s][lane] x 16 B, byte 2 j of the lane's 16 B,
+// with kk = k % 64, h = kk / 32, s = (kk % 32) / 8, j = kk % 8, lane = m % 32 + 32 h: lane (r, h) of
+// step s holds the 8 bf16 of its v_mfma_f32_32x32x16_bf16 A fragment (the same in-stage K permutation
+// as the fragment-tiled weight copy, gemm_retile).  A producer applies the consumer's RMSNorm weight
+// before splitting (x * nw) and publishes per-row partial sums of squares of the un-normed x; the
+// consumer scales by rsqrt(sum / K + eps) after the dot product.
+#pragma once
+#include "common.h"
+
+namespace xs {
+
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+
+// byte offset of element (m, k), part 0 (part p adds p * XS_PART)
+constexpr int XS_PART = 4 * 64 * 16;
+__host__ __device__ __forceinline__ size_t off(int K, int m, int k) {
+  const int nks = K >> 6, kk = k & 63;
+  const int lane = (m & 31) + 32 * (kk >> 5);
+  return ((((size_t)(m >> 5) * nks + (k >> 6)) * 3 * 4 + ((kk >> 3) & 3)) * 64 + lane) * 16 + (kk & 7) * 2;
+}
+__host__ __device__ __forceinline__ size_t bytes(int M, int K) { return (size_t)((M + 31) / 32) * 32 * K * 6; }
+
+// x -> hi, mid, lo by truncation (hi = x with its low 16 bits cleared, mid the same of the exact
+// remainder, lo the rest: <= 8 significant bits): x = hi + mid + lo exactly; returned as bf16 bits.
+__device__ __forceinline__ void split3(float v, uint32_t& h, uint32_t& m, uint32_t& l) {
+  const uint32_t u = __float_as_uint(v);
+  h = u & 0xFFFF0000u;
+  const float r = v - __uint_as_float(h);
+  m = __float_as_uint(r) & 0xFFFF0000u;
+  l = __float_as_uint(r - __uint_as_float(m));
+}
+
+// four consecutive columns k .. k+3 (k % 4 == 0) of row m: one 8-byte store per part
+__device__ __forceinline__ void store4(void* base, int K, int m, int k, const float (&v)[4]) {
+  uint32_t h[4], md[4], l[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) split3(v[q], h[q], md[q], l[q]);
+  uint8_t* p = reinterpret_cast<uint8_t*>(base) + off(K, m, k);
+  *reinterpret_cast<u32x2_t*>(p) =
+      u32x2_t{__builtin_amdgcn_perm(h[1], h[0], 0x07060302u), __builtin_amdgcn_perm(h[3], h[2], 0x07060302u)};
+  *reinterpret_cast<u32x2_t*>(p + XS_PART) =
+      u32x2_t{__builtin_amdgcn_perm(md[1], md[0], 0x07060302u), __builtin_amdgcn_perm(md[3], md[2], 0x07060302u)};
+  *reinterpret_cast<u32x2_t*>(p + 2 * XS_PART) =
+      u32x2_t{__builtin_amdgcn_perm(l[1], l[0], 0x07060302u), __builtin_amdgcn_perm(l[3], l[2], 0x07060302u)};
+}
+
+// one element (2-byte store per part)
+__device__ __forceinline__ void store1(void* base, int K, int m, int k, float v) {
+  uint32_t h, md, l;
+  split3(v, h, md, l);
+  uint16_t* p = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(base) + off(K, m, k));
+  p[0] = (uint16_t)(h >> 16);
+  p[XS_PART / 2] = (uint16_t)(md >> 16);
+  p[XS_PART] = (uint16_t)(l >> 16);
+}
+
+}  // namespace xs

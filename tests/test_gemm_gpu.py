@@ -164,3 +164,39 @@ def test_csm_1b_bf16_batch_composition_invariance():
     assert len(c1) == frames and first_divergence(c1, c32) is None, "codes depend on the batch composition"
     for a, b in zip(l1, l32):
         assert np.abs(a - b).max() <= 2e-3 * np.abs(a).max()
+
+
+@pytest.mark.parametrize("B", [8, 24])
+def test_streaming_decoder_matches_wide_gemm(B):
+    """The batched depth decoder at codebook steps >= 2 on the streaming matrix-core GEMM over
+    pre-split activations (gemm_xs.hip; option gemm_xs) against the same frames on gemm_wide_kernel:
+    identical greedy codes, ci logits within fp32 summation-order noise (both sum exact fp32
+    products), 4 frames, csm_1b bf16."""
+    from csm_mlx import _lib
+    from csm_mlx.generation import FrameCache
+    from csm_mlx.sampling import Sampler
+    from csm_mlx.tokenizers import tokenize_text_segment
+    args, w = csm_weights("1b")
+    K, V = args.n_audio_codebooks, args.n_audio_vocab
+    Vp = (V + 7) // 8 * 8
+    prompts = [tokenize_text_segment(prompt_ids(900 + b, 9 + b % 4), 0, K) for b in range(B)]
+    model = _model(args, w, "bf16", B)
+    L = _lib.lib()
+    out = []
+    for on in (0, 1):
+        _lib.check(L.csm_set_option(model.engine, b"gemm_xs", on))
+        cache = FrameCache(model, B, Sampler(0.0, 0), [0] * B)
+        cache.prefill_batch([(b, t, m) for b, (t, m) in enumerate(prompts)])
+        logs = []
+        for _ in range(4):
+            cache.run(1)
+            logs.append(cache.debug("ci_logits", (K - 1, B, Vp))[:, :, :V].copy())
+        hist, n, _ = cache.codes()
+        out.append((hist.copy(), n.copy(), logs))
+        del cache
+    _lib.check(L.csm_set_option(model.engine, b"gemm_xs", 1))
+    del model
+    (h0, n0, l0), (h1, n1, l1) = out
+    assert np.array_equal(n0, n1) and np.array_equal(h0, h1), "streaming decoder codes differ from gemm_wide"
+    for a, b in zip(l0, l1):
+        assert np.abs(a - b).max() <= 1e-4 * np.abs(a).max()
