@@ -147,13 +147,16 @@ struct csm_engine {
   // csm_set_option "qkv0_tab_batched" 0: batched (matrix-core) frames run layer 0's QKV projection
   // instead of gathering it from the folded table (A/B and parity checks)
   bool no_tab_batched = false;
-  // batched depth decoder (8..64 utterances, bf16, codebook steps >= 2) on the streaming matrix-core
-  // GEMM over pre-split activations (gemm_xs.hip): split rows x * norm [64][Dd], attention output,
-  // SiLU*up rows [64][F] (xs.h layout), per-row partial sums of squares [64 tiles][64 rows].
+  // batched depth decoder (8..64 utterances, bf16 or int4, codebook steps >= 2) on the streaming
+  // matrix-core GEMM over pre-split activations (gemm_xs.hip): split rows x * norm [64][Dd], attention
+  // output, SiLU*up rows [64][F] (xs.h layout), per-row partial sums of squares [64 tiles][64 rows],
+  // half-group sums for int4.  Config 4 3917 vs 3729 frames/s on gemm_wide (r03).
   // csm_set_option "gemm_xs" / CSM_GEMM_XS=0 turn it off.
-  bool xs_on = [] { const char* v = getenv("CSM_GEMM_XS"); return v && v[0] == '1'; }();  // default off until measured
+  bool xs_on = [] { const char* v = getenv("CSM_GEMM_XS"); return !(v && v[0] == '0'); }();
   void *xs_D = nullptr, *xs_A = nullptr, *xs_F = nullptr;
   float* xs_ss = nullptr;
+  bool bb_xs_on = [] { const char* v = getenv("CSM_BB_XS"); return v && v[0] == '1'; }();
+  float *hs_D = nullptr, *hs_A = nullptr, *hs_F = nullptr;  // int4 engines: half-group sums of the split rows
   GemmWs ws;         // split-K slabs + tickets of this engine's MFMA launches (ensure_batch sizes them)
   // persistent frame decoder (dec_frame.hip) for batch-1 greedy bf16 frames: hand-off granules, tag
   // epoch, timeout flag; csm_set_option "dec_frame" / CSM_DEC_FRAME=0 turn it off
@@ -331,7 +334,7 @@ long long* run_stack(csm_engine* e, Stack& s, float* x, int M, float* q, float* 
 bool dec_xs_eligible(csm_engine* e, int M) {
   const Stack& s = e->dec;
   const int Dd = s.d.hidden, F = s.d.intermediate;
-  return e->xs_on && e->xs_D && M >= GEMM_MFMA_MIN_M && M <= GEMM_XS_MAX_M && e->wdt == WDT_BF16 &&
+  return e->xs_on && e->xs_D && M >= GEMM_MFMA_MIN_M && M <= GEMM_XS_MAX_M && (e->wdt == WDT_BF16 || e->wdt == WDT_Q4) &&
          e->head_wdt == WDT_BF16 && !e->fuse_mlp && s.d.head_dim == 128 && s.S_cap <= 32 &&
          gemm_xs_eligible(s.qkv_rows(), Dd, M, e->wdt) && gemm_xs_eligible(Dd, s.q_dim(), M, e->wdt) &&
          gemm_xs_eligible(2 * F, Dd, M, e->wdt) && gemm_xs_eligible(Dd, F, M, e->wdt) &&
@@ -344,6 +347,10 @@ void run_dec_xs(csm_engine* e, int M, const RowMap& rm, hipStream_t st, const At
   const csm_llama_dims& d = s.d;
   const int D = d.hidden, F = d.intermediate;
   const int ss_o = gemm_xs_tiles(D, s.q_dim(), M), ss_d = gemm_xs_tiles(D, F, M);
+  const bool q4 = e->wdt == WDT_Q4;  // int4 consumers also read the half-group sums of their operand
+  float* hsD = q4 ? e->hs_D : nullptr;
+  float* hsA = q4 ? e->hs_A : nullptr;
+  float* hsF = q4 ? e->hs_F : nullptr;
   for (int i = 0; i < d.n_layers; ++i) {
     LayerW& l = s.L[i];
     if (i > 0) {  // norm1 + QKV + RoPE + KV append from the split rows the previous down wrote
@@ -351,33 +358,34 @@ void run_dec_xs(csm_engine* e, int M, const RowMap& rm, hipStream_t st, const At
       g.W = l.wqkv; g.N = s.qkv_rows(); g.K = D; g.M = M; g.nw = l.n1; g.eps = d.eps;
       g.out = e->dq; g.os = s.q_dim(); g.Hq = d.n_heads; g.Hkv = d.n_kv_heads; g.hd = d.head_dim;
       g.S_cap = s.S_cap; g.rope = s.rope; g.kc = l.kc; g.vc = l.vc; g.rm = rm;
-      g.xs_in = e->xs_D; g.ss_in = e->xs_ss; g.ss_n = ss_d; g.ss_stride = GEMM_XS_MAX_M;
-      launch_gemm_xs(g, EPI_QKV, st);
+      g.xs_in = e->xs_D; g.ss_in = e->xs_ss; g.ss_n = ss_d; g.ss_stride = GEMM_XS_MAX_M; g.hs_in = hsD;
+      launch_gemm_xs(g, EPI_QKV, st, false, e->wdt);
     }
     AttnParams a = i == 0 ? attn0 : AttnParams{};
     a.q = e->dq; a.qs = s.q_dim(); a.M = M; a.kc = l.kc; a.vc = l.vc; a.Hq = d.n_heads; a.Hkv = d.n_kv_heads;
     a.S_cap = s.S_cap; a.scale = 1.0f / sqrtf((float)d.head_dim); a.mode = ATTN_CAUSAL; a.window = 0; a.rm = rm;
-    a.out = e->datt; a.os = s.q_dim(); a.xs_out = e->xs_A; a.xs_K = s.q_dim();
+    a.out = e->datt; a.os = s.q_dim(); a.xs_out = e->xs_A; a.xs_K = s.q_dim(); a.hs_out = hsA;
     launch_attn(a, d.head_dim, st);
     {  // o_proj + residual -> x; split (x * n2) + sums of squares for gate/up
       GemvParams g = gp(e);
       g.W = l.wo; g.N = D; g.K = s.q_dim(); g.M = M; g.out = e->dx; g.os = D; g.xs_in = e->xs_A;
       g.xs_out = e->xs_D; g.xs_nw = l.n2; g.ss_out = e->xs_ss; g.ss_stride = GEMM_XS_MAX_M; g.xs_K = D;
-      launch_gemm_xs(g, EPI_ADD, st);
+      g.hs_in = hsA; g.hs_out = hsD;
+      launch_gemm_xs(g, EPI_ADD, st, false, e->wdt);
     }
     {  // norm2 + gate/up + SiLU*up -> split h
       GemvParams g = gp(e);
       g.W = l.wgu; g.N = 2 * F; g.K = D; g.M = M; g.nw = l.n2; g.eps = d.eps; g.out = nullptr; g.os = F;
       g.xs_in = e->xs_D; g.ss_in = e->xs_ss; g.ss_n = ss_o; g.ss_stride = GEMM_XS_MAX_M;
-      g.xs_out = e->xs_F; g.xs_K = F;
-      launch_gemm_xs(g, EPI_SILU_MUL, st);
+      g.xs_out = e->xs_F; g.xs_K = F; g.hs_in = hsD; g.hs_out = hsF;
+      launch_gemm_xs(g, EPI_SILU_MUL, st, false, e->wdt);
     }
     {  // down + residual -> x; split (x * next norm) + sums of squares
       GemvParams g = gp(e);
       g.W = l.wd; g.N = D; g.K = F; g.M = M; g.out = e->dx; g.os = D; g.xs_in = e->xs_F;
       g.xs_out = e->xs_D; g.xs_nw = i + 1 < d.n_layers ? s.L[i + 1].n1 : s.norm; g.ss_out = e->xs_ss;
-      g.ss_stride = GEMM_XS_MAX_M; g.xs_K = D;
-      launch_gemm_xs(g, EPI_ADD, st);
+      g.ss_stride = GEMM_XS_MAX_M; g.xs_K = D; g.hs_in = hsF; g.hs_out = hsD;
+      launch_gemm_xs(g, EPI_ADD, st, false, e->wdt);
     }
   }
 }
@@ -388,7 +396,7 @@ void run_dec_xs(csm_engine* e, int M, const RowMap& rm, hipStream_t st, const At
 bool bb_xs_eligible(csm_engine* e, int M) {
   const Stack& s = e->bb;
   const int D = s.d.hidden, F = s.d.intermediate;
-  return e->xs_on && e->xs_D && M >= GEMM_MFMA_MIN_M && M <= GEMM_XS_MAX_M && e->wdt == WDT_BF16 &&
+  return e->xs_on && e->xs_D && M >= GEMM_MFMA_MIN_M && M <= GEMM_XS_MAX_M && (e->wdt == WDT_BF16 || e->wdt == WDT_Q4) &&
          !e->fuse_mlp && D % 512 == 0 && D / 512 <= 64 && gemm_xs_eligible(s.qkv_rows(), D, M, e->wdt) &&
          gemm_xs_eligible(D, s.q_dim(), M, e->wdt) && gemm_xs_eligible(2 * F, D, M, e->wdt) &&
          gemm_xs_eligible(D, F, M, e->wdt) && gemm_xs_tiles(D, F, M) <= 64 && gemm_xs_tiles(D, s.q_dim(), M) <= 64;
@@ -399,6 +407,10 @@ void run_bb_xs(csm_engine* e, int M, const RowMap& rm, hipStream_t st) {
   const csm_llama_dims& d = s.d;
   const int D = d.hidden, F = d.intermediate;
   const int ss_o = gemm_xs_tiles(D, s.q_dim(), M), ss_d = gemm_xs_tiles(D, F, M);
+  const bool q4 = e->wdt == WDT_Q4;  // int4 consumers also read the half-group sums of their operand
+  float* hsD = q4 ? e->hs_D : nullptr;
+  float* hsA = q4 ? e->hs_A : nullptr;
+  float* hsF = q4 ? e->hs_F : nullptr;
   for (int i = 0; i < d.n_layers; ++i) {
     LayerW& l = s.L[i];
     {  // norm1 + QKV + RoPE + KV append
@@ -407,33 +419,36 @@ void run_bb_xs(csm_engine* e, int M, const RowMap& rm, hipStream_t st) {
       g.out = e->q; g.os = s.q_dim(); g.Hq = d.n_heads; g.Hkv = d.n_kv_heads; g.hd = d.head_dim;
       g.S_cap = s.S_cap; g.rope = s.rope; g.kc = l.kc; g.vc = l.vc; g.rm = rm;
       g.xs_in = e->xs_D; g.ss_in = e->xs_ss; g.ss_n = i == 0 ? D / 512 : ss_d; g.ss_stride = GEMM_XS_MAX_M;
-      launch_gemm_xs(g, EPI_QKV, st, gemv_nt(0));
+      g.hs_in = hsD;
+      launch_gemm_xs(g, EPI_QKV, st, gemv_nt(0), e->wdt);
     }
     AttnParams a{};
     a.q = e->q; a.qs = s.q_dim(); a.M = M; a.kc = l.kc; a.vc = l.vc; a.Hq = d.n_heads; a.Hkv = d.n_kv_heads;
     a.S_cap = s.S_cap; a.scale = 1.0f / sqrtf((float)d.head_dim); a.mode = ATTN_CAUSAL; a.window = 0; a.rm = rm;
-    a.out = e->att; a.os = s.q_dim(); a.xs_out = e->xs_A; a.xs_K = s.q_dim();
+    a.out = e->att; a.os = s.q_dim(); a.xs_out = e->xs_A; a.xs_K = s.q_dim(); a.hs_out = hsA;
     launch_attn(a, d.head_dim, st);
     {  // o_proj + residual
       GemvParams g = gp(e);
       g.W = l.wo; g.N = D; g.K = s.q_dim(); g.M = M; g.out = e->x; g.os = D; g.xs_in = e->xs_A;
       g.xs_out = e->xs_D; g.xs_nw = l.n2; g.ss_out = e->xs_ss; g.ss_stride = GEMM_XS_MAX_M; g.xs_K = D;
-      launch_gemm_xs(g, EPI_ADD, st, gemv_nt(0));
+      g.hs_in = hsA; g.hs_out = hsD;
+      launch_gemm_xs(g, EPI_ADD, st, gemv_nt(0), e->wdt);
     }
     {  // norm2 + gate/up + SiLU*up
       GemvParams g = gp(e);
       g.W = l.wgu; g.N = 2 * F; g.K = D; g.M = M; g.nw = l.n2; g.eps = d.eps; g.out = nullptr; g.os = F;
       g.xs_in = e->xs_D; g.ss_in = e->xs_ss; g.ss_n = ss_o; g.ss_stride = GEMM_XS_MAX_M;
-      g.xs_out = e->xs_F; g.xs_K = F;
-      launch_gemm_xs(g, EPI_SILU_MUL, st, gemv_nt(0));
+      g.xs_out = e->xs_F; g.xs_K = F; g.hs_in = hsD; g.hs_out = hsF;
+      launch_gemm_xs(g, EPI_SILU_MUL, st, gemv_nt(0), e->wdt);
     }
     {  // down + residual (the last layer's rows go to the final norm in fp32 only)
       GemvParams g = gp(e);
-      g.W = l.wd; g.N = D; g.K = F; g.M = M; g.out = e->x; g.os = D; g.xs_in = e->xs_F;
+      g.W = l.wd; g.N = D; g.K = F; g.M = M; g.out = e->x; g.os = D; g.xs_in = e->xs_F; g.hs_in = hsF;
       if (i + 1 < d.n_layers) {
         g.xs_out = e->xs_D; g.xs_nw = s.L[i + 1].n1; g.ss_out = e->xs_ss; g.ss_stride = GEMM_XS_MAX_M; g.xs_K = D;
+        g.hs_out = hsD;
       }
-      launch_gemm_xs(g, EPI_ADD, st, gemv_nt(0));
+      launch_gemm_xs(g, EPI_ADD, st, gemv_nt(0), e->wdt);
     }
   }
 }
@@ -486,9 +501,12 @@ void enqueue_body(csm_engine* e, hipStream_t st) {
   EmbedParams ep{};
   ep.codes = e->codes; ep.text_emb = e->text_emb; ep.audio_emb = e->audio_emb; ep.V = e->V; ep.K = e->K;
   ep.D = e->D; ep.out = e->x; ep.pos_inc = e->pos;
-  const bool bb_xs = !bb_step_eligible(e) && bb_xs_eligible(e, B);
+  // the backbone's projections measured no faster on gemm_xs than on gemm_wide at 32-64 rows (its
+  // long-K down and QKV slower, profiles/r03_gemm_xs_shapes.txt): opt-in (option bb_xs / CSM_BB_XS=1)
+  const bool bb_xs = e->bb_xs_on && !bb_step_eligible(e) && bb_xs_eligible(e, B);
   if (bb_xs) {
     ep.xs_out = e->xs_D; ep.xs_nw = e->bb.L[0].n1; ep.ss_out = e->xs_ss; ep.ss_stride = GEMM_XS_MAX_M;
+    ep.hs_out = e->wdt == WDT_Q4 ? e->hs_D : nullptr;
   }
   embed(e, ep, B, st);
   if (bb_step_eligible(e)) {
@@ -665,7 +683,7 @@ void enqueue_head_phase(csm_engine* e, hipStream_t st, int phase) {
     if (xs_dec) {  // the head reads the split rows (x * final norm) the last down wrote
       g.xs_in = e->xs_D; g.ss_in = e->xs_ss; g.ss_n = gemm_xs_tiles(Dd, e->dec.d.intermediate, M);
       g.ss_stride = GEMM_XS_MAX_M;
-      launch_gemm_xs(g, greedy ? EPI_ARGMAX : EPI_STORE, st);
+      launch_gemm_xs(g, greedy ? EPI_ARGMAX : EPI_STORE, st, gemv_nt(2), e->head_wdt);
     } else if (!(ablate() & 64)) {
       launch_gemv(g, e->head_wdt, greedy ? EPI_ARGMAX : EPI_STORE, 1, st);
     }
@@ -768,6 +786,7 @@ void ensure_batch(csm_engine* e, int B) {
     e->xs_A = e->balloc(bA);
     e->xs_F = e->balloc(bF);
     e->xs_ss = (float*)e->balloc((size_t)64 * xm * 4);
+    for (float** h : {&e->hs_D, &e->hs_A, &e->hs_F}) *h = (float*)e->balloc(bF / 6 / xm / 32 * xs::HS_ROWS * 4 + 4096);
   }
 }
 
@@ -1740,10 +1759,11 @@ int csm_bench_gemv(csm_engine* e, int which, int M, int iters, float* avg_us, do
     if (M <= 0 || M > 2 * e->B_max || iters <= 0) throw CsmError(CSM_ERR_ARG, "bad bench arguments");
     HIPCHK(hipSetDevice(e->dev));
     if (e->tiled_dirty) build_tiled(e);
-    Stack& s = (which / 4 == 0) ? e->bb : e->dec;
-    const int tag = (which / 4 == 0) ? 0 : 1;
-    float* x = (which / 4 == 0) ? e->x : e->dx;
-    float* mlp = (which / 4 == 0) ? e->mlp : e->dmlp;
+    const int stack = (which & 7) / 4;
+    Stack& s = stack == 0 ? e->bb : e->dec;
+    const int tag = stack == 0 ? 0 : 1;
+    float* x = stack == 0 ? e->x : e->dx;
+    float* mlp = stack == 0 ? e->mlp : e->dmlp;
     const int D = s.d.hidden, F = s.d.intermediate;
     const int kind = which % 4;
     // one launch per layer in turn, as the frame does, so the weight working set (and hence
@@ -1759,13 +1779,27 @@ int csm_bench_gemv(csm_engine* e, int which, int M, int iters, float* avg_us, do
         g.W = l.wd; g.N = D; g.K = F; g.x = mlp; g.xs = F; g.M = M; g.out = x; g.os = D; epi = EPI_ADD; norm = 0;
       } else if (kind == 2) {  // norm + QKV + RoPE + KV append (position 0)
         g.W = l.wqkv; g.N = s.qkv_rows(); g.K = D; g.x = x; g.xs = D; g.M = M; g.nw = l.n1; g.eps = s.d.eps;
-        g.out = (which / 4 == 0) ? e->q : e->dq; g.os = s.q_dim(); g.Hq = s.d.n_heads; g.Hkv = s.d.n_kv_heads;
+        g.out = stack == 0 ? e->q : e->dq; g.os = s.q_dim(); g.Hq = s.d.n_heads; g.Hkv = s.d.n_kv_heads;
         g.hd = s.d.head_dim; g.S_cap = s.S_cap; g.rope = s.rope; g.kc = l.kc; g.vc = l.vc; g.rm = RowMap{1, 0, nullptr, 0};
         epi = EPI_QKV; norm = 1;
       } else {  // o_proj + residual
-        g.W = l.wo; g.N = D; g.K = s.q_dim(); g.x = (which / 4 == 0) ? e->att : e->datt; g.xs = s.q_dim(); g.M = M;
+        g.W = l.wo; g.N = D; g.K = s.q_dim(); g.x = stack == 0 ? e->att : e->datt; g.xs = s.q_dim(); g.M = M;
         g.out = x; g.os = D; epi = EPI_ADD; norm = 0;
       }
+      return g;
+    };
+    // which & 8: the streaming matrix-core GEMM (gemm_xs) of the same projection at M rows, with the
+    // decoder path's operands and producer outputs (split rows in, split rows + sums out; lab timing)
+    const bool xsb = (which & 8) != 0;
+    auto xs_params = [&](GemvParams g, int epi) {
+      const int Dm = s.d.hidden;
+      g.x = nullptr;
+      g.xs_in = (epi == EPI_ADD && g.K == F) ? e->xs_F : (epi == EPI_ADD ? e->xs_A : e->xs_D);
+      g.ss_in = e->xs_ss; g.ss_n = gemm_xs_tiles(Dm, F, M); g.ss_stride = GEMM_XS_MAX_M;
+      const bool noprod = (which & 16) != 0;  // lab: without the producer outputs (their cost)
+      if (epi == EPI_SILU_MUL) { g.out = noprod ? mlp : nullptr; if (!noprod) { g.xs_out = e->xs_F; g.xs_K = F; } }
+      if (epi == EPI_ADD && !noprod) { g.xs_out = e->xs_D; g.xs_nw = s.L[0].n1; g.ss_out = e->xs_ss; g.xs_K = Dm; }
+      if (e->wdt == WDT_Q4) { g.hs_in = e->hs_D; g.hs_out = (epi == EPI_SILU_MUL) ? e->hs_F : e->hs_A; }
       return g;
     };
     int epi = 0, norm = 0;
@@ -1774,12 +1808,21 @@ int csm_bench_gemv(csm_engine* e, int which, int M, int iters, float* avg_us, do
     nbytes += (size_t)M * g.K * 4 + (size_t)M * (epi == EPI_SILU_MUL ? F : D) * 4 * (epi == EPI_ADD ? 2 : 1);
     const char* lenv = getenv("CSM_BENCH_LAYERS");  // lab: rotate over fewer layers (cache residency)
     const int nl = lenv ? std::max(1, std::min(atoi(lenv), s.d.n_layers)) : s.d.n_layers;
-    for (int i = 0; i < nl; ++i) { GemvParams gi = params(i, epi, norm); launch_gemv(gi, e->wdt, epi, norm, e->st, tag); }
+    auto run1 = [&](int i) {
+      GemvParams gi = params(i % nl, epi, norm);
+      if (xsb) {
+        if (!norm) gi.nw = nullptr;
+        launch_gemm_xs(xs_params(gi, epi), epi, e->st, tag == 0 && gemv_nt(0), e->wdt);
+      } else {
+        launch_gemv(gi, e->wdt, epi, norm, e->st, tag);
+      }
+    };
+    for (int i = 0; i < nl; ++i) run1(i);
     hipEvent_t a, b;
     HIPCHK(hipEventCreate(&a));
     HIPCHK(hipEventCreate(&b));
     HIPCHK(hipEventRecord(a, e->st));
-    for (int i = 0; i < iters; ++i) { GemvParams gi = params(i % nl, epi, norm); launch_gemv(gi, e->wdt, epi, norm, e->st, tag); }
+    for (int i = 0; i < iters; ++i) run1(i);
     HIPCHK(hipEventRecord(b, e->st));
     HIPCHK(hipEventSynchronize(b));
     float ms = 0.f;
@@ -1909,6 +1952,10 @@ int csm_set_option(csm_engine* e, const char* key, int value) {
     else if (k == "gemm_xs") {
       if (!e) throw CsmError(CSM_ERR_ARG, "gemm_xs needs an engine");
       e->xs_on = value != 0;
+    }
+    else if (k == "bb_xs") {
+      if (!e) throw CsmError(CSM_ERR_ARG, "bb_xs needs an engine");
+      e->bb_xs_on = value != 0;
     }
     else if (k == "qkv0_tab_batched") {
       if (!e) throw CsmError(CSM_ERR_ARG, "qkv0_tab_batched needs an engine");

@@ -95,6 +95,9 @@ struct GemvParams {
   const float* xs_nw;
   float* ss_out;
   int xs_K;
+  // int4 consumers: half-group sums of the split rows (xs.h): produced into hs_out, consumed from hs_in
+  float* hs_out;
+  const float* hs_in;
 };
 
 // order-preserving float <-> uint32 keys (radix select of the top-k threshold)
@@ -242,6 +245,7 @@ struct EmbedParams {
   const float* xs_nw;
   float* ss_out;
   int ss_stride;
+  float* hs_out;         // int4 consumer: half-group sums of the split rows (xs.h)
 };
 
 struct AttnParams {
@@ -270,8 +274,10 @@ struct AttnParams {
   float* g_xout;
   int g_D;
   // streaming matrix-core path: the attention output also written split (xs.h) for the o_proj GEMM
+  // (+ its half-group sums for an int4 o_proj)
   void* xs_out;
   int xs_K;
+  float* hs_out;
 };
 
 struct SampleParams {
@@ -374,7 +380,7 @@ bool gemm_reserve(GemmWs& ws, int N, int K, int M);
 constexpr int GEMM_XS_MAX_M = 64;
 bool gemm_xs_eligible(int N, int K, int M, int wdt);
 int gemm_xs_tiles(int N, int K, int M);       // column tiles of a launch (ss / arg-max partials per row)
-void launch_gemm_xs(const GemvParams& p, int epi, hipStream_t st, bool nt = false);
+void launch_gemm_xs(const GemvParams& p, int epi, hipStream_t st, bool nt = false, int wdt = WDT_BF16);
 bool gemm_xs_reserve(GemmWs& ws, int N, int K, int M);
 // Fragment-tiled weight copy for the MFMA path: per 32-row tile and 64-K stage, the bytes each lane
 // of a wave loads for v_mfma_f32_32x32x16_bf16's B operand, contiguous (bf16: 4 KB = 4 steps x 64

@@ -77,12 +77,22 @@ __global__ __launch_bounds__(64) void embed_rows_kernel(EmbedParams p) {
     for (int e = 0; e < 8; ++e) s = fmaf(acc[e], acc[e], s);
     s = wave_sum(s);
     if (t == 0) p.ss_out[(size_t)blockIdx.y * p.ss_stride + m] = s;
+    float hsum = 0.f;
 #pragma unroll
     for (int hf = 0; hf < 2; ++hf) {
       float v[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = acc[4 * hf + u] * p.xs_nw[d0 + 4 * hf + u];
+      for (int u = 0; u < 4; ++u) {
+        v[u] = acc[4 * hf + u] * p.xs_nw[d0 + 4 * hf + u];
+        hsum += v[u];
+      }
       xs::store4(p.xs_out, p.D, m, d0 + 4 * hf, v);
+    }
+    if (p.hs_out) {  // half-group sums (32 columns = 4 lanes, in column order) for int4 consumers
+      const int b4 = t & ~3;
+      const float h0 = __shfl(hsum, b4, 64), h1 = __shfl(hsum, b4 + 1, 64), h2 = __shfl(hsum, b4 + 2, 64),
+                  h3 = __shfl(hsum, b4 + 3, 64);
+      if ((t & 3) == 0) p.hs_out[(size_t)(d0 / 32) * xs::HS_ROWS + m] = ((h0 + h1) + h2) + h3;
     }
   }
 }
@@ -510,6 +520,14 @@ struct AttnLds {
   float qs[4][HD];
 };
 
+// Half-group sums of one wave's 64 consecutive split values (column c0 + lane): a butterfly over each
+// 32-lane half (every lane of a half ends with the same sum), written by lanes 0 and 32.
+__device__ __forceinline__ void xs_half_sum(float* hs, int m, int c0, float v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 32; o <<= 1) v += __shfl_xor(v, o, 64);
+  if ((lane & 31) == 0) hs[(size_t)((c0 + lane) / 32) * xs::HS_ROWS + m] = v;
+}
+
 template <int HD>
 __device__ __forceinline__ void attn_block(const AttnParams& p, int m, int kvh, AttnLds<HD>& L) {
   constexpr int KP = HD + 4;  // padded K row (floats)
@@ -607,7 +625,10 @@ __device__ __forceinline__ void attn_block(const AttnParams& p, int m, int kvh, 
 #pragma unroll
   for (int i = 0; i < NO; ++i) {
     out[lane + 64 * i] = o[i] * inv;
-    if (p.xs_out) xs::store1(p.xs_out, p.xs_K, m, h * HD + lane + 64 * i, o[i] * inv);  // streaming o_proj
+    if (p.xs_out) {  // streaming o_proj (+ half-group sums for an int4 one)
+      xs::store1(p.xs_out, p.xs_K, m, h * HD + lane + 64 * i, o[i] * inv);
+      if (p.hs_out) xs_half_sum(p.hs_out, m, h * HD + 64 * i, o[i] * inv, lane);
+    }
   }
 }
 
@@ -733,7 +754,10 @@ __global__ __launch_bounds__(64) void attn_short_kernel(AttnParams p) {
   for (int i = 0; i < HD / 64; ++i) out[threadIdx.x + 64 * i] = o[i];
   if (p.xs_out)  // split for the streaming o_proj GEMM (gemm_xs.hip)
 #pragma unroll
-    for (int i = 0; i < HD / 64; ++i) xs::store1(p.xs_out, p.xs_K, m, h * HD + threadIdx.x + 64 * i, o[i]);
+    for (int i = 0; i < HD / 64; ++i) {
+      xs::store1(p.xs_out, p.xs_K, m, h * HD + threadIdx.x + 64 * i, o[i]);
+      if (p.hs_out) xs_half_sum(p.hs_out, m, h * HD + 64 * i, o[i], threadIdx.x);
+    }
 }
 
 template <int HD>

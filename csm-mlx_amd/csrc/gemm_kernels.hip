@@ -36,6 +36,7 @@
 #include <cstdlib>
 
 #include "csm_kernels.h"
+#include "xs.h"
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
@@ -77,20 +78,6 @@ __device__ __forceinline__ float row16_sum(float v) {
   v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
   v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
   return v;
-}
-
-// one uint32 of MLX int4 nibbles (k = 8s .. 8s+7, low nibble first) -> 8 exact bf16 (u32x4 of pairs):
-// bytes of the even / odd nibbles through v_cvt_f32_ubyte*, the floats' high halves paired by v_perm
-__device__ __forceinline__ u32x4_t q4_word_bf16(uint32_t u) {
-  const uint32_t a = u & 0x0F0F0F0Fu, b = (u >> 4) & 0x0F0F0F0Fu;
-  u32x4_t o;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const uint32_t fa = __float_as_uint((float)((a >> (8 * i)) & 0xFFu));
-    const uint32_t fb = __float_as_uint((float)((b >> (8 * i)) & 0xFFu));
-    o[i] = __builtin_amdgcn_perm(fb, fa, 0x07060302u);  // {hi16(fa), hi16(fb)}
-  }
-  return o;
 }
 
 // Split-K combine (the last slice of a tile to arrive): every slice's partial is read with 16-B sc1
@@ -298,7 +285,7 @@ __global__ __launch_bounds__(256) void gemm_wide_kernel(GemvParams p) {
         for (int i = 0; i < RTW; ++i) {
           if constexpr (Q4) {  // (KW = 2: the wave's half of the 4 words, selected without indexing)
             const uint32_t word = KW == 2 ? (kh ? g.w[i][0][NS + s] : g.w[i][0][s]) : g.w[i][0][s];
-            b[i] = __builtin_bit_cast(bf16x8_t, q4_word_bf16(word));
+            b[i] = __builtin_bit_cast(bf16x8_t, xs::q4_word_bf16(word));
           } else {
             b[i] = __builtin_bit_cast(bf16x8_t, g.w[i][s]);
           }

@@ -43,7 +43,46 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, int bytes)
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, RSRC3);
 }
 
-template <int MT, int RTW, int PD, bool NT>
+// Q4: int4 weights (MLX affine, group 64 = one stage) from the fragment-tiled int4 copy: the nibbles
+// enter the matrix cores as exact bf16 integers, per stage S_g = sum q x (three products per step as
+// for bf16), folded as acc += scale * S_g + bias * X_g with X_g the stage's activation sum per row
+// (the producers' half-group sums, xs.h) -- the arithmetic of gemm_wide_kernel's int4 path.
+constexpr int Q4_WST_MAX = 16;  // stages per wave whose X_g an int4 block stages in LDS
+constexpr int SS_MAX = 64 * 64;  // sums-of-squares partials a normed launch stages (tiles x rows)
+
+// Split-K combine by the last slice to arrive: every slice's partial tile read with 16-B sc1 loads, up
+// to 32 loads in flight per thread (UB vectors x KS slices per round), summed in slice order.
+template <int KS, int NB, int NBR, int NTH>
+__device__ __forceinline__ void combine(__amdgpu_buffer_rsrc_t rs, float (*ct)[NBR + 1], int mrows, int slab_f, int tid) {
+  constexpr int NQ = NB * NBR / 4, U = (NQ + NTH - 1) / NTH, UB = (32 / KS) < 1 ? 1 : (32 / KS);
+  const int nq = mrows * (NBR / 4);
+#pragma unroll
+  for (int u0 = 0; u0 < U; u0 += UB) {
+    f32x4_t v[UB][KS];
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int q = min(tid + NTH * (u0 + u), nq - 1);
+#pragma unroll
+      for (int s = 0; s < KS; ++s) v[u][s] = __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, q * 16, s * slab_f * 4, SC1));
+    }
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int q = tid + NTH * (u0 + u);
+      if (u0 + u < U && q < nq) {
+        f32x4_t sum = v[u][0];
+#pragma unroll
+        for (int s = 1; s < KS; ++s) sum += v[u][s];
+        const int ml = q / (NBR / 4), j = (q % (NBR / 4)) * 4;
+        ct[ml][j] = sum.x;
+        ct[ml][j + 1] = sum.y;
+        ct[ml][j + 2] = sum.z;
+        ct[ml][j + 3] = sum.w;
+      }
+    }
+  }
+}
+
+template <bool Q4, int MT, int RTW, int PD, bool NT>
 __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
   constexpr int NB = 32 * MT, NBR = 32 * RTW, NTH = 64 * XW;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -52,11 +91,25 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
   const int nks = p.K / XK, nt32 = (p.N + 31) / 32;
   const int ks = p.ksplit, nst = nks / ks, wst = nst / XW, ws0 = blockIdx.y * nst + wave * wst;
   const __amdgpu_buffer_rsrc_t wrs = rsrc(p.Wt, 0x7fffffff), ars = rsrc(p.xs_in, 0x7fffffff), zrs = rsrc(p.Wt, 0);
-  int wv[RTW];
+  int wv[RTW], sv[RTW];
 #pragma unroll
-  for (int i = 0; i < RTW; ++i) wv[i] = (min(n0 / 32 + i, nt32 - 1) * nks * 4 * 64 + lane) * 16;
+  for (int i = 0; i < RTW; ++i) {
+    const int T = min(n0 / 32 + i, nt32 - 1);
+    wv[i] = Q4 ? T * nks * 1024 + 16 * lane : (T * nks * 4 * 64 + lane) * 16;
+    sv[i] = nt32 * nks * 1024 + (T * nks * 32 + (lane & 31)) * 4;  // int4: the lane's scale|bias words
+  }
+  __shared__ __attribute__((aligned(16))) float xg[Q4 ? XW : 1][Q4 ? Q4_WST_MAX : 1][NB];
+  if constexpr (Q4) {  // X_g of this block's stages: the two half-group sums, in order
+    for (int e = tid; e < XW * wst * NB; e += NTH) {
+      const int w = e / (wst * NB), j = (e / NB) % wst, m = e % NB;
+      const int st = blockIdx.y * nst + w * wst + j;
+      xg[w][j][m] = p.hs_in[(size_t)(2 * st) * xs::HS_ROWS + m] + p.hs_in[(size_t)(2 * st + 1) * xs::HS_ROWS + m];
+    }
+    __syncthreads();
+  }
   struct St {
-    u32x4_t w[RTW][4];
+    u32x4_t w[RTW][Q4 ? 1 : 4];
+    uint32_t sb[RTW];
     u32x4_t a[MT][3][4];
   };
   // stage j of this wave (j >= wst: zero-sized descriptors, no traffic) -- straight-line loads
@@ -65,10 +118,16 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
     const int st = ws0 + (live ? j : 0);
     const __amdgpu_buffer_rsrc_t wr = live ? wrs : zrs, ar = live ? ars : zrs;
 #pragma unroll
-    for (int i = 0; i < RTW; ++i)
+    for (int i = 0; i < RTW; ++i) {
+      if constexpr (Q4) {
+        g.w[i][0] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(wr, wv[i], st * 1024, NT ? 2 : 0));
+        g.sb[i] = __builtin_amdgcn_raw_buffer_load_b32(wr, sv[i], st * 128, 0);
+      } else {
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
-        g.w[i][s] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(wr, wv[i], (st * 4 + s) * 1024, NT ? 2 : 0));
+        for (int s = 0; s < 4; ++s)
+          g.w[i][s] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(wr, wv[i], (st * 4 + s) * 1024, NT ? 2 : 0));
+      }
+    }
 #pragma unroll
     for (int t = 0; t < MT; ++t)
 #pragma unroll
@@ -82,23 +141,93 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
   for (int t = 0; t < MT; ++t)
 #pragma unroll
     for (int i = 0; i < RTW; ++i) acc[t][i] = f32x16_t{};
+  // Epilogue operands prefetched into LDS by LDS-DMA before the first weight stage (no registers held
+  // across the K loop, no dependent global round trips after it): the RMSNorm sums-of-squares partials,
+  // the residual rows of an EPI_ADD tile, the producer's norm-weight columns.
+  __shared__ float sss[SS_MAX + 2 * 64 * XW];  // [t][NB] partial sums of squares
+  __shared__ float res[NB * NBR + 64 * XW];    // [NB][NBR] residual rows (EPI_ADD)
+  __shared__ float nws[64];                    // xs_nw[col0 .. col0 + ncol)
+  const bool norm = p.nw != nullptr;
+  const bool silu = p.epi == EPI_SILU_MUL;
+  const int mrows = min(NB, p.M);
+  {
+    if (norm) {
+      const int tot = p.ss_n * NB;
+      for (int i0 = wave * 64; i0 < tot; i0 += NTH) {
+        const int i = min(i0 + lane, tot - 1), t = i / NB, m = min(i % NB, mrows - 1);
+        __builtin_amdgcn_global_load_lds(p.ss_in + (size_t)t * p.ss_stride + m, &sss[i0], 4, 0, 0);
+      }
+    }
+    if (p.epi == EPI_ADD) {
+      const int tot = mrows * NBR;
+      for (int i0 = wave * 64; i0 < tot; i0 += NTH) {
+        const int i = min(i0 + lane, tot - 1), m = i / NBR, n = min(n0 + i % NBR, p.N - 1);
+        __builtin_amdgcn_global_load_lds(p.out + (size_t)m * p.os + n, &res[i0], 4, 0, 0);
+      }
+    }
+    if (p.xs_out && p.xs_nw && wave == 0) {
+      const int col0 = silu ? n0 / 2 : n0, ncol = silu ? NBR / 2 : NBR, colN = silu ? p.N / 2 : p.N;
+      __builtin_amdgcn_global_load_lds(p.xs_nw + min(col0 + min(lane, ncol - 1), colN - 1), &nws[0], 4, 0, 0);
+    }
+  }
   St g[PD];
 #pragma unroll
   for (int d = 0; d < PD; ++d) load(d, g[d]);
   asm volatile("" ::: "memory");  // the ring's loads stay where they are issued (no sinking to their use)
+  const int hrow = 4 * (lane >> 5);  // int4 fold: lane (r, h) register jj holds batch row (jj & 3) + 8 (jj >> 2) + 4 h
   for (int j0 = 0; j0 < wst; j0 += PD) {
 #pragma unroll
     for (int d = 0; d < PD; ++d) {
+      if constexpr (Q4) {
+        f32x16_t gq[MT][RTW];
 #pragma unroll
-      for (int s = 0; s < 4; ++s)
+        for (int t = 0; t < MT; ++t)
 #pragma unroll
-        for (int q = 0; q < 3; ++q)
+          for (int i = 0; i < RTW; ++i) gq[t][i] = f32x16_t{};
 #pragma unroll
-          for (int t = 0; t < MT; ++t)
+        for (int s = 0; s < 4; ++s) {
+          bf16x8_t b[RTW];
 #pragma unroll
-            for (int i = 0; i < RTW; ++i)
-              acc[t][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, g[d].a[t][q][s]),
-                                                                   __builtin_bit_cast(bf16x8_t, g[d].w[i][s]), acc[t][i], 0, 0, 0);
+          for (int i = 0; i < RTW; ++i) b[i] = __builtin_bit_cast(bf16x8_t, xs::q4_word_bf16(g[d].w[i][0][s]));
+#pragma unroll
+          for (int q = 0; q < 3; ++q)
+#pragma unroll
+            for (int t = 0; t < MT; ++t)
+#pragma unroll
+              for (int i = 0; i < RTW; ++i)
+                gq[t][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, g[d].a[t][q][s]), b[i], gq[t][i], 0, 0, 0);
+        }
+        const int jst = j0 + d;
+#pragma unroll
+        for (int t = 0; t < MT; ++t) {
+          float xr[16];
+#pragma unroll
+          for (int q4 = 0; q4 < 4; ++q4) {
+            const f32x4_t x4 = *reinterpret_cast<const f32x4_t*>(&xg[wave][jst][32 * t + 8 * q4 + hrow]);
+            xr[4 * q4] = x4.x; xr[4 * q4 + 1] = x4.y; xr[4 * q4 + 2] = x4.z; xr[4 * q4 + 3] = x4.w;
+          }
+#pragma unroll
+          for (int i = 0; i < RTW; ++i) {
+            const float sc = bf16_lo(g[d].sb[i]), bi = bf16_hi(g[d].sb[i]);
+#pragma unroll
+            for (int jj = 0; jj < 16; ++jj) {
+              acc[t][i][jj] = fmaf(sc, gq[t][i][jj], acc[t][i][jj]);
+              acc[t][i][jj] = fmaf(bi, xr[jj], acc[t][i][jj]);
+            }
+          }
+        }
+      } else {
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int q = 0; q < 3; ++q)
+#pragma unroll
+            for (int t = 0; t < MT; ++t)
+#pragma unroll
+              for (int i = 0; i < RTW; ++i)
+                acc[t][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, g[d].a[t][q][s]),
+                                                                     __builtin_bit_cast(bf16x8_t, g[d].w[i][s]), acc[t][i], 0, 0, 0);
+      }
       load(j0 + d + PD, g[d]);
       asm volatile("" ::: "memory");
     }
@@ -109,7 +238,9 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
   __shared__ float ct[NB][NBR + 1];
   __shared__ float hb[NB][NBR / 2 + 1];
   __shared__ float rsc[NB];
+  __shared__ float pss[NB][NBR / 8 + 1], phs[NB][NBR / 8 + 1];  // producer: 8-column partial sums
   __shared__ int last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the LDS-DMA prefetch too; the barrier below publishes it)
 #pragma unroll
   for (int t = 0; t < MT; ++t)
 #pragma unroll
@@ -126,7 +257,6 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
     ct[ml][c] = v;
   }
   __syncthreads();
-  const int mrows = min(NB, p.M);
   if (ks > 1) {
     // slice partial [NB][NBR] write-through, ticket; the last slice to arrive sums all in slice order
     const int slab_f = NB * NBR;
@@ -148,33 +278,22 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
     }
     __syncthreads();
     if (!last) return;
-    for (int q = tid; q < mrows * (NBR / 4); q += NTH) {
-      f32x4_t v[MAX_SLICES];
-#pragma unroll
-      for (int s = 0; s < MAX_SLICES; ++s)
-        if (s < ks) v[s] = __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, q * 16, s * slab_f * 4, SC1));
-      f32x4_t sum = v[0];
-#pragma unroll
-      for (int s = 1; s < MAX_SLICES; ++s)
-        if (s < ks) sum += v[s];
-      const int ml = q / (NBR / 4), j = (q % (NBR / 4)) * 4;
-      ct[ml][j] = sum.x;
-      ct[ml][j + 1] = sum.y;
-      ct[ml][j + 2] = sum.z;
-      ct[ml][j + 3] = sum.w;
+    switch (ks) {
+      case 2: combine<2, NB, NBR, NTH>(rs, ct, mrows, slab_f, tid); break;
+      case 4: combine<4, NB, NBR, NTH>(rs, ct, mrows, slab_f, tid); break;
+      case 8: combine<8, NB, NBR, NTH>(rs, ct, mrows, slab_f, tid); break;
+      default: combine<16, NB, NBR, NTH>(rs, ct, mrows, slab_f, tid); break;
     }
     __syncthreads();
   }
   // ---- epilogue
-  const bool norm = p.nw != nullptr;
   if (norm && tid < mrows) {
     float s = 0.f;
-    for (int t = 0; t < p.ss_n; ++t) s += p.ss_in[(size_t)t * p.ss_stride + tid];
+    for (int t = 0; t < p.ss_n; ++t) s += sss[t * NB + tid];
     rsc[tid] = rsqrtf(s / (float)p.K + p.eps);
   }
   __syncthreads();
   const bool prod = p.xs_out != nullptr;
-  const bool silu = p.epi == EPI_SILU_MUL;
   for (int e = tid; e < mrows * (NBR / 2); e += NTH) {
     const int ml = e / (NBR / 2), rp = (e % (NBR / 2)) * 2, n = n0 + rp;
     float va = ct[ml][rp], vb = ct[ml][rp + 1];
@@ -185,8 +304,8 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
     if (n >= p.N) continue;
     if (p.epi == EPI_ADD) {  // residual add (no fused-MLP accumulator / column scale on this path)
       float* o = p.out + (size_t)ml * p.os + n;
-      va = o[0] + va;
-      vb = o[1] + vb;
+      va = res[ml * NBR + rp] + va;
+      vb = res[ml * NBR + rp + 1] + vb;
       o[0] = va;
       o[1] = vb;
     } else if (silu) {  // rows 2j (gate), 2j+1 (up) -> h[j]
@@ -201,23 +320,38 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
   }
   if (prod || p.epi == EPI_ARGMAX) __syncthreads();
   if (prod) {
+    // the produced rows, 8 columns (one 16-B fragment per part) per thread step; per-row sums of squares
+    // (un-normed values) and half-group sums (split values) as 8-column partials in LDS, then summed in
+    // column order
     const int ncol = silu ? NBR / 2 : NBR, col0 = silu ? n0 / 2 : n0, colN = silu ? p.N / 2 : p.N;
-    for (int q = tid; q < mrows * (ncol / 4); q += NTH) {
-      const int ml = q / (ncol / 4), c = (q % (ncol / 4)) * 4, col = col0 + c;
-      if (col >= colN) continue;
-      float v[4];
+    const int ng = ncol / 8;
+    for (int q = tid; q < mrows * ng; q += NTH) {
+      const int ml = q / ng, g8 = q % ng, c = 8 * g8, col = col0 + c;
+      float v[8], sq = 0.f, hsum = 0.f;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        v[u] = silu ? hb[ml][c + u] : ct[ml][c + u];
-        if (p.xs_nw) v[u] *= p.xs_nw[col + u];
+      for (int u = 0; u < 8; ++u) {
+        const float x = silu ? hb[ml][c + u] : ct[ml][c + u];
+        sq = fmaf(x, x, sq);
+        v[u] = p.xs_nw ? x * nws[c + u] : x;
+        hsum += v[u];
       }
-      xs::store4(p.xs_out, p.xs_K, ml, col, v);
+      if (col < colN) xs::store8(p.xs_out, p.xs_K, ml, col, v);
+      pss[ml][g8] = sq;
+      phs[ml][g8] = hsum;
     }
-    if (p.ss_out && !silu && tid < mrows) {  // sum of squares of this tile's new values, column order
-      float s = 0.f;
-      for (int c = 0; c < ncol && col0 + c < colN; ++c) s = fmaf(ct[tid][c], ct[tid][c], s);
-      p.ss_out[(size_t)tile * p.ss_stride + tid] = s;
+    __syncthreads();
+    if (p.ss_out && !silu && tid < mrows) {
+      float sq = 0.f;
+      for (int g8 = 0; g8 < ng; ++g8) sq += pss[tid][g8];
+      p.ss_out[(size_t)tile * p.ss_stride + tid] = sq;
     }
+    if (p.hs_out)  // 32-column halves (4 partials each)
+      for (int q = tid; q < mrows * (ncol / 32); q += NTH) {
+        const int ml = q / (ncol / 32), hh = q % (ncol / 32);
+        if (col0 + 32 * hh >= colN) continue;
+        p.hs_out[(size_t)((col0 + 32 * hh) / 32) * xs::HS_ROWS + ml] =
+            ((phs[ml][4 * hh] + phs[ml][4 * hh + 1]) + phs[ml][4 * hh + 2]) + phs[ml][4 * hh + 3];
+      }
   }
   if (p.epi == EPI_ARGMAX && tid < mrows) {
     unsigned long long best = 0;
@@ -237,7 +371,10 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
 // has >= 256 blocks while every wave keeps >= 1 stage; ring depth <= 4 stages (<= 2 at 64 rows).
 void xs_shape(int N, int K, int M, bool head, int& rtw, int& ks, int& pd) {
   const int nks = K / XK;
-  rtw = (N >= 4096 || K >= 4096 || head) ? 2 : 1;
+  // long-K projections (down) on 32-row tiles: twice the tiles, half the split-K slices and a quarter of
+  // the partial bytes to combine -- 12.1 vs 16.7 us for the decoder down at 32 rows (tools/gemm_bench.py)
+  static const int rtw_long = [] { const char* v = getenv("CSM_XS_LONGK_RTW"); return v ? atoi(v) : 1; }();
+  rtw = (N >= 4096 || head) ? 2 : (K >= 4096 ? rtw_long : 1);
   const int tiles = (N + 32 * rtw - 1) / (32 * rtw);
   ks = 1;
   while (tiles * ks < 256 && ks < MAX_SLICES && nks / (ks * 2) >= XW && nks % (ks * 2) == 0) ks *= 2;
@@ -258,7 +395,14 @@ size_t xs_need(int N, int K, int M, bool head, size_t& tk) {
 }  // namespace
 
 bool gemm_xs_eligible(int N, int K, int M, int wdt) {
-  return wdt == WDT_BF16 && M >= 1 && M <= GEMM_XS_MAX_M && N % 2 == 0 && K % XK == 0 && K / XK >= XW;
+  if (!(wdt == WDT_BF16 || wdt == WDT_Q4) || M < 1 || M > GEMM_XS_MAX_M || N % 2 || K % XK || K / XK < XW) return false;
+  if (wdt == WDT_Q4)  // the X_g stage table holds <= Q4_WST_MAX stages per wave
+    for (int h = 0; h < 2; ++h) {
+      int rtw, ks, pd;
+      xs_shape(N, K, M, h == 1, rtw, ks, pd);
+      if (K / XK / ks / XW > Q4_WST_MAX) return false;
+    }
+  return true;
 }
 
 int gemm_xs_tiles(int N, int K, int M) {
@@ -295,7 +439,7 @@ bool gemm_xs_reserve(GemmWs& ws, int N, int K, int Mmax) {
   return moved;
 }
 
-void launch_gemm_xs(const GemvParams& p0, int epi, hipStream_t st, bool nt_w) {
+void launch_gemm_xs(const GemvParams& p0, int epi, hipStream_t st, bool nt_w, int wdt) {
   GemvParams p = p0;
   p.epi = epi;
   p.Wt = nullptr;
@@ -303,14 +447,18 @@ void launch_gemm_xs(const GemvParams& p0, int epi, hipStream_t st, bool nt_w) {
     const auto ti = p.ws->tiled.find(p.W);
     if (ti != p.ws->tiled.end()) p.Wt = ti->second;
   }
-  if (!p.Wt || !p.xs_in || p.M > GEMM_XS_MAX_M || p.xacc || p.oacc || p.scale) {
+  if (!p.Wt || !p.xs_in || p.M > GEMM_XS_MAX_M || p.xacc || p.oacc || p.scale || (wdt == WDT_Q4 && !p.hs_in) ||
+      !gemm_xs_eligible(p.N, p.K, p.M, wdt)) {
     fprintf(stderr, "csm: gemm_xs launch without a tiled weight / split activations, or with an unsupported option (N=%d K=%d M=%d)\n",
             p.N, p.K, p.M);
     abort();
   }
-  const bool head = epi == EPI_ARGMAX;
+  // 64-row tiles for the heads (arg-max partial count) and for SiLU*up producers (32 whole output
+  // columns per tile: the int4 consumer's half-group sums never span two tiles)
+  const bool head = epi == EPI_ARGMAX || epi == EPI_SILU_MUL;
   int rtw, ks, pd;
   xs_shape(p.N, p.K, p.M, head, rtw, ks, pd);
+  if (wdt == WDT_Q4 && rtw == 2 && pd > 2) pd = 2;  // the int4 fold's per-group products: a shorter ring (no spills)
   p.ksplit = ks;
   const int tiles = (p.N + 32 * rtw - 1) / (32 * rtw);
   if (ks > 1) {
@@ -325,13 +473,17 @@ void launch_gemm_xs(const GemvParams& p0, int epi, hipStream_t st, bool nt_w) {
   }
   // non-temporal weight loads: the audio_head slices and the backbone (read once per frame) stay out of the
   // caches the decoder's weights are re-read from
-  const bool nt = head || nt_w;
+  const bool nt = epi == EPI_ARGMAX || nt_w;
   const dim3 grid(tiles, ks);
-#define GX_K(MT_, RTW_, PD_) do { if (nt) hipLaunchKernelGGL((gemm_xs_kernel<MT_, RTW_, PD_, true>), grid, dim3(64 * XW), 0, st, p); \
-                                  else hipLaunchKernelGGL((gemm_xs_kernel<MT_, RTW_, PD_, false>), grid, dim3(64 * XW), 0, st, p); } while (0)
-#define GX_P(MT_, RTW_) do { if (pd == 4) GX_K(MT_, RTW_, (MT_ == 1 ? 4 : 2)); else if (pd == 2) GX_K(MT_, RTW_, 2); else GX_K(MT_, RTW_, 1); } while (0)
-  if (p.M > 32) { if (rtw == 2) GX_P(2, 2); else GX_P(2, 1); }
-  else { if (rtw == 2) GX_P(1, 2); else GX_P(1, 1); }
+#define GX_K(Q_, MT_, RTW_, PD_) do { if (nt) hipLaunchKernelGGL((gemm_xs_kernel<Q_, MT_, RTW_, PD_, true>), grid, dim3(64 * XW), 0, st, p); \
+                                      else hipLaunchKernelGGL((gemm_xs_kernel<Q_, MT_, RTW_, PD_, false>), grid, dim3(64 * XW), 0, st, p); } while (0)
+#define GX_P(Q_, MT_, RTW_) do { if (pd == 4) GX_K(Q_, MT_, RTW_, (MT_ == 1 ? 4 : 2)); else if (pd == 2) GX_K(Q_, MT_, RTW_, 2); \
+                                 else GX_K(Q_, MT_, RTW_, 1); } while (0)
+#define GX_M(Q_) do { if (p.M > 32) { if (rtw == 2) GX_P(Q_, 2, 2); else GX_P(Q_, 2, 1); } \
+                      else { if (rtw == 2) GX_P(Q_, 1, 2); else GX_P(Q_, 1, 1); } } while (0)
+  if (wdt == WDT_Q4) GX_M(true);
+  else GX_M(false);
+#undef GX_M
 #undef GX_P
 #undef GX_K
 }

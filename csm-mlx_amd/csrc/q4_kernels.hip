@@ -9,6 +9,7 @@
 #include <climits>
 
 #include "csm_kernels.h"
+#include "xs.h"
 
 // ============================================================================ quantize
 // One thread per (row, group of 64): MLX affine rule in fp32 (IEEE div / rint, as numpy does in the
@@ -151,6 +152,30 @@ __global__ __launch_bounds__(256) void embed_rows_q4_kernel(EmbedParams p, int n
     }
     *reinterpret_cast<float4*>(out + d0) = make_float4(acc[0], acc[1], acc[2], acc[3]);
     *reinterpret_cast<float4*>(out + d0 + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
+    if (p.xs_out) {  // streaming backbone operand, as embed_rows_kernel: split (x * n1), sums of squares
+      const int t = threadIdx.x & 63;  // per 512 columns (one wave), half-group sums per 32 (4 lanes)
+      float sq = 0.f, hsum = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sq = fmaf(acc[e], acc[e], sq);
+      sq = wave_sum(sq);
+      if (t == 0) p.ss_out[(size_t)(d0 / 512) * p.ss_stride + m] = sq;
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf) {
+        float v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          v[u] = acc[4 * hf + u] * p.xs_nw[d0 + 4 * hf + u];
+          hsum += v[u];
+        }
+        xs::store4(p.xs_out, p.D, m, d0 + 4 * hf, v);
+      }
+      if (p.hs_out) {
+        const int b4 = t & ~3;
+        const float h0 = __shfl(hsum, b4, 64), h1 = __shfl(hsum, b4 + 1, 64), h2 = __shfl(hsum, b4 + 2, 64),
+                    h3 = __shfl(hsum, b4 + 3, 64);
+        if ((t & 3) == 0) p.hs_out[(size_t)(d0 / 32) * xs::HS_ROWS + m] = ((h0 + h1) + h2) + h3;
+      }
+    }
   }
 }
 

@@ -52,6 +52,23 @@ __device__ __forceinline__ void store4(void* base, int K, int m, int k, const fl
       u32x2_t{__builtin_amdgcn_perm(l[1], l[0], 0x07060302u), __builtin_amdgcn_perm(l[3], l[2], 0x07060302u)};
 }
 
+// eight consecutive columns k .. k+7 (k % 8 == 0) of row m: one lane's whole 16-B fragment per part
+__device__ __forceinline__ void store8(void* base, int K, int m, int k, const float (&v)[8]) {
+  uint32_t h[8], md[8], l[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) split3(v[q], h[q], md[q], l[q]);
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  uint8_t* p = reinterpret_cast<uint8_t*>(base) + off(K, m, k);
+  *reinterpret_cast<u32x4*>(p) = u32x4{__builtin_amdgcn_perm(h[1], h[0], 0x07060302u), __builtin_amdgcn_perm(h[3], h[2], 0x07060302u),
+                                      __builtin_amdgcn_perm(h[5], h[4], 0x07060302u), __builtin_amdgcn_perm(h[7], h[6], 0x07060302u)};
+  *reinterpret_cast<u32x4*>(p + XS_PART) =
+      u32x4{__builtin_amdgcn_perm(md[1], md[0], 0x07060302u), __builtin_amdgcn_perm(md[3], md[2], 0x07060302u),
+            __builtin_amdgcn_perm(md[5], md[4], 0x07060302u), __builtin_amdgcn_perm(md[7], md[6], 0x07060302u)};
+  *reinterpret_cast<u32x4*>(p + 2 * XS_PART) =
+      u32x4{__builtin_amdgcn_perm(l[1], l[0], 0x07060302u), __builtin_amdgcn_perm(l[3], l[2], 0x07060302u),
+            __builtin_amdgcn_perm(l[5], l[4], 0x07060302u), __builtin_amdgcn_perm(l[7], l[6], 0x07060302u)};
+}
+
 // one element (2-byte store per part)
 __device__ __forceinline__ void store1(void* base, int K, int m, int k, float v) {
   uint32_t h, md, l;
@@ -60,6 +77,26 @@ __device__ __forceinline__ void store1(void* base, int K, int m, int k, float v)
   p[0] = (uint16_t)(h >> 16);
   p[XS_PART / 2] = (uint16_t)(md >> 16);
   p[XS_PART] = (uint16_t)(l >> 16);
+}
+
+// int4 consumers (MLX affine, w = scale * q + bias per group of 64 k) need the group sums
+// X_g = sum_{k in g} a[m][k] of the split rows (the bias term): producers also publish half-group
+// sums hs[k / 32][HS_ROWS] (32 columns, summed in column order), the consumer adds the two halves.
+constexpr int HS_ROWS = 64;
+
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+// one uint32 of MLX int4 nibbles (k = 8s .. 8s+7, low nibble first) -> 8 exact bf16 (u32x4 of pairs):
+// bytes of the even / odd nibbles through v_cvt_f32_ubyte*, the floats' high halves paired by v_perm
+__device__ __forceinline__ u32x4_t q4_word_bf16(uint32_t u) {
+  const uint32_t a = u & 0x0F0F0F0Fu, b = (u >> 4) & 0x0F0F0F0Fu;
+  u32x4_t o;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t fa = __float_as_uint((float)((a >> (8 * i)) & 0xFFu));
+    const uint32_t fb = __float_as_uint((float)((b >> (8 * i)) & 0xFFu));
+    o[i] = __builtin_amdgcn_perm(fb, fa, 0x07060302u);  // {hi16(fa), hi16(fb)}
+  }
+  return o;
 }
 
 }  // namespace xs

@@ -166,12 +166,13 @@ def test_csm_1b_bf16_batch_composition_invariance():
         assert np.abs(a - b).max() <= 2e-3 * np.abs(a).max()
 
 
-@pytest.mark.parametrize("B", [8, 24])
-def test_streaming_decoder_matches_wide_gemm(B):
+@pytest.mark.parametrize("B,dtype,bb", [(8, "bf16", 0), (24, "bf16", 0), (24, "q4", 0), (24, "bf16", 1)])
+def test_streaming_decoder_matches_wide_gemm(B, dtype, bb):
     """The batched depth decoder at codebook steps >= 2 on the streaming matrix-core GEMM over
-    pre-split activations (gemm_xs.hip; option gemm_xs) against the same frames on gemm_wide_kernel:
-    identical greedy codes, ci logits within fp32 summation-order noise (both sum exact fp32
-    products), 4 frames, csm_1b bf16."""
+    pre-split activations (gemm_xs.hip; option gemm_xs, on by default) against the same frames on
+    gemm_wide_kernel: identical greedy codes, ci logits within fp32 summation-order noise (both sum
+    exact fp32 products), 4 frames, csm_1b bf16 and int4; bb=1 also runs the backbone's projections
+    on it (option bb_xs, opt-in)."""
     from csm_mlx import _lib
     from csm_mlx.generation import FrameCache
     from csm_mlx.sampling import Sampler
@@ -180,11 +181,12 @@ def test_streaming_decoder_matches_wide_gemm(B):
     K, V = args.n_audio_codebooks, args.n_audio_vocab
     Vp = (V + 7) // 8 * 8
     prompts = [tokenize_text_segment(prompt_ids(900 + b, 9 + b % 4), 0, K) for b in range(B)]
-    model = _model(args, w, "bf16", B)
+    model = _model(args, w, dtype, B)
     L = _lib.lib()
     out = []
     for on in (0, 1):
         _lib.check(L.csm_set_option(model.engine, b"gemm_xs", on))
+        _lib.check(L.csm_set_option(model.engine, b"bb_xs", on * bb))
         cache = FrameCache(model, B, Sampler(0.0, 0), [0] * B)
         cache.prefill_batch([(b, t, m) for b, (t, m) in enumerate(prompts)])
         logs = []
@@ -195,6 +197,7 @@ def test_streaming_decoder_matches_wide_gemm(B):
         out.append((hist.copy(), n.copy(), logs))
         del cache
     _lib.check(L.csm_set_option(model.engine, b"gemm_xs", 1))
+    _lib.check(L.csm_set_option(model.engine, b"bb_xs", 0))
     del model
     (h0, n0, l0), (h1, n1, l1) = out
     assert np.array_equal(n0, n1) and np.array_equal(h0, h1), "streaming decoder codes differ from gemm_wide"

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Per-projection microbench of the batched MFMA GEMM (csm_bench_gemv: one launch per layer in turn,
 HIP events on the engine stream) for csm_1b at a few row counts.
-usage: python tools/gemm_bench.py bf16|q4 [M ...]   -> one line per (stack, projection, M)"""
+usage: python tools/gemm_bench.py bf16|q4 [M ...]   -> one line per (stack, projection, M)
+GB_XS=1: also the streaming matrix-core GEMM over pre-split activations (gemm_xs, which | 8) beside it."""
 import ctypes
 import os
 import sys
@@ -21,7 +22,9 @@ tot = {}
 for M in Ms:
     for stack in (1, 0):
         for kind in range(4):
-            us, nb = ctypes.c_float(0), ctypes.c_double(0)
-            _lib.check(L.csm_bench_gemv(model.engine, stack * 4 + kind, M, iters, ctypes.byref(us), ctypes.byref(nb)))
-            print(f"{dtype} M={M:3d} {'dec' if stack else 'bb '} {names[kind]:7s} {us.value:8.2f} us "
-                  f"{nb.value / 1e6:8.2f} MB {nb.value / us.value / 1e3:7.0f} GB/s", flush=True)
+            for xs in ((0, 8, 24) if os.environ.get("GB_XS") == "1" and M <= 64 else (0,)):
+                us, nb = ctypes.c_float(0), ctypes.c_double(0)
+                _lib.check(L.csm_bench_gemv(model.engine, stack * 4 + kind + xs, M, iters, ctypes.byref(us),
+                                            ctypes.byref(nb)))
+                print(f"{dtype} M={M:3d} {'dec' if stack else 'bb '} {names[kind]:7s} { {0: 'wide', 8: 'xs  ', 24: 'xs-p'}[xs] } "
+                      f"{us.value:8.2f} us {nb.value / 1e6:8.2f} MB {nb.value / us.value / 1e3:7.0f} GB/s", flush=True)
