@@ -170,12 +170,17 @@ def context_audio(g: int, seg: int, seconds: float = 5.0):
     return (0.1 * x + rng.normal(0.0, 0.01, t.shape)).astype(np.float32)
 
 
-def context_prompts(mine, K: int = 32):
-    """Config 5 prompts: 3 context Segments (12 text ids + 5 s audio, Mimi-encoded) + the 12-id text."""
+def context_segments(mine):
+    """Config 5 input data: 3 context Segments per utterance (12 text ids + 5 s of synthetic audio).
+    Built once, outside the timed region (the audio is the workload's input, like the prompt ids)."""
     from csm_mlx.segment import Segment
+    return [Segment(seg % 2, prompt_ids(10_000 + 10 * g + seg), context_audio(g, seg)) for g in mine for seg in range(3)]
+
+
+def context_prompts(mine, segs, K: int = 32):
+    """Config 5 prompts: the 3 context Segments (Mimi-encoded: generation.py:108-125, timed) + the 12-id text."""
     from csm_mlx.tokenizers import tokenize_segments_batch, tokenize_text_segment
     # every utterance's context audio goes through ONE batched Mimi encode (same-length segments)
-    segs = [Segment(seg % 2, prompt_ids(10_000 + 10 * g + seg), context_audio(g, seg)) for g in mine for seg in range(3)]
     enc = tokenize_segments_batch(segs, n_audio_codebooks=K)
     out = []
     for u, g in enumerate(mine):
@@ -366,6 +371,8 @@ def main():
         return [998] + [int(x) for x in rng.integers(0, 990, 3 + g % 4)] + [999]
     if not cfg["context"]:
         prompts = [tokenize_text_segment(ids_of(g), 0, K) for g in mine]
+    else:
+        ctx_segs = context_segments(mine)
     last = {}
 
     phases = {} if args.phases else None
@@ -373,7 +380,7 @@ def main():
     def step():
         # config 5: the context Segments' Mimi encode is part of every step (generation.py:108-125)
         t_enc = time.perf_counter()
-        pr = context_prompts(mine) if cfg["context"] else prompts
+        pr = context_prompts(mine, ctx_segs) if cfg["context"] else prompts
         if phases is not None and cfg["context"]:
             phases["mimi_encode"] = phases.get("mimi_encode", 0.0) + time.perf_counter() - t_enc
         if cfg["stream"]:

@@ -36,11 +36,19 @@ constexpr int QKV = (HQ + 2 * HKV) * HD;  // 3072
 constexpr int NATT = HQ;                  // attention workgroups: one per query head
 constexpr unsigned SPIN_LIMIT = 1u << 22; // ~0.1 s of s_sleep per hand-off before declaring failure
 
-// granule regions (u64 offsets), double-buffered by hand-off parity
+// granule regions (u64 offsets), double-buffered by hand-off parity.  The all-gather regions (E2,
+// E3, E5: every workgroup reads every granule) are written in REP replicas, workgroup w reading
+// replica w % REP (dec_frame.hip: fewer readers per granule; speed only, never correctness).
+// Measured: 581-584 us (REP 1 / 8) -> 569 us (REP 4) per row (profiles/r03_ab_replicas.txt).
+#ifndef BB_REP
+#define BB_REP 4
+#endif
+constexpr int REP = BB_REP;
+__host__ __device__ constexpr size_t rs_of(size_t per) { return (per + 511) / 512 * 512 + 32; }
 constexpr size_t G_QKV = 0;                                   // [2][QKV]
-constexpr size_t G_ATT = G_QKV + 2 * QKV;                     // [2][D]
-constexpr size_t G_X = G_ATT + 2 * D;                         // [2][D]
-constexpr size_t G_PART = G_X + 2 * D;                        // [2][NWG][D]
+constexpr size_t G_ATT = G_QKV + 2 * QKV;                     // [2][REP][rs(D)]
+constexpr size_t G_X = G_ATT + 2 * REP * rs_of(D);            // [2][REP][rs(D)]
+constexpr size_t G_PART = G_X + 2 * REP * rs_of(D);           // [2][NWG][D]
 constexpr size_t G_TOTAL = G_PART + (size_t)2 * NWG * D;
 
 struct Lds {
@@ -69,6 +77,14 @@ struct Ctx {
   }
   __device__ unsigned tag() const { return tag0 + (unsigned)e; }
   __device__ u64* buf(size_t region, size_t per) const { return p.gbuf + region + (size_t)(e & 1) * per; }
+  // replicated all-gather regions: this workgroup's replica (reads), and a store to every replica
+  __device__ u64* rbuf(size_t region, size_t per) const {
+    return p.gbuf + region + ((size_t)(e & 1) * REP + (size_t)(w % REP)) * rs_of(per);
+  }
+  // one replica r of granule i (publishing lanes spread over the replicas: one store each)
+  __device__ void put(size_t region, size_t per, size_t i, float v, int r) const {
+    gput(p.gbuf + region + ((size_t)(e & 1) * REP + (size_t)r) * rs_of(per) + i, v, tag());
+  }
   // profiling: the 100 MHz real-time clock when this WG passed hand-off e (slot e + 1; slot 0 = start)
   __device__ void stamp(int slot) const {
     if (p.stamps && tid == 0 && slot < BB_STEP_STAMPS) p.stamps[(size_t)w * BB_STEP_STAMPS + slot] = __builtin_amdgcn_s_memrealtime();
@@ -297,7 +313,7 @@ __device__ __forceinline__ void phase_attn(Ctx& c, int l, int pos) {
   c.L.ao[c.wave][c.lane] = o;
   if (c.lane == 0) { c.L.am[c.wave] = m_run; c.L.al[c.wave] = l_run; }
   __syncthreads();
-  if (c.wave == 0) {
+  if (c.wave < REP) {  // wave r combines (identically) and publishes replica r
     float M = -INFINITY;
 #pragma unroll
     for (int v = 0; v < 8; ++v) M = fmaxf(M, c.L.am[v]);
@@ -308,7 +324,7 @@ __device__ __forceinline__ void phase_attn(Ctx& c, int l, int pos) {
       Ls = fmaf(c.L.al[v], wv, Ls);
       O = fmaf(c.L.ao[v][c.lane], wv, O);
     }
-    gput(c.buf(G_ATT, D) + a * HD + c.lane, O / Ls, c.tag());  // E2
+    c.put(G_ATT, D, a * HD + c.lane, O / Ls, c.wave);  // E2
   }
 }
 
@@ -319,9 +335,9 @@ __device__ __forceinline__ void phase_o(Ctx& c, const WO& W) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) s[i] = dot8(W.a[i], xc);
   rows_reduce<4>(c, s);
-  if (c.tid < 8) {
-    const int h = c.tid / 4, i = c.tid % 4, n = 8 * c.w + c.tid;
-    gput(c.buf(G_X, D) + n, c.L.x[n] + row_total(c, h, i), c.tag());
+  if (c.tid < 8 * REP) {
+    const int q = c.tid / REP, h = q / 4, i = q % 4, n = 8 * c.w + q;
+    c.put(G_X, D, n, c.L.x[n] + row_total(c, h, i), c.tid % REP);
   }
 }
 
@@ -374,9 +390,9 @@ __device__ __forceinline__ void phase_reduce(Ctx& c) {
     const float* r = c.L.red[c.wave];
     float s = ((r[4 * c.lane] + r[4 * c.lane + 1]) + r[4 * c.lane + 2]) + r[4 * c.lane + 3];
     s = wave_sum(s);
-    if (c.lane == 0) {
+    if (c.lane < REP) {
       const int n = 8 * c.w + c.wave;
-      gput(c.buf(G_X, D) + n, c.L.x[n] + s, c.tag());
+      c.put(G_X, D, n, c.L.x[n] + s, c.lane);
     }
   }
 }
@@ -416,12 +432,12 @@ __global__ __launch_bounds__(NT, 1) void bb_step_kernel(BbStepArgs p) {
       phase_attn(c, l, pos);                          // waits E1, -> E2
       load_mq(c, l, 1, mq[1]);
     }
-    gather<D / NT>(c, c.buf(G_ATT, D), D, L.att);     // E2
+    gather<D / NT>(c, c.rbuf(G_ATT, D), D, L.att);     // E2
     ++c.e;
     c.refresh();
     phase_o(c, wo);                                   // -> E3
     if (l + 1 < NL) load_q(c, l + 1, wq);
-    gather<D / NT>(c, c.buf(G_X, D), D, L.x);         // E3
+    gather<D / NT>(c, c.rbuf(G_X, D), D, L.x);         // E3
     ++c.e;
     c.refresh();
     rms(c, nw2, L.xn);
@@ -440,7 +456,7 @@ __global__ __launch_bounds__(NT, 1) void bb_step_kernel(BbStepArgs p) {
     nw1 = nw_fetch(c, l + 1 < NL ? p.n1[l + 1] : p.norm);
     c.refresh();
     phase_reduce(c);                                  // waits E4, -> E5
-    gather<D / NT>(c, c.buf(G_X, D), D, L.x);         // E5
+    gather<D / NT>(c, c.rbuf(G_X, D), D, L.x);         // E5
     ++c.e;
   }
   // final norm of the last row -> h_last (generation.py:42 reads norm(h[:, -1]))

@@ -103,13 +103,26 @@ struct Lds {
 
 namespace {
 
-// Granule buffer regions (u64 offsets), each double-buffered by hand-off parity.
-constexpr size_t G_X = 0;                                  // [2][MAXM][D] x slices
-constexpr size_t G_QKV = G_X + 2 * MAXM * D;               // [2][MAXM][QKV]
-constexpr size_t G_PART = G_QKV + 2 * MAXM * QKV;          // [2][NWG][MAXM][D] down partials
-constexpr size_t G_ARG = G_PART + (size_t)2 * NWG * MAXM * D;  // [2][NWG][2] arg-max keys
-constexpr size_t G_LOG = G_ARG + 2 * NWG * 2;              // [2][VMAX] logits (sampling)
-constexpr size_t G_TOTAL = G_LOG + 2 * VMAX;
+// Granule buffer regions (u64 offsets), each double-buffered by hand-off parity.  The all-gather
+// regions (every workgroup reads every granule) are written in REP replicas: a producer stores each
+// granule REP times, workgroup w polls replica w % REP -- the workgroups of one XCD under the
+// observed round-robin placement (speed only, never correctness), so each granule has 256 / REP
+// readers instead of 256 (MI355X_MICROARCH.md allgather row: 256 -> 32 readers of a 16 KB sweep
+// -1.9 us).  Replicas are 4 KB-aligned plus a 256-B skew so they fall on different channels.
+// The reduce-scatter region (G_PART: each granule has one reader) is not replicated.  Measured
+// (profiles/r03_ab_replicas.txt): 2394 -> 2325 us per frame at REP 4 or 8 with the replica stores
+// spread over lanes (stored serially by one lane, REP 8 cost more on the publish than it saved).
+#ifndef DF_REP
+#define DF_REP 4
+#endif
+constexpr int REP = DF_REP;
+__host__ __device__ constexpr size_t rs_of(size_t per) { return (per + 511) / 512 * 512 + 32; }
+constexpr size_t G_X = 0;                                               // [2][REP][rs(MAXM*D)] x slices
+constexpr size_t G_QKV = G_X + 2 * REP * rs_of(MAXM * D);               // [2][REP][rs(MAXM*QKV)]
+constexpr size_t G_PART = G_QKV + 2 * REP * rs_of(MAXM * QKV);          // [2][NWG][MAXM][D] down partials
+constexpr size_t G_ARG = G_PART + (size_t)2 * NWG * MAXM * D;           // [2][REP][rs(NWG*2)] arg-max keys
+constexpr size_t G_LOG = G_ARG + 2 * REP * rs_of(NWG * 2);              // [2][REP][rs(VMAX)] logits (sampling)
+constexpr size_t G_TOTAL = G_LOG + 2 * REP * rs_of(VMAX);
 
 struct Ctx {
   const DecFrameArgs& p;
@@ -133,6 +146,18 @@ struct Ctx {
   }
   __device__ unsigned tag() const { return tag0 + (unsigned)e; }
   __device__ u64* buf(size_t region, size_t per) const { return p.gbuf + region + (size_t)(e & 1) * per; }
+  // replicated all-gather regions: this workgroup's replica (reads), and a store to every replica
+  __device__ u64* rbuf(size_t region, size_t per) const {
+    return p.gbuf + region + ((size_t)(e & 1) * REP + (size_t)(w % REP)) * rs_of(per);
+  }
+  // one replica r of granule i: the publishing lanes are spread over the replicas (lane-parallel
+  // stores, one per lane), so a hand-off costs its producer one store instruction, not REP
+  __device__ void put(size_t region, size_t per, size_t i, float v, int r) const {
+    gput(p.gbuf + region + ((size_t)(e & 1) * REP + (size_t)r) * rs_of(per) + i, v, tag());
+  }
+  __device__ void put_u(size_t region, size_t per, size_t i, unsigned v, int r) const {
+    gput_u(p.gbuf + region + ((size_t)(e & 1) * REP + (size_t)r) * rs_of(per) + i, v, tag());
+  }
 };
 
 // Wait until granules [0, n) of buf carry `tag`; values -> out (LDS).  Threads take granules
@@ -265,9 +290,8 @@ __device__ __forceinline__ void phase_qkv(Ctx& c, int pos0, const WQkv& W) {
     if (c.lane == 0) { c.L.wsum[c.wave][0] = s0; if constexpr (M == 2) c.L.wsum[c.wave][1] = s1; }
   }
   __syncthreads();
-  u64* g = c.buf(G_QKV, MAXM * QKV);
-  if (c.tid < 3 * M) {  // RoPE pair j of row m: rows n, n+1 = 6w + 2j, +1
-    const int m = c.tid / 3, j = c.tid % 3, n = 6 * c.w + 2 * j;
+  if (c.tid < 3 * M * REP) {  // RoPE pair j of row m: rows n, n+1 = 6w + 2j, +1 -> replica rr
+    const int pr = c.tid / REP, rr = c.tid % REP, m = pr / 3, j = pr % 3, n = 6 * c.w + 2 * j;
     float a = c.L.wsum[2 * j][m], b = c.L.wsum[2 * j + 1][m];
     if (n < (HQ + HKV) * HD) {
       const int d = n % HD;
@@ -276,8 +300,8 @@ __device__ __forceinline__ void phase_qkv(Ctx& c, int pos0, const WQkv& W) {
       a = y0;
       b = y1;
     }
-    gput(g + (size_t)m * QKV + n, a, c.tag());
-    gput(g + (size_t)m * QKV + n + 1, b, c.tag());
+    c.put(G_QKV, MAXM * QKV, (size_t)m * QKV + n, a, rr);
+    c.put(G_QKV, MAXM * QKV, (size_t)m * QKV + n + 1, b, rr);
   }
 }
 
@@ -406,10 +430,10 @@ __device__ __forceinline__ void phase_o(Ctx& c, const WO& W) {
     if (c.lane == 0) { c.L.wsum[c.wave][0] = s0; if constexpr (M == 2) c.L.wsum[c.wave][1] = s1; }
   }
   __syncthreads();
-  if (c.tid < 4 * M) {
-    const int m = c.tid / 4, r = c.tid % 4, n = 4 * c.w + r;
+  if (c.tid < 4 * M * REP) {
+    const int q = c.tid / REP, m = q / 4, r = q % 4, n = 4 * c.w + r;
     const float o = c.L.wsum[2 * r][m] + c.L.wsum[2 * r + 1][m];
-    gput(c.buf(G_X, MAXM * D) + (size_t)m * D + n, c.L.x[m][n] + o, c.tag());
+    c.put(G_X, MAXM * D, (size_t)m * D + n, c.L.x[m][n] + o, c.tid % REP);
   }
 }
 
@@ -494,9 +518,9 @@ __device__ __forceinline__ void phase_reduce(Ctx& c) {
     const float* r = c.L.red[c.wave];
     float s = ((r[4 * c.lane] + r[4 * c.lane + 1]) + r[4 * c.lane + 2]) + r[4 * c.lane + 3];
     s = wave_sum(s);
-    if (c.lane == 0) {
+    if (c.lane < REP) {
       const int m = c.wave / 4, n = 4 * c.w + c.wave % 4;
-      gput(c.buf(G_X, MAXM * D) + (size_t)m * D + n, c.L.x[m][n] + s, c.tag());
+      c.put(G_X, MAXM * D, (size_t)m * D + n, c.L.x[m][n] + s, c.lane);
     }
   }
 }
@@ -524,28 +548,26 @@ __device__ __forceinline__ void phase_head(Ctx& c, const bf16_t* W, int n_valid,
     if (c.lane == 0 && xr < n_valid) logits[xr] = t;
   }
   if (c.p.temperature > 0.f) {  // sampling: every logit to every workgroup (sample_code)
-    u64* g = c.buf(G_LOG, VMAX);
-    if (c.lane == 0 && row < n_valid) gput(g + row, s, c.tag());
-    if (c.lane == 0 && c.wave == 0 && c.w < 3 && xr < n_valid) gput(g + xr, t, c.tag());
+    if (c.lane < REP && row < n_valid) c.put(G_LOG, VMAX, row, s, c.lane);
+    if (c.lane < REP && c.wave == 0 && c.w < 3 && xr < n_valid) c.put(G_LOG, VMAX, xr, t, c.lane);
     __syncthreads();
     return;
   }
   if (c.lane == 0) reinterpret_cast<unsigned long long*>(c.L.wsum)[c.wave] = best;
   __syncthreads();
-  if (c.tid == 0) {
+  if (c.tid < REP) {
     const unsigned long long* k = reinterpret_cast<const unsigned long long*>(c.L.wsum);
     unsigned long long b = k[0];
     for (int i = 1; i < 8; ++i) b = k[i] > b ? k[i] : b;
-    u64* g = c.buf(G_ARG, NWG * 2) + 2 * c.w;
-    gput_u(g, (unsigned)(b >> 32), c.tag());
-    gput_u(g + 1, (unsigned)b, c.tag());
+    c.put_u(G_ARG, NWG * 2, 2 * c.w, (unsigned)(b >> 32), c.tid);
+    c.put_u(G_ARG, NWG * 2, 2 * c.w + 1, (unsigned)b, c.tid);
   }
   __syncthreads();
 }
 
 // Gather the 256 arg-max keys -> code (every WG identical)
 __device__ __forceinline__ int gather_code(Ctx& c, int V) {
-  gather<1>(c, c.buf(G_ARG, NWG * 2), NWG * 2, &c.L.red[0][0]);
+  gather<1>(c, c.rbuf(G_ARG, NWG * 2), NWG * 2, &c.L.red[0][0]);
   if (c.wave == 0) {
     const unsigned* u = reinterpret_cast<const unsigned*>(&c.L.red[0][0]);
     unsigned long long b = 0;
@@ -579,7 +601,7 @@ __device__ __forceinline__ int sample_code(Ctx& c, int V, int cb) {
     const int v = c.tid + NT * i;
     gn[i] = v < V ? gumbel_noise(key, v) : 0.0;
   }
-  gather<NPT>(c, c.buf(G_LOG, VMAX), V, c.L.lg);
+  gather<NPT>(c, c.rbuf(G_LOG, VMAX), V, c.L.lg);
   float thr = -INFINITY;
   if (p.top_k > 0 && p.top_k < V) {
     // radix select, 8 bits per pass; threads 0..255 hold digit 255 - tid for the suffix count
@@ -720,7 +742,7 @@ __device__ __forceinline__ void decoder_layer(Ctx& c, int l, int step, int pos0,
     // them in vmcnt order), still ahead of the hand-off wait they hide under
     kv_issue(c, l, pos0, kv);
     load_dn(c, l, r.wd);
-    gather<(M * QKV + NT - 1) / NT>(c, c.buf(G_QKV, MAXM * QKV), M * QKV, &L.qkv[0][0]);
+    gather<(M * QKV + NT - 1) / NT>(c, c.rbuf(G_QKV, MAXM * QKV), M * QKV, &L.qkv[0][0]);
     ++c.e;
     kv_store(c, pos0, kv);
     kv_append<M>(c, pos0);
@@ -736,7 +758,7 @@ __device__ __forceinline__ void decoder_layer(Ctx& c, int l, int step, int pos0,
   c.mark();
   load_gu<GU_EARLY, 8>(c, l, r.wg);
   if (!LAST) { load_qkv(c, l + 1, r.wq); load_o(c, l + 1, r.wo); }
-  gather<M * D / NT>(c, c.buf(G_X, MAXM * D), M * D, &L.x[0][0]);
+  gather<M * D / NT>(c, c.rbuf(G_X, MAXM * D), M * D, &L.x[0][0]);
   ++c.e;
   c.refresh();
   rms_rows<M>(c, nw2);
@@ -752,7 +774,7 @@ __device__ __forceinline__ void decoder_layer(Ctx& c, int l, int step, int pos0,
   }
   c.refresh();
   phase_reduce<M>(c);                                 // waits E4, -> E5
-  gather<M * D / NT>(c, c.buf(G_X, MAXM * D), M * D, &L.x[0][0]);
+  gather<M * D / NT>(c, c.rbuf(G_X, MAXM * D), M * D, &L.x[0][0]);
   ++c.e;
 }
 
@@ -810,10 +832,13 @@ __global__ __launch_bounds__(NT, 1) void dec_frame_kernel(DecFrameArgs p) {
     s = wave_sum(s);
     if (c.lane == 0) L.wsum[c.wave][0] = s;
     __syncthreads();
-    if (c.tid < 4) gput(c.buf(G_X, MAXM * D) + 4 * c.w + c.tid, L.wsum[2 * c.tid][0] + L.wsum[2 * c.tid + 1][0], c.tag());
+    if (c.tid < 4 * REP) {
+      const int q = c.tid / REP;
+      c.put(G_X, MAXM * D, 4 * c.w + q, L.wsum[2 * q][0] + L.wsum[2 * q + 1][0], c.tid % REP);
+    }
   }
   const int c0 = head_code(c, p.V, 0);
-  gather<2>(c, c.buf(G_X, MAXM * D), D, L.x[0]);  // x row 0 = projection(h_last)
+  gather<2>(c, c.rbuf(G_X, MAXM * D), D, L.x[0]);  // x row 0 = projection(h_last)
   ++c.e;
   if (c.w == 0 && c.tid == 0) p.codes[0] = c0;
   // x row 1 = projection(E_a[c0]) from the folded table (bit-identical to the projection GEMV)

@@ -37,7 +37,7 @@ def main():
     busy = 0.0
     for r in sel:
         d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-        k = r["Kernel_Name"].replace("void ", "")
+        k = r["Kernel_Name"].replace("void ", "").replace("(anonymous namespace)::", "")
         k = k.split("(")[0][:90]
         per[k][0] += 1
         per[k][1] += d
