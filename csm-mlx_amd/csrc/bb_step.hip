@@ -57,6 +57,7 @@ struct Lds {
   float att[D];          // attention output (o_proj input)
   float red[8][NWG];     // reduce-scatter staging [row][producer]
   float wsum[8][8];      // per-wave partial dots
+  float sq[8];           // per-wave partial sums of squares of the gathered x (folded RMSNorm)
   float hb[32];          // this WG's SiLU*up columns
   float2 rope[HD / 2];   // (cos, sin) at the step's position
   float q[HD], kn[HD], vn[HD];          // attention WGs: the head's q and the new k / v row
@@ -153,6 +154,48 @@ __device__ __forceinline__ void rms(Ctx& c, const Nw& nw, float* out) {
   __syncthreads();
 }
 
+// Folded RMSNorm (BB_FOLD, as dec_frame.hip): an x hand-off is gathered into x and xn = x * nw (the
+// next consumer's norm weight) with per-wave sums of squares; consumers dot against the
+// un-normalised xn and scale by rsqrt(mean(x^2) + eps) -- one barrier and one serial pass fewer.
+#ifndef BB_FOLD
+#define BB_FOLD 1
+#endif
+__device__ __forceinline__ void gather_x(Ctx& c, const u64* buf, const Nw& nw) {
+  constexpr int GPT = D / NT;
+  const unsigned tag = c.tag();
+  u64 g[GPT];
+#pragma unroll
+  for (int u = 0; u < GPT; ++u) g[u] = gload(buf + c.tid + u * NT);
+  for (unsigned spin = 0;; ++spin) {
+    bool ok = true;
+#pragma unroll
+    for (int u = 0; u < GPT; ++u) ok &= (unsigned)(g[u] >> 32) == tag;
+    if (ok || spin_fail(c, spin)) break;
+    __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+    for (int u = 0; u < GPT; ++u)
+      if ((unsigned)(g[u] >> 32) != tag) g[u] = gload(buf + c.tid + u * NT);
+  }
+  c.stamp(c.e + 1);
+  float sq = 0.f;
+#pragma unroll
+  for (int u = 0; u < GPT; ++u) {
+    const float v = __uint_as_float((unsigned)g[u]);
+    c.L.x[c.tid + u * NT] = v;
+    c.L.xn[c.tid + u * NT] = v * nw.v[u];
+    sq = fmaf(v, v, sq);
+  }
+  sq = wave_sum(sq);
+  if (c.lane == 0) c.L.sq[c.wave] = sq;
+  __syncthreads();
+}
+__device__ __forceinline__ float row_rs(const Ctx& c) {
+  float s = c.L.sq[0];
+#pragma unroll
+  for (int w = 1; w < 8; ++w) s += c.L.sq[w];
+  return rsqrtf(s / (float)D + c.p.eps);
+}
+
 // ---- weight slices held in registers
 // QKV / o_proj: thread (half h = tid >> 8, chunk c = tid & 255) holds chunk c of rows 6h+i / 4h+i
 struct WQ { u32x4_t a[6]; };
@@ -203,7 +246,7 @@ __device__ __forceinline__ float row_total(const Ctx& c, int h, int i) {
 }
 
 // QKV rows 12w.. (RoPE at pos), published to E1; k / v rows also appended to the cache at pos
-__device__ __forceinline__ void phase_qkv(Ctx& c, int l, int pos, const WQ& W) {
+__device__ __forceinline__ void phase_qkv(Ctx& c, int l, int pos, const WQ& W, bool sc) {
   float s[6];
   const float* xc = c.L.xn + 8 * (c.tid & 255);
 #pragma unroll
@@ -212,6 +255,11 @@ __device__ __forceinline__ void phase_qkv(Ctx& c, int l, int pos, const WQ& W) {
   if (c.tid < 6) {  // pair j: rows n, n + 1 of half h
     const int h = c.tid / 3, i0 = 2 * (c.tid % 3), n = 12 * c.w + 6 * h + i0;
     float a = row_total(c, h, i0), b = row_total(c, h, i0 + 1);
+    if (sc) {  // folded RMSNorm: the row scale after the dot product
+      const float rs = row_rs(c);
+      a *= rs;
+      b *= rs;
+    }
     if (n < (HQ + HKV) * HD) {
       const float2 cs = c.L.rope[(n % HD) / 2];
       const float y0 = a * cs.x - b * cs.y, y1 = b * cs.x + a * cs.y;
@@ -344,7 +392,7 @@ __device__ __forceinline__ void phase_o(Ctx& c, const WO& W) {
 // MLP quarter Q: the wave's gate/up pair -> SiLU*up column 8Q + wave (LDS), then this quarter's 8
 // columns of the down split-K into the four row accumulators (column chunks added in order 0..3)
 template <int Q>
-__device__ __forceinline__ void phase_mq(Ctx& c, const WMq& m, float (&acc)[4]) {
+__device__ __forceinline__ void phase_mq(Ctx& c, const WMq& m, float (&acc)[4], float rs) {
   float t[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
@@ -353,7 +401,7 @@ __device__ __forceinline__ void phase_mq(Ctx& c, const WMq& m, float (&acc)[4]) 
     for (int j = 1; j < 4; ++j) s += dot8(m.g[i][j], c.L.xn + 8 * (c.lane + 64 * j));
     t[i] = wave_sum(s);
   }
-  if (c.lane == 0) c.L.hb[8 * Q + c.wave] = silu_f(t[0]) * t[1];
+  if (c.lane == 0) c.L.hb[8 * Q + c.wave] = silu_f(rs * t[0]) * (rs * t[1]);
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -415,8 +463,10 @@ __global__ __launch_bounds__(NT, 1) void bb_step_kernel(BbStepArgs p) {
   __syncthreads();
   for (int l = 0; l < NL; ++l) {
     c.refresh();
-    rms(c, nw1, L.xn);
-    phase_qkv(c, l, pos, wq);                         // -> E1
+    // layers >= 1 (folded): the previous layer's E5 gather already wrote xn = x * n1
+    const bool fold1 = BB_FOLD && l > 0;
+    if (!fold1) rms(c, nw1, L.xn);
+    phase_qkv(c, l, pos, wq, fold1);                  // -> E1
     ++c.e;                                            // E1 is read by the attention workgroups only
     const bool attn_wg = c.w < NATT;
     // the o_proj rows and the first two MLP quarters stream while the attention runs; the attention
@@ -437,17 +487,23 @@ __global__ __launch_bounds__(NT, 1) void bb_step_kernel(BbStepArgs p) {
     c.refresh();
     phase_o(c, wo);                                   // -> E3
     if (l + 1 < NL) load_q(c, l + 1, wq);
+#if BB_FOLD
+    gather_x(c, c.rbuf(G_X, D), nw2);                 // E3 -> x, xn = x * n2
+    const float rs2 = row_rs(c);
+#else
     gather<D / NT>(c, c.rbuf(G_X, D), D, L.x);         // E3
+    const float rs2 = 1.f;
+#endif
     ++c.e;
     c.refresh();
-    rms(c, nw2, L.xn);
+    if (!BB_FOLD) rms(c, nw2, L.xn);
     float acc[4];
-    phase_mq<0>(c, mq[0], acc);
+    phase_mq<0>(c, mq[0], acc, rs2);
     load_mq(c, l, 2, mq[2]);
-    phase_mq<1>(c, mq[1], acc);
+    phase_mq<1>(c, mq[1], acc, rs2);
     load_mq(c, l, 3, mq[3]);
-    phase_mq<2>(c, mq[2], acc);
-    phase_mq<3>(c, mq[3], acc);
+    phase_mq<2>(c, mq[2], acc, rs2);
+    phase_mq<3>(c, mq[3], acc, rs2);
     {
       u64* g = c.buf(G_PART, (size_t)NWG * D) + (size_t)c.w * D;
 #pragma unroll
@@ -456,14 +512,25 @@ __global__ __launch_bounds__(NT, 1) void bb_step_kernel(BbStepArgs p) {
     nw1 = nw_fetch(c, l + 1 < NL ? p.n1[l + 1] : p.norm);
     c.refresh();
     phase_reduce(c);                                  // waits E4, -> E5
+#if BB_FOLD
+    gather_x(c, c.rbuf(G_X, D), nw1);                 // E5 -> x, xn = x * (next n1 | final norm)
+#else
     gather<D / NT>(c, c.rbuf(G_X, D), D, L.x);         // E5
+#endif
     ++c.e;
   }
   // final norm of the last row -> h_last (generation.py:42 reads norm(h[:, -1]))
   c.refresh();
+#if BB_FOLD
+  if (c.w == 0) {
+    const float rs = row_rs(c);
+    for (int k = c.tid; k < D; k += NT) p.h_last[k] = L.xn[k] * rs;
+  }
+#else
   rms(c, nw1, L.xn);
   if (c.w == 0)
     for (int k = c.tid; k < D; k += NT) p.h_last[k] = L.xn[k];
+#endif
   c.stamp(BB_STEP_STAMPS - 1);
   if (c.w == 0 && c.tid == 0) __hip_atomic_store(p.epoch, c.tag0 - 1u + (unsigned)c.e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

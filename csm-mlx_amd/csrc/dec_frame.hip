@@ -92,6 +92,7 @@ struct Lds {
   float hb[MAXM][32];      // this WG's h columns
   float red[4 * MAXM][256];// reduce-scatter staging [row][producer]
   float wsum[8][MAXM * 8]; // per-wave partial dots
+  float sq[8][MAXM];       // per-wave partial sums of squares of the gathered x rows (folded RMSNorm)
   float Ks[HKV][32][HD + 4];// cached keys of this layer (rows padded: conflict-free row-parallel reads)
   float Vs[HKV][32][HD];    // cached values
   float lg[VMAX];          // sampling: the head's logits, gathered from every workgroup
@@ -220,6 +221,61 @@ __device__ __forceinline__ void rms_rows(Ctx& c, float2 nw, int m0 = 0) {
   __syncthreads();
 }
 
+// Folded RMSNorm (DF_FOLD): an x hand-off is gathered straight into x and into xn = x * nw (the next
+// consumer's norm weight) with per-wave sums of squares; the consumer dots against the un-normalised
+// xn and scales its results by rsqrt(mean(x^2) + eps) -- one barrier and one pass over the rows
+// fewer per norm (the batched path's xs.h does the same: row scale after the dot product).
+#ifndef DF_FOLD
+#define DF_FOLD 1
+#endif
+template <int M>
+__device__ __forceinline__ void gather_x(Ctx& c, const u64* buf, float2 nw) {
+  static_assert(D == 2 * NT, "granule tid + NT u is element (u / 2, tid + NT (u % 2))");
+  constexpr int GPT = M * D / NT;
+  const unsigned tag = c.tag();
+  u64 g[GPT];
+#pragma unroll
+  for (int u = 0; u < GPT; ++u) g[u] = gload(buf + c.tid + u * NT);
+  for (unsigned spin = 0;; ++spin) {
+    bool ok = true;
+#pragma unroll
+    for (int u = 0; u < GPT; ++u) ok &= (unsigned)(g[u] >> 32) == tag;
+    if (ok) break;
+    if (spin >= SPIN_LIMIT || ((spin & 255) == 255 && __hip_atomic_load(c.p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+      __hip_atomic_store(c.p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+    for (int u = 0; u < GPT; ++u)
+      if ((unsigned)(g[u] >> 32) != tag) g[u] = gload(buf + c.tid + u * NT);
+  }
+  c.stamp();
+  float sq[MAXM];
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const float v0 = __uint_as_float((unsigned)g[2 * m]), v1 = __uint_as_float((unsigned)g[2 * m + 1]);
+    c.L.x[m][c.tid] = v0;
+    c.L.x[m][c.tid + NT] = v1;
+    c.L.xn[m][c.tid] = v0 * nw.x;
+    c.L.xn[m][c.tid + NT] = v1 * nw.y;
+    sq[m] = fmaf(v1, v1, v0 * v0);
+  }
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const float t = wave_sum(sq[m]);
+    if (c.lane == 0) c.L.sq[c.wave][m] = t;
+  }
+  __syncthreads();
+}
+// rsqrt(mean(x^2) + eps) of gathered row m (the 8 wave partials in order)
+__device__ __forceinline__ float row_rs(const Ctx& c, int m) {
+  float s = c.L.sq[0][m];
+#pragma unroll
+  for (int w = 1; w < 8; ++w) s += c.L.sq[w][m];
+  return rsqrtf(s / (float)D + c.p.eps);
+}
+
 // ---- weight slices held in registers (issued ahead of use)
 struct WQkv { u32x4_t a, b; };      // waves 0..5: row 6w+wave, chunks lane / lane+64
 struct WO { u32x4_t a; };            // row 4w + wave/2, chunk (wave&1)*64 + lane
@@ -279,7 +335,7 @@ __device__ __forceinline__ void load_head(Ctx& c, const bf16_t* W, int K, WHd& r
 
 // ---- phases
 // QKV rows of this WG for M rows at positions pos0..pos0+M-1 (RoPE), published to E1.
-template <int M>
+template <int M, bool SC>
 __device__ __forceinline__ void phase_qkv(Ctx& c, int pos0, const WQkv& W) {
   if (c.wave < 6) {
     float s0 = 0.f, s1 = 0.f;
@@ -293,6 +349,11 @@ __device__ __forceinline__ void phase_qkv(Ctx& c, int pos0, const WQkv& W) {
   if (c.tid < 3 * M * REP) {  // RoPE pair j of row m: rows n, n+1 = 6w + 2j, +1 -> replica rr
     const int pr = c.tid / REP, rr = c.tid % REP, m = pr / 3, j = pr % 3, n = 6 * c.w + 2 * j;
     float a = c.L.wsum[2 * j][m], b = c.L.wsum[2 * j + 1][m];
+    if (SC) {  // folded RMSNorm: the row scale after the dot product
+      const float rs = row_rs(c, m);
+      a *= rs;
+      b *= rs;
+    }
     if (n < (HQ + HKV) * HD) {
       const int d = n % HD;
       const float2 cs = c.L.rope[m][d / 2];
@@ -438,7 +499,7 @@ __device__ __forceinline__ void phase_o(Ctx& c, const WO& W) {
 }
 
 // gate/up (64 rows -> h[32]) and the split-K down partials of this WG's columns -> E4 granules
-template <int M>
+template <int M, bool SC>
 __device__ __forceinline__ void phase_mlp(Ctx& c, const WGu& G, const WDn& Wd) {
   {
     float s[8][2];
@@ -456,8 +517,9 @@ __device__ __forceinline__ void phase_mlp(Ctx& c, const WGu& G, const WDn& Wd) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) t[i] = wave_sum(s[i][m]);
       if (c.lane < 4) {  // pair j = 4*wave + lane: rows 2j (gate), 2j+1 (up) of the WG slice
-        const float gt = c.lane == 0 ? t[0] : (c.lane == 1 ? t[2] : (c.lane == 2 ? t[4] : t[6]));
-        const float up = c.lane == 0 ? t[1] : (c.lane == 1 ? t[3] : (c.lane == 2 ? t[5] : t[7]));
+        const float rs = SC ? row_rs(c, m) : 1.f;
+        const float gt = rs * (c.lane == 0 ? t[0] : (c.lane == 1 ? t[2] : (c.lane == 2 ? t[4] : t[6])));
+        const float up = rs * (c.lane == 0 ? t[1] : (c.lane == 1 ? t[3] : (c.lane == 2 ? t[5] : t[7])));
         c.L.hb[m][4 * c.wave + c.lane] = silu_f(gt) * up;
       }
     }
@@ -528,21 +590,22 @@ __device__ __forceinline__ void phase_reduce(Ctx& c) {
 // Head rows of this WG on row xn[0] (K = 1024 or 2048) -> arg-max key -> E6 granules (hi, lo words)
 template <int KH>
 __device__ __forceinline__ void phase_head(Ctx& c, const bf16_t* W, int n_valid, const u32x4_t (&wa)[KH / 512],
-                                           const u32x4_t (&wx)[KH / 512], float* logits) {
+                                           const u32x4_t (&wx)[KH / 512], float* logits, int xm = 0, float rs = 1.f) {
   constexpr int CPL = KH / 512;  // chunks per lane
   const int row = 8 * c.w + c.wave;
+  const float* xin = c.L.xn[xm];  // input row (folded RMSNorm: un-normalised, scaled by rs after the dot)
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < CPL; ++i) s += dot8(wa[i], c.L.xn[0] + 8 * (c.lane + 64 * i));
-  s = wave_sum(s);
+  for (int i = 0; i < CPL; ++i) s += dot8(wa[i], xin + 8 * (c.lane + 64 * i));
+  s = wave_sum(s) * rs;
   unsigned long long best = row < n_valid ? pack_argmax(s, row) : 0ull;
   if (c.lane == 0 && row < n_valid) logits[row] = s;
   const int xr = 2048 + c.w;
   float t = 0.f;
   if (c.wave == 0 && c.w < 3) {
 #pragma unroll
-    for (int i = 0; i < CPL; ++i) t += dot8(wx[i], c.L.xn[0] + 8 * (c.lane + 64 * i));
-    t = wave_sum(t);
+    for (int i = 0; i < CPL; ++i) t += dot8(wx[i], xin + 8 * (c.lane + 64 * i));
+    t = wave_sum(t) * rs;
     const unsigned long long k2 = xr < n_valid ? pack_argmax(t, xr) : 0ull;
     best = k2 > best ? k2 : best;
     if (c.lane == 0 && xr < n_valid) logits[xr] = t;
@@ -736,8 +799,9 @@ __device__ __forceinline__ void decoder_layer(Ctx& c, int l, int step, int pos0,
   } else {
     KvRegs kv;
     if (FIRST && c.tid < M * (HD / 2)) L.rope[c.tid / (HD / 2)][c.tid % (HD / 2)] = rp;
-    rms_rows<M>(c, r.nw1);  // (its barriers also publish the RoPE rows)
-    phase_qkv<M>(c, pos0, r.wq);                      // -> E1
+    // layers >= 1 (folded): the previous layer's E5 gather already wrote xn = x * n1
+    if (FIRST || !DF_FOLD) rms_rows<M>(c, r.nw1);  // (its barriers also publish the RoPE rows)
+    phase_qkv<M, DF_FOLD && !FIRST>(c, pos0, r.wq);   // -> E1
     // prefetches issued after the publish (its RoPE operand load would otherwise retire behind
     // them in vmcnt order), still ahead of the hand-off wait they hide under
     kv_issue(c, l, pos0, kv);
@@ -758,11 +822,15 @@ __device__ __forceinline__ void decoder_layer(Ctx& c, int l, int step, int pos0,
   c.mark();
   load_gu<GU_EARLY, 8>(c, l, r.wg);
   if (!LAST) { load_qkv(c, l + 1, r.wq); load_o(c, l + 1, r.wo); }
+#if DF_FOLD
+  gather_x<M>(c, c.rbuf(G_X, MAXM * D), nw2);        // E3 -> x, xn = x * n2
+#else
   gather<M * D / NT>(c, c.rbuf(G_X, MAXM * D), M * D, &L.x[0][0]);
+#endif
   ++c.e;
   c.refresh();
-  rms_rows<M>(c, nw2);
-  phase_mlp<M>(c, r.wg, r.wd);                        // -> E4
+  if (!DF_FOLD) rms_rows<M>(c, nw2);
+  phase_mlp<M, DF_FOLD>(c, r.wg, r.wd);                // -> E4
   r.nw1 = nw_fetch(c, LAST ? p.norm : p.n1[l + 1]);  // next layer's norm, or the final one
   c.mark();
   if (LAST) {
@@ -774,7 +842,11 @@ __device__ __forceinline__ void decoder_layer(Ctx& c, int l, int step, int pos0,
   }
   c.refresh();
   phase_reduce<M>(c);                                 // waits E4, -> E5
+#if DF_FOLD
+  gather_x<M>(c, c.rbuf(G_X, MAXM * D), r.nw1);      // E5 -> x, xn = x * (next n1 | final norm)
+#else
   gather<M * D / NT>(c, c.rbuf(G_X, MAXM * D), M * D, &L.x[0][0]);
+#endif
   ++c.e;
 }
 
@@ -788,8 +860,13 @@ __device__ __forceinline__ void run_step(Ctx& c, int step, Pre& r) {
   decoder_layer<M, false, true>(c, NL - 1, step, pos0, r);
   // ci head on the last row: final norm, audio_head[step - 1] (generation.py:79)
   c.refresh();
+#if DF_FOLD
+  phase_head<D>(c, p.audio_head + (size_t)(step - 1) * p.VP * D, p.V, r.wh.a, r.wh.x, p.ci_logits + (size_t)(step - 1) * p.VP,
+                M - 1, row_rs(c, M - 1));  // -> E6
+#else
   rms_rows<1>(c, r.nw1, M - 1);
   phase_head<D>(c, p.audio_head + (size_t)(step - 1) * p.VP * D, p.V, r.wh.a, r.wh.x, p.ci_logits + (size_t)(step - 1) * p.VP);  // -> E6
+#endif
   KvRegs kv0;  // layer 0's cached K/V rows of the next step: in flight during the head's hand-off,
   if (step + 1 < p.K) kv_issue(c, 0, step + 1, kv0);
   const int ci = head_code(c, p.V, step);
