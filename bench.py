@@ -213,7 +213,16 @@ def frame_weight_bytes(model) -> float:
             + (K - 1) * (stack(dec) + _wbytes(model, dec.hidden_size, bb.hidden_size) + V * dec.hidden_size * head_b))
 
 
+def _decoder_xs(model, batch: int) -> bool:
+    """The batched depth decoder runs on the streaming GEMM (gemm_xs.hip) at 8..64 rows, bf16 / int4
+    (csm_engine.hip dec_xs_eligible; option gemm_xs / CSM_GEMM_XS=0 turns it off)."""
+    return 8 <= batch <= 64 and model.dtype in ("bf16", "q4") and os.environ.get("CSM_GEMM_XS", "1") != "0"
+
+
 def _kernel_name(model, batch: int, stack: str) -> str:
+    if stack == "decoder" and _decoder_xs(model, batch):
+        return (f"gemm_xs_kernel<Q4={'true' if model.dtype == 'q4' else 'false'}> = decoder gate/up + SiLU*up as a "
+                f"streaming exact-split MFMA GEMM over {batch} rows (split operands written by the producers)")
     if batch >= 8 and model.dtype in ("bf16", "q4"):
         return (f"gemm_wide_kernel<Q4={'true' if model.dtype == 'q4' else 'false'}> = {stack} RMSNorm + gate/up + "
                 f"SiLU*up as an exact-split MFMA GEMM over {batch} rows (fragment-tiled weights)")
@@ -250,8 +259,10 @@ def rooflines(model, batch: int):
 
     def gemv(which, stack):
         us, nb = ctypes.c_float(0), ctypes.c_double(0)
-        _lib.check(L.csm_bench_gemv(model.engine, which, batch, 400, ctypes.byref(us), ctypes.byref(nb)))
-        return entry(us.value, nb.value, _kernel_name(model, batch, stack), f"{stack}_gate_up/{model.dtype}/B{batch}")
+        xs = stack == "decoder" and _decoder_xs(model, batch)      # the kernel the frame runs (| 8: gemm_xs)
+        _lib.check(L.csm_bench_gemv(model.engine, which | (8 if xs else 0), batch, 400, ctypes.byref(us), ctypes.byref(nb)))
+        return entry(us.value, nb.value, _kernel_name(model, batch, stack),
+                     f"{stack}_gate_up{'_xs' if xs else ''}/{model.dtype}/B{batch}")
 
     us, nb = ctypes.c_float(0), ctypes.c_double(0)
     if batch == 1 and L.csm_bench_bb_step(model.engine, 20, ctypes.byref(us), ctypes.byref(nb)) == 0:

@@ -92,6 +92,15 @@ struct Ctx {
   }
 };
 
+// BB_PROBE_DELAY: sleeps before the first probe of a hand-off wait (the producers are still working
+// when a workgroup starts waiting; an early probe returns stale and its re-polls load the lines every
+// workgroup polls -- dec_frame.hip measured -6 % per frame from the same delay).
+#ifndef BB_PROBE_DELAY
+#define BB_PROBE_DELAY 32
+#endif
+__device__ __forceinline__ void probe_delay() {
+  if (BB_PROBE_DELAY > 0) __builtin_amdgcn_s_sleep(BB_PROBE_DELAY);
+}
 __device__ __forceinline__ bool spin_fail(Ctx& c, unsigned spin) {
   if (spin >= SPIN_LIMIT || ((spin & 255) == 255 && __hip_atomic_load(c.p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
     __hip_atomic_store(c.p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -105,6 +114,7 @@ template <int GPT>
 __device__ __forceinline__ void gather(Ctx& c, const u64* buf, int n, float* out) {
   const unsigned tag = c.tag();
   u64 g[GPT];
+  probe_delay();
 #pragma unroll
   for (int u = 0; u < GPT; ++u) {
     const int i = c.tid + u * NT;
@@ -164,6 +174,7 @@ __device__ __forceinline__ void gather_x(Ctx& c, const u64* buf, const Nw& nw) {
   constexpr int GPT = D / NT;
   const unsigned tag = c.tag();
   u64 g[GPT];
+  probe_delay();
 #pragma unroll
   for (int u = 0; u < GPT; ++u) g[u] = gload(buf + c.tid + u * NT);
   for (unsigned spin = 0;; ++spin) {
@@ -289,6 +300,7 @@ __device__ __forceinline__ void phase_attn(Ctx& c, int l, int pos) {
     if (c.tid < 3 * HD) {
       const int part = c.tid / HD, d = c.tid % HD;
       const int idx = part == 0 ? a * HD + d : (part == 1 ? HQ * HD + g * HD + d : (HQ + HKV) * HD + g * HD + d);
+      probe_delay();
       u64 v = gload(buf + idx);
       for (unsigned spin = 0; (unsigned)(v >> 32) != tag; ++spin) {
         if (spin_fail(c, spin)) break;
@@ -417,6 +429,7 @@ __device__ __forceinline__ void phase_reduce(Ctx& c) {
   const int v = c.tid >> 1, half = c.tid & 1;
   const u64* src = g + (size_t)v * D + 8 * c.w + 4 * half;
   u64 q[4];
+  probe_delay();
 #pragma unroll
   for (int u = 0; u < 4; ++u) q[u] = gload(src + u);
   for (unsigned spin = 0;; ++spin) {

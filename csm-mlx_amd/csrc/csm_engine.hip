@@ -88,6 +88,11 @@ struct csm_engine {
   // proj_tab[cb][code] at position cb + 1 (fp32, built by the same QKV GEMV); codebook steps >= 2 then
   // skip layer 0's QKV launch and its attention gathers the row (AttnParams::g_tab).
   float* qkv0_tab = nullptr;
+  // csm_set_option "tab_rep" (env CSM_TAB_REP): copies of proj_tab + qkv0_tab the persistent frame
+  // decoder spreads its workgroups over (every workgroup loads the same two rows after each head)
+  int tab_rep = [] { const char* v = getenv("CSM_TAB_REP"); return v ? std::max(1, std::min(atoi(v), DEC_FRAME_TAB_REPS)) : 1; }();
+  float* tab_copies = nullptr;  // [tab_rep - 1][proj_tab | qkv0_tab]
+  int tab_copies_n = 0;         // replicas tab_copies holds up to date (0 after a table rebuild)
   bool use_qkv0_tab = [] { const char* v = getenv("CSM_QKV0_TAB"); return !(v && v[0] == '0'); }();  // csm_set_option "qkv0_tab"
   bool qkv0_built = false;
   // fragment-tiled copies of the matrices the MFMA path reads (build_tiled; ws.tiled maps them)
@@ -205,6 +210,7 @@ struct csm_engine {
     if (g_head) (void)hipGraphExecDestroy(g_head);
     for (void* p : allocs) (void)hipFree(p);
     for (void* p : batch_allocs) (void)hipFree(p);
+    if (tab_copies) (void)hipFree(tab_copies);
     gemm_ws_free(ws);
     if (st) (void)hipStreamDestroy(st);
   }
@@ -559,6 +565,15 @@ void enqueue_dec_frame_only(csm_engine* e, hipStream_t st) {
   a.norm = e->dec.norm; a.rope = e->dec.rope; a.S_cap = e->dec.S_cap; a.eps = e->dec.d.eps;
   a.c0_head = (const bf16_t*)e->c0_head; a.proj = (const bf16_t*)e->proj; a.audio_head = (const bf16_t*)e->audio_head;
   a.proj_tab = e->proj_tab; a.qkv0_tab = e->qkv0_tab; a.h_last = e->h_last;
+  a.tab_reps = e->tab_copies_n == e->tab_rep - 1 ? e->tab_rep : 1;
+  {
+    const size_t np = (size_t)(e->K - 1) * e->V * e->Dd, nq = (size_t)(e->K - 1) * e->V * e->dec.qkv_rows();
+    for (int r = 0; r < DEC_FRAME_TAB_REPS; ++r) {
+      const float* base = r > 0 && r < a.tab_reps ? e->tab_copies + (size_t)(r - 1) * (np + nq) : nullptr;
+      a.proj_tabs[r] = base ? base : e->proj_tab;
+      a.qkv0_tabs[r] = base ? base + np : e->qkv0_tab;
+    }
+  }
   a.V = e->V; a.VP = e->Vpad; a.K = e->K; a.codes = e->codes; a.c0_logits = e->c0_logits; a.ci_logits = e->ci_logits;
   a.gbuf = (unsigned long long*)e->df_gbuf; a.epoch = e->df_epoch; a.err = e->df_err; a.stamps = e->df_stamps;
   static const int wnt = [] { const char* v = getenv("CSM_DF_WNT"); return v ? atoi(v) : 0; }();
@@ -859,6 +874,24 @@ void build_proj_table(csm_engine* e) {
   HIPCHK(hipStreamSynchronize(e->st));
   HIPCHK(hipGetLastError());
   e->qkv0_built = true;
+  e->tab_copies_n = 0;
+}
+
+// the table replicas the frame decoder reads (option tab_rep), refreshed after a table rebuild
+void build_tab_copies(csm_engine* e) {
+  if (e->tab_rep <= 1 || !e->qkv0_built || e->tab_copies_n == e->tab_rep - 1) return;
+  const size_t np = (size_t)(e->K - 1) * e->V * e->Dd, nq = (size_t)(e->K - 1) * e->V * e->dec.qkv_rows();
+  if (e->tab_copies) (void)hipFree(e->tab_copies);
+  e->tab_copies = nullptr;
+  HIPCHK(hipMalloc(&e->tab_copies, (size_t)(e->tab_rep - 1) * (np + nq) * 4));
+  for (int r = 0; r < e->tab_rep - 1; ++r) {
+    float* dst = e->tab_copies + (size_t)r * (np + nq);
+    HIPCHK(hipMemcpyAsync(dst, e->proj_tab, np * 4, hipMemcpyDeviceToDevice, e->st));
+    HIPCHK(hipMemcpyAsync(dst + np, e->qkv0_tab, nq * 4, hipMemcpyDeviceToDevice, e->st));
+  }
+  HIPCHK(hipStreamSynchronize(e->st));
+  e->tab_copies_n = e->tab_rep - 1;
+  e->g_B = -1;  // the captured frame graph holds the table pointers
 }
 
 
@@ -1321,6 +1354,7 @@ int csm_begin(csm_engine* e, int B, const uint64_t* seeds, float temperature, in
     ensure_batch(e, B);
     if (e->tiled_dirty) build_tiled(e);
     if (e->proj_tab_dirty) build_proj_table(e);
+    build_tab_copies(e);
     e->pos_host.assign(B, -1);
     e->B = B;
     e->temperature = temperature;
@@ -1925,6 +1959,12 @@ int csm_set_option(csm_engine* e, const char* key, int value) {
     } else if (k == "fold_proj") {
       if (!e) throw CsmError(CSM_ERR_ARG, "fold_proj needs an engine");
       e->fold_proj = value != 0;
+    }
+    else if (k == "tab_rep") {
+      if (!e || value < 1 || value > DEC_FRAME_TAB_REPS) throw CsmError(CSM_ERR_ARG, "tab_rep needs an engine and 1..8 replicas");
+      e->tab_rep = value;
+      e->tab_copies_n = 0;  // rebuilt at the next csm_begin
+      e->g_B = -1;
     }
     else if (k == "qkv0_tab") {
       if (!e) throw CsmError(CSM_ERR_ARG, "qkv0_tab needs an engine");

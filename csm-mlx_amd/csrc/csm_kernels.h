@@ -426,6 +426,7 @@ void launch_bb_step(const BbStepArgs& p, hipStream_t st);
 const void* bb_step_kernel_ptr();
 
 constexpr int DEC_FRAME_LAYERS = 4;
+constexpr int DEC_FRAME_TAB_REPS = 8;  // max replicas of the folded tables (option tab_rep)
 struct DecFrameArgs {
   const bf16_t* wqkv[DEC_FRAME_LAYERS];
   const bf16_t* wo[DEC_FRAME_LAYERS];
@@ -444,6 +445,11 @@ struct DecFrameArgs {
   const bf16_t* audio_head;              // [K-1][VP][1024]
   const float* proj_tab;                 // [K-1][V][1024]
   const float* qkv0_tab;                 // [K-1][V][1536]
+  // table replicas (csm_set_option "tab_rep"): workgroup w reads replica w % tab_reps (replica 0 = the
+  // tables above) -- every workgroup loads the same rows after each head, so fewer readers per row
+  const float* proj_tabs[DEC_FRAME_TAB_REPS];
+  const float* qkv0_tabs[DEC_FRAME_TAB_REPS];
+  int tab_reps;
   const float* h_last;                   // [2048]
   int V, VP, K;
   int* codes;                            // [K] of utterance 0

@@ -132,6 +132,7 @@ struct Ctx {
   unsigned tag0;
   int e;  // hand-off counter
   int ps = 0;  // phase-mark counter (profiling stamps 512..1007)
+  int code = 0;  // the last head's code (every thread holds it)
   __device__ void mark() {
     if (p.stamps && tid == 0 && ps < 496) p.stamps[(size_t)w * DEC_FRAME_STAMPS + 512 + ps] = __builtin_amdgcn_s_memrealtime();
     ++ps;
@@ -161,39 +162,50 @@ struct Ctx {
   }
 };
 
+// Hand-off waits (handoff.h poll_granules): DF_POLL2 keeps two probes in flight, DF_POLL_GAP
+// sleeps apart.
+#ifndef DF_POLL2
+#define DF_POLL2 0
+#endif
+#ifndef DF_PROBE_DELAY
+#define DF_PROBE_DELAY 24
+#endif
+#ifndef DF_REPOLL
+#define DF_REPOLL 2
+#endif
+#ifndef DF_POLL_GAP
+#define DF_POLL_GAP 8
+#endif
+__device__ __forceinline__ bool spin_fail(Ctx& c, unsigned spin) {
+  if (spin >= SPIN_LIMIT || ((spin & 255) == 255 && __hip_atomic_load(c.p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+    __hip_atomic_store(c.p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return true;
+  }
+  return false;
+}
+// use(x): the lane-local consumption of the matched probe
+template <int GPT, typename F>
+__device__ __forceinline__ void poll(Ctx& c, const u64* base, const int (&off)[GPT], const bool (&val)[GPT], F&& use) {
+  poll_granules<GPT, DF_POLL2 != 0, DF_POLL_GAP, DF_PROBE_DELAY, DF_REPOLL>(base, off, val, c.tag(), [&](unsigned spin) { return spin_fail(c, spin); }, use);
+  c.stamp();
+}
+
 // Wait until granules [0, n) of buf carry `tag`; values -> out (LDS).  Threads take granules
-// tid, tid + NT, ... (at most GPT each), issue every load first, then re-poll stale ones.
+// tid, tid + NT, ... (at most GPT each).
 template <int GPT>
 __device__ __forceinline__ void gather(Ctx& c, const u64* buf, int n, float* out) {
-  const unsigned tag = c.tag();
-  u64 g[GPT];
+  int off[GPT];
+  bool val[GPT];
 #pragma unroll
   for (int u = 0; u < GPT; ++u) {
-    const int i = c.tid + u * NT;
-    g[u] = i < n ? gload(buf + i) : ((u64)tag << 32);
+    off[u] = c.tid + u * NT;
+    val[u] = off[u] < n;
   }
-  for (unsigned spin = 0;; ++spin) {
-    bool ok = true;
+  poll<GPT>(c, buf, off, val, [&](const u64 (&g)[GPT]) {
 #pragma unroll
-    for (int u = 0; u < GPT; ++u) ok &= (unsigned)(g[u] >> 32) == tag;
-    if (ok) break;
-    if (spin >= SPIN_LIMIT || ((spin & 255) == 255 && __hip_atomic_load(c.p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-      __hip_atomic_store(c.p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      break;
-    }
-    __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-    for (int u = 0; u < GPT; ++u) {
-      const int i = c.tid + u * NT;
-      if (i < n && (unsigned)(g[u] >> 32) != tag) g[u] = gload(buf + i);
-    }
-  }
-  c.stamp();
-#pragma unroll
-  for (int u = 0; u < GPT; ++u) {
-    const int i = c.tid + u * NT;
-    if (i < n) out[i] = __uint_as_float((unsigned)g[u]);
-  }
+    for (int u = 0; u < GPT; ++u)
+      if (val[u]) out[off[u]] = __uint_as_float((unsigned)g[u]);
+  });
   __syncthreads();
 }
 
@@ -232,35 +244,25 @@ template <int M>
 __device__ __forceinline__ void gather_x(Ctx& c, const u64* buf, float2 nw) {
   static_assert(D == 2 * NT, "granule tid + NT u is element (u / 2, tid + NT (u % 2))");
   constexpr int GPT = M * D / NT;
-  const unsigned tag = c.tag();
-  u64 g[GPT];
+  int off[GPT];
+  bool val[GPT];
 #pragma unroll
-  for (int u = 0; u < GPT; ++u) g[u] = gload(buf + c.tid + u * NT);
-  for (unsigned spin = 0;; ++spin) {
-    bool ok = true;
-#pragma unroll
-    for (int u = 0; u < GPT; ++u) ok &= (unsigned)(g[u] >> 32) == tag;
-    if (ok) break;
-    if (spin >= SPIN_LIMIT || ((spin & 255) == 255 && __hip_atomic_load(c.p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-      __hip_atomic_store(c.p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      break;
-    }
-    __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-    for (int u = 0; u < GPT; ++u)
-      if ((unsigned)(g[u] >> 32) != tag) g[u] = gload(buf + c.tid + u * NT);
+  for (int u = 0; u < GPT; ++u) {
+    off[u] = c.tid + u * NT;
+    val[u] = true;
   }
-  c.stamp();
   float sq[MAXM];
+  poll<GPT>(c, buf, off, val, [&](const u64 (&g)[GPT]) {
 #pragma unroll
-  for (int m = 0; m < M; ++m) {
-    const float v0 = __uint_as_float((unsigned)g[2 * m]), v1 = __uint_as_float((unsigned)g[2 * m + 1]);
-    c.L.x[m][c.tid] = v0;
-    c.L.x[m][c.tid + NT] = v1;
-    c.L.xn[m][c.tid] = v0 * nw.x;
-    c.L.xn[m][c.tid + NT] = v1 * nw.y;
-    sq[m] = fmaf(v1, v1, v0 * v0);
-  }
+    for (int m = 0; m < M; ++m) {
+      const float v0 = __uint_as_float((unsigned)g[2 * m]), v1 = __uint_as_float((unsigned)g[2 * m + 1]);
+      c.L.x[m][c.tid] = v0;
+      c.L.x[m][c.tid + NT] = v1;
+      c.L.xn[m][c.tid] = v0 * nw.x;
+      c.L.xn[m][c.tid + NT] = v1 * nw.y;
+      sq[m] = fmaf(v1, v1, v0 * v0);
+    }
+  });
 #pragma unroll
   for (int m = 0; m < M; ++m) {
     const float t = wave_sum(sq[m]);
@@ -404,6 +406,36 @@ __device__ __forceinline__ void kv_append(Ctx& c, int pos0) {
   }
 }
 
+// DF_KVDIRECT: the q | k | v hand-off (and layer 0's table row) is written straight to its places --
+// q to L.qkv, the new k / v rows into the LDS history at pos0 + m -- so no kv_append pass and one
+// barrier fewer before the attention.
+#ifndef DF_KVDIRECT
+#define DF_KVDIRECT 1
+#endif
+__device__ __forceinline__ void qkv_place(Ctx& c, int m, int r, int pos0, float v) {
+  if (r < HQ * HD) c.L.qkv[m][r] = v;
+  else if (r < (HQ + HKV) * HD) c.L.Ks[(r - HQ * HD) / HD][pos0 + m][r % HD] = v;
+  else c.L.Vs[(r - (HQ + HKV) * HD) / HD][pos0 + m][r % HD] = v;
+}
+template <int M>
+__device__ __forceinline__ void gather_qkv(Ctx& c, const u64* buf, int pos0, const KvRegs& kv) {
+  constexpr int GPT = (M * QKV + NT - 1) / NT;
+  int off[GPT];
+  bool val[GPT];
+#pragma unroll
+  for (int u = 0; u < GPT; ++u) {
+    off[u] = c.tid + u * NT;
+    val[u] = off[u] < M * QKV;
+  }
+  poll<GPT>(c, buf, off, val, [&](const u64 (&g)[GPT]) {
+#pragma unroll
+    for (int u = 0; u < GPT; ++u)
+      if (val[u]) qkv_place(c, off[u] / QKV, off[u] % QKV, pos0, __uint_as_float((unsigned)g[u]));
+  });
+  kv_store(c, pos0, kv);
+  __syncthreads();
+}
+
 // Attention of rows m < M (positions pos0 + m) over keys 0..pos0+m, all in c.L.Ks / Vs (kv_store +
 // kv_append).  Every WG computes all heads (wave = head), as attn_short_head: lane = (key kj =
 // lane & 31, half hh of the head dims), scores from two half dots added by one shuffle,
@@ -473,8 +505,8 @@ __device__ __forceinline__ void phase_attn(Ctx& c, int pos0, int layer) {
   if (c.tid < M) {
     const int m = c.tid, r = c.w, gg = r / HD, d = r % HD;
     const size_t off = ((size_t)gg * c.p.S_cap + pos0 + m) * HD + d;
-    sc1_store_f(c.p.kc[layer] + off, c.L.qkv[m][HQ * HD + r]);
-    sc1_store_f(c.p.vc[layer] + off, c.L.qkv[m][(HQ + HKV) * HD + r]);
+    sc1_store_f(c.p.kc[layer] + off, c.L.Ks[gg][pos0 + m][d]);
+    sc1_store_f(c.p.vc[layer] + off, c.L.Vs[gg][pos0 + m][d]);
   }
   __syncthreads();
 }
@@ -543,37 +575,23 @@ __device__ __forceinline__ void phase_mlp(Ctx& c, const WGu& G, const WDn& Wd) {
 // Reduce-scatter: rows 4w..4w+3 of every producer's partials (fixed order), + residual -> E5
 template <int M>
 __device__ __forceinline__ void phase_reduce(Ctx& c) {
-  const unsigned tag = c.tag();
   const u64* g = c.buf(G_PART, (size_t)NWG * MAXM * D);
   const int v = c.tid >> 1, half = c.tid & 1;
-  u64 q[MAXM][2];
+  int off[2 * M];
+  bool val[2 * M];
 #pragma unroll
-  for (int m = 0; m < MAXM; ++m)
+  for (int m = 0; m < M; ++m)
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
-      q[m][u] = m < M ? gload(g + ((size_t)v * MAXM + m) * D + 4 * c.w + 2 * half + u) : ((u64)tag << 32);
-  for (unsigned spin = 0;; ++spin) {
-    bool ok = true;
-#pragma unroll
-    for (int m = 0; m < MAXM; ++m) ok &= ((unsigned)(q[m][0] >> 32) == tag) & ((unsigned)(q[m][1] >> 32) == tag);
-    if (ok) break;
-    if (spin >= SPIN_LIMIT || ((spin & 255) == 255 && __hip_atomic_load(c.p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
-      __hip_atomic_store(c.p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      break;
+    for (int u = 0; u < 2; ++u) {
+      off[2 * m + u] = (v * MAXM + m) * D + 4 * c.w + 2 * half + u;
+      val[2 * m + u] = true;
     }
-    __builtin_amdgcn_s_sleep(1);
+  poll<2 * M>(c, g, off, val, [&](const u64 (&q)[2 * M]) {
 #pragma unroll
-    for (int m = 0; m < MAXM; ++m)
+    for (int m = 0; m < M; ++m)
 #pragma unroll
-      for (int u = 0; u < 2; ++u)
-        if (m < M && (unsigned)(q[m][u] >> 32) != tag) q[m][u] = gload(g + ((size_t)v * MAXM + m) * D + 4 * c.w + 2 * half + u);
-  }
-  c.stamp();
-#pragma unroll
-  for (int m = 0; m < MAXM; ++m)
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-      if (m < M) c.L.red[4 * m + 2 * half + u][v] = __uint_as_float((unsigned)q[m][u]);
+      for (int u = 0; u < 2; ++u) c.L.red[4 * m + 2 * half + u][v] = __uint_as_float((unsigned)q[2 * m + u]);
+  });
   __syncthreads();
   ++c.e;  // the x hand-off that follows
   if (c.wave < 4 * M) {
@@ -628,25 +646,30 @@ __device__ __forceinline__ void phase_head(Ctx& c, const bf16_t* W, int n_valid,
   __syncthreads();
 }
 
-// Gather the 256 arg-max keys -> code (every WG identical)
+// Gather the 256 arg-max keys -> code (every WG identical).  Thread t polls granule t (word t & 1 of
+// key t / 2); the two words meet by one lane swap, every wave takes the max of its 32 keys, and one
+// barrier joins the 8 wave maxima -- the max of exact keys, so the order is immaterial.
 __device__ __forceinline__ int gather_code(Ctx& c, int V) {
-  gather<1>(c, c.rbuf(G_ARG, NWG * 2), NWG * 2, &c.L.red[0][0]);
-  if (c.wave == 0) {
-    const unsigned* u = reinterpret_cast<const unsigned*>(&c.L.red[0][0]);
-    unsigned long long b = 0;
-    for (int i = c.lane; i < NWG; i += 64) {
-      const unsigned long long k = ((unsigned long long)u[2 * i] << 32) | u[2 * i + 1];
-      b = k > b ? k : b;
-    }
+  static_assert(NWG * 2 == NT, "one key word per thread");
+  const int off[1] = {c.tid};
+  const bool val[1] = {true};
+  unsigned wv = 0;
+  poll<1>(c, c.rbuf(G_ARG, NWG * 2), off, val, [&](const u64 (&g)[1]) { wv = (unsigned)g[0]; });
+  const unsigned ov = __shfl_xor(wv, 1, 64);
+  unsigned long long b = (c.tid & 1) ? (((unsigned long long)ov << 32) | wv) : (((unsigned long long)wv << 32) | ov);
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const unsigned long long t = __shfl_xor(b, o, 64);
-      b = t > b ? t : b;
-    }
-    if (c.lane == 0) c.L.code = min(max(unpack_argmax(b), 0), V - 1);
+  for (int o = 32; o > 1; o >>= 1) {
+    const unsigned long long t = __shfl_xor(b, o, 64);
+    b = t > b ? t : b;
   }
+  unsigned long long* wk = reinterpret_cast<unsigned long long*>(&c.L.red[0][0]);
+  if (c.lane == 0) wk[c.wave] = b;
   __syncthreads();
-  return c.L.code;
+  b = wk[0];
+#pragma unroll
+  for (int i = 1; i < NT / 64; ++i) b = wk[i] > b ? wk[i] : b;
+  c.code = min(max(unpack_argmax(b), 0), V - 1);
+  return c.code;
 }
 
 // Sampling (temperature > 0): gather the head's V logits, then -- identically in every workgroup --
@@ -745,7 +768,8 @@ __device__ __forceinline__ int sample_code(Ctx& c, int V, int cb) {
     c.L.code = min(max(b, 0), V - 1);  // NaN logits leave no winner: clamp (as sample_kernel)
   }
   __syncthreads();
-  return c.L.code;
+  c.code = c.L.code;
+  return c.code;
 }
 
 // the code of a head: greedy arg-max of the published keys, or the sampler over the logits
@@ -780,8 +804,9 @@ __device__ __forceinline__ void decoder_layer(Ctx& c, int l, int step, int pos0,
   if (FIRST && step > 1) {
     // q | k | v of input row proj_tab[step - 1][code] at position `step`, and the row itself; both
     // loads are in flight together, ahead of the down prefetch (vmcnt retires in issue order)
-    const float* t = p.qkv0_tab + ((size_t)(step - 1) * p.V + L.code) * QKV;
-    const float* xr = p.proj_tab + ((size_t)(step - 1) * p.V + L.code) * D;
+    const int tr = c.w % p.tab_reps;  // table replica of this workgroup (fewer readers per row)
+    const float* t = p.qkv0_tabs[tr] + ((size_t)(step - 1) * p.V + c.code) * QKV;
+    const float* xr = p.proj_tabs[tr] + ((size_t)(step - 1) * p.V + c.code) * D;
     float tv[(QKV + NT - 1) / NT], xv[D / NT];
 #pragma unroll
     for (int j = 0; j < (QKV + NT - 1) / NT; ++j) tv[j] = c.tid + j * NT < QKV ? t[c.tid + j * NT] : 0.f;
@@ -790,12 +815,18 @@ __device__ __forceinline__ void decoder_layer(Ctx& c, int l, int step, int pos0,
     load_dn(c, l, r.wd);
 #pragma unroll
     for (int j = 0; j < (QKV + NT - 1) / NT; ++j)
-      if (c.tid + j * NT < QKV) L.qkv[0][c.tid + j * NT] = tv[j];
+      if (c.tid + j * NT < QKV) {
+        if (DF_KVDIRECT) qkv_place(c, 0, c.tid + j * NT, pos0, tv[j]);
+        else L.qkv[0][c.tid + j * NT] = tv[j];
+      }
 #pragma unroll
     for (int j = 0; j < D / NT; ++j) L.x[0][c.tid + j * NT] = xv[j];
     if (c.tid < M * (HD / 2)) L.rope[c.tid / (HD / 2)][c.tid % (HD / 2)] = rp;
     __syncthreads();  // L.qkv complete before kv_append reads it
-    kv_append<M>(c, pos0);
+    if (!DF_KVDIRECT) {
+      kv_append<M>(c, pos0);
+      __syncthreads();
+    }
   } else {
     KvRegs kv;
     if (FIRST && c.tid < M * (HD / 2)) L.rope[c.tid / (HD / 2)][c.tid % (HD / 2)] = rp;
@@ -806,12 +837,17 @@ __device__ __forceinline__ void decoder_layer(Ctx& c, int l, int step, int pos0,
     // them in vmcnt order), still ahead of the hand-off wait they hide under
     kv_issue(c, l, pos0, kv);
     load_dn(c, l, r.wd);
+#if DF_KVDIRECT
+    gather_qkv<M>(c, c.rbuf(G_QKV, MAXM * QKV), pos0, kv);  // (its barrier publishes the history too)
+    ++c.e;
+#else
     gather<(M * QKV + NT - 1) / NT>(c, c.rbuf(G_QKV, MAXM * QKV), M * QKV, &L.qkv[0][0]);
     ++c.e;
     kv_store(c, pos0, kv);
     kv_append<M>(c, pos0);
+    __syncthreads();
+#endif
   }
-  __syncthreads();
   c.refresh();
   c.mark();
   const float2 nw2 = nw_fetch(c, p.n2[l]);

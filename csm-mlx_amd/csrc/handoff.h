@@ -54,6 +54,63 @@ __device__ __forceinline__ u32x4_t bload(const void* base, int voff, int soff) {
   return __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, soff, AUX));
 }
 
+// Wait until this thread's granules base[off[u]] (u < GPT, val[u]) carry `tag`, then use(probe).
+// TWO: two probes in flight, the second issued GAP sleeps after the first, each re-issued whole as
+// soon as its predecessor returns stale -- a probe returns every half round trip, so a hand-off is
+// seen about a quarter round trip sooner than by one probe re-polled on its return.  Every load is
+// unconditional (an unused entry reads granule 0 and counts as current) and use() runs on the exit
+// the matched probe left by: no branch around a load and no copy of a probe's registers at a merge,
+// so the compiler's vmcnt waits stay exact (a check waits for its own probe, the other stays in
+// flight).  A granule's tag only moves from stale to current during a wait (its buffer is rewritten
+// only after every workgroup has published the next hand-off), so any all-current probe is the
+// hand-off.  fail(spin): the bounded-spin / error-flag test.  DELAY: sleeps before the first probe
+// (fewer wasted probes while the producers are still working); REPOLL: sleeps between re-polls.
+// Measured (profiles/r03_ab_poll.txt): TWO costs the frame decoder +12 % (every re-issued probe adds
+// sc1 traffic on the lines every workgroup polls), so both kernels keep one probe.
+template <int GPT, bool TWO, int GAP, int DELAY, int REPOLL, typename Fail, typename F>
+__device__ __forceinline__ void poll_granules(const u64* base, const int (&off)[GPT], const bool (&val)[GPT], unsigned tag,
+                                              Fail&& fail, F&& use) {
+  auto cur = [&](const u64 (&x)[GPT]) {
+    bool ok = true;
+#pragma unroll
+    for (int u = 0; u < GPT; ++u) ok &= !val[u] || (unsigned)(x[u] >> 32) == tag;
+    return ok;
+  };
+  auto probe = [&](u64 (&x)[GPT]) {
+#pragma unroll
+    for (int u = 0; u < GPT; ++u) x[u] = gload(base + (val[u] ? off[u] : 0));
+  };
+  if constexpr (DELAY > 0) __builtin_amdgcn_s_sleep(DELAY);
+  if constexpr (TWO) {
+    u64 a[GPT], b[GPT];
+    probe(a);
+    __builtin_amdgcn_s_sleep(GAP);
+    probe(b);
+    for (unsigned spin = 0;; spin += 2) {
+      if (cur(a) || fail(spin)) {
+        use(a);
+        break;
+      }
+      probe(a);
+      if (cur(b)) {
+        use(b);
+        break;
+      }
+      probe(b);
+    }
+  } else {
+    u64 g[GPT];
+    probe(g);
+    for (unsigned spin = 0; !cur(g) && !fail(spin); ++spin) {
+      __builtin_amdgcn_s_sleep(REPOLL);
+#pragma unroll
+      for (int u = 0; u < GPT; ++u)
+        if (val[u] && (unsigned)(g[u] >> 32) != tag) g[u] = gload(base + off[u]);
+    }
+    use(g);
+  }
+}
+
 // threadIdx.x through an opaque move: lane-dependent addresses derived from it inside the frame loop
 // are recomputed per iteration instead of being hoisted out of the loop and held (spilled) for the
 // whole frame.
