@@ -98,8 +98,16 @@ struct Ctx {
 #ifndef BB_PROBE_DELAY
 #define BB_PROBE_DELAY 32
 #endif
+// BB_DELAY_E2: the E2 wait of the 224 workgroups that run no attention (they wait the whole attention)
+#ifndef BB_EARLY_MQ2
+#define BB_EARLY_MQ2 1
+#endif
+#ifndef BB_DELAY_E2
+#define BB_DELAY_E2 BB_PROBE_DELAY
+#endif
+template <int DELAY = BB_PROBE_DELAY>
 __device__ __forceinline__ void probe_delay() {
-  if (BB_PROBE_DELAY > 0) __builtin_amdgcn_s_sleep(BB_PROBE_DELAY);
+  if (DELAY > 0) __builtin_amdgcn_s_sleep(DELAY);
 }
 __device__ __forceinline__ bool spin_fail(Ctx& c, unsigned spin) {
   if (spin >= SPIN_LIMIT || ((spin & 255) == 255 && __hip_atomic_load(c.p.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
@@ -110,11 +118,11 @@ __device__ __forceinline__ bool spin_fail(Ctx& c, unsigned spin) {
 }
 
 // Wait until granules [0, n) of buf carry this hand-off's tag; values -> out (LDS).
-template <int GPT>
+template <int GPT, int DELAY = BB_PROBE_DELAY>
 __device__ __forceinline__ void gather(Ctx& c, const u64* buf, int n, float* out) {
   const unsigned tag = c.tag();
   u64 g[GPT];
-  probe_delay();
+  probe_delay<DELAY>();
 #pragma unroll
   for (int u = 0; u < GPT; ++u) {
     const int i = c.tid + u * NT;
@@ -489,13 +497,19 @@ __global__ __launch_bounds__(NT, 1) void bb_step_kernel(BbStepArgs p) {
     // during E4 / E5 -- none faster.
     load_o(c, l, wo);
     load_mq(c, l, 0, mq[0]);
-    if (!attn_wg) load_mq(c, l, 1, mq[1]);
+    if (!attn_wg) {
+      load_mq(c, l, 1, mq[1]);
+      // BB_EARLY_MQ2: the 224 workgroups without attention wait the whole attention at E2, so their
+      // third quarter streams there too instead of inside the MLP
+      if (BB_EARLY_MQ2) load_mq(c, l, 2, mq[2]);
+    }
     const Nw nw2 = nw_fetch(c, p.n2[l]);
     if (attn_wg) {
       phase_attn(c, l, pos);                          // waits E1, -> E2
       load_mq(c, l, 1, mq[1]);
     }
-    gather<D / NT>(c, c.rbuf(G_ATT, D), D, L.att);     // E2
+    if (attn_wg) gather<D / NT>(c, c.rbuf(G_ATT, D), D, L.att);  // E2
+    else gather<D / NT, BB_DELAY_E2>(c, c.rbuf(G_ATT, D), D, L.att);
     ++c.e;
     c.refresh();
     phase_o(c, wo);                                   // -> E3
@@ -512,7 +526,7 @@ __global__ __launch_bounds__(NT, 1) void bb_step_kernel(BbStepArgs p) {
     if (!BB_FOLD) rms(c, nw2, L.xn);
     float acc[4];
     phase_mq<0>(c, mq[0], acc, rs2);
-    load_mq(c, l, 2, mq[2]);
+    if (attn_wg || !BB_EARLY_MQ2) load_mq(c, l, 2, mq[2]);
     phase_mq<1>(c, mq[1], acc, rs2);
     load_mq(c, l, 3, mq[3]);
     phase_mq<2>(c, mq[2], acc, rs2);

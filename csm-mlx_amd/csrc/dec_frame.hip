@@ -173,6 +173,22 @@ struct Ctx {
 #ifndef DF_REPOLL
 #define DF_REPOLL 2
 #endif
+// per hand-off kind (E1 q|k|v, E3 / E5 x, E4 down partials, E6 arg-max keys), default DF_PROBE_DELAY
+#ifndef DF_DELAY_E1
+#define DF_DELAY_E1 DF_PROBE_DELAY
+#endif
+#ifndef DF_DELAY_E3
+#define DF_DELAY_E3 DF_PROBE_DELAY
+#endif
+#ifndef DF_DELAY_E4
+#define DF_DELAY_E4 DF_PROBE_DELAY
+#endif
+#ifndef DF_DELAY_E5
+#define DF_DELAY_E5 40
+#endif
+#ifndef DF_DELAY_E6
+#define DF_DELAY_E6 DF_PROBE_DELAY
+#endif
 #ifndef DF_POLL_GAP
 #define DF_POLL_GAP 8
 #endif
@@ -184,9 +200,9 @@ __device__ __forceinline__ bool spin_fail(Ctx& c, unsigned spin) {
   return false;
 }
 // use(x): the lane-local consumption of the matched probe
-template <int GPT, typename F>
+template <int GPT, int DELAY = DF_PROBE_DELAY, typename F>
 __device__ __forceinline__ void poll(Ctx& c, const u64* base, const int (&off)[GPT], const bool (&val)[GPT], F&& use) {
-  poll_granules<GPT, DF_POLL2 != 0, DF_POLL_GAP, DF_PROBE_DELAY, DF_REPOLL>(base, off, val, c.tag(), [&](unsigned spin) { return spin_fail(c, spin); }, use);
+  poll_granules<GPT, DF_POLL2 != 0, DF_POLL_GAP, DELAY, DF_REPOLL>(base, off, val, c.tag(), [&](unsigned spin) { return spin_fail(c, spin); }, use);
   c.stamp();
 }
 
@@ -240,7 +256,7 @@ __device__ __forceinline__ void rms_rows(Ctx& c, float2 nw, int m0 = 0) {
 #ifndef DF_FOLD
 #define DF_FOLD 1
 #endif
-template <int M>
+template <int M, int DELAY>
 __device__ __forceinline__ void gather_x(Ctx& c, const u64* buf, float2 nw) {
   static_assert(D == 2 * NT, "granule tid + NT u is element (u / 2, tid + NT (u % 2))");
   constexpr int GPT = M * D / NT;
@@ -252,7 +268,7 @@ __device__ __forceinline__ void gather_x(Ctx& c, const u64* buf, float2 nw) {
     val[u] = true;
   }
   float sq[MAXM];
-  poll<GPT>(c, buf, off, val, [&](const u64 (&g)[GPT]) {
+  poll<GPT, DELAY>(c, buf, off, val, [&](const u64 (&g)[GPT]) {
 #pragma unroll
     for (int m = 0; m < M; ++m) {
       const float v0 = __uint_as_float((unsigned)g[2 * m]), v1 = __uint_as_float((unsigned)g[2 * m + 1]);
@@ -427,7 +443,7 @@ __device__ __forceinline__ void gather_qkv(Ctx& c, const u64* buf, int pos0, con
     off[u] = c.tid + u * NT;
     val[u] = off[u] < M * QKV;
   }
-  poll<GPT>(c, buf, off, val, [&](const u64 (&g)[GPT]) {
+  poll<GPT, DF_DELAY_E1>(c, buf, off, val, [&](const u64 (&g)[GPT]) {
 #pragma unroll
     for (int u = 0; u < GPT; ++u)
       if (val[u]) qkv_place(c, off[u] / QKV, off[u] % QKV, pos0, __uint_as_float((unsigned)g[u]));
@@ -586,7 +602,7 @@ __device__ __forceinline__ void phase_reduce(Ctx& c) {
       off[2 * m + u] = (v * MAXM + m) * D + 4 * c.w + 2 * half + u;
       val[2 * m + u] = true;
     }
-  poll<2 * M>(c, g, off, val, [&](const u64 (&q)[2 * M]) {
+  poll<2 * M, DF_DELAY_E4>(c, g, off, val, [&](const u64 (&q)[2 * M]) {
 #pragma unroll
     for (int m = 0; m < M; ++m)
 #pragma unroll
@@ -654,7 +670,7 @@ __device__ __forceinline__ int gather_code(Ctx& c, int V) {
   const int off[1] = {c.tid};
   const bool val[1] = {true};
   unsigned wv = 0;
-  poll<1>(c, c.rbuf(G_ARG, NWG * 2), off, val, [&](const u64 (&g)[1]) { wv = (unsigned)g[0]; });
+  poll<1, DF_DELAY_E6>(c, c.rbuf(G_ARG, NWG * 2), off, val, [&](const u64 (&g)[1]) { wv = (unsigned)g[0]; });
   const unsigned ov = __shfl_xor(wv, 1, 64);
   unsigned long long b = (c.tid & 1) ? (((unsigned long long)ov << 32) | wv) : (((unsigned long long)wv << 32) | ov);
 #pragma unroll
@@ -859,7 +875,7 @@ __device__ __forceinline__ void decoder_layer(Ctx& c, int l, int step, int pos0,
   load_gu<GU_EARLY, 8>(c, l, r.wg);
   if (!LAST) { load_qkv(c, l + 1, r.wq); load_o(c, l + 1, r.wo); }
 #if DF_FOLD
-  gather_x<M>(c, c.rbuf(G_X, MAXM * D), nw2);        // E3 -> x, xn = x * n2
+  gather_x<M, DF_DELAY_E3>(c, c.rbuf(G_X, MAXM * D), nw2);  // E3 -> x, xn = x * n2
 #else
   gather<M * D / NT>(c, c.rbuf(G_X, MAXM * D), M * D, &L.x[0][0]);
 #endif
@@ -879,7 +895,7 @@ __device__ __forceinline__ void decoder_layer(Ctx& c, int l, int step, int pos0,
   c.refresh();
   phase_reduce<M>(c);                                 // waits E4, -> E5
 #if DF_FOLD
-  gather_x<M>(c, c.rbuf(G_X, MAXM * D), r.nw1);      // E5 -> x, xn = x * (next n1 | final norm)
+  gather_x<M, DF_DELAY_E5>(c, c.rbuf(G_X, MAXM * D), r.nw1);  // E5 -> x, xn = x * (next n1 | final norm)
 #else
   gather<M * D / NT>(c, c.rbuf(G_X, MAXM * D), M * D, &L.x[0][0]);
 #endif
