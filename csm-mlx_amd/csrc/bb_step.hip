@@ -23,6 +23,8 @@
 // (x * rsqrt(mean(x^2) + eps) * w), RoPE on interleaved pairs (attention.py:157-177, the engine's
 // EPI_QKV convention), softmax with max subtraction, every reduction in a fixed order
 // (deterministic run to run; summation order differs from the launch path's GEMVs).
+#include <type_traits>
+
 #include "csm_kernels.h"
 #include "handoff.h"
 
@@ -99,6 +101,9 @@ struct Ctx {
 #define BB_PROBE_DELAY 32
 #endif
 // BB_DELAY_E2: the E2 wait of the 224 workgroups that run no attention (they wait the whole attention)
+#ifndef BB_ATTN_LATE_PF
+#define BB_ATTN_LATE_PF 0
+#endif
 #ifndef BB_EARLY_MQ2
 #define BB_EARLY_MQ2 1
 #endif
@@ -300,7 +305,25 @@ __device__ __forceinline__ void phase_qkv(Ctx& c, int l, int pos, const WQ& W, b
 // earlier launches), key pos from the E1 granules.  Wave v takes 64-key blocks v, v + 8, ...: lane j
 // scores key 64 b + j (q . k over 64 dims, four fixed FMA chains), online softmax per wave, P.V with
 // lane = head dim over the block's keys in order; waves combined in order 0..7 -> E2.
-__device__ __forceinline__ void phase_attn(Ctx& c, int l, int pos) {
+struct KvPass { float4 kv[4], vv[4]; };  // one 128-key pass of K / V rows in flight
+
+// K / V rows k0 .. k0 + 127 of the pass (keys < pos from the cache, key pos from the E1 granules)
+__device__ __forceinline__ void kv_pass_load(const Ctx& c, const float* K, const float* V, int pos, int k0, KvPass& kp) {
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int idx = c.tid + NT * u, r = idx >> 4, c4 = idx & 15, j = k0 + r;
+    const float4* ks = reinterpret_cast<const float4*>(j < pos ? K + (size_t)j * HD : c.L.kn);
+    const float4* vs = reinterpret_cast<const float4*>(j < pos ? V + (size_t)j * HD : c.L.vn);
+    kp.kv[u] = j <= pos ? ks[c4] : make_float4(0.f, 0.f, 0.f, 0.f);
+    kp.vv[u] = j <= pos ? vs[c4] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+// Attention of query head a (WG a < NATT), in two parts so the caller can issue its weight prefetch
+// between them (BB_ATTN_LATE_PF: after the E1 poll and the first pass's K / V loads, so neither
+// queues behind it):
+// attn_begin: the E1 wait (q_a, k_g, v_g) and the first pass's K / V loads.
+__device__ __forceinline__ void attn_begin(Ctx& c, int l, int pos, KvPass& kp) {
   const int a = c.w, g = a / (HQ / HKV);
   {  // E1 (the hand-off before c.e): q_a, k_g, v_g
     const u64* buf = c.p.gbuf + G_QKV + (size_t)((c.e - 1) & 1) * QKV;
@@ -323,6 +346,13 @@ __device__ __forceinline__ void phase_attn(Ctx& c, int l, int pos) {
     __syncthreads();
     c.stamp(c.e);  // E1 (index e - 1) passed
   }
+  kv_pass_load(c, c.p.kc[l] + (size_t)g * c.p.S_cap * HD, c.p.vc[l] + (size_t)g * c.p.S_cap * HD, pos, 0, kp);
+}
+
+// attn_rest: keys 0..pos over 8 waves x 64-key blocks (wave v takes blocks v, v + 8, ...), online
+// softmax per wave, waves combined in order 0..7 -> E2.
+__device__ __forceinline__ void attn_rest(Ctx& c, int l, int pos, KvPass& kp) {
+  const int a = c.w, g = a / (HQ / HKV);
   const float* K = c.p.kc[l] + (size_t)g * c.p.S_cap * HD;
   const float* V = c.p.vc[l] + (size_t)g * c.p.S_cap * HD;
   const int n = pos + 1;
@@ -331,21 +361,13 @@ __device__ __forceinline__ void phase_attn(Ctx& c, int l, int pos) {
   // weight prefetch can stay in flight through the attention); 64-key block b of the pass is wave
   // (2 * pass + b) % 8's, so every wave still takes blocks v, v + 8, ... in increasing order
   for (int k0 = 0; k0 < n; k0 += 128) {
-    float4 kv[4], vv[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int idx = c.tid + NT * u, r = idx >> 4, c4 = idx & 15, j = k0 + r;
-      const float4* ks = reinterpret_cast<const float4*>(j < pos ? K + (size_t)j * HD : c.L.kn);
-      const float4* vs = reinterpret_cast<const float4*>(j < pos ? V + (size_t)j * HD : c.L.vn);
-      kv[u] = j <= pos ? ks[c4] : make_float4(0.f, 0.f, 0.f, 0.f);
-      vv[u] = j <= pos ? vs[c4] : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
+    if (k0 > 0) kv_pass_load(c, K, V, pos, k0, kp);  // (pass 0 was loaded by attn_begin)
     __syncthreads();  // the previous pass is consumed
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int idx = c.tid + NT * u, r = idx >> 4, c4 = idx & 15;
-      *reinterpret_cast<float4*>(&c.L.Ks[r][4 * c4]) = kv[u];
-      *reinterpret_cast<float4*>(&c.L.Vs[r][4 * c4]) = vv[u];
+      *reinterpret_cast<float4*>(&c.L.Ks[r][4 * c4]) = kp.kv[u];
+      *reinterpret_cast<float4*>(&c.L.Vs[r][4 * c4]) = kp.vv[u];
     }
     __syncthreads();
     const int blk = c.wave - ((k0 >> 6) & 7);  // this wave's block within the pass (0 or 1), if any
@@ -495,6 +517,8 @@ __global__ __launch_bounds__(NT, 1) void bb_step_kernel(BbStepArgs p) {
     // CU's memory pipeline, and E2 waits on them).  Measured alternatives: both
     // quarters after the attention, the third quarter during E3, the next layer's first quarter
     // during E4 / E5 -- none faster.
+    KvPass kp;
+    if (attn_wg && BB_ATTN_LATE_PF) attn_begin(c, l, pos, kp);  // waits E1, first K / V pass in flight
     load_o(c, l, wo);
     load_mq(c, l, 0, mq[0]);
     if (!attn_wg) {
@@ -505,7 +529,8 @@ __global__ __launch_bounds__(NT, 1) void bb_step_kernel(BbStepArgs p) {
     }
     const Nw nw2 = nw_fetch(c, p.n2[l]);
     if (attn_wg) {
-      phase_attn(c, l, pos);                          // waits E1, -> E2
+      if (!BB_ATTN_LATE_PF) attn_begin(c, l, pos, kp);
+      attn_rest(c, l, pos, kp);                       // -> E2
       load_mq(c, l, 1, mq[1]);
     }
     if (attn_wg) gather<D / NT>(c, c.rbuf(G_ATT, D), D, L.att);  // E2

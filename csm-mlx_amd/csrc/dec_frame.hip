@@ -164,6 +164,12 @@ struct Ctx {
 
 // Hand-off waits (handoff.h poll_granules): DF_POLL2 keeps two probes in flight, DF_POLL_GAP
 // sleeps apart.
+#ifndef DF_DN_EARLY
+#define DF_DN_EARLY 0
+#endif
+#ifndef DF_GU_E45
+#define DF_GU_E45 0   // gate/up rows per wave of the next layer fetched during E4 / E5 (<= GU_EARLY)
+#endif
 #ifndef DF_POLL2
 #define DF_POLL2 0
 #endif
@@ -852,7 +858,7 @@ __device__ __forceinline__ void decoder_layer(Ctx& c, int l, int step, int pos0,
     // prefetches issued after the publish (its RoPE operand load would otherwise retire behind
     // them in vmcnt order), still ahead of the hand-off wait they hide under
     kv_issue(c, l, pos0, kv);
-    load_dn(c, l, r.wd);
+    if (FIRST || !DF_DN_EARLY) load_dn(c, l, r.wd);
 #if DF_KVDIRECT
     gather_qkv<M>(c, c.rbuf(G_QKV, MAXM * QKV), pos0, kv);  // (its barrier publishes the history too)
     ++c.e;
@@ -867,7 +873,8 @@ __device__ __forceinline__ void decoder_layer(Ctx& c, int l, int step, int pos0,
   c.refresh();
   c.mark();
   const float2 nw2 = nw_fetch(c, p.n2[l]);
-  load_gu<0, GU_EARLY>(c, l, r.wg);
+  if (FIRST || DF_GU_E45 == 0) load_gu<0, GU_EARLY>(c, l, r.wg);  // (layers >= 1: rows < DF_GU_E45 came at E4 / E5)
+  else if (DF_GU_E45 < GU_EARLY) load_gu<DF_GU_E45, GU_EARLY>(c, l, r.wg);
   phase_attn<M>(c, pos0, l);
   c.mark();
   phase_o<M>(c, r.wo);                                // -> E3
@@ -883,6 +890,10 @@ __device__ __forceinline__ void decoder_layer(Ctx& c, int l, int step, int pos0,
   c.refresh();
   if (!DF_FOLD) rms_rows<M>(c, nw2);
   phase_mlp<M, DF_FOLD>(c, r.wg, r.wd);                // -> E4
+  // DF_DN_EARLY: the next layer's down slices stream during this layer's E4 / E5 (its registers
+  // were just consumed) instead of during the next E1 wait
+  if (DF_DN_EARLY && !LAST) load_dn(c, l + 1, r.wd);
+  if (DF_GU_E45 > 0 && !LAST) load_gu<0, DF_GU_E45>(c, l + 1, r.wg);
   r.nw1 = nw_fetch(c, LAST ? p.norm : p.n1[l + 1]);  // next layer's norm, or the final one
   c.mark();
   if (LAST) {
