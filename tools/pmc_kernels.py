@@ -21,7 +21,7 @@ top = int(sys.argv[sys.argv.index("--top") + 1]) if "--top" in sys.argv else 25
 
 
 def kname(r):
-    n = r.get("Kernel_Name", "").replace("void ", "")
+    n = r.get("Kernel_Name", "").replace("void ", "").replace("(anonymous namespace)::", "")
     return n.split("(")[0][:90]
 
 
