@@ -123,7 +123,8 @@ constexpr size_t G_QKV = G_X + 2 * REP * rs_of(MAXM * D);               // [2][R
 constexpr size_t G_PART = G_QKV + 2 * REP * rs_of(MAXM * QKV);          // [2][NWG][MAXM][D] down partials
 constexpr size_t G_ARG = G_PART + (size_t)2 * NWG * MAXM * D;           // [2][REP][rs(NWG*2)] arg-max keys
 constexpr size_t G_LOG = G_ARG + 2 * REP * rs_of(NWG * 2);              // [2][REP][rs(VMAX)] logits (sampling)
-constexpr size_t G_TOTAL = G_LOG + 2 * REP * rs_of(VMAX);
+constexpr size_t G_GUM = G_LOG + 2 * REP * rs_of(VMAX);               // [2][REP][rs(NWG*3)] Gumbel-max keys
+constexpr size_t G_TOTAL = G_GUM + 2 * REP * rs_of(NWG * 3);
 
 struct Ctx {
   const DecFrameArgs& p;
@@ -164,6 +165,9 @@ struct Ctx {
 
 // Hand-off waits (handoff.h poll_granules): DF_POLL2 keeps two probes in flight, DF_POLL_GAP
 // sleeps apart.
+#ifndef DF_DN_AFTER_E1
+#define DF_DN_AFTER_E1 0
+#endif
 #ifndef DF_DN_EARLY
 #define DF_DN_EARLY 0
 #endif
@@ -627,10 +631,22 @@ __device__ __forceinline__ void phase_reduce(Ctx& c) {
   }
 }
 
+// Temperature sampling without a top-k threshold (the reference generate()'s default, generation.py:
+// 51-54, :102): handled by per-workgroup Gumbel-max keys (phase_head / gumbel_code), not by handing
+// every logit to every workgroup.
+__device__ __forceinline__ bool gumbel_local(const DecFrameArgs& p) {
+  return p.temperature > 0.f && (p.top_k <= 0 || p.top_k >= p.V);
+}
+// order-preserving double -> u64 (larger value, larger key; every non-NaN value above key 0)
+__device__ __forceinline__ unsigned long long dkey(double d) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(d);
+  return (u >> 63) ? ~u : (u | (1ull << 63));
+}
+
 // Head rows of this WG on row xn[0] (K = 1024 or 2048) -> arg-max key -> E6 granules (hi, lo words)
 template <int KH>
 __device__ __forceinline__ void phase_head(Ctx& c, const bf16_t* W, int n_valid, const u32x4_t (&wa)[KH / 512],
-                                           const u32x4_t (&wx)[KH / 512], float* logits, int xm = 0, float rs = 1.f) {
+                                           const u32x4_t (&wx)[KH / 512], float* logits, int cb, int xm = 0, float rs = 1.f) {
   constexpr int CPL = KH / 512;  // chunks per lane
   const int row = 8 * c.w + c.wave;
   const float* xin = c.L.xn[xm];  // input row (folded RMSNorm: un-normalised, scaled by rs after the dot)
@@ -650,7 +666,40 @@ __device__ __forceinline__ void phase_head(Ctx& c, const bf16_t* W, int n_valid,
     best = k2 > best ? k2 : best;
     if (c.lane == 0 && xr < n_valid) logits[xr] = t;
   }
-  if (c.p.temperature > 0.f) {  // sampling: every logit to every workgroup (sample_code)
+  if (gumbel_local(c.p)) {
+    // temperature sampling with no top-k filter: the Gumbel-max is a max over independent perturbed
+    // logits, so each workgroup reduces its own rows and hands on one (value, index) key
+    const float inv_t = 1.0f / c.p.temperature;
+    const uint64_t key = gumbel_key(c.p.seeds[0], c.p.frame_ctr[0] * c.p.K + cb);
+    unsigned long long bk = 0ull;
+    int bi = 0x7fffffff;
+    auto cand = [&](float l, int v) {  // sample_code's rule: perturbed value strictly above -inf, first max
+      if (!(l >= -INFINITY)) return;   // NaN logits never win
+      double val = (double)(l * inv_t) + gumbel_noise(key, v);
+      if (!(val > -INFINITY)) return;
+      if (val == 0.0) val = 0.0;       // -0 and +0 compare equal in sample_code: one key
+      const unsigned long long k = dkey(val);
+      if (k > bk || (k == bk && v < bi)) { bk = k; bi = v; }
+    };
+    if (c.lane == 0 && row < n_valid) cand(s, row);
+    if (c.lane == 0 && c.wave == 0 && c.w < 3 && xr < n_valid) cand(t, xr);
+    unsigned long long* gk = reinterpret_cast<unsigned long long*>(&c.L.wsum[0][0]);
+    int* gi = reinterpret_cast<int*>(gk + 8);
+    if (c.lane == 0) { gk[c.wave] = bk; gi[c.wave] = bi; }
+    __syncthreads();
+    if (c.tid < REP) {
+      unsigned long long b = gk[0];
+      int ib = gi[0];
+      for (int i = 1; i < 8; ++i)
+        if (gk[i] > b || (gk[i] == b && gi[i] < ib)) { b = gk[i]; ib = gi[i]; }
+      c.put_u(G_GUM, NWG * 3, 3 * c.w, (unsigned)(b >> 32), c.tid);
+      c.put_u(G_GUM, NWG * 3, 3 * c.w + 1, (unsigned)b, c.tid);
+      c.put_u(G_GUM, NWG * 3, 3 * c.w + 2, (unsigned)ib, c.tid);
+    }
+    __syncthreads();
+    return;
+  }
+  if (c.p.temperature > 0.f) {  // sampling with top-k: every logit to every workgroup (sample_code)
     if (c.lane < REP && row < n_valid) c.put(G_LOG, VMAX, row, s, c.lane);
     if (c.lane < REP && c.wave == 0 && c.w < 3 && xr < n_valid) c.put(G_LOG, VMAX, xr, t, c.lane);
     __syncthreads();
@@ -794,9 +843,54 @@ __device__ __forceinline__ int sample_code(Ctx& c, int V, int cb) {
   return c.code;
 }
 
-// the code of a head: greedy arg-max of the published keys, or the sampler over the logits
+// Gather the 256 workgroups' Gumbel-max keys (value key hi, lo, index) -> code: max value, lowest
+// index on ties; no candidate anywhere (every logit NaN or -inf) -> V - 1, as sample_kernel.
+__device__ __forceinline__ int gumbel_code(Ctx& c, int V) {
+  constexpr int NG = NWG * 3, GPT = (NG + NT - 1) / NT;
+  int off[GPT];
+  bool val[GPT];
+#pragma unroll
+  for (int u = 0; u < GPT; ++u) {
+    off[u] = c.tid + u * NT;
+    val[u] = off[u] < NG;
+  }
+  unsigned* words = reinterpret_cast<unsigned*>(&c.L.red[0][0]);
+  poll<GPT, DF_DELAY_E6>(c, c.rbuf(G_GUM, NWG * 3), off, val, [&](const u64 (&g)[GPT]) {
+#pragma unroll
+    for (int u = 0; u < GPT; ++u)
+      if (val[u]) words[off[u]] = (unsigned)g[u];
+  });
+  __syncthreads();
+  unsigned long long b = 0ull;
+  int ib = 0x7fffffff;
+  if (c.tid < NWG) {
+    b = ((unsigned long long)words[3 * c.tid] << 32) | words[3 * c.tid + 1];
+    ib = (int)words[3 * c.tid + 2];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long ob = __shfl_xor(b, o, 64);
+    const int oi = __shfl_xor(ib, o, 64);
+    if (ob > b || (ob == b && oi < ib)) { b = ob; ib = oi; }
+  }
+  unsigned long long* wk = reinterpret_cast<unsigned long long*>(&c.L.wsum[0][0]);
+  int* wi = reinterpret_cast<int*>(wk + 8);
+  __syncthreads();  // (words read by every wave before wsum is reused)
+  if (c.lane == 0 && c.wave < NWG / 64) { wk[c.wave] = b; wi[c.wave] = ib; }
+  __syncthreads();
+  b = wk[0];
+  ib = wi[0];
+#pragma unroll
+  for (int i = 1; i < NWG / 64; ++i)
+    if (wk[i] > b || (wk[i] == b && wi[i] < ib)) { b = wk[i]; ib = wi[i]; }
+  c.code = b == 0ull ? V - 1 : min(max(ib, 0), V - 1);
+  return c.code;
+}
+
+// the code of a head: greedy arg-max of the published keys, or the sampler
 __device__ __forceinline__ int head_code(Ctx& c, int V, int cb) {
-  return c.p.temperature > 0.f ? sample_code(c, V, cb) : gather_code(c, V);
+  if (c.p.temperature <= 0.f) return gather_code(c, V);
+  return gumbel_local(c.p) ? gumbel_code(c, V) : sample_code(c, V, cb);
 }
 
 // Registers carried between phases (prefetched weights, norm weights)
@@ -858,7 +952,7 @@ __device__ __forceinline__ void decoder_layer(Ctx& c, int l, int step, int pos0,
     // prefetches issued after the publish (its RoPE operand load would otherwise retire behind
     // them in vmcnt order), still ahead of the hand-off wait they hide under
     kv_issue(c, l, pos0, kv);
-    if (FIRST || !DF_DN_EARLY) load_dn(c, l, r.wd);
+    if ((FIRST || !DF_DN_EARLY) && !DF_DN_AFTER_E1) load_dn(c, l, r.wd);
 #if DF_KVDIRECT
     gather_qkv<M>(c, c.rbuf(G_QKV, MAXM * QKV), pos0, kv);  // (its barrier publishes the history too)
     ++c.e;
@@ -873,6 +967,8 @@ __device__ __forceinline__ void decoder_layer(Ctx& c, int l, int step, int pos0,
   c.refresh();
   c.mark();
   const float2 nw2 = nw_fetch(c, p.n2[l]);
+  // DF_DN_AFTER_E1: the down slices issued after the q|k|v wait (not ahead of it) on layers that wait
+  if (DF_DN_AFTER_E1 && !(FIRST && step > 1)) load_dn(c, l, r.wd);
   if (FIRST || DF_GU_E45 == 0) load_gu<0, GU_EARLY>(c, l, r.wg);  // (layers >= 1: rows < DF_GU_E45 came at E4 / E5)
   else if (DF_GU_E45 < GU_EARLY) load_gu<DF_GU_E45, GU_EARLY>(c, l, r.wg);
   phase_attn<M>(c, pos0, l);
@@ -925,10 +1021,10 @@ __device__ __forceinline__ void run_step(Ctx& c, int step, Pre& r) {
   c.refresh();
 #if DF_FOLD
   phase_head<D>(c, p.audio_head + (size_t)(step - 1) * p.VP * D, p.V, r.wh.a, r.wh.x, p.ci_logits + (size_t)(step - 1) * p.VP,
-                M - 1, row_rs(c, M - 1));  // -> E6
+                step, M - 1, row_rs(c, M - 1));  // -> E6
 #else
   rms_rows<1>(c, r.nw1, M - 1);
-  phase_head<D>(c, p.audio_head + (size_t)(step - 1) * p.VP * D, p.V, r.wh.a, r.wh.x, p.ci_logits + (size_t)(step - 1) * p.VP);  // -> E6
+  phase_head<D>(c, p.audio_head + (size_t)(step - 1) * p.VP * D, p.V, r.wh.a, r.wh.x, p.ci_logits + (size_t)(step - 1) * p.VP, step);  // -> E6
 #endif
   KvRegs kv0;  // layer 0's cached K/V rows of the next step: in flight during the head's hand-off,
   if (step + 1 < p.K) kv_issue(c, 0, step + 1, kv0);
@@ -966,7 +1062,7 @@ __global__ __launch_bounds__(NT, 1) void dec_frame_kernel(DecFrameArgs p) {
   load_o(c, 0, r.wo);
   for (int k = c.tid; k < DB; k += NT) L.xn[0][k] = p.h_last[k];
   __syncthreads();
-  phase_head<DB>(c, p.c0_head, p.V, c0a, c0x, p.c0_logits);  // -> G_ARG (hand-off 0)
+  phase_head<DB>(c, p.c0_head, p.V, c0a, c0x, p.c0_logits, 0);  // -> G_ARG (hand-off 0)
   {
     float s = dot8(pa[0], L.xn[0] + 8 * (128 * (c.wave & 1) + c.lane)) + dot8(pa[1], L.xn[0] + 8 * (128 * (c.wave & 1) + c.lane + 64));
     s = wave_sum(s);
