@@ -376,8 +376,13 @@ void xs_shape(int N, int K, int M, bool head, int& rtw, int& ks, int& pd) {
   static const int rtw_long = [] { const char* v = getenv("CSM_XS_LONGK_RTW"); return v ? atoi(v) : 1; }();
   rtw = (N >= 4096 || head) ? 2 : (K >= 4096 ? rtw_long : 1);
   const int tiles = (N + 32 * rtw - 1) / (32 * rtw);
+  // split-K slices until the grid has >= `target` blocks (CSM_XS_BLOCKS lab knob; the short-K small
+  // projections -- QKV / o -- can take a lower target: CSM_XS_SMALL_BLOCKS)
+  static const int target = [] { const char* v = getenv("CSM_XS_BLOCKS"); return v ? atoi(v) : 256; }();
+  static const int small_target = [] { const char* v = getenv("CSM_XS_SMALL_BLOCKS"); return v ? atoi(v) : 256; }();
+  const int tgt = (N <= 2048 && K <= 2048 && !head) ? small_target : target;
   ks = 1;
-  while (tiles * ks < 256 && ks < MAX_SLICES && nks / (ks * 2) >= XW && nks % (ks * 2) == 0) ks *= 2;
+  while (tiles * ks < tgt && ks < MAX_SLICES && nks / (ks * 2) >= XW && nks % (ks * 2) == 0) ks *= 2;
   const int wst = nks / ks / XW;
   const int cap = M > 32 ? (rtw == 2 ? 1 : 2) : 4;
   pd = 1;

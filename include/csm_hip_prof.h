@@ -44,7 +44,11 @@ int csm_bench_bb_step(csm_engine* e, int iters, float* avg_us, double* bytes);
  * "bb_step" (batch-1 bf16 backbone rows on the persistent backbone step, bb_step.hip: 16 blocks + the
  * final norm in one launch, default 1), "dec_frame_stamps" / "bb_step_stamps" (per-hand-off clock
  * stamps of the persistent kernels, read back with csm_debug_read, default 0), "linear_mfma" (csm_linear runs the batched frame's MFMA GEMM at >= 8 rows instead of the GEMV,
- * default 0: the GEMM's kernel tests). */
+ * default 0: the GEMM's kernel tests), "gemm_xs" (the batched depth decoder on the streaming
+ * matrix-core GEMM, gemm_xs.hip, default 1), "bb_xs" (the batched backbone on it too, default 0),
+ * "prefill_rows" (row cap of one csm_prefill_batch group, 0 = the engine's capacity), "tab_rep"
+ * (1..8 copies of the folded proj_tab / qkv0_tab that the persistent frame decoder spreads its
+ * workgroups over, default 1: 650 MB per extra copy on csm_1b). */
 int csm_set_option(csm_engine* e, const char* key, int value);
 
 #ifdef __cplusplus
