@@ -125,6 +125,20 @@ __device__ __forceinline__ bool spin_fail(Ctx& c, unsigned spin) {
 // Wait until granules [0, n) of buf carry this hand-off's tag; values -> out (LDS).
 template <int GPT, int DELAY = BB_PROBE_DELAY>
 __device__ __forceinline__ void gather(Ctx& c, const u64* buf, int n, float* out) {
+#if BB_PAIR16
+  // granule pairs 2t + D/2 h (n == D: every pair whole)
+  const unsigned tag = c.tag();
+  const int poff[GPT / 2] = {2 * c.tid, D / 2 + 2 * c.tid};
+  poll_pairs<GPT / 2, DELAY, 1>(buf, 0x7fffffff, poff, tag, [&](unsigned spin) { return spin_fail(c, spin); },
+                                [&](const u32x4_t (&g)[GPT / 2]) {
+#pragma unroll
+    for (int h = 0; h < GPT / 2; ++h)
+      *reinterpret_cast<float2*>(&out[poff[h]]) = make_float2(__uint_as_float(g[h].x), __uint_as_float(g[h].z));
+  });
+  c.stamp(c.e + 1);
+  __syncthreads();
+  (void)n;
+#else
   const unsigned tag = c.tag();
   u64 g[GPT];
   probe_delay<DELAY>();
@@ -152,14 +166,28 @@ __device__ __forceinline__ void gather(Ctx& c, const u64* buf, int n, float* out
     if (i < n) out[i] = __uint_as_float((unsigned)g[u]);
   }
   __syncthreads();
+#endif
 }
 
-// xn[k] = x[k] * rsqrt(mean(x^2) + eps) * nw[k]; nw elements tid + 512 j fetched a phase ahead
+// BB_PAIR16 (as dec_frame.hip DF_PAIR16): the x / attention-output hand-offs and the down partials
+// polled as granule pairs, one 16-B load each; thread t then owns elements 2t, 2t + 1, 1024 + 2t,
+// 1024 + 2t + 1 of a row (else t + 512 j)
+#ifndef BB_PAIR16
+#define BB_PAIR16 1
+#endif
+// BB_E4_16: each thread's down rows are el(k) and its partials go out two granules per 16-B store
+#ifndef BB_E4_16
+#define BB_E4_16 0
+#endif
+__device__ __forceinline__ int el(const Ctx& c, int j) {
+  return BB_PAIR16 ? (j >> 1) * (D / 2) + 2 * c.tid + (j & 1) : c.tid + j * NT;
+}
+// xn[k] = x[k] * rsqrt(mean(x^2) + eps) * nw[k]; nw elements el(j) fetched a phase ahead
 struct Nw { float v[D / NT]; };
 __device__ __forceinline__ Nw nw_fetch(const Ctx& c, const float* nw) {
   Nw r;
 #pragma unroll
-  for (int j = 0; j < D / NT; ++j) r.v[j] = nw[c.tid + j * NT];
+  for (int j = 0; j < D / NT; ++j) r.v[j] = nw[el(c, j)];
   return r;
 }
 __device__ __forceinline__ void rms(Ctx& c, const Nw& nw, float* out) {
@@ -173,7 +201,7 @@ __device__ __forceinline__ void rms(Ctx& c, const Nw& nw, float* out) {
   __syncthreads();
   const float r = rsqrtf(c.L.wsum[0][0] / (float)D + c.p.eps);
 #pragma unroll
-  for (int j = 0; j < D / NT; ++j) out[c.tid + j * NT] = c.L.x[c.tid + j * NT] * r * nw.v[j];
+  for (int j = 0; j < D / NT; ++j) out[el(c, j)] = c.L.x[el(c, j)] * r * nw.v[j];
   __syncthreads();
 }
 
@@ -186,6 +214,22 @@ __device__ __forceinline__ void rms(Ctx& c, const Nw& nw, float* out) {
 __device__ __forceinline__ void gather_x(Ctx& c, const u64* buf, const Nw& nw) {
   constexpr int GPT = D / NT;
   const unsigned tag = c.tag();
+  float sq = 0.f;
+#if BB_PAIR16
+  const int poff[GPT / 2] = {2 * c.tid, D / 2 + 2 * c.tid};
+  poll_pairs<GPT / 2, BB_PROBE_DELAY, 1>(buf, 0x7fffffff, poff, tag, [&](unsigned spin) { return spin_fail(c, spin); },
+                                         [&](const u32x4_t (&g)[GPT / 2]) {
+#pragma unroll
+    for (int h = 0; h < GPT / 2; ++h) {
+      const float v0 = __uint_as_float(g[h].x), v1 = __uint_as_float(g[h].z);
+      *reinterpret_cast<float2*>(&c.L.x[poff[h]]) = make_float2(v0, v1);
+      *reinterpret_cast<float2*>(&c.L.xn[poff[h]]) = make_float2(v0 * nw.v[2 * h], v1 * nw.v[2 * h + 1]);
+      sq = fmaf(v0, v0, sq);
+      sq = fmaf(v1, v1, sq);
+    }
+  });
+  c.stamp(c.e + 1);
+#else
   u64 g[GPT];
   probe_delay();
 #pragma unroll
@@ -201,7 +245,6 @@ __device__ __forceinline__ void gather_x(Ctx& c, const u64* buf, const Nw& nw) {
       if ((unsigned)(g[u] >> 32) != tag) g[u] = gload(buf + c.tid + u * NT);
   }
   c.stamp(c.e + 1);
-  float sq = 0.f;
 #pragma unroll
   for (int u = 0; u < GPT; ++u) {
     const float v = __uint_as_float((unsigned)g[u]);
@@ -209,6 +252,7 @@ __device__ __forceinline__ void gather_x(Ctx& c, const u64* buf, const Nw& nw) {
     c.L.xn[c.tid + u * NT] = v * nw.v[u];
     sq = fmaf(v, v, sq);
   }
+#endif
   sq = wave_sum(sq);
   if (c.lane == 0) c.L.sq[c.wave] = sq;
   __syncthreads();
@@ -250,7 +294,8 @@ __device__ __forceinline__ void load_mq(Ctx& c, int l, int Q, WMq& r) {
   // chunk 4w + Q of [F/8][D][8]: row n at byte (n * 8) * 2
   const bf16_t* d = c.p.wdc[l] + (size_t)(4 * c.w + Q) * D * 8;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) r.d[k] = bload<2>(d, c.tid * 16, k * NT * 8 * 2);
+  for (int k = 0; k < 4; ++k)  // rows el(k): 2t + (k & 1) + 1024 (k >> 1) with BB_E4_16, else t + 512 k
+    r.d[k] = BB_E4_16 ? bload<2>(d, c.tid * 32, ((k >> 1) * (D / 2) + (k & 1)) * 16) : bload<2>(d, c.tid * 16, k * NT * 8 * 2);
 }
 
 // per-row partial sums of a (half, chunk)-split projection: wave partials -> wsum[wave][i]
@@ -458,6 +503,19 @@ __device__ __forceinline__ void phase_reduce(Ctx& c) {
   const u64* g = c.buf(G_PART, (size_t)NWG * D);
   const int v = c.tid >> 1, half = c.tid & 1;
   const u64* src = g + (size_t)v * D + 8 * c.w + 4 * half;
+#if BB_PAIR16
+  const int poff[2] = {v * D + 8 * c.w + 4 * half, v * D + 8 * c.w + 4 * half + 2};
+  poll_pairs<2, BB_PROBE_DELAY, 1>(g, 0x7fffffff, poff, tag, [&](unsigned spin) { return spin_fail(c, spin); },
+                                   [&](const u32x4_t (&q)[2]) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      c.L.red[4 * half + 2 * h][v] = __uint_as_float(q[h].x);
+      c.L.red[4 * half + 2 * h + 1][v] = __uint_as_float(q[h].z);
+    }
+  });
+  c.stamp(c.e + 1);
+  (void)src;
+#else
   u64 q[4];
   probe_delay();
 #pragma unroll
@@ -475,6 +533,7 @@ __device__ __forceinline__ void phase_reduce(Ctx& c) {
   c.stamp(c.e + 1);
 #pragma unroll
   for (int u = 0; u < 4; ++u) c.L.red[4 * half + u][v] = __uint_as_float((unsigned)q[u]);
+#endif
   __syncthreads();
   ++c.e;  // the x hand-off that follows
   {
@@ -558,8 +617,18 @@ __global__ __launch_bounds__(NT, 1) void bb_step_kernel(BbStepArgs p) {
     phase_mq<3>(c, mq[3], acc, rs2);
     {
       u64* g = c.buf(G_PART, (size_t)NWG * D) + (size_t)c.w * D;
+      if (BB_E4_16) {  // rows 2t, 2t + 1 (+ 1024): two granules per 16-B sc1 store   -> E4
+        const unsigned tg = c.tag();
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(g, 0, 0x7fffffff, 0x00020000);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) gput(g + c.tid + NT * k, acc[k], c.tag());   // -> E4
+        for (int h = 0; h < 2; ++h) {
+          const u32x4_t v = {__float_as_uint(acc[2 * h]), tg, __float_as_uint(acc[2 * h + 1]), tg};
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rs, (h * (D / 2) + 2 * c.tid) * 8, 0, 16);
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) gput(g + c.tid + NT * k, acc[k], c.tag());   // -> E4
+      }
     }
     nw1 = nw_fetch(c, l + 1 < NL ? p.n1[l + 1] : p.norm);
     c.refresh();

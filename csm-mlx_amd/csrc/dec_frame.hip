@@ -220,6 +220,37 @@ __device__ __forceinline__ void poll(Ctx& c, const u64* base, const int (&off)[G
 // tid, tid + NT, ... (at most GPT each).
 template <int GPT>
 __device__ __forceinline__ void gather(Ctx& c, const u64* buf, int n, float* out) {
+#if DF_PAIR16
+  // granule pairs (2i, 2i + 1), i = tid, tid + NT, ...; a granule past n (odd n) counts as current
+  constexpr int GPP = (GPT + 1) / 2;
+  const int np = (n + 1) / 2;
+  int poff[GPP];
+#pragma unroll
+  for (int u = 0; u < GPP; ++u) poff[u] = 2 * min(c.tid + u * NT, np - 1);
+  const unsigned tag = c.tag();
+  if (DF_PROBE_DELAY > 0) __builtin_amdgcn_s_sleep(DF_PROBE_DELAY);
+  auto cur1 = [&](const u32x4_t& x, int i) { return x.y == tag && (i + 1 >= n || x.w == tag); };
+  u32x4_t g[GPP];
+#pragma unroll
+  for (int u = 0; u < GPP; ++u) g[u] = sc1_load16(buf, poff[u] * 8, 0x7fffffff);
+  for (unsigned spin = 0;; ++spin) {
+    bool ok = true;
+#pragma unroll
+    for (int u = 0; u < GPP; ++u) ok &= cur1(g[u], poff[u]);
+    if (ok || spin_fail(c, spin)) break;
+    __builtin_amdgcn_s_sleep(DF_REPOLL);
+#pragma unroll
+    for (int u = 0; u < GPP; ++u)
+      if (!cur1(g[u], poff[u])) g[u] = sc1_load16(buf, poff[u] * 8, 0x7fffffff);
+  }
+  c.stamp();
+#pragma unroll
+  for (int u = 0; u < GPP; ++u)
+    if (c.tid + u * NT < np) {
+      out[poff[u]] = __uint_as_float(g[u].x);
+      if (poff[u] + 1 < n) out[poff[u] + 1] = __uint_as_float(g[u].z);
+    }
+#else
   int off[GPT];
   bool val[GPT];
 #pragma unroll
@@ -232,12 +263,20 @@ __device__ __forceinline__ void gather(Ctx& c, const u64* buf, int n, float* out
     for (int u = 0; u < GPT; ++u)
       if (val[u]) out[off[u]] = __uint_as_float((unsigned)g[u]);
   });
+#endif
   __syncthreads();
 }
 
 // xn[m][k] = x[m][k] * rsqrt(mean(x^2) + eps) * nw[k] for rows m < M (every WG computes the same)
 // RMSNorm weight elements tid and tid + 512 (every element a thread scales), fetched a phase ahead
-__device__ __forceinline__ float2 nw_fetch(const Ctx& c, const float* nw) { return make_float2(nw[c.tid], nw[c.tid + NT]); }
+// DF_PAIR16: x hand-offs (E3 / E5) and the down partials (E4) polled as granule pairs, one 16-B load
+// each (thread t owns elements 2t, 2t + 1 of a row instead of t, t + NT)
+#ifndef DF_PAIR16
+#define DF_PAIR16 1
+#endif
+__device__ __forceinline__ int el0(const Ctx& c) { return DF_PAIR16 ? 2 * c.tid : c.tid; }
+__device__ __forceinline__ int el1(const Ctx& c) { return DF_PAIR16 ? 2 * c.tid + 1 : c.tid + NT; }
+__device__ __forceinline__ float2 nw_fetch(const Ctx& c, const float* nw) { return make_float2(nw[el0(c)], nw[el1(c)]); }
 
 template <int M>
 __device__ __forceinline__ void rms_rows(Ctx& c, float2 nw, int m0 = 0) {
@@ -253,8 +292,8 @@ __device__ __forceinline__ void rms_rows(Ctx& c, float2 nw, int m0 = 0) {
   __syncthreads();
   for (int m = 0; m < M; ++m) {
     const float r = rsqrtf(c.L.wsum[0][m] / (float)D + c.p.eps);
-    c.L.xn[m][c.tid] = c.L.x[m0 + m][c.tid] * r * nw.x;
-    c.L.xn[m][c.tid + NT] = c.L.x[m0 + m][c.tid + NT] * r * nw.y;
+    c.L.xn[m][el0(c)] = c.L.x[m0 + m][el0(c)] * r * nw.x;
+    c.L.xn[m][el1(c)] = c.L.x[m0 + m][el1(c)] * r * nw.y;
   }
   __syncthreads();
 }
@@ -278,6 +317,23 @@ __device__ __forceinline__ void gather_x(Ctx& c, const u64* buf, float2 nw) {
     val[u] = true;
   }
   float sq[MAXM];
+#if DF_PAIR16
+  int poff[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) poff[m] = m * D + 2 * c.tid;
+  poll_pairs<M, DELAY, DF_REPOLL>(buf, 0x7fffffff, poff, c.tag(), [&](unsigned spin) { return spin_fail(c, spin); },
+                                  [&](const u32x4_t (&g)[M]) {
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const float v0 = __uint_as_float(g[m].x), v1 = __uint_as_float(g[m].z);
+      *reinterpret_cast<float2*>(&c.L.x[m][2 * c.tid]) = make_float2(v0, v1);
+      *reinterpret_cast<float2*>(&c.L.xn[m][2 * c.tid]) = make_float2(v0 * nw.x, v1 * nw.y);
+      sq[m] = fmaf(v1, v1, v0 * v0);
+    }
+  });
+  c.stamp();
+  (void)off; (void)val;
+#else
   poll<GPT, DELAY>(c, buf, off, val, [&](const u64 (&g)[GPT]) {
 #pragma unroll
     for (int m = 0; m < M; ++m) {
@@ -289,6 +345,7 @@ __device__ __forceinline__ void gather_x(Ctx& c, const u64* buf, float2 nw) {
       sq[m] = fmaf(v1, v1, v0 * v0);
     }
   });
+#endif
 #pragma unroll
   for (int m = 0; m < M; ++m) {
     const float t = wave_sum(sq[m]);
@@ -336,14 +393,19 @@ __device__ __forceinline__ void load_gu(Ctx& c, int l, WGu& r) {
     r.a[i][1] = bload(base, v, i * D * 2 + 1024);
   }
 }
+// DF_E4_16: thread t computes down rows 2t, 2t + 1 (not t, t + 512) and publishes both partials in
+// one 16-B sc1 store (two granules, each with its own tag)
+#ifndef DF_E4_16
+#define DF_E4_16 1
+#endif
 __device__ __forceinline__ void load_dn(Ctx& c, int l, WDn& r) {
   const bf16_t* base = c.p.wdc[l] + (size_t)(2 * c.w) * D * 16;
-  const int v = c.tid * 16 * 2;
+  const int v = DF_E4_16 ? c.tid * 16 * 2 * 2 : c.tid * 16 * 2;
 #pragma unroll
   for (int s = 0; s < 2; ++s)
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-      const int so = (q * D * 16 + 512 * s * 16) * 2;
+      const int so = DF_E4_16 ? (q * D * 16 + s * 16) * 2 : (q * D * 16 + 512 * s * 16) * 2;
       r.a[s][q][0] = bload(base, v, so);
       r.a[s][q][1] = bload(base, v, so + 16);
     }
@@ -453,11 +515,30 @@ __device__ __forceinline__ void gather_qkv(Ctx& c, const u64* buf, int pos0, con
     off[u] = c.tid + u * NT;
     val[u] = off[u] < M * QKV;
   }
+#if DF_PAIR16
+  constexpr int NP = M * QKV / 2, GPP = (NP + NT - 1) / NT;  // granule pairs; thread t: pairs t, t + NT
+  int poff[GPP];
+#pragma unroll
+  for (int u = 0; u < GPP; ++u) poff[u] = 2 * min(c.tid + u * NT, NP - 1);  // (a clamped pair is re-read, unused)
+  poll_pairs<GPP, DF_DELAY_E1, DF_REPOLL>(buf, 0x7fffffff, poff, c.tag(), [&](unsigned spin) { return spin_fail(c, spin); },
+                                          [&](const u32x4_t (&g)[GPP]) {
+#pragma unroll
+    for (int u = 0; u < GPP; ++u)
+      if (c.tid + u * NT < NP) {
+        const int i = poff[u];
+        qkv_place(c, i / QKV, i % QKV, pos0, __uint_as_float(g[u].x));
+        qkv_place(c, (i + 1) / QKV, (i + 1) % QKV, pos0, __uint_as_float(g[u].z));
+      }
+  });
+  c.stamp();
+  (void)off; (void)val;
+#else
   poll<GPT, DF_DELAY_E1>(c, buf, off, val, [&](const u64 (&g)[GPT]) {
 #pragma unroll
     for (int u = 0; u < GPT; ++u)
       if (val[u]) qkv_place(c, off[u] / QKV, off[u] % QKV, pos0, __uint_as_float((unsigned)g[u]));
   });
+#endif
   kv_store(c, pos0, kv);
   __syncthreads();
 }
@@ -585,16 +666,31 @@ __device__ __forceinline__ void phase_mlp(Ctx& c, const WGu& G, const WDn& Wd) {
   if (c.tid < MAXM) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this layer's K/V cache stores
   __syncthreads();
   u64* g = c.buf(G_PART, (size_t)NWG * MAXM * D) + (size_t)c.w * MAXM * D;
+  float a[2][2];  // [row 2t + s | t + 512 s][utterance row m]
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
-    float a0 = 0.f, a1 = 0.f;
+    a[s][0] = 0.f;
+    a[s][1] = 0.f;
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-      dotm<M>(Wd.a[s][q][0], c.L.hb[0] + 16 * q, c.L.hb[1] + 16 * q, a0, a1);
-      dotm<M>(Wd.a[s][q][1], c.L.hb[0] + 16 * q + 8, c.L.hb[1] + 16 * q + 8, a0, a1);
+      dotm<M>(Wd.a[s][q][0], c.L.hb[0] + 16 * q, c.L.hb[1] + 16 * q, a[s][0], a[s][1]);
+      dotm<M>(Wd.a[s][q][1], c.L.hb[0] + 16 * q + 8, c.L.hb[1] + 16 * q + 8, a[s][0], a[s][1]);
     }
-    gput(g + c.tid + 512 * s, a0, c.tag());
-    if (M > 1) gput(g + D + c.tid + 512 * s, a1, c.tag());
+  }
+  if (DF_E4_16) {
+    const unsigned tg = c.tag();
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(g, 0, 0x7fffffff, 0x00020000);
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const u32x4_t v = {__float_as_uint(a[0][m]), tg, __float_as_uint(a[1][m]), tg};
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rs, (m * D + 2 * c.tid) * 8, 0, 16);  // sc1
+    }
+  } else {
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      gput(g + c.tid + 512 * s, a[s][0], c.tag());
+      if (M > 1) gput(g + D + c.tid + 512 * s, a[s][1], c.tag());
+    }
   }
 }
 
@@ -612,12 +708,28 @@ __device__ __forceinline__ void phase_reduce(Ctx& c) {
       off[2 * m + u] = (v * MAXM + m) * D + 4 * c.w + 2 * half + u;
       val[2 * m + u] = true;
     }
+#if DF_PAIR16
+  int poff[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) poff[m] = off[2 * m];
+  poll_pairs<M, DF_DELAY_E4, DF_REPOLL>(g, 0x7fffffff, poff, c.tag(), [&](unsigned spin) { return spin_fail(c, spin); },
+                                        [&](const u32x4_t (&q)[M]) {
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      c.L.red[4 * m + 2 * half][v] = __uint_as_float(q[m].x);
+      c.L.red[4 * m + 2 * half + 1][v] = __uint_as_float(q[m].z);
+    }
+  });
+  c.stamp();
+  (void)val;
+#else
   poll<2 * M, DF_DELAY_E4>(c, g, off, val, [&](const u64 (&q)[2 * M]) {
 #pragma unroll
     for (int m = 0; m < M; ++m)
 #pragma unroll
       for (int u = 0; u < 2; ++u) c.L.red[4 * m + 2 * half + u][v] = __uint_as_float((unsigned)q[2 * m + u]);
   });
+#endif
   __syncthreads();
   ++c.e;  // the x hand-off that follows
   if (c.wave < 4 * M) {
@@ -722,14 +834,26 @@ __device__ __forceinline__ void phase_head(Ctx& c, const bf16_t* W, int n_valid,
 // barrier joins the 8 wave maxima -- the max of exact keys, so the order is immaterial.
 __device__ __forceinline__ int gather_code(Ctx& c, int V) {
   static_assert(NWG * 2 == NT, "one key word per thread");
+#if DF_PAIR16
+  // key t = granule pair t: threads t < NWG poll one pair each (the others hold key 0)
+  unsigned long long b = 0ull;
+  if (c.tid < NWG) {
+    const int poff[1] = {2 * c.tid};
+    poll_pairs<1, DF_DELAY_E6, DF_REPOLL>(c.rbuf(G_ARG, NWG * 2), 0x7fffffff, poff, c.tag(),
+                                          [&](unsigned spin) { return spin_fail(c, spin); },
+                                          [&](const u32x4_t (&g)[1]) { b = ((unsigned long long)g[0].x << 32) | g[0].z; });
+  }
+  c.stamp();
+#else
   const int off[1] = {c.tid};
   const bool val[1] = {true};
   unsigned wv = 0;
   poll<1, DF_DELAY_E6>(c, c.rbuf(G_ARG, NWG * 2), off, val, [&](const u64 (&g)[1]) { wv = (unsigned)g[0]; });
   const unsigned ov = __shfl_xor(wv, 1, 64);
   unsigned long long b = (c.tid & 1) ? (((unsigned long long)ov << 32) | wv) : (((unsigned long long)wv << 32) | ov);
+#endif
 #pragma unroll
-  for (int o = 32; o > 1; o >>= 1) {
+  for (int o = 32; o > (DF_PAIR16 ? 0 : 1); o >>= 1) {
     const unsigned long long t = __shfl_xor(b, o, 64);
     b = t > b ? t : b;
   }

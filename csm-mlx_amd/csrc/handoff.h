@@ -111,6 +111,29 @@ __device__ __forceinline__ void poll_granules(const u64* base, const int (&off)[
   }
 }
 
+// poll_granules over granule PAIRS: one 16-B sc1 load per pair (granules 2i, 2i + 1: their tags in
+// words 1 and 3), pair offsets in granules (even).  Same protocol and vmcnt discipline as
+// poll_granules (one probe, stale pairs re-polled); use(x) gets the u32x4 of every pair.
+template <int GPP, int DELAY, int REPOLL, typename Fail, typename F>
+__device__ __forceinline__ void poll_pairs(const u64* base, int bytes, const int (&off)[GPP], unsigned tag, Fail&& fail, F&& use) {
+  auto cur1 = [&](const u32x4_t& x) { return x.y == tag && x.w == tag; };
+  if constexpr (DELAY > 0) __builtin_amdgcn_s_sleep(DELAY);
+  u32x4_t g[GPP];
+#pragma unroll
+  for (int u = 0; u < GPP; ++u) g[u] = sc1_load16(base, off[u] * 8, bytes);
+  for (unsigned spin = 0;; ++spin) {
+    bool ok = true;
+#pragma unroll
+    for (int u = 0; u < GPP; ++u) ok &= cur1(g[u]);
+    if (ok || fail(spin)) break;
+    __builtin_amdgcn_s_sleep(REPOLL);
+#pragma unroll
+    for (int u = 0; u < GPP; ++u)
+      if (!cur1(g[u])) g[u] = sc1_load16(base, off[u] * 8, bytes);
+  }
+  use(g);
+}
+
 // threadIdx.x through an opaque move: lane-dependent addresses derived from it inside the frame loop
 // are recomputed per iteration instead of being hoisted out of the loop and held (spilled) for the
 // whole frame.
