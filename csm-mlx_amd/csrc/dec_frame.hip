@@ -178,7 +178,7 @@ struct Ctx {
 #define DF_POLL2 0
 #endif
 #ifndef DF_PROBE_DELAY
-#define DF_PROBE_DELAY 24
+#define DF_PROBE_DELAY 16
 #endif
 #ifndef DF_REPOLL
 #define DF_REPOLL 2
