@@ -398,6 +398,9 @@ __device__ __forceinline__ void load_gu(Ctx& c, int l, WGu& r) {
 #ifndef DF_E4_16
 #define DF_E4_16 1
 #endif
+#ifndef DF_TAB16
+#define DF_TAB16 1
+#endif
 __device__ __forceinline__ void load_dn(Ctx& c, int l, WDn& r) {
   const bf16_t* base = c.p.wdc[l] + (size_t)(2 * c.w) * D * 16;
   const int v = DF_E4_16 ? c.tid * 16 * 2 * 2 : c.tid * 16 * 2;
@@ -1047,6 +1050,29 @@ __device__ __forceinline__ void decoder_layer(Ctx& c, int l, int step, int pos0,
     const int tr = c.w % p.tab_reps;  // table replica of this workgroup (fewer readers per row)
     const float* t = p.qkv0_tabs[tr] + ((size_t)(step - 1) * p.V + c.code) * QKV;
     const float* xr = p.proj_tabs[tr] + ((size_t)(step - 1) * p.V + c.code) * D;
+#if DF_TAB16
+    // DF_TAB16: the two rows as 16-B loads (640 float4: q|k|v 0..383, x 384..639; thread t takes
+    // float4 t and, t < 128, float4 512 + t), one round trip, fewer load instructions
+    constexpr int NQ4 = QKV / 4, NX4 = D / 4;
+    const float4* t4 = reinterpret_cast<const float4*>(t);
+    const float4* x4 = reinterpret_cast<const float4*>(xr);
+    const int i0 = c.tid, i1 = NT + c.tid;
+    const float4 va = i0 < NQ4 ? t4[i0] : x4[i0 - NQ4];
+    const float4 vb = i1 < NQ4 + NX4 ? x4[min(i1, NQ4 + NX4 - 1) - NQ4] : make_float4(0.f, 0.f, 0.f, 0.f);
+    load_dn(c, l, r.wd);
+    auto put4 = [&](int i, const float4 v) {
+      if (i < NQ4) {
+        qkv_place(c, 0, 4 * i, pos0, v.x);
+        qkv_place(c, 0, 4 * i + 1, pos0, v.y);
+        qkv_place(c, 0, 4 * i + 2, pos0, v.z);
+        qkv_place(c, 0, 4 * i + 3, pos0, v.w);
+      } else {
+        *reinterpret_cast<float4*>(&L.x[0][4 * (i - NQ4)]) = v;
+      }
+    };
+    put4(i0, va);
+    if (i1 < NQ4 + NX4) put4(i1, vb);
+#else
     float tv[(QKV + NT - 1) / NT], xv[D / NT];
 #pragma unroll
     for (int j = 0; j < (QKV + NT - 1) / NT; ++j) tv[j] = c.tid + j * NT < QKV ? t[c.tid + j * NT] : 0.f;
@@ -1061,6 +1087,7 @@ __device__ __forceinline__ void decoder_layer(Ctx& c, int l, int step, int pos0,
       }
 #pragma unroll
     for (int j = 0; j < D / NT; ++j) L.x[0][c.tid + j * NT] = xv[j];
+#endif
     if (c.tid < M * (HD / 2)) L.rope[c.tid / (HD / 2)][c.tid % (HD / 2)] = rp;
     __syncthreads();  // L.qkv complete before kv_append reads it
     if (!DF_KVDIRECT) {
