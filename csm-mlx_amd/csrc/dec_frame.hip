@@ -552,6 +552,11 @@ __device__ __forceinline__ void gather_qkv(Ctx& c, const u64* buf, int pos0, con
 // max-subtracted softmax, P.V in key order with the V rows read 8 keys at a time (all in flight
 // together; rows past the last key are read but not used).  The new K/V rows go to the cache,
 // spread over the workgroups, for later steps.
+// DF_PV: the P.V loop's V reads -- 0: two 4-B reads per key (dims lane, lane + 64); 1: one 8-B read
+// (dims 2 lane, +1); 2: one 16-B read per key over key halves (lane >> 5), the halves' sums exchanged
+#ifndef DF_PV
+#define DF_PV 2
+#endif
 template <int M>
 __device__ __forceinline__ void phase_attn(Ctx& c, int pos0, int layer) {
   const int h = c.wave, g = h / (HQ / HKV);
@@ -585,6 +590,63 @@ __device__ __forceinline__ void phase_attn(Ctx& c, int pos0, int layer) {
     const float pj = kj < n ? expf(s - mx) : 0.f;
     const float l_run = wave_sum(hh == 0 ? pj : 0.f);
     const int pji = __float_as_int(pj);
+#if DF_PV == 1
+    // lane = dims 2 lane, 2 lane + 1 (one 8-B V read per key), keys in order
+    float o0 = 0.f, o1 = 0.f;
+#pragma unroll
+    for (int j0 = 0; j0 < 32; j0 += 8) {
+      if (j0 < n) {
+        float2 vv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) vv[u] = *reinterpret_cast<const float2*>(&c.L.Vs[g][j0 + u][2 * c.lane]);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if (j0 + u < n) {
+            const float pb = __int_as_float(__builtin_amdgcn_readlane(pji, j0 + u));
+            o0 = fmaf(pb, vv[u].x, o0);
+            o1 = fmaf(pb, vv[u].y, o1);
+          }
+        }
+      }
+    }
+    const float inv = 1.f / l_run;
+    *reinterpret_cast<float2*>(&c.L.att[m][h * HD + 2 * c.lane]) = make_float2(o0 * inv, o1 * inv);
+#elif DF_PV == 2
+    // lane = (key half kv = lane >> 5: keys 16 kv + u, dims 4 (lane & 31) .. +3): one 16-B V read per
+    // key, the halves' sums added (keys 0-15 first) by one exchange
+    const int kv = c.lane >> 5, dq = c.lane & 31;
+    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int u0 = 0; u0 < 16; u0 += 8) {
+      if (u0 < n) {
+        float4 vv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) vv[u] = *reinterpret_cast<const float4*>(&c.L.Vs[g][16 * kv + u0 + u][4 * dq]);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const float pa = __int_as_float(__builtin_amdgcn_readlane(pji, u0 + u));
+          const float pb = __int_as_float(__builtin_amdgcn_readlane(pji, 16 + u0 + u));
+          const float p = kv ? pb : pa;
+          if (16 * kv + u0 + u < n) {
+            o.x = fmaf(p, vv[u].x, o.x);
+            o.y = fmaf(p, vv[u].y, o.y);
+            o.z = fmaf(p, vv[u].z, o.z);
+            o.w = fmaf(p, vv[u].w, o.w);
+          }
+        }
+      }
+    }
+    float4 t;
+    t.x = __shfl_xor(o.x, 32, 64);
+    t.y = __shfl_xor(o.y, 32, 64);
+    t.z = __shfl_xor(o.z, 32, 64);
+    t.w = __shfl_xor(o.w, 32, 64);
+    if (kv == 0) {
+      const float inv = 1.f / l_run;
+      *reinterpret_cast<float4*>(&c.L.att[m][h * HD + 4 * dq]) =
+          make_float4((o.x + t.x) * inv, (o.y + t.y) * inv, (o.z + t.z) * inv, (o.w + t.w) * inv);
+    }
+#else
     float o0 = 0.f, o1 = 0.f;
 #pragma unroll
     for (int j0 = 0; j0 < 32; j0 += 8) {
@@ -608,6 +670,7 @@ __device__ __forceinline__ void phase_attn(Ctx& c, int pos0, int layer) {
     const float inv = 1.f / l_run;
     c.L.att[m][h * HD + c.lane] = o0 * inv;
     c.L.att[m][h * HD + c.lane + 64] = o1 * inv;
+#endif
   }
   // the new K / V rows -> cache, spread over the workgroups (WG w stores element w of each row:
   // 2 heads x 128 = 256 elements), write-through; the storing threads drain them (vmcnt(0)) before
