@@ -83,13 +83,22 @@ __global__ __launch_bounds__(256) void gemm64_kernel(P p) {
 }
 
 // ---------------------------------------------------------------------------- causal conv1d
+// Few output steps per utterance (streaming decode_step: 2-16 per frame) leave most columns of a
+// 64-wide time tile empty while every (utterance, Cout tile) block still reads its whole weight
+// panel, so below 64 steps the batch is folded into the columns (fold = Tout: column = b * Tout + t,
+// grid.z = 1).  Each output's summation order is unchanged (bit-identical results).
 struct ConvProblem {
   ConvParams c;
   int M, N;
+  int fold;  // > 0: columns are (utterance, step) pairs of `fold` steps each
   static constexpr bool B_KCONTIG = false;
   __device__ int kdim() const { return c.Cin * c.k; }
   __device__ float a(int, int co, int kk) const { return c.w[(size_t)co * c.Cin * c.k + kk]; }
   __device__ float b(int z, int kk, int t) const {
+    if (fold) {
+      z = t / fold;
+      t -= z * fold;
+    }
     const int ci = kk / c.k, j = kk - ci * c.k;
     int u = t * c.stride + j * c.dil - c.pad_l;
     if (u < 0 || u >= c.Tin) {
@@ -100,22 +109,35 @@ struct ConvProblem {
     return c.elu_in ? elu_f(v) : v;
   }
   __device__ void store(int z, int co, int t, float v) const {
+    if (fold) {
+      z = t / fold;
+      t -= z * fold;
+    }
     if (c.bias) v += c.bias[co];
     if (c.resid) v += c.resid[(size_t)z * c.r_bstride + (size_t)co * c.r_cstride + c.r_off + t];
     c.y[(size_t)z * c.y_bstride + (size_t)co * c.y_cstride + c.y_off + t] = v;
   }
 };
 
+// CSM_MIMI_CONV_FOLD=1: batch folding on (opt-in until measured on the GPU)
+static bool conv_fold_enabled() {
+  static const bool v = [] { const char* e = getenv("CSM_MIMI_CONV_FOLD"); return e && atoi(e) != 0; }();
+  return v;
+}
+
 void launch_conv1d(const ConvParams& p, hipStream_t st) {
-  ConvProblem pr{p, p.Cout, p.Tout};
-  dim3 grid((p.Tout + 63) / 64, (p.Cout + 63) / 64, p.B);
+  const bool fold = p.Tout < 64 && p.B > 1 && conv_fold_enabled();
+  ConvProblem pr{p, p.Cout, fold ? p.B * p.Tout : p.Tout, fold ? p.Tout : 0};
+  dim3 grid((pr.N + 63) / 64, (p.Cout + 63) / 64, fold ? 1 : p.B);
   hipLaunchKernelGGL(gemm64_kernel<ConvProblem>, grid, dim3(256), 0, st, pr);
 }
 
 // ---------------------------------------------------------------------------- transposed conv (k = 2s)
+// fold > 0: columns are (utterance, input) pairs of `fold` inputs each, grid.z = the s phases
 struct ConvTrProblem {
   ConvTrParams c;
   int M, N;
+  int fold;
   static constexpr bool B_KCONTIG = false;
   __device__ int kdim() const { return c.Cin * 2; }
   __device__ float a(int z, int co, int kk) const {
@@ -123,7 +145,11 @@ struct ConvTrProblem {
     return c.wt[((size_t)r * c.Cout + co) * c.Cin * 2 + kk];
   }
   __device__ float b(int z, int kk, int i) const {
-    const int bb = z / c.s;
+    int bb = z / c.s;
+    if (fold) {
+      bb = i / fold;
+      i -= bb * fold;
+    }
     const int ci = kk >> 1, e = kk & 1;
     const int ti = c.t_in0 + i - e;
     if (ti < 0) return 0.f;
@@ -131,15 +157,21 @@ struct ConvTrProblem {
     return c.elu_in ? elu_f(v) : v;
   }
   __device__ void store(int z, int co, int i, float v) const {
-    const int bb = z / c.s, r = z % c.s;
+    int bb = z / c.s;
+    const int r = z % c.s;
+    if (fold) {
+      bb = i / fold;
+      i -= bb * fold;
+    }
     if (c.bias) v += c.bias[co];
     c.y[(size_t)bb * c.y_bstride + (size_t)co * c.y_cstride + c.y_off + (size_t)i * c.s + r] = v;
   }
 };
 
 void launch_convtr(const ConvTrParams& p, hipStream_t st) {
-  ConvTrProblem pr{p, p.Cout, p.n_in};
-  dim3 grid((p.n_in + 63) / 64, (p.Cout + 63) / 64, p.B * p.s);
+  const bool fold = p.n_in < 64 && p.B > 1 && conv_fold_enabled();
+  ConvTrProblem pr{p, p.Cout, fold ? p.B * p.n_in : p.n_in, fold ? p.n_in : 0};
+  dim3 grid((pr.N + 63) / 64, (p.Cout + 63) / 64, fold ? p.s : p.B * p.s);
   hipLaunchKernelGGL(gemm64_kernel<ConvTrProblem>, grid, dim3(256), 0, st, pr);
 }
 
