@@ -119,9 +119,10 @@ struct ConvProblem {
   }
 };
 
-// CSM_MIMI_CONV_FOLD=1: batch folding on (opt-in until measured on the GPU)
+// CSM_MIMI_CONV_FOLD=0: no batch folding (A/B).  Measured: config 3 (B = 32 streaming decode_step)
+// 2932 -> 3253 frames/s (profiles/r03_ab_mimi.txt)
 static bool conv_fold_enabled() {
-  static const bool v = [] { const char* e = getenv("CSM_MIMI_CONV_FOLD"); return e && atoi(e) != 0; }();
+  static const bool v = [] { const char* e = getenv("CSM_MIMI_CONV_FOLD"); return !e || atoi(e) != 0; }();
   return v;
 }
 
@@ -208,9 +209,12 @@ struct LinProblem {
 // chip idle (8-32 blocks), so row-major linears of <= 32 rows go through the decode GEMV instead
 // (fp32 weights, same epilogues: y = gelu(v) / out += scale * v).  Measured: config 3 (B = 32
 // decode_step) 2083 -> 2123 frames/s; at 125 rows (one-shot decode of a 10 s utterance) neutral, and
-// 16 rows per weight pass was slower (2001).  CSM_MIMI_GEMV_M sets the largest row count (0 = never).
+// 16 rows per weight pass was slower (2001).  Round 3: the codec transformer's rows at B = 32 are 64
+// (two 25 Hz steps per frame), where gemm64 left the N = 512 outputs on 8 workgroups: cutoff 64,
+// config 3 2932 -> 3076 frames/s (profiles/r03_ab_mimi.txt).  CSM_MIMI_GEMV_M sets the largest row
+// count (0 = never).
 static int mimi_gemv_rows() {
-  static const int v = [] { const char* e = getenv("CSM_MIMI_GEMV_M"); return e ? atoi(e) : 32; }();
+  static const int v = [] { const char* e = getenv("CSM_MIMI_GEMV_M"); return e ? atoi(e) : 64; }();
   return v;
 }
 

@@ -114,3 +114,45 @@ def test_codes_past_the_codebook_clamp():
     y, yc = codec.decode(codes), codec.decode(clamped)
     assert np.array_equal(y, yc)
     assert _rms(y, o.decode(codes)) <= 1e-4
+
+
+_FOLD_SCRIPT = r"""
+import dataclasses, sys
+import numpy as np
+sys.path[:0] = [sys.argv[2] + "/csm-mlx_amd", sys.argv[2]]
+from csm_mlx.config import MIMI_CONFIGURATION
+from csm_mlx.mimi import MimiCodec
+from csm_mlx.weights import synthetic_mimi_weights
+m = dataclasses.replace(MIMI_CONFIGURATION["mimi_202407"], attn_mode="mlx")
+codec = MimiCodec(m, max_batch=3, max_frames=200)
+codec.load_weights(synthetic_mimi_weights(m))
+codes = np.random.default_rng(11).integers(0, m.bins, (3, m.n_q, 5)).astype(np.int32)
+codec.reset_state(3)
+np.save(sys.argv[1], np.concatenate([codec.decode_step(codes[:, :, f: f + 1]) for f in range(5)], axis=2))
+"""
+
+
+def test_decode_step_batch_folding_bit_identical(tmp_path):
+    """Batched streaming decode_step (B = 3, 1-16 output steps per conv per frame): the conv /
+    transposed-conv GEMMs with the batch folded into the column tiles (CSM_MIMI_CONV_FOLD=1) give
+    bit-identical PCM to the per-utterance grid, and match the oracle's streaming decode."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    outs = {}
+    for fold in ("0", "1"):
+        out = str(tmp_path / f"pcm_{fold}.npy")
+        env = dict(os.environ, CSM_MIMI_CONV_FOLD=fold)
+        r = subprocess.run([sys.executable, "-c", _FOLD_SCRIPT, out, root], env=env, capture_output=True,
+                           text=True, timeout=180)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs[fold] = np.load(out)
+    assert outs["0"].shape == outs["1"].shape == (3, 1, 5 * 1920)
+    assert np.array_equal(outs["0"], outs["1"]), _rms(outs["0"], outs["1"])
+    m, _, o = _pair("mimi_202407", "mlx", max_batch=1)
+    codes = np.random.default_rng(11).integers(0, m.bins, (3, m.n_q, 5)).astype(np.int32)
+    for b in range(3):
+        o.reset_state()
+        ref = np.concatenate([o.decode_step(codes[b: b + 1, :, f: f + 1]) for f in range(5)], axis=2)
+        assert _rms(outs["1"][b: b + 1], ref) <= 1e-4, (b, _rms(outs["1"][b: b + 1], ref))
