@@ -56,6 +56,37 @@ def dist_env():
     return int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)), int(os.environ.get("LOCAL_RANK", 0))
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launcher_argv(argv, gpus: int, port: int):
+    """The child command ``python bench.py --gpus N ...`` runs when no launcher set WORLD_SIZE: one rank
+    per GPU under torch.distributed.run on this node, rendezvous on 127.0.0.1, same bench arguments."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *argv]
+
+
+def resolve_world(gpus, env=None):
+    """(world size, launch-self?) from --gpus and the launcher's WORLD_SIZE.  A WORLD_SIZE that
+    disagrees with an explicit --gpus is an error (the line would report the wrong n_gpus)."""
+    env = os.environ if env is None else env
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if gpus is not None and gpus != world:
+            raise SystemExit(f"bench.py: --gpus {gpus} but the launcher started WORLD_SIZE={world} ranks")
+        return world, False
+    gpus = 1 if gpus is None else gpus
+    if gpus < 1:
+        raise SystemExit(f"bench.py: --gpus must be >= 1, got {gpus}")
+    return gpus, gpus > 1
+
+
 def aggregate(frames_local: float, dt_local: float, world: int, device=None):
     """(sum of frames over ranks, max time over ranks); device None = CPU tensors (gloo)."""
     if world == 1:
@@ -283,7 +314,9 @@ def rooflines(model, batch: int):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks, one per GPU of this node (default 1, or the launcher's WORLD_SIZE); without a "
+                         "launcher, N > 1 starts torch.distributed.run with N ranks as a child process")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=1, help="utterances per GPU")
@@ -312,9 +345,22 @@ def main():
     if args.config:
         args.batch, args.dtype = cfg["batch"], cfg["dtype"]
 
+    world_req, launch = resolve_world(args.gpus)
+    if launch:
+        # no launcher: start one, as a child process (this process has made no GPU call and never
+        # execs); rank 0's JSON line reaches our stdout directly, its exit code is ours
+        import subprocess
+        env = dict(os.environ)
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        rc = subprocess.call(launcher_argv(sys.argv[1:], world_req, _free_port()), env=env)
+        sys.exit(rc)
+
     rank, world, local = dist_env()
+    # under a launcher (WORLD_SIZE set) the process group exists even at world 1, so the RCCL
+    # broadcast / gather code runs on a one-GPU box exactly as on eight
+    use_dist = "WORLD_SIZE" in os.environ
     dev = None
-    if world > 1:
+    if use_dist:
         # torch (and its HIP runtime) first, so RCCL and the engine share one runtime
         import torch
         import torch.distributed as dist
@@ -326,13 +372,13 @@ def main():
         else:
             dist.init_process_group("gloo")
     from csm_mlx import _lib
-    if world == 1:
+    if not use_dist:
         n_dev = ctypes.c_int(0)
         _lib.check(_lib.lib().csm_device_count(ctypes.byref(n_dev)))
         device = local % max(1, n_dev.value)
 
     def barrier_sync():
-        if world > 1:
+        if use_dist:
             import torch
             import torch.distributed as dist
             dist.barrier()
@@ -343,9 +389,9 @@ def main():
     from csm_mlx.generation import generate_batch
     from csm_mlx.tokenizers import tokenize_text_segment
 
-    bcast = world > 1 and args.weights == "bcast"
+    bcast = use_dist and args.weights == "bcast"
     model = build_model(args.dtype, args.batch, device=device, model_name=args.model, load=not bcast or rank == 0)
-    if world > 1:
+    if use_dist:
         import torch
         if world > max(1, torch.cuda.device_count()):
             # rehearsal with several ranks on one GPU: the persistent kernels need every CU of the
@@ -410,8 +456,8 @@ def main():
                                  decode=decode, with_codes=decode, timings=phases)
             codes, pcm_l = out if decode else (out, None)
             n = sum(len(c) for c in codes)
-        if world > 1:   # result collection: one all-gather per kind (RCCL over xGMI / gloo)
-            codes, pcm_l = gather_results(codes, pcm_l, args.frames, FRAME_SAMPLES, dev)
+        if use_dist:    # result collection: one gather per kind to rank 0 (RCCL over xGMI / gloo)
+            codes, pcm_l = gather_results(codes, pcm_l, args.frames, FRAME_SAMPLES, dev, dst=0)
         last["codes"], last["pcm"] = codes, pcm_l
         return n
 
@@ -438,6 +484,12 @@ def main():
                           "and one audio-head slice x31) in this engine's storage format, x frame steps/s per GPU; "
                           "one frame step advances every utterance of the GPU's batch by one frame"}
 
+    results_info = {"collection": "none (one rank)"}
+    if use_dist:
+        up = args.batch * ((1 + args.frames * K) * 4 + (args.frames * FRAME_SAMPLES * 4 if decode else 0))
+        results_info = {"collection": f"{args.dist_backend} gather to rank 0 per step (codes + lengths int32"
+                                      f"{', PCM float32' if decode else ''}), inside the timed region",
+                        "host_bytes_per_rank_up": int(up), "host_bytes_rank0_down": int(up * world)}
     if rank == 0 and args.dump:
         z = {f"codes_{i}": c for i, c in enumerate(last["codes"])}
         if last["pcm"] is not None:
@@ -465,7 +517,8 @@ def main():
                        "model": "csm_1b (synthetic seed-0 weights)", "global_batch": args.batch * world,
                        "per_gpu_batch": args.batch, "frames": args.frames, "mimi_decode": decode,
                        "parallelism": f"dp{world}", "rtf": round(total_frames / max_dt / 12.5, 2),
-                       "weights": weights_info},
+                       "weights": weights_info,
+                       "results": results_info},
             "roofline": roof["dominant"],
             "roofline_backbone": roof["backbone_gate_up"],
             "roofline_frame": roof_frame,
@@ -475,7 +528,7 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(args.cpu_frames)
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if use_dist:
         import torch.distributed as dist
         dist.destroy_process_group()
 

@@ -2,9 +2,10 @@
 
 Utterances are independent (no cross-utterance state), so N processes -- one per GPU, launched by
 ``torch.distributed.run`` -- each generate a contiguous shard of the global batch with no collective
-on the data path.  At the end the per-utterance results (codes and PCM) are collected with one
-``all_gather_into_tensor`` per kind (codes + lengths int32, PCM float32): RCCL over xGMI when the process group is "nccl" (the tensors
-are staged on this rank's GPU), gloo on CPU tensors otherwise.  The reference is batch-1 and
+on the data path.  At the end the per-utterance results (codes and PCM) are collected on rank 0
+with one ``gather`` per kind (codes + lengths int32, PCM float32): RCCL over xGMI when the process
+group is "nccl" (the tensors are staged on this rank's GPU, and only rank 0 copies the gathered
+result back to the host), gloo on CPU tensors otherwise.  The reference is batch-1 and
 single-device (/root/reference/csm_mlx/generation.py:19, :124, :156); this is the build's
 extension, not a translation of anything there.
 """
@@ -100,35 +101,55 @@ def _pack(items: Sequence[np.ndarray], width: int, dtype) -> Tuple[np.ndarray, n
 
 
 def gather_results(codes: Sequence[np.ndarray], pcm: Optional[Sequence[np.ndarray]], max_frames: int,
-                   frame_samples: int = 1920, device=None):
-    """All-gather every rank's per-utterance results in global utterance order.
+                   frame_samples: int = 1920, device=None, dst: Optional[int] = 0):
+    """Collect every rank's per-utterance results in global utterance order on rank ``dst``
+    (``dst=None``: on every rank, one all-gather per kind).
 
     codes: this rank's utterances, each (F_b, K) int32 (F_b <= max_frames); pcm: each (F_b *
     frame_samples,) float32 or None.  Every rank holds the same number of utterances (``shard``).
-    device: torch device of the RCCL communicator ("nccl" group), None for gloo / CPU.
-    Returns (codes list, pcm list or None) over all ranks' utterances."""
+    device: torch device of the RCCL communicator ("nccl" group), None for gloo / CPU.  On the nccl
+    group the gathered tensors stay on ``dst``'s GPU until one device-to-host copy per kind; the
+    other ranks copy nothing back, so per-rank host traffic is its own shard's bytes (upload) and
+    ``world`` x that on ``dst`` (download).
+    Returns (codes list, pcm list or None) over all ranks' utterances on the receiving ranks, and
+    (None, None) on the others."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size()
+    rank = dist.get_rank()
+    recv = dst is None or rank == dst
     K = codes[0].shape[1] if len(codes) else 0
     c_pad, c_len = _pack([np.asarray(c, np.int32).reshape(-1, K) for c in codes], max_frames, np.int32)
     codes_row = np.concatenate([c_len.astype(np.int32)[:, None], c_pad.reshape(len(codes), -1)], axis=1)
 
-    def all_gather(a: np.ndarray) -> np.ndarray:
+    def collect(a: np.ndarray) -> Optional[np.ndarray]:
         local = torch.from_numpy(np.ascontiguousarray(a))
         if device is not None:
             local = local.to(device)
-        full = torch.empty((world * local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype,
-                           device=local.device)
-        dist.all_gather_into_tensor(full, local)
-        return full.cpu().numpy()
-    full = all_gather(codes_row)                                   # [world * n_local, 1 + F*K] int32
+        full = None
+        if recv:
+            full = torch.empty((world * local.shape[0],) + tuple(local.shape[1:]), dtype=local.dtype,
+                               device=local.device)
+        if dst is None:
+            dist.all_gather_into_tensor(full, local)
+        else:
+            dist.gather(local, list(full.chunk(world)) if recv else None, dst=dst)
+        if device is not None:
+            # the RCCL kernel must have drained on EVERY rank before the engine's next persistent
+            # launch, which needs all CUs of the device (a sending rank has nothing to copy back)
+            torch.cuda.synchronize(device)
+        return full.cpu().numpy() if recv else None
+    full = collect(codes_row)                                      # [world * n_local, 1 + F*K] int32
+    p_all = None
+    if pcm is not None:
+        p_pad, _ = _pack([np.asarray(p, np.float32) for p in pcm], max_frames * frame_samples, np.float32)
+        p_all = collect(p_pad)                                     # [world * n_local, F * 1920] float32
+    if not recv:
+        return None, None
     lens = full[:, 0].astype(np.int64)
     c_all = full[:, 1:].reshape(-1, max_frames, K)
     out_codes = [c_all[i, : lens[i]].copy() for i in range(len(lens))]
     out_pcm = None
-    if pcm is not None:
-        p_pad, _ = _pack([np.asarray(p, np.float32) for p in pcm], max_frames * frame_samples, np.float32)
-        p_all = all_gather(p_pad)                                  # [world * n_local, F * 1920] float32
+    if p_all is not None:
         out_pcm = [p_all[i, : lens[i] * frame_samples].copy() for i in range(len(lens))]
     return out_codes, out_pcm

@@ -47,7 +47,6 @@ struct Stack {
   float* norm = nullptr;
   float* rope = nullptr;  // [S][hd/2][2]
   int S_cap = 0;
-  long long* acc[2] = {nullptr, nullptr};  // fused-MLP fixed-point accumulators (ping-pong by layer parity)
   int qkv_rows() const { return (d.n_heads + 2 * d.n_kv_heads) * d.head_dim; }
   int q_dim() const { return d.n_heads * d.head_dim; }
 };
@@ -88,11 +87,6 @@ struct csm_engine {
   // proj_tab[cb][code] at position cb + 1 (fp32, built by the same QKV GEMV); codebook steps >= 2 then
   // skip layer 0's QKV launch and its attention gathers the row (AttnParams::g_tab).
   float* qkv0_tab = nullptr;
-  // csm_set_option "tab_rep" (env CSM_TAB_REP): copies of proj_tab + qkv0_tab the persistent frame
-  // decoder spreads its workgroups over (every workgroup loads the same two rows after each head)
-  int tab_rep = [] { const char* v = getenv("CSM_TAB_REP"); return v ? std::max(1, std::min(atoi(v), DEC_FRAME_TAB_REPS)) : 1; }();
-  float* tab_copies = nullptr;  // [tab_rep - 1][proj_tab | qkv0_tab]
-  int tab_copies_n = 0;         // replicas tab_copies holds up to date (0 after a table rebuild)
   bool use_qkv0_tab = [] { const char* v = getenv("CSM_QKV0_TAB"); return !(v && v[0] == '0'); }();  // csm_set_option "qkv0_tab"
   bool qkv0_built = false;
   // fragment-tiled copies of the matrices the MFMA path reads (build_tiled; ws.tiled maps them)
@@ -133,19 +127,8 @@ struct csm_engine {
   std::vector<void*> allocs;
   std::vector<void*> batch_allocs;
   std::vector<int> pos_host;
-  // depth-decoder attention recomputed inside the o_proj launch (dec_attn_oproj_kernel, CSM_FUSE_ATTN=1
-  // or csm_set_option("fuse_attn", 1); bit-identical results).  Off: on MI355X the redundant
-  // per-block attention (12.4 us eager) costs more than attention + o_proj launched separately
-  // (6.1 + 5.3 us) plus the boundary it removes -- 205 vs 227 frames/s.
-  bool fuse_attn = false;
   bool fold_proj = true;  // csm_set_option "fold_proj": decoder steps >= 2 read the folded table
   bool linear_mfma = false;  // csm_set_option "linear_mfma": csm_linear on the MFMA GEMM (kernel tests)
-  // csm_set_option "fuse_mlp" / CSM_FUSE_MLP=1: one-launch MLP (gate/up + SiLU*up + down, 64-bit
-  // fixed-point atomics) for <= 4 rows.  Off: the atomics' memory-side serialization (512 blocks add
-  // into the same D outputs) costs more than the launch it saves -- 197.9 vs 235.0 frames/s; with
-  // the atomics removed (invalid results) the one-launch MLP ran at 264 frames/s.
-  bool fuse_mlp = [] { const char* v = getenv("CSM_FUSE_MLP"); return v && v[0] == '1'; }();
-  int acc_rows = 0;  // rows of the fused-MLP accumulators (the fused path runs for M <= acc_rows)
   // csm_set_option "prefill_rows": row cap of one csm_prefill_batch group (0 = M_cap); lowering it makes
   // small test batches take the multi-group path that config 5's 64 x 248-row contexts take
   int prefill_rows = 0;
@@ -210,7 +193,6 @@ struct csm_engine {
     if (g_head) (void)hipGraphExecDestroy(g_head);
     for (void* p : allocs) (void)hipFree(p);
     for (void* p : batch_allocs) (void)hipFree(p);
-    if (tab_copies) (void)hipFree(tab_copies);
     gemm_ws_free(ws);
     if (st) (void)hipStreamDestroy(st);
   }
@@ -237,7 +219,7 @@ void alloc_stack(csm_engine* e, Stack& s, const csm_llama_dims& d, int S_cap, co
     l.wo = e->alloc(e->wbytes(D, s.q_dim()));
     l.wgu = e->alloc(e->wbytes(2 * F, D));
     l.wd = e->alloc(e->wbytes(D, F));
-    if (e->wdt == WDT_BF16 && fused_mlp_chunk((int)D) && F % fused_mlp_chunk((int)D) == 0) l.wdc = e->alloc(D * F * 2);
+    if (e->wdt == WDT_BF16 && wdc_chunk((int)D) && F % wdc_chunk((int)D) == 0) l.wdc = e->alloc(D * F * 2);
     l.n1 = (float*)e->alloc(D * 4);
     l.n2 = (float*)e->alloc(D * 4);
     const std::string p = std::string(prefix) + ".layers." + std::to_string(i);
@@ -265,19 +247,12 @@ int ablate() {
 // One Llama block stack over M rows of the residual stream x (in place).
 // gather0: x-gather fields for layer 0's QKV GEMV (its input rows come from a table; the GEMV also
 // writes them to x as the residual stream).
-// Returns the fused-MLP accumulator still pending after the last layer (its reader -- the heads or
-// the final norm -- must add it), or null when the stack ran the two-launch MLP.
-// Fused MLP bookkeeping: layer i's MLP adds into acc[i & 1]; layer i+1's QKV reads x + acc[i & 1]
-// and its o_proj folds acc[i & 1] into x and zeroes it; layer 0's o_proj zeroes acc[1] (left by the
-// previous call's last layer, already consumed).
-long long* run_stack(csm_engine* e, Stack& s, float* x, int M, float* q, float* att, float* mlp, const RowMap& rm,
+void run_stack(csm_engine* e, Stack& s, float* x, int M, float* q, float* att, float* mlp, const RowMap& rm,
                      hipStream_t st, const GemvParams* gather0 = nullptr, const AttnParams* attn0 = nullptr) {
   const csm_llama_dims& d = s.d;
   const int tag = (&s == &e->dec) ? 1 : 0;
   const int D = d.hidden, F = d.intermediate, hd = d.head_dim, Hq = d.n_heads, Hkv = d.n_kv_heads;
   const int ab = tag ? ablate() : (ablate() >> 8) & 31;  // bits 0-4 decoder, 8-12 backbone
-  const bool fused = e->fuse_mlp && e->wdt == WDT_BF16 && s.L[0].wdc && s.acc[0] && M <= e->acc_rows &&
-                     fused_mlp_supported(D, F, M) && !(ab & 24);
   for (int i = 0; i < d.n_layers; ++i) {
     LayerW& l = s.L[i];
     GemvParams g = gp(e);
@@ -285,8 +260,6 @@ long long* run_stack(csm_engine* e, Stack& s, float* x, int M, float* q, float* 
     g.W = l.wqkv; g.N = s.qkv_rows(); g.K = D; g.x = x; g.xs = D; g.M = M; g.nw = l.n1; g.eps = d.eps;
     g.out = q; g.os = s.q_dim(); g.Hq = Hq; g.Hkv = Hkv; g.hd = hd; g.S_cap = s.S_cap; g.rope = s.rope;
     g.kc = l.kc; g.vc = l.vc; g.rm = rm;
-    if (fused && i > 0) g.xacc = s.acc[(i - 1) & 1];
-    g.acc_ss = e->acc_rows * D;
     if (i == 0 && gather0) {
       g.xpart = gather0->xpart; g.xpart_stride = gather0->xpart_stride; g.xpart_n = gather0->xpart_n;
       g.xtab = gather0->xtab; g.xtab_f32 = gather0->xtab_f32; g.xV = gather0->xV; g.xcb = gather0->xcb;
@@ -294,31 +267,15 @@ long long* run_stack(csm_engine* e, Stack& s, float* x, int M, float* q, float* 
     }
     const bool gathered = (i == 0 && attn0);  // layer 0 QKV from the folded table (attention gathers it)
     if (!(ab & 2) && !gathered) launch_gemv(g, e->wdt, EPI_QKV, 1, st, tag);
-    // attention (+ o_proj + residual fused for the short depth-decoder KV)
+    // attention, then o_proj + residual
     AttnParams a = gathered ? *attn0 : AttnParams{};
     a.q = q; a.qs = s.q_dim(); a.M = M; a.kc = l.kc; a.vc = l.vc; a.Hq = Hq; a.Hkv = Hkv; a.S_cap = s.S_cap;
     a.scale = 1.0f / sqrtf((float)hd); a.mode = ATTN_CAUSAL; a.window = 0; a.rm = rm; a.out = att;
     a.os = s.q_dim();
     g = gp(e);
     g.W = l.wo; g.N = D; g.K = s.q_dim(); g.x = att; g.xs = s.q_dim(); g.M = M; g.out = x; g.os = D;
-    if (fused) {
-      g.oacc = s.acc[(i + 1) & 1];
-      g.oacc_add = i > 0;
-      g.acc_ss = e->acc_rows * D;
-    }
-    if (tag == 1 && e->fuse_attn && !(ab & 5) && dec_attn_oproj_supported(g, a, hd)) {
-      launch_dec_attn_oproj(g, a, e->wdt, st, tag);
-    } else {
-      if (!(ab & 1)) launch_attn(a, hd, st);
-      if (!(ab & 4)) launch_gemv(g, e->wdt, EPI_ADD, 0, st, tag);
-    }
-    if (fused) {  // norm2 + gate/up + SiLU*up + down in one launch, into acc[i & 1]
-      MlpParams mp{};
-      mp.x = x; mp.xs = D; mp.M = M; mp.nw = l.n2; mp.eps = d.eps; mp.wgu = l.wgu; mp.wdc = l.wdc;
-      mp.acc = s.acc[i & 1]; mp.F = F; mp.acc_ss = e->acc_rows * D;
-      launch_fused_mlp(mp, D, gemv_nt(tag), st);
-      continue;
-    }
+    if (!(ab & 1)) launch_attn(a, hd, st);
+    if (!(ab & 4)) launch_gemv(g, e->wdt, EPI_ADD, 0, st, tag);
     // norm2 + gate/up + SiLU*up
     g = gp(e);
     g.W = l.wgu; g.N = 2 * F; g.K = D; g.x = x; g.xs = D; g.M = M; g.nw = l.n2; g.eps = d.eps; g.out = mlp;
@@ -329,7 +286,6 @@ long long* run_stack(csm_engine* e, Stack& s, float* x, int M, float* q, float* 
     g.W = l.wd; g.N = D; g.K = F; g.x = mlp; g.xs = F; g.M = M; g.out = x; g.os = D;
     if (!(ab & 16)) launch_gemv(g, e->wdt, EPI_ADD, 0, st, tag);
   }
-  return fused ? s.acc[(d.n_layers - 1) & 1] : nullptr;
 }
 
 // The batched depth decoder at codebook steps >= 2 (generation.py:72-89 at batch M) on the streaming
@@ -337,14 +293,19 @@ long long* run_stack(csm_engine* e, Stack& s, float* x, int M, float* q, float* 
 // and every projection's epilogue writes the split activations of the next one (xs.h) -- o_proj:
 // the new residual x * n2 (+ per-row sums of squares), gate/up: SiLU*up, down: the new residual x *
 // (next layer's n1, or the final norm for the head) -- so no launch re-normalises or re-splits rows.
+int head_blocks(int N, int K, int M, int wdt);
+
 bool dec_xs_eligible(csm_engine* e, int M) {
   const Stack& s = e->dec;
   const int Dd = s.d.hidden, F = s.d.intermediate;
   return e->xs_on && e->xs_D && M >= GEMM_MFMA_MIN_M && M <= GEMM_XS_MAX_M && (e->wdt == WDT_BF16 || e->wdt == WDT_Q4) &&
-         e->head_wdt == WDT_BF16 && !e->fuse_mlp && s.d.head_dim == 128 && s.S_cap <= 32 &&
+         e->head_wdt == WDT_BF16 && s.d.head_dim == 128 && s.S_cap <= 32 &&
          gemm_xs_eligible(s.qkv_rows(), Dd, M, e->wdt) && gemm_xs_eligible(Dd, s.q_dim(), M, e->wdt) &&
          gemm_xs_eligible(2 * F, Dd, M, e->wdt) && gemm_xs_eligible(Dd, F, M, e->wdt) &&
-         gemm_xs_eligible(e->Vpad, Dd, M, e->head_wdt) && gemm_xs_tiles(Dd, F, M) <= 64 &&
+         gemm_xs_eligible(e->Vpad, Dd, M, e->head_wdt) &&
+         // the next step's row gather reads head_blocks() arg-max partials per row: the streaming head
+         // must write exactly that many (one per 64-row tile)
+         gemm_xs_tiles(e->Vpad, Dd, M, true) == head_blocks(e->Vpad, Dd, M, e->head_wdt) && gemm_xs_tiles(Dd, F, M) <= 64 &&
          gemm_xs_tiles(Dd, s.q_dim(), M) <= 64;
 }
 
@@ -403,7 +364,7 @@ bool bb_xs_eligible(csm_engine* e, int M) {
   const Stack& s = e->bb;
   const int D = s.d.hidden, F = s.d.intermediate;
   return e->xs_on && e->xs_D && M >= GEMM_MFMA_MIN_M && M <= GEMM_XS_MAX_M && (e->wdt == WDT_BF16 || e->wdt == WDT_Q4) &&
-         !e->fuse_mlp && D % 512 == 0 && D / 512 <= 64 && gemm_xs_eligible(s.qkv_rows(), D, M, e->wdt) &&
+         D % 512 == 0 && D / 512 <= 64 && gemm_xs_eligible(s.qkv_rows(), D, M, e->wdt) &&
          gemm_xs_eligible(D, s.q_dim(), M, e->wdt) && gemm_xs_eligible(2 * F, D, M, e->wdt) &&
          gemm_xs_eligible(D, F, M, e->wdt) && gemm_xs_tiles(D, F, M) <= 64 && gemm_xs_tiles(D, s.q_dim(), M) <= 64;
 }
@@ -471,7 +432,7 @@ int head_blocks(int N, int K, int M, int wdt) { return gemv_partials(N, K, M, wd
 // engine has csm_1b's backbone shapes in bf16 (with the chunk-major down copies) and the device has
 // the 256 CUs its one-workgroup-per-CU grid assumes (every workgroup must be resident).
 bool bb_step_eligible(csm_engine* e) {
-  if (!e->bb_step || !e->bb_gbuf || e->B != 1 || e->wdt != WDT_BF16 || e->fuse_mlp) return false;
+  if (!e->bb_step || !e->bb_gbuf || e->B != 1 || e->wdt != WDT_BF16) return false;
   const csm_llama_dims& d = e->bb.d;
   if (d.hidden != 2048 || d.intermediate != 8192 || d.n_heads != 32 || d.n_kv_heads != 8 || d.head_dim != 64 ||
       d.n_layers != BB_STEP_LAYERS)
@@ -522,11 +483,11 @@ void enqueue_body(csm_engine* e, hipStream_t st) {
   RowMap rm{1, 0, e->pos, 0};
   if (bb_xs) {
     run_bb_xs(e, B, rm, st);
-    launch_rmsnorm_rows(e->x, e->D, e->bb.norm, e->bb.d.eps, e->D, e->h_last, e->D, B, st, nullptr, 0);
+    launch_rmsnorm_rows(e->x, e->D, e->bb.norm, e->bb.d.eps, e->D, e->h_last, e->D, B, st);
     return;
   }
-  const long long* pend = run_stack(e, e->bb, e->x, B, e->q, e->att, e->mlp, rm, st);
-  launch_rmsnorm_rows(e->x, e->D, e->bb.norm, e->bb.d.eps, e->D, e->h_last, e->D, B, st, pend, e->acc_rows * e->D);
+  run_stack(e, e->bb, e->x, B, e->q, e->att, e->mlp, rm, st);
+  launch_rmsnorm_rows(e->x, e->D, e->bb.norm, e->bb.d.eps, e->D, e->h_last, e->D, B, st);
 }
 
 // The persistent frame decoder runs the whole head of a batch-1 frame (greedy, or sampled: its heads
@@ -565,15 +526,6 @@ void enqueue_dec_frame_only(csm_engine* e, hipStream_t st) {
   a.norm = e->dec.norm; a.rope = e->dec.rope; a.S_cap = e->dec.S_cap; a.eps = e->dec.d.eps;
   a.c0_head = (const bf16_t*)e->c0_head; a.proj = (const bf16_t*)e->proj; a.audio_head = (const bf16_t*)e->audio_head;
   a.proj_tab = e->proj_tab; a.qkv0_tab = e->qkv0_tab; a.h_last = e->h_last;
-  a.tab_reps = e->tab_copies_n == e->tab_rep - 1 ? e->tab_rep : 1;
-  {
-    const size_t np = (size_t)(e->K - 1) * e->V * e->Dd, nq = (size_t)(e->K - 1) * e->V * e->dec.qkv_rows();
-    for (int r = 0; r < DEC_FRAME_TAB_REPS; ++r) {
-      const float* base = r > 0 && r < a.tab_reps ? e->tab_copies + (size_t)(r - 1) * (np + nq) : nullptr;
-      a.proj_tabs[r] = base ? base : e->proj_tab;
-      a.qkv0_tabs[r] = base ? base + np : e->qkv0_tab;
-    }
-  }
   a.V = e->V; a.VP = e->Vpad; a.K = e->K; a.codes = e->codes; a.c0_logits = e->c0_logits; a.ci_logits = e->ci_logits;
   a.gbuf = (unsigned long long*)e->df_gbuf; a.epoch = e->df_epoch; a.err = e->df_err; a.stamps = e->df_stamps;
   static const int wnt = [] { const char* v = getenv("CSM_DF_WNT"); return v ? atoi(v) : 0; }();
@@ -653,7 +605,6 @@ void enqueue_head_phase(csm_engine* e, hipStream_t st, int phase) {
     GemvParams g0 = g;  // steps >= 2: layer 0 gathers projection(E_a[c]) from the folded table
     g0.xtab = e->proj_tab; g0.xtab_f32 = 1; g0.xtab_q4_rows = 0;
     RowMap rm = (i == 1) ? RowMap{2, 0, nullptr, 0} : RowMap{1, 0, nullptr, i};
-    const long long* pend = nullptr;  // fused-MLP output of the last decoder layer, read by the head
     const bool use_tab = folded && e->use_qkv0_tab && e->qkv0_built && !e->no_tab_batched;
     const bool xs_dec = use_tab && dec_xs_eligible(e, M);  // streaming matrix-core decoder + head
     if (!use_tab && (gemm_mfma_eligible(Dd, D, M, e->wdt) || gemm_mfma_eligible(e->dec.qkv_rows(), Dd, M, e->wdt))) {
@@ -670,7 +621,7 @@ void enqueue_head_phase(csm_engine* e, hipStream_t st, int phase) {
         gr.K = Dd; gr.out = e->dx; gr.os = Dd;
         launch_gather_rows(gr, e->wdt, st);
       }
-      pend = run_stack(e, e->dec, e->dx, M, e->dq, e->datt, e->dmlp, rm, st, nullptr);
+      run_stack(e, e->dec, e->dx, M, e->dq, e->datt, e->dmlp, rm, st, nullptr);
     } else if (use_tab) {
       // layer 0's q | k | v and input row gathered from the folded tables by the attention (no layer-0
       // QKV projection); at >= 8 rows the other projections run on the matrix cores
@@ -680,10 +631,10 @@ void enqueue_head_phase(csm_engine* e, hipStream_t st, int phase) {
       a0.g_codes = e->codes; a0.g_codes_K = K; a0.g_cb = i - 1;
       a0.g_xtab = e->proj_tab + (size_t)(i - 1) * V * Dd; a0.g_xout = e->dx; a0.g_D = Dd;
       if (xs_dec) run_dec_xs(e, M, rm, st, a0);
-      else pend = run_stack(e, e->dec, e->dx, M, e->dq, e->datt, e->dmlp, rm, st, nullptr, &a0);
+      else run_stack(e, e->dec, e->dx, M, e->dq, e->datt, e->dmlp, rm, st, nullptr, &a0);
     } else {
       if (!folded) launch_gemv(g, e->wdt, EPI_STORE, 0, st);
-      pend = run_stack(e, e->dec, e->dx, M, e->dq, e->datt, e->dmlp, rm, st, folded ? &g0 : nullptr);
+      run_stack(e, e->dec, e->dx, M, e->dq, e->datt, e->dmlp, rm, st, folded ? &g0 : nullptr);
     }
     // ci_logits = norm(hidden[:, -1]) @ audio_head[i-1]  (generation.py:79)
     g = gp(e);
@@ -691,10 +642,6 @@ void enqueue_head_phase(csm_engine* e, hipStream_t st, int phase) {
     g.x = e->dx + (i == 1 ? Dd : 0); g.xs = (i == 1 ? 2 * Dd : Dd); g.M = B; g.nw = e->dec.norm;
     g.eps = e->dec.d.eps; g.out = e->ci_logits + (size_t)(i - 1) * B * Vp; g.os = Vp;
     g.part = part(i); g.part_stride = e->part_stride; g.n_valid = V;
-    if (pend) {
-      g.xacc = pend + (i == 1 ? Dd : 0);
-      g.acc_ss = e->acc_rows * Dd;
-    }
     if (xs_dec) {  // the head reads the split rows (x * final norm) the last down wrote
       g.xs_in = e->xs_D; g.ss_in = e->xs_ss; g.ss_n = gemm_xs_tiles(Dd, e->dec.d.intermediate, M);
       g.ss_stride = GEMM_XS_MAX_M;
@@ -766,10 +713,6 @@ void ensure_batch(csm_engine* e, int B) {
   // partial slots per row: enough for any head tiling (c0 / ci heads, dense or q4; >= Vp/2 blocks never occur)
   e->part_stride = (int)(Vp / 2);
   e->part = (unsigned long long*)e->balloc(K * Bm * (size_t)e->part_stride * 8);
-  // fused-MLP accumulators (zeroed here; kept zero between uses by the o_proj that folds them)
-  e->acc_rows = 4;
-  for (Stack* s : {&e->bb, &e->dec})
-    for (int k = 0; k < 2; ++k) s->acc[k] = (long long*)e->balloc((size_t)ACC_SLOTS * e->acc_rows * s->d.hidden * 8);
   // split-K scratch of the MFMA path for every projection shape at its largest row count
   for (Stack* s : {&e->bb, &e->dec}) {
     const int Dm = s->d.hidden, F = s->d.intermediate, rows = (s == &e->bb) ? std::max(e->M_cap, (int)Bm) : 2 * (int)Bm;
@@ -874,25 +817,8 @@ void build_proj_table(csm_engine* e) {
   HIPCHK(hipStreamSynchronize(e->st));
   HIPCHK(hipGetLastError());
   e->qkv0_built = true;
-  e->tab_copies_n = 0;
 }
 
-// the table replicas the frame decoder reads (option tab_rep), refreshed after a table rebuild
-void build_tab_copies(csm_engine* e) {
-  if (e->tab_rep <= 1 || !e->qkv0_built || e->tab_copies_n == e->tab_rep - 1) return;
-  const size_t np = (size_t)(e->K - 1) * e->V * e->Dd, nq = (size_t)(e->K - 1) * e->V * e->dec.qkv_rows();
-  if (e->tab_copies) (void)hipFree(e->tab_copies);
-  e->tab_copies = nullptr;
-  HIPCHK(hipMalloc(&e->tab_copies, (size_t)(e->tab_rep - 1) * (np + nq) * 4));
-  for (int r = 0; r < e->tab_rep - 1; ++r) {
-    float* dst = e->tab_copies + (size_t)r * (np + nq);
-    HIPCHK(hipMemcpyAsync(dst, e->proj_tab, np * 4, hipMemcpyDeviceToDevice, e->st));
-    HIPCHK(hipMemcpyAsync(dst + np, e->qkv0_tab, nq * 4, hipMemcpyDeviceToDevice, e->st));
-  }
-  HIPCHK(hipStreamSynchronize(e->st));
-  e->tab_copies_n = e->tab_rep - 1;
-  e->g_B = -1;  // the captured frame graph holds the table pointers
-}
 
 
 // Where an MLX Linear/Embedding weight lives in the engine: rows row0 + r*rstep (r < n) of a
@@ -1046,7 +972,6 @@ int csm_engine_create(const csm_dims* dims, int device, int weight_dtype, int ma
     }
     HIPCHK(hipSetDevice(device));
     std::unique_ptr<csm_engine> e(new csm_engine());
-    if (const char* v = getenv("CSM_FUSE_ATTN")) e->fuse_attn = v[0] != '0';
     e->dims = *dims;
     e->dev = device;
     e->wdt = weight_dtype == CSM_F32 ? WDT_F32 : (weight_dtype == CSM_Q4 ? WDT_Q4 : WDT_BF16);
@@ -1180,8 +1105,8 @@ int csm_load_tensor(csm_engine* e, const char* cname, const void* host, int src_
         expect({D, F});
         auto h = conv(numel());
         HIPCHK(hipMemcpy(l.wd, h.data(), h.size(), hipMemcpyHostToDevice));
-        if (l.wdc) {  // fused MLP: columns chunk-major [F/R][D][R] (bf16)
-          const int R = fused_mlp_chunk(D);
+        if (l.wdc) {  // persistent kernels: columns chunk-major [F/R][D][R] (bf16)
+          const int R = wdc_chunk(D);
           const uint16_t* src = reinterpret_cast<const uint16_t*>(h.data());
           std::vector<uint16_t> t2((size_t)D * F);
           for (int c = 0; c < F / R; ++c)
@@ -1354,7 +1279,6 @@ int csm_begin(csm_engine* e, int B, const uint64_t* seeds, float temperature, in
     ensure_batch(e, B);
     if (e->tiled_dirty) build_tiled(e);
     if (e->proj_tab_dirty) build_proj_table(e);
-    build_tab_copies(e);
     e->pos_host.assign(B, -1);
     e->B = B;
     e->temperature = temperature;
@@ -1412,10 +1336,9 @@ int csm_prefill(csm_engine* e, int b, int T, const int32_t* tokens, const uint8_
     ep.K = K; ep.D = e->D; ep.out = e->x;
     embed(e, ep, T, e->st);
     RowMap rm{T, b, nullptr, start};
-    const long long* pend = run_stack(e, e->bb, e->x, T, e->q, e->att, e->mlp, rm, e->st);
+    run_stack(e, e->bb, e->x, T, e->q, e->att, e->mlp, rm, e->st);
     launch_rmsnorm_rows(e->x + (size_t)(T - 1) * e->D, e->D, e->bb.norm, e->bb.d.eps, e->D,
-                        e->h_last + (size_t)b * e->D, e->D, 1, e->st, pend ? pend + (size_t)(T - 1) * e->D : nullptr,
-                        e->acc_rows * e->D);
+                        e->h_last + (size_t)b * e->D, e->D, 1, e->st);
     e->pos_host[b] = start + T - 1;  // position of the last processed backbone row
     HIPCHK(hipMemcpyAsync(e->pos + b, &e->pos_host[b], 4, hipMemcpyHostToDevice, e->st));
     HIPCHK(hipStreamSynchronize(e->st));
@@ -1471,11 +1394,11 @@ int csm_prefill_batch(csm_engine* e, int n, const int32_t* utts, const int32_t* 
       RowMap rm{1, 0, nullptr, 0};
       rm.row_b = e->row_b;
       rm.row_pos = e->row_pos;
-      const long long* pend = run_stack(e, e->bb, e->x, R, e->q, e->att, e->mlp, rm, e->st);
+      run_stack(e, e->bb, e->x, R, e->q, e->att, e->mlp, rm, e->st);
       for (int i = i0; i < i1; ++i) {  // h_last = norm(last row) of each utterance
         const size_t last = row0[i + 1] - 1 - row0[i0];
         launch_rmsnorm_rows(e->x + last * e->D, e->D, e->bb.norm, e->bb.d.eps, e->D, e->h_last + (size_t)utts[i] * e->D,
-                            e->D, 1, e->st, pend ? pend + last * e->D : nullptr, e->acc_rows * e->D);
+                            e->D, 1, e->st);
       }
       HIPCHK(hipStreamSynchronize(e->st));  // the host row tables are reused by the next group
       HIPCHK(hipGetLastError());
@@ -1947,24 +1870,12 @@ int csm_bench_bb_step(csm_engine* e, int iters, float* avg_us, double* bytes) {
 int csm_set_option(csm_engine* e, const char* key, int value) {
   CSM_TRY {
     const std::string k(key ? key : "");
-    if (k == "fuse_attn") {
-      if (!e) throw CsmError(CSM_ERR_ARG, "fuse_attn needs an engine");
-      e->fuse_attn = value != 0;
-    }
-    else if (k == "nt_mask") gemv_set_nt_mask(value);
-    else if (k == "gemv_xl") gemv_set_xl(value);
-    else if (k == "linear_mfma") {
+    if (k == "linear_mfma") {
       if (!e) throw CsmError(CSM_ERR_ARG, "linear_mfma needs an engine");
       e->linear_mfma = value != 0;
     } else if (k == "fold_proj") {
       if (!e) throw CsmError(CSM_ERR_ARG, "fold_proj needs an engine");
       e->fold_proj = value != 0;
-    }
-    else if (k == "tab_rep") {
-      if (!e || value < 1 || value > DEC_FRAME_TAB_REPS) throw CsmError(CSM_ERR_ARG, "tab_rep needs an engine and 1..8 replicas");
-      e->tab_rep = value;
-      e->tab_copies_n = 0;  // rebuilt at the next csm_begin
-      e->g_B = -1;
     }
     else if (k == "qkv0_tab") {
       if (!e) throw CsmError(CSM_ERR_ARG, "qkv0_tab needs an engine");
@@ -2010,10 +1921,6 @@ int csm_set_option(csm_engine* e, const char* key, int value) {
       const int one = 1;
       for (int* f : {e->df_err, e->bb_err})
         if (f && value) HIPCHK(hipMemcpy(f, &one, 4, hipMemcpyHostToDevice));
-    }
-    else if (k == "fuse_mlp") {
-      if (!e) throw CsmError(CSM_ERR_ARG, "fuse_mlp needs an engine");
-      e->fuse_mlp = value != 0;
     }
     else throw CsmError(CSM_ERR_ARG, "unknown option " + k);
     if (e) e->g_B = -1;  // re-capture the frame graphs with the new setting

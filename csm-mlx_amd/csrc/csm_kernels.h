@@ -8,21 +8,6 @@ enum { WDT_F32 = 0, WDT_BF16 = 1, WDT_Q4 = 2 };  // WDT_Q4: MLX affine int4, gro
 enum { EPI_STORE = 0, EPI_ADD = 1, EPI_SILU_MUL = 2, EPI_QKV = 3, EPI_GELU = 4, EPI_ARGMAX = 5 };
 enum { ATTN_CAUSAL = 0, ATTN_WINDOW = 1, ATTN_BLOCK = 2 };
 
-// Residual contributions of the fused MLP are summed as 64-bit fixed point (units of 2^-32) with
-// integer atomics: integer addition is associative, so the total is independent of block order.
-// The accumulator is replicated ACC_SLOTS times (block c adds into slot c % ACC_SLOTS): the memory-side
-// atomic units serialize adds to one 64-B line, so spreading the F/R blocks over slots divides that
-// serialization; readers sum the slots (integer, exact) in slot order.
-constexpr double ACC_ONE = 4294967296.0;
-constexpr int ACC_SLOTS = 1;  // 8 slots measured slower (184.7 vs 197.9 frames/s fused; consumers pay the slot reads)
-__device__ __forceinline__ float acc_to_f(long long v) { return (float)((double)v * (1.0 / ACC_ONE)); }
-__device__ __forceinline__ long long acc_slots_sum(const long long* a, size_t ss) {
-  long long t = 0;
-#pragma unroll
-  for (int s = 0; s < ACC_SLOTS; ++s) t += a[(size_t)s * ss];
-  return t;
-}
-
 // MFMA-path state owned by one engine (csm_engine::ws): split-K slice partials and arrival tickets,
 // sized by gemm_reserve outside graph capture, and the fragment-tiled copy of every weight matrix
 // the matrix cores read (row-major matrix -> its tiled copy, gemm_retile).
@@ -68,11 +53,6 @@ struct GemvParams {
   int xtab_q4_rows;     // int4 weights: total rows of the (quantized) gathered table
   float* x_copy;        // if set: block 0 also stores the raw (un-normed) x rows here [M][K]
   float* qkv_tab;       // EPI_QKV table build: rows [M][(Hq + 2 Hkv) hd] instead of q / KV cache
-  // fused-MLP residual accumulator (64-bit fixed point, ACC_ONE units; see fused_mlp_kernel):
-  const long long* xacc;  // staging reads x + acc (row m at xacc + m * xs, as x): the pending MLP output
-  long long* oacc;        // EPI_ADD: out = (out + acc) + a when oacc_add (else out += a); acc zeroed
-  int oacc_add;
-  int acc_ss;             // elements between accumulator slots
   // MFMA path split-K (set by launch_gemm_mfma from ws): slice partials [ksplit][M][N], sum-of-squares [ksplit][M]
   GemmWs* ws;            // the calling engine's scratch (host pointer; required for split launches)
   const void* Wt;        // the weight's fragment-tiled copy (looked up in ws->tiled by launch_gemm_mfma)
@@ -173,24 +153,8 @@ __device__ __forceinline__ void gemv_epilogue_pair(const GemvParams& p, int m, i
         a *= p.scale[n];
         b *= p.scale[n + 1];
       }
-      if (p.oacc) {  // fold the pending fused-MLP output into the residual and clear it
-        long long* ac = p.oacc + (size_t)m * p.os + n;
-        if (p.oacc_add) {
-          o[0] = (o[0] + acc_to_f(acc_slots_sum(ac, p.acc_ss))) + a;
-          o[1] = (o[1] + acc_to_f(acc_slots_sum(ac + 1, p.acc_ss))) + b;
-        } else {
-          o[0] += a;
-          o[1] += b;
-        }
-#pragma unroll
-        for (int s2 = 0; s2 < ACC_SLOTS; ++s2) {
-          ac[(size_t)s2 * p.acc_ss] = 0;
-          ac[(size_t)s2 * p.acc_ss + 1] = 0;
-        }
-      } else {
-        o[0] += a;
-        o[1] += b;
-      }
+      o[0] += a;
+      o[1] += b;
       break;
     }
     case EPI_ARGMAX: {  // logits (c0 / ci heads); the packed block arg-max is reduced by the caller
@@ -322,30 +286,12 @@ void launch_to_f32(const void* src, int wdt, float* dst, size_t n, hipStream_t s
 void launch_attn(const AttnParams& p, int hd, hipStream_t st);
 // rows per block of the GEMV launch for (N, K, M): N must be a multiple of it
 int gemv_rows_per_block(int N, int K, int M);
-// depth-decoder attention recomputed inside every o_proj block (+ residual): one launch
-bool dec_attn_oproj_supported(const GemvParams& p, const AttnParams& a, int hd);
-void launch_dec_attn_oproj(const GemvParams& p, const AttnParams& a, int wdt, hipStream_t st, int tag);
-void gemv_set_nt_mask(int mask);
-void gemv_set_xl(int on);
-// xacc (optional): pending fused-MLP accumulator added to x (same layout as x)
 void launch_rmsnorm_rows(const float* x, int xs, const float* w, float eps, int D, float* out, int os, int M,
-                         hipStream_t st, const long long* xacc = nullptr, int acc_ss = 0);
+                         hipStream_t st);
 
-// ---- fused MLP (decode regime, bf16): x + down(silu(gate(norm(x))) * up(norm(x))) in one launch
-struct MlpParams {
-  const float* x;          // [M][xs] residual rows (attention already added)
-  int xs, M;
-  const float* nw;         // post_attention_layernorm weight
-  float eps;
-  const void* wgu;         // [2F][D] gate/up rows interleaved (row 2j gate_j, 2j+1 up_j)
-  const void* wdc;         // down_proj columns chunk-major: [F/R][D][R] (R = fused_mlp_chunk(D))
-  long long* acc;          // [ACC_SLOTS][M][xs] fixed-point accumulator of down(h), zero on entry
-  int F;
-  int acc_ss;              // elements between slots
-};
-int fused_mlp_chunk(int D);                  // intermediate rows per block (0: shape unsupported)
-bool fused_mlp_supported(int D, int F, int M);
-void launch_fused_mlp(const MlpParams& p, int D, bool nt, hipStream_t st);
+// down_proj columns re-laid chunk-major [F/R][D][R] for the persistent kernels (dec_frame / bb_step):
+// R = wdc_chunk(D) consecutive intermediate columns per chunk (0: no chunk-major copy for this width)
+int wdc_chunk(int D);
 bool gemv_nt(int tag);                       // non-temporal weight loads for this stack tag
 void launch_sample(const SampleParams& p, int wdt, int B, hipStream_t st);
 void launch_advance(const AdvanceParams& p, hipStream_t st);
@@ -379,7 +325,8 @@ bool gemm_reserve(GemmWs& ws, int N, int K, int M);
 // Streaming matrix-core GEMM over pre-split activations (gemm_xs.hip): bf16 weights, <= 64 rows
 constexpr int GEMM_XS_MAX_M = 64;
 bool gemm_xs_eligible(int N, int K, int M, int wdt);
-int gemm_xs_tiles(int N, int K, int M);       // column tiles of a launch (ss / arg-max partials per row)
+// column tiles of a launch: sums-of-squares partials per row, or (head: an EPI_ARGMAX / SiLU launch) arg-max partials
+int gemm_xs_tiles(int N, int K, int M, bool head = false);
 void launch_gemm_xs(const GemvParams& p, int epi, hipStream_t st, bool nt = false, int wdt = WDT_BF16);
 bool gemm_xs_reserve(GemmWs& ws, int N, int K, int M);
 // Fragment-tiled weight copy for the MFMA path: per 32-row tile and 64-K stage, the bytes each lane
@@ -426,7 +373,6 @@ void launch_bb_step(const BbStepArgs& p, hipStream_t st);
 const void* bb_step_kernel_ptr();
 
 constexpr int DEC_FRAME_LAYERS = 4;
-constexpr int DEC_FRAME_TAB_REPS = 8;  // max replicas of the folded tables (option tab_rep)
 struct DecFrameArgs {
   const bf16_t* wqkv[DEC_FRAME_LAYERS];
   const bf16_t* wo[DEC_FRAME_LAYERS];
@@ -445,11 +391,6 @@ struct DecFrameArgs {
   const bf16_t* audio_head;              // [K-1][VP][1024]
   const float* proj_tab;                 // [K-1][V][1024]
   const float* qkv0_tab;                 // [K-1][V][1536]
-  // table replicas (csm_set_option "tab_rep"): workgroup w reads replica w % tab_reps (replica 0 = the
-  // tables above) -- every workgroup loads the same rows after each head, so fewer readers per row
-  const float* proj_tabs[DEC_FRAME_TAB_REPS];
-  const float* qkv0_tabs[DEC_FRAME_TAB_REPS];
-  int tab_reps;
   const float* h_last;                   // [2048]
   int V, VP, K;
   int* codes;                            // [K] of utterance 0

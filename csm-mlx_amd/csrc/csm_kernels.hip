@@ -330,20 +330,10 @@ __global__ __launch_bounds__(256) void gemv_xl_kernel(GemvParams p) {
       const WT* xw = g16 ? (const WT*)p.xtab + trow : nullptr;
       const float* xf = gathered ? (const float*)p.xtab + trow : p.x + (size_t)(p.x_step1 ? (i >> 1) : i) * p.xs;
       float* xc = (p.x_copy && blockIdx.x == 0) ? p.x_copy + (size_t)i * p.K : nullptr;
-      const long long* xa = p.xacc ? p.xacc + (size_t)(p.x_step1 ? (i >> 1) : i) * p.xs : nullptr;
       for (int k = tid * 8; k < p.K; k += 256 * 8) {
         float xv[8];
         if (g16) W8<WT>::load(xw + k, xv);
         else W8<float>::load(xf + k, xv);
-        if (xa) {  // residual + the pending fused-MLP output (slots summed in order)
-          long long t[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-          for (int s2 = 0; s2 < ACC_SLOTS; ++s2)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) t[j] += xa[(size_t)s2 * p.acc_ss + k + j];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) xv[j] += acc_to_f(t[j]);
-        }
         if (xc) {
           *reinterpret_cast<float4*>(xc + k) = make_float4(xv[0], xv[1], xv[2], xv[3]);
           *reinterpret_cast<float4*>(xc + k + 4) = make_float4(xv[4], xv[5], xv[6], xv[7]);
@@ -463,8 +453,7 @@ __global__ __launch_bounds__(256) void gemv_xl_kernel(GemvParams p) {
 // V rows HD floats) with online-softmax state (m_run, l_run, o).  The q.k dot runs as four
 // independent FMA chains (one per float4 lane) and P.V broadcasts p_j with v_readlane (scalar, no
 // LDS round trip) four keys at a time so the V reads are in flight together: the single-chain /
-// ds_bpermute form spent ~3 us of dependent latency per head at 32 keys.  Shared by attn_block and
-// dec_attn_oproj_kernel, so both produce bit-identical outputs.
+// ds_bpermute form spent ~3 us of dependent latency per head at 32 keys.
 template <int HD>
 __device__ __forceinline__ void attn_chunk(const float* qr_, const float* Kc, const float* Vc, int n, int lane,
                                            float& m_run, float& l_run, float (&o)[HD / 64]) {
@@ -766,118 +755,14 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnParams p) {
   attn_block<HD>(p, blockIdx.x / p.Hkv, blockIdx.x % p.Hkv, L);
 }
 
-// ============================================================================ decoder attention + o_proj
-// The depth decoder attends over <= 32 cached positions (generation.py:70-77).  One launch does the
-// attention of every head AND the o_proj GEMV (+ residual): 8 waves; wave h runs attn_short_head for
-// (row, head h) into LDS (K rows / V columns straight from L2 into VGPRs, one round trip), while the
-// block's o_proj weight rows are already in flight; then the o_proj dot products run from LDS with
-// gemv_xl_kernel's G = 128 K-slicing and reduction order.  Attention and projection arithmetic are
-// those of attn_short_kernel + gemv_xl_kernel, so outputs are bit-identical to the two launches.
-// Every block recomputes the attention (M <= 2 rows x 8 heads x <= 32 keys: ~64 KB of K/V from L2).
-// With g_tab (layer 0, steps >= 2) the residual row is fused: x = proj_tab[cb][code] + o_proj(att).
-constexpr int DA_M = 2;       // rows (decoder step 1: [h_last, c0] rows)
-constexpr int DA_QD = 1024;   // Hq * head_dim
-constexpr int DA_HQ = 8;      // q heads (one wave each)
-
-template <typename WT, int RPT, int TAG>
-__global__ __launch_bounds__(512) void dec_attn_oproj_kernel(GemvParams p, AttnParams a) {
-  constexpr int HD = 128, G = 128, NG = 512 / G, RPB = NG * RPT, NO = HD / 64;
-  constexpr bool NT = (TAG & 4) != 0;
-  __shared__ __attribute__((aligned(16))) float qsh[DA_HQ][HD];
-  __shared__ __attribute__((aligned(16))) float xo[DA_M][DA_QD];  // attention output = o_proj input
-  __shared__ float red[8][DA_M][RPT];
-  __shared__ int gcode[DA_M];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int grp = tid / G, gt = tid % G;
-  const int row0 = blockIdx.x * RPB + grp * RPT;
-  // (1) o_proj weights in flight (K = 1024 = one G*8 step per thread)
-  Raw8<WT> wr[RPT];
-#pragma unroll
-  for (int r = 0; r < RPT; ++r) wr[r].template load<NT>((const WT*)p.W + (size_t)(row0 + r) * p.K + gt * 8);
-  // (2) attention: wave -> (row, head) pairs
-  for (int idx = wave; idx < p.M * a.Hq; idx += 8) {
-    const int m = idx / a.Hq, h = idx % a.Hq;
-    float o[NO];
-    int c = 0;
-    const bool side = blockIdx.x == 0;  // cache row + code written once
-    attn_short_head<HD, 32>(a, m, h, lane, qsh[wave], o, side, side, false, &c);
-#pragma unroll
-    for (int i = 0; i < NO; ++i) xo[m][h * HD + lane + 64 * i] = o[i];
-    if (h == 0 && lane == 0) gcode[m] = c;
-  }
-  __syncthreads();
-  // (3) o_proj from LDS
-  float acc[DA_M][RPT];
-#pragma unroll
-  for (int i = 0; i < DA_M; ++i)
-#pragma unroll
-    for (int r = 0; r < RPT; ++r) acc[i][r] = 0.f;
-  {
-    float w[RPT][8];
-#pragma unroll
-    for (int r = 0; r < RPT; ++r) wr[r].get(w[r]);
-#pragma unroll
-    for (int i = 0; i < DA_M; ++i) {
-      if (i < p.M) {
-        const float4 x0 = *reinterpret_cast<const float4*>(&xo[i][gt * 8]);
-        const float4 x1 = *reinterpret_cast<const float4*>(&xo[i][gt * 8 + 4]);
-        const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-#pragma unroll
-        for (int r = 0; r < RPT; ++r)
-#pragma unroll
-          for (int j = 0; j < 8; ++j) acc[i][r] = fmaf(w[r][j], xv[j], acc[i][r]);
-      }
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < DA_M; ++i)
-#pragma unroll
-    for (int r = 0; r < RPT; ++r) {
-      const float v = wave_sum(acc[i][r]);
-      if (lane == 0) red[wave][i][r] = v;
-    }
-  __syncthreads();
-  constexpr int WPG = G / 64;
-  constexpr int NPAIR = NG * DA_M * (RPT / 2);
-  if (tid < NPAIR) {
-    const int g = tid / (DA_M * (RPT / 2));
-    const int rem = tid % (DA_M * (RPT / 2));
-    const int i = rem / (RPT / 2), rp = (rem % (RPT / 2)) * 2;
-    if (i < p.M) {
-      float va = 0.f, vb = 0.f;
-#pragma unroll
-      for (int w2 = 0; w2 < WPG; ++w2) {
-        va += red[g * WPG + w2][i][rp];
-        vb += red[g * WPG + w2][i][rp + 1];
-      }
-      const int n = blockIdx.x * RPB + g * RPT + rp;
-      if (a.g_tab) {  // residual = the folded decoder input row
-        const float* xs = a.g_xtab + (size_t)gcode[i] * a.g_D;
-        float* o = p.out + (size_t)i * p.os + n;
-        o[0] = xs[n] + va;
-        o[1] = xs[n + 1] + vb;
-        if (p.oacc) {  // the previous step's last-layer MLP accumulator: consumed, clear it
-          for (int s2 = 0; s2 < ACC_SLOTS; ++s2) {
-            p.oacc[(size_t)s2 * p.acc_ss + (size_t)i * p.os + n] = 0;
-            p.oacc[(size_t)s2 * p.acc_ss + (size_t)i * p.os + n + 1] = 0;
-          }
-        }
-      } else {
-        gemv_epilogue_pair(p, i, n, va, vb);
-      }
-    }
-  }
-}
-
 // ============================================================================ rmsnorm rows
 // out[m] = rmsnorm(x[row(m)]) ; optionally also scatter to dec_in[2m] (decoder step-1 rows).
 __global__ __launch_bounds__(256) void rmsnorm_rows_kernel(const float* x, int xs, const float* w, float eps, int D,
-                                                            float* out, int os, const long long* xacc, int acc_ss) {
+                                                            float* out, int os) {
   __shared__ float red[4];
   const int m = blockIdx.x;
   const float* xr = x + (size_t)m * xs;
-  const long long* xa = xacc ? xacc + (size_t)m * xs : nullptr;
-  auto xv = [&](int d) { return xa ? xr[d] + acc_to_f(acc_slots_sum(xa + d, acc_ss)) : xr[d]; };
+  auto xv = [&](int d) { return xr[d]; };
   float ss = 0.f;
   for (int d = threadIdx.x; d < D; d += blockDim.x) ss += xv(d) * xv(d);
   ss = wave_sum(ss);
@@ -1134,11 +1019,18 @@ __global__ __launch_bounds__(256) void sample_filtered_kernel(SampleParams p) {
     for (int r = 0; r < SAMPLE_NPT; ++r) kp[r] = kp[r] && (suf[r] + later > p.top_p_cut);
   }
   if (p.use_min_p) {
-    // the best kept lp (kept entries are a prefix of the sorted order: position 0 if any)
+    // the best kept lp, a block max over the kept entries (oracle filter_keep: lp[keep].max()).  Not
+    // simply sorted position 0: top_k keeps by the raw logit while the sort is by the fp32-rounded
+    // lp = l - lse with index-ascending ties, so a dropped entry can sort ahead of a kept one.
+    float bm = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < SAMPLE_NPT; ++r)
+      if (kp[r]) bm = fmaxf(bm, lpv[r]);
+    bm = wave_max(bm);
     __syncthreads();
-    if (tid == 0) fred[0] = kp[0] ? lpv[0] : -INFINITY;
+    if (lane == 0) fred[wave] = bm;
     __syncthreads();
-    const float tmin = fred[0] + p.log_min_p;
+    const float tmin = fmaxf(fmaxf(fred[0], fred[1]), fmaxf(fred[2], fred[3])) + p.log_min_p;
 #pragma unroll
     for (int r = 0; r < SAMPLE_NPT; ++r) kp[r] = kp[r] && (!(lpv[r] < tmin) || SAMPLE_NPT * tid + r < p.min_keep);
   }
@@ -1216,9 +1108,8 @@ __global__ void advance_kernel(AdvanceParams p) {
 // other shape is latency-bound and best at G = 128 (K >= 1024).  RPT = 2 wins everywhere at M = 1.
 // LDS-staged activations for the decode regime (gemv_xl_kernel): 1 = on for K <= 2048, 3 = also the
 // K = 8192 down projections (measured slower: dec down 5.96 vs 5.77 us, 231.6 vs 234.8 frames/s),
-// 0 = off.  CSM_GEMV_XL overrides the default (A/B runs).
-static int g_gemv_xl = [] { const char* e = getenv("CSM_GEMV_XL"); return e ? atoi(e) : 1; }();
-void gemv_set_xl(int on) { g_gemv_xl = on; }
+// 0 = off.  CSM_GEMV_XL overrides the default (A/B runs; read once per process).
+static const int g_gemv_xl = [] { const char* e = getenv("CSM_GEMV_XL"); return e ? atoi(e) : 1; }();
 
 static void gemv_tiling(int N, int K, int M, int& G, int& RPT) {
   (void)M;
@@ -1276,14 +1167,10 @@ int gemv_rows_per_block(int N, int K, int M) {
 // Weight-load cache policy per stack tag (bit t set -> non-temporal loads for tag t).  The
 // backbone streams 1.95 GB per frame once; the decoder's 221 MB are re-read 31x per frame and
 // can stay resident in the 256 MiB Infinity Cache if the backbone stream does not evict them.
-static int g_nt_mask = -1;
-void gemv_set_nt_mask(int mask) { g_nt_mask = mask; }
+// CSM_NT_MASK overrides the default (A/B runs; read once per process).
 static int gemv_nt_mask() {
-  if (g_nt_mask < 0) {
-    const char* e = getenv("CSM_NT_MASK");
-    g_nt_mask = e ? atoi(e) : 5;  // backbone + heads (measured: 209.9 vs 202.0 fps all-default)
-  }
-  return g_nt_mask;
+  static const int m = [] { const char* e = getenv("CSM_NT_MASK"); return e ? atoi(e) : 5; }();  // backbone + heads (measured: 209.9 vs 202.0 fps all-default)
+  return m;
 }
 
 // Folded-table builds (csm_engine.hip build_proj_table): every row of a table in ONE launch of
@@ -1382,175 +1269,13 @@ void launch_attn(const AttnParams& p, int hd, hipStream_t st) {
 }
 
 void launch_rmsnorm_rows(const float* x, int xs, const float* w, float eps, int D, float* out, int os, int M,
-                         hipStream_t st, const long long* xacc, int acc_ss) {
-  hipLaunchKernelGGL(rmsnorm_rows_kernel, dim3(M), dim3(256), 0, st, x, xs, w, eps, D, out, os, xacc, acc_ss);
+                         hipStream_t st) {
+  hipLaunchKernelGGL(rmsnorm_rows_kernel, dim3(M), dim3(256), 0, st, x, xs, w, eps, D, out, os);
 }
 
-// ============================================================================ fused MLP (decode)
-// One Llama MLP (mlx_lm MLP wired by models.py:50-51) for M <= MT rows in ONE launch:
-//   x += down(silu(gate(norm2(x))) * up(norm2(x)))
-// Block c owns R consecutive intermediate rows j (gate/up weight rows 2j, 2j+1 -- the engine's
-// interleaved layout) and the matching R columns of down_proj, re-laid chunk-major at load
-// (wdc[c][n][0..R)).  (1) Every weight byte of the block (2R gate/up rows, D x R down slice) is put
-// in flight first; (2) x * norm weight is staged in LDS exactly as gemv_xl_kernel stages it, and the
-// gate/up dots use its K-slicing, wave reduction and epilogue (G = 64): h is bit-identical to the
-// two-launch path; (3) h (R values per row) goes to LDS; (4) the block's partial down product for
-// all D outputs is added to a 64-bit fixed-point accumulator (units 2^-32) with integer atomics --
-// associative, so the sum over the F/R blocks is deterministic whatever the arrival order.  The
-// next reader of the residual (QKV / head staging, final norm) adds the accumulator; the next
-// o_proj folds it into x and zeroes it (GemvParams::xacc / oacc).  Saves the down launch and the
-// h round trip through HBM/L2 per layer.
-template <int D, int R, int MT, bool NT>
-__global__ __launch_bounds__(256) void fused_mlp_kernel(MlpParams p) {
-  constexpr int G = 64, NG = 4, RPT = 2 * R / NG;  // one wave per group of RPT gate/up rows
-  constexpr int KS = D / (G * 8);                   // K steps per lane
-  constexpr int NQ = D / 256;                       // down outputs per thread
-  constexpr int LN = R / 8;                         // 16-B loads per down row slice
-  static_assert(RPT % 2 == 0 && KS >= 1 && NQ >= 1 && LN >= 1, "fused MLP tiling");
-  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  __shared__ __attribute__((aligned(16))) float xl[MT][D];
-  __shared__ float rss[4][MT];
-  __shared__ float hs[MT][R];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int c = blockIdx.x;
-  const int row0 = c * 2 * R + wave * RPT;
-  // (1) all weight loads in flight
-  const bf16_t* Wg = (const bf16_t*)p.wgu;
-  Raw8<bf16_t> wr[KS][RPT];
-#pragma unroll
-  for (int s = 0; s < KS; ++s)
-#pragma unroll
-    for (int r = 0; r < RPT; ++r) wr[s][r].template load<NT>(Wg + (size_t)(row0 + r) * D + lane * 8 + s * G * 8);
-  const bf16_t* Wd = (const bf16_t*)p.wdc + (size_t)c * D * R;
-  u32x4 wd[NQ][LN];
-#pragma unroll
-  for (int q = 0; q < NQ; ++q)
-#pragma unroll
-    for (int l = 0; l < LN; ++l) {
-      const u32x4* src = reinterpret_cast<const u32x4*>(Wd + (size_t)(tid + 256 * q) * R + l * 8);
-      if constexpr (NT) wd[q][l] = __builtin_nontemporal_load(src);
-      else wd[q][l] = *src;
-    }
-  // (2) stage x * nw (gemv_xl_kernel (2b), dense rows)
-#pragma unroll
-  for (int i = 0; i < MT; ++i) {
-    float ssp = 0.f;
-    if (i < p.M) {
-      const float* xf = p.x + (size_t)i * p.xs;
-      for (int k = tid * 8; k < D; k += 256 * 8) {
-        float xv[8], nw[8];
-        W8<float>::load(xf + k, xv);
-        W8<float>::load(p.nw + k, nw);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          ssp = fmaf(xv[j], xv[j], ssp);
-          xv[j] *= nw[j];
-        }
-        *reinterpret_cast<float4*>(&xl[i][k]) = make_float4(xv[0], xv[1], xv[2], xv[3]);
-        *reinterpret_cast<float4*>(&xl[i][k + 4]) = make_float4(xv[4], xv[5], xv[6], xv[7]);
-      }
-    }
-    const float v = wave_sum(ssp);
-    if (lane == 0) rss[wave][i] = v;
-  }
-  __syncthreads();
-  // (3) gate/up dots from LDS, wave reduction, SiLU(gate) * up -> hs
-  float acc[MT][RPT];
-#pragma unroll
-  for (int i = 0; i < MT; ++i)
-#pragma unroll
-    for (int r = 0; r < RPT; ++r) acc[i][r] = 0.f;
-#pragma unroll
-  for (int s = 0; s < KS; ++s) {
-    const int k = lane * 8 + s * G * 8;
-    float w[RPT][8];
-#pragma unroll
-    for (int r = 0; r < RPT; ++r) wr[s][r].get(w[r]);
-#pragma unroll
-    for (int i = 0; i < MT; ++i) {
-      if (i < p.M) {
-        const float4 x0 = *reinterpret_cast<const float4*>(&xl[i][k]);
-        const float4 x1 = *reinterpret_cast<const float4*>(&xl[i][k + 4]);
-        const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-#pragma unroll
-        for (int r = 0; r < RPT; ++r)
-#pragma unroll
-          for (int j = 0; j < 8; ++j) acc[i][r] = fmaf(w[r][j], xv[j], acc[i][r]);
-      }
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < MT; ++i)
-#pragma unroll
-    for (int r = 0; r < RPT; ++r) acc[i][r] = wave_sum(acc[i][r]);
-  if (lane == 0) {
-#pragma unroll
-    for (int i = 0; i < MT; ++i) {
-      if (i < p.M) {
-        const float sq = (rss[0][i] + rss[1][i]) + (rss[2][i] + rss[3][i]);
-        const float sc = rsqrtf(sq / (float)D + p.eps);
-#pragma unroll
-        for (int rp = 0; rp < RPT; rp += 2) {
-          const float a = (0.f + acc[i][rp]) * sc, b = (0.f + acc[i][rp + 1]) * sc;
-          hs[i][(wave * RPT + rp) >> 1] = silu_f(a) * b;
-        }
-      }
-    }
-  }
-  __syncthreads();
-  // (4) partial down product of this block's R intermediate rows -> fixed-point atomics
-#pragma unroll
-  for (int q = 0; q < NQ; ++q) {
-    const int n = tid + 256 * q;
-    float wf[R];
-#pragma unroll
-    for (int l = 0; l < LN; ++l) {
-      const u32x4 u = wd[q][l];
-      wf[l * 8 + 0] = bf16_lo(u.x); wf[l * 8 + 1] = bf16_hi(u.x); wf[l * 8 + 2] = bf16_lo(u.y);
-      wf[l * 8 + 3] = bf16_hi(u.y); wf[l * 8 + 4] = bf16_lo(u.z); wf[l * 8 + 5] = bf16_hi(u.z);
-      wf[l * 8 + 6] = bf16_lo(u.w); wf[l * 8 + 7] = bf16_hi(u.w);
-    }
-#pragma unroll
-    for (int i = 0; i < MT; ++i) {
-      if (i < p.M) {
-        float pv = 0.f;
-#pragma unroll
-        for (int j = 0; j < R; ++j) pv = fmaf(wf[j], hs[i][j], pv);
-        const long long fx = __double2ll_rn((double)pv * ACC_ONE);
-        if (p.F > 0)
-          atomicAdd(reinterpret_cast<unsigned long long*>(p.acc + (size_t)(c % ACC_SLOTS) * p.acc_ss + (size_t)i * p.xs + n),
-                    (unsigned long long)fx);
-        else if (fx == 0x123456789ll) p.acc[0] = fx;  // lab: atomics skipped (results invalid)
-      }
-    }
-  }
-}
-
-int fused_mlp_chunk(int D) { return D == 1024 ? 16 : (D == 2048 ? 8 : 0); }
-
-bool fused_mlp_supported(int D, int F, int M) {
-  const int R = fused_mlp_chunk(D);
-  return R && M >= 1 && M <= 4 && F % R == 0;
-}
+int wdc_chunk(int D) { return D == 1024 ? 16 : (D == 2048 ? 8 : 0); }
 
 bool gemv_nt(int tag) { return (gemv_nt_mask() >> tag) & 1; }
-
-static bool g_mlp_lab_noatomic = [] { const char* e = getenv("CSM_LAB_MLP_NOATOMIC"); return e && e[0] == '1'; }();
-
-void launch_fused_mlp(const MlpParams& p0, int D, bool nt, hipStream_t st) {
-  const int R = fused_mlp_chunk(D);
-  const dim3 grid(p0.F / R);
-  MlpParams p = p0;
-  if (g_mlp_lab_noatomic) p.F = -p.F;
-#define FM_L(D_, R_, MT_) do { if (nt) hipLaunchKernelGGL((fused_mlp_kernel<D_, R_, MT_, true>), grid, dim3(256), 0, st, p); \
-                               else hipLaunchKernelGGL((fused_mlp_kernel<D_, R_, MT_, false>), grid, dim3(256), 0, st, p); } while (0)
-  if (D == 1024) {
-    if (p.M == 1) FM_L(1024, 16, 1); else FM_L(1024, 16, 4);
-  } else {
-    if (p.M == 1) FM_L(2048, 8, 1); else FM_L(2048, 8, 4);
-  }
-#undef FM_L
-}
 
 void launch_sample(const SampleParams& p, int wdt, int B, hipStream_t st) {
   if (p.V > 256 * SAMPLE_NPT) {
@@ -1599,33 +1324,6 @@ void launch_forced_ce(const float* c0, const float* ci, const int* forced, float
 void launch_advance(const AdvanceParams& p, hipStream_t st) {
   if (p.K > 64) throw CsmError(CSM_ERR_ARG, "advance: at most 64 codebooks");
   hipLaunchKernelGGL(advance_kernel, dim3(1), dim3(256), 0, st, p);
-}
-
-bool dec_attn_oproj_supported(const GemvParams& p, const AttnParams& a, int hd) {
-  // rows of one step (<= 2), <= 32 positions, 8 q heads of 128, o_proj K = 1024 (one G = 128 step)
-  return hd == 128 && p.M <= DA_M && a.S_cap <= 32 && a.Hq == DA_HQ && a.Hq * hd == DA_QD && p.K == DA_QD &&
-         p.N % 32 == 0 && a.mode == ATTN_CAUSAL;
-}
-
-static int g_da_rpt = [] { const char* e = getenv("CSM_DA_RPT"); return e ? atoi(e) : 4; }();
-
-void launch_dec_attn_oproj(const GemvParams& p0, const AttnParams& a, int wdt, hipStream_t st, int tag) {
-  GemvParams p = p0;
-  p.epi = EPI_ADD;
-  p.nw = nullptr;
-  const bool nt = (gemv_nt_mask() >> tag) & 1;
-  const int rpt = g_da_rpt == 2 ? 2 : (g_da_rpt == 8 ? 8 : 4);
-  const int blocks = p.N / (4 * rpt);
-#define DA_L(WT_, R_, T_) hipLaunchKernelGGL((dec_attn_oproj_kernel<WT_, R_, T_>), dim3(blocks), dim3(512), 0, st, p, a)
-#define DA_R(WT_, T_) do { if (rpt == 2) DA_L(WT_, 2, T_); else if (rpt == 8) DA_L(WT_, 8, T_); else DA_L(WT_, 4, T_); } while (0)
-  if (wdt == WDT_BF16) {
-    if (nt) DA_R(bf16_t, 5);
-    else DA_R(bf16_t, 1);
-  } else {
-    DA_R(float, 1);
-  }
-#undef DA_R
-#undef DA_L
 }
 
 // ============================================================================ stored-row reads

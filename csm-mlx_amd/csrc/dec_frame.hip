@@ -1110,9 +1110,8 @@ __device__ __forceinline__ void decoder_layer(Ctx& c, int l, int step, int pos0,
   if (FIRST && step > 1) {
     // q | k | v of input row proj_tab[step - 1][code] at position `step`, and the row itself; both
     // loads are in flight together, ahead of the down prefetch (vmcnt retires in issue order)
-    const int tr = c.w % p.tab_reps;  // table replica of this workgroup (fewer readers per row)
-    const float* t = p.qkv0_tabs[tr] + ((size_t)(step - 1) * p.V + c.code) * QKV;
-    const float* xr = p.proj_tabs[tr] + ((size_t)(step - 1) * p.V + c.code) * D;
+    const float* t = p.qkv0_tab + ((size_t)(step - 1) * p.V + c.code) * QKV;
+    const float* xr = p.proj_tab + ((size_t)(step - 1) * p.V + c.code) * D;
 #if DF_TAB16
     // DF_TAB16: the two rows as 16-B loads (640 float4: q|k|v 0..383, x 384..639; thread t takes
     // float4 t and, t < 128, float4 512 + t), one round trip, fewer load instructions

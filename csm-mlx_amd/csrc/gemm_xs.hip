@@ -12,7 +12,7 @@
 // K loop.  Lab (profiles/r03_lab_gemm_stream.txt): decoder gate/up at 32 rows 8.8 us against
 // 14.7 us for gemm_wide_kernel, QKV 3.3 against 10.4 (before the split-K combine).
 //
-// Block = 2 waves over one K slice (the slice's stages split between them, partial tiles added in a
+// Block = 4 waves (2 where K is short) over one K slice (the slice's stages split between them, partial tiles added in a
 // fixed order through LDS), 32 * RTW weight rows, 32 * MT batch rows.  Exactness as gemm_wide: the
 // activation parts are exact, products exact in fp32, fp32 accumulation; the RMSNorm row scale is
 // applied after the dot product (the producer multiplied the norm weight in before splitting).
@@ -34,7 +34,7 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(1))) unsigned int gu32;
 
 constexpr int XK = 64;                 // K per stage
-constexpr int XW = 2;                  // waves per block
+constexpr int XW_MAX = 4;              // waves per block: 2, or 4 where the grid would leave SIMDs idle
 constexpr int RSRC3 = 0x00020000;      // buffer descriptor word 3 (raw 32-bit format)
 constexpr int SC1 = 16;                // cache policy: sc1 (agent-coherent)
 constexpr int MAX_SLICES = 16;
@@ -82,7 +82,7 @@ __device__ __forceinline__ void combine(__amdgpu_buffer_rsrc_t rs, float (*ct)[N
   }
 }
 
-template <bool Q4, int MT, int RTW, int PD, bool NT>
+template <bool Q4, int MT, int RTW, int PD, bool NT, int XW>
 __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
   constexpr int NB = 32 * MT, NBR = 32 * RTW, NTH = 64 * XW;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -369,7 +369,7 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
 // Launch shape: RTW 2 (64-row tiles) for the wide and the long-K projections and for the heads (the
 // arg-max partial count then equals gemm_wide's 64-row tiles), else 1; K slices doubled until the grid
 // has >= 256 blocks while every wave keeps >= 1 stage; ring depth <= 4 stages (<= 2 at 64 rows).
-void xs_shape(int N, int K, int M, bool head, int& rtw, int& ks, int& pd) {
+void xs_shape(int N, int K, int M, bool head, int& rtw, int& ks, int& pd, int& xw) {
   const int nks = K / XK;
   // long-K projections (down) on 32-row tiles: twice the tiles, half the split-K slices and a quarter of
   // the partial bytes to combine -- 12.1 vs 16.7 us for the decoder down at 32 rows (tools/gemm_bench.py)
@@ -381,17 +381,25 @@ void xs_shape(int N, int K, int M, bool head, int& rtw, int& ks, int& pd) {
   static const int target = [] { const char* v = getenv("CSM_XS_BLOCKS"); return v ? atoi(v) : 256; }();
   static const int small_target = [] { const char* v = getenv("CSM_XS_SMALL_BLOCKS"); return v ? atoi(v) : 256; }();
   const int tgt = (N <= 2048 && K <= 2048 && !head) ? small_target : target;
+  // waves per block; the block's K slice is split between them.  4 (one per SIMD of the CU the block
+  // occupies) against 2: QKV 9.4 -> 7.2 us and o 8.0 -> 6.8 us at 32 bf16 rows, int4 gate/up 24.7 -> 16.1
+  // and down 20.6 -> 16.1 us at 64 rows; config 4 3667 -> 3816, config 5 3501 -> 4035 frames/s
+  // (profiles/r04_ab_xs_waves.txt).  Lab knob CSM_XS_WAVES=2 restores the two-wave blocks.
+  static const int waves = [] { const char* v = getenv("CSM_XS_WAVES"); return v && atoi(v) == 2 ? 2 : 4; }();
+  xw = nks >= 2 * waves ? waves : 2;
   ks = 1;
-  while (tiles * ks < tgt && ks < MAX_SLICES && nks / (ks * 2) >= XW && nks % (ks * 2) == 0) ks *= 2;
-  const int wst = nks / ks / XW;
-  const int cap = M > 32 ? (rtw == 2 ? 1 : 2) : 4;
+  while (tiles * ks < tgt && ks < MAX_SLICES && nks / (ks * 2) >= xw && nks % (ks * 2) == 0) ks *= 2;
+  const int wst = nks / ks / xw;
+  // ring depth at 64 rows with 64-row tiles (lab knob CSM_XS_PD64, default 1: register budget)
+  static const int cap64 = [] { const char* v = getenv("CSM_XS_PD64"); return v ? std::max(1, atoi(v)) : 1; }();
+  const int cap = M > 32 ? (rtw == 2 ? cap64 : 2) : 4;
   pd = 1;
   while (pd * 2 <= cap && wst % (pd * 2) == 0) pd *= 2;
 }
 
 size_t xs_need(int N, int K, int M, bool head, size_t& tk) {
-  int rtw, ks, pd;
-  xs_shape(N, K, M, head, rtw, ks, pd);
+  int rtw, ks, pd, xw;
+  xs_shape(N, K, M, head, rtw, ks, pd, xw);
   const size_t tiles = (N + 32 * rtw - 1) / (32 * rtw);
   tk = tiles;
   return ks > 1 ? tiles * ks * (size_t)(M > 32 ? 64 : 32) * 32 * rtw * 4 : 0;
@@ -400,19 +408,19 @@ size_t xs_need(int N, int K, int M, bool head, size_t& tk) {
 }  // namespace
 
 bool gemm_xs_eligible(int N, int K, int M, int wdt) {
-  if (!(wdt == WDT_BF16 || wdt == WDT_Q4) || M < 1 || M > GEMM_XS_MAX_M || N % 2 || K % XK || K / XK < XW) return false;
+  if (!(wdt == WDT_BF16 || wdt == WDT_Q4) || M < 1 || M > GEMM_XS_MAX_M || N % 2 || K % XK || K / XK < 2) return false;
   if (wdt == WDT_Q4)  // the X_g stage table holds <= Q4_WST_MAX stages per wave
     for (int h = 0; h < 2; ++h) {
-      int rtw, ks, pd;
-      xs_shape(N, K, M, h == 1, rtw, ks, pd);
-      if (K / XK / ks / XW > Q4_WST_MAX) return false;
+      int rtw, ks, pd, xw;
+      xs_shape(N, K, M, h == 1, rtw, ks, pd, xw);
+      if (K / XK / ks / xw > Q4_WST_MAX) return false;
     }
   return true;
 }
 
-int gemm_xs_tiles(int N, int K, int M) {
-  int rtw, ks, pd;
-  xs_shape(N, K, M, false, rtw, ks, pd);
+int gemm_xs_tiles(int N, int K, int M, bool head) {
+  int rtw, ks, pd, xw;
+  xs_shape(N, K, M, head, rtw, ks, pd, xw);
   return (N + 32 * rtw - 1) / (32 * rtw);
 }
 
@@ -452,7 +460,7 @@ void launch_gemm_xs(const GemvParams& p0, int epi, hipStream_t st, bool nt_w, in
     const auto ti = p.ws->tiled.find(p.W);
     if (ti != p.ws->tiled.end()) p.Wt = ti->second;
   }
-  if (!p.Wt || !p.xs_in || p.M > GEMM_XS_MAX_M || p.xacc || p.oacc || p.scale || (wdt == WDT_Q4 && !p.hs_in) ||
+  if (!p.Wt || !p.xs_in || p.M > GEMM_XS_MAX_M || p.scale || (wdt == WDT_Q4 && !p.hs_in) ||
       !gemm_xs_eligible(p.N, p.K, p.M, wdt)) {
     fprintf(stderr, "csm: gemm_xs launch without a tiled weight / split activations, or with an unsupported option (N=%d K=%d M=%d)\n",
             p.N, p.K, p.M);
@@ -461,8 +469,8 @@ void launch_gemm_xs(const GemvParams& p0, int epi, hipStream_t st, bool nt_w, in
   // 64-row tiles for the heads (arg-max partial count) and for SiLU*up producers (32 whole output
   // columns per tile: the int4 consumer's half-group sums never span two tiles)
   const bool head = epi == EPI_ARGMAX || epi == EPI_SILU_MUL;
-  int rtw, ks, pd;
-  xs_shape(p.N, p.K, p.M, head, rtw, ks, pd);
+  int rtw, ks, pd, xw;
+  xs_shape(p.N, p.K, p.M, head, rtw, ks, pd, xw);
   if (wdt == WDT_Q4 && rtw == 2 && pd > 2) pd = 2;  // the int4 fold's per-group products: a shorter ring (no spills)
   p.ksplit = ks;
   const int tiles = (p.N + 32 * rtw - 1) / (32 * rtw);
@@ -480,8 +488,9 @@ void launch_gemm_xs(const GemvParams& p0, int epi, hipStream_t st, bool nt_w, in
   // caches the decoder's weights are re-read from
   const bool nt = epi == EPI_ARGMAX || nt_w;
   const dim3 grid(tiles, ks);
-#define GX_K(Q_, MT_, RTW_, PD_) do { if (nt) hipLaunchKernelGGL((gemm_xs_kernel<Q_, MT_, RTW_, PD_, true>), grid, dim3(64 * XW), 0, st, p); \
-                                      else hipLaunchKernelGGL((gemm_xs_kernel<Q_, MT_, RTW_, PD_, false>), grid, dim3(64 * XW), 0, st, p); } while (0)
+#define GX_W(Q_, MT_, RTW_, PD_, NT_) do { if (xw == 4) hipLaunchKernelGGL((gemm_xs_kernel<Q_, MT_, RTW_, PD_, NT_, 4>), grid, dim3(256), 0, st, p); \
+                                             else hipLaunchKernelGGL((gemm_xs_kernel<Q_, MT_, RTW_, PD_, NT_, 2>), grid, dim3(128), 0, st, p); } while (0)
+#define GX_K(Q_, MT_, RTW_, PD_) do { if (nt) GX_W(Q_, MT_, RTW_, PD_, true); else GX_W(Q_, MT_, RTW_, PD_, false); } while (0)
 #define GX_P(Q_, MT_, RTW_) do { if (pd == 4) GX_K(Q_, MT_, RTW_, (MT_ == 1 ? 4 : 2)); else if (pd == 2) GX_K(Q_, MT_, RTW_, 2); \
                                  else GX_K(Q_, MT_, RTW_, 1); } while (0)
 #define GX_M(Q_) do { if (p.M > 32) { if (rtw == 2) GX_P(Q_, 2, 2); else GX_P(Q_, 2, 1); } \
@@ -491,4 +500,5 @@ void launch_gemm_xs(const GemvParams& p0, int epi, hipStream_t st, bool nt_w, in
 #undef GX_M
 #undef GX_P
 #undef GX_K
+#undef GX_W
 }

@@ -114,6 +114,14 @@ __device__ __forceinline__ void poll_granules(const u64* base, const int (&off)[
 // poll_granules over granule PAIRS: one 16-B sc1 load per pair (granules 2i, 2i + 1: their tags in
 // words 1 and 3), pair offsets in granules (even).  Same protocol and vmcnt discipline as
 // poll_granules (one probe, stale pairs re-polled); use(x) gets the u32x4 of every pair.
+// Tearing: correctness needs each naturally aligned 8-B half of a 16-B sc1 load (and of a producer's
+// 16-B sc1 store of two granules) to be seen whole, never a fresh tag beside a stale value.  The HIP /
+// HSA memory model promises that only for aligned atomics of <= 8 B; on gfx950 under ROCm 7.2 16-B
+// sc1 accesses are observed untorn at 8-B halves, not as an architectural guarantee
+// (/opt/skills/guides/MI355X_MICROARCH.md, inter-workgroup visibility: "R2's granule ... also for 16-B
+// sc1 halves").  The guard is the data: the 125-frame bf16 fixtures (tests/test_long_gpu.py) and the
+// determinism checks (tests/test_dec_frame_gpu.py) run every frame through these polls, and a torn
+// read would put a stale partial into a sum and change codes or logits.
 template <int GPP, int DELAY, int REPOLL, typename Fail, typename F>
 __device__ __forceinline__ void poll_pairs(const u64* base, int bytes, const int (&off)[GPP], unsigned tag, Fail&& fail, F&& use) {
   auto cur1 = [&](const u32x4_t& x) { return x.y == tag && x.w == tag; };

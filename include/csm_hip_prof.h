@@ -34,21 +34,19 @@ int csm_bench_dec_frame(csm_engine* e, int iters, float* avg_us, double* bytes);
  * engine does not run it (not batch-1 bf16 csm_1b shapes, or no frame run yet). */
 int csm_bench_bb_step(csm_engine* e, int iters, float* avg_us, double* bytes);
 
-/* Tuning / debug switches (re-capture the frame graphs): "fuse_attn" (decoder attention recomputed
- * inside the o_proj launch, default 0), "nt_mask" (bit t: non-temporal weight loads for stack tag
- * t, default 5), "gemv_xl" (decode GEMVs with LDS-staged activations, default 1), "fold_proj"
- * (decoder steps >= 2 gather projection(E_a[c]) from a table built at csm_begin, default 1),
- * "qkv0_tab" (decoder layer 0's q, k, v gathered from a table at steps >= 2, default 1),
- * "fuse_mlp" (one-launch MLP for <= 4 rows, default 0), "dec_frame" (batch-1 greedy bf16 frames on the
+/* Tuning / debug switches (re-capture the frame graphs), per engine: "fold_proj" (decoder steps >= 2
+ * gather projection(E_a[c]) from a table built at csm_begin, default 1), "qkv0_tab" (decoder layer 0's
+ * q, k, v gathered from a table at steps >= 2, default 1), "qkv0_tab_batched" (0: batched frames run
+ * layer 0's QKV projection instead, default 1), "dec_frame" (batch-1 greedy bf16 frames on the
  * persistent frame decoder, dec_frame.hip: codebook0_head + 31 decoder steps in one launch, default 1),
  * "bb_step" (batch-1 bf16 backbone rows on the persistent backbone step, bb_step.hip: 16 blocks + the
  * final norm in one launch, default 1), "dec_frame_stamps" / "bb_step_stamps" (per-hand-off clock
- * stamps of the persistent kernels, read back with csm_debug_read, default 0), "linear_mfma" (csm_linear runs the batched frame's MFMA GEMM at >= 8 rows instead of the GEMV,
- * default 0: the GEMM's kernel tests), "gemm_xs" (the batched depth decoder on the streaming
- * matrix-core GEMM, gemm_xs.hip, default 1), "bb_xs" (the batched backbone on it too, default 0),
- * "prefill_rows" (row cap of one csm_prefill_batch group, 0 = the engine's capacity), "tab_rep"
- * (1..8 copies of the folded proj_tab / qkv0_tab that the persistent frame decoder spreads its
- * workgroups over, default 1: 650 MB per extra copy on csm_1b). */
+ * stamps of the persistent kernels, read back with csm_debug_read, default 0), "linear_mfma" (csm_linear
+ * runs the batched frame's MFMA GEMM at >= 8 rows instead of the GEMV, default 0: the GEMM's kernel
+ * tests), "gemm_xs" (the batched depth decoder on the streaming matrix-core GEMM, gemm_xs.hip,
+ * default 1), "bb_xs" (the batched backbone on it too, default 0), "prefill_rows" (row cap of one
+ * csm_prefill_batch group, 0 = the engine's capacity), "inject_handoff_error" (test hook).
+ * Process-wide lab knobs are environment variables read once (CSM_NT_MASK, CSM_GEMV_XL, CSM_XS_*). */
 int csm_set_option(csm_engine* e, const char* key, int value);
 
 #ifdef __cplusplus

@@ -239,7 +239,12 @@ def filter_keep(logits: np.ndarray, top_k: int, top_p: float, min_p: float, min_
     Order for the sorts: lp descending, equal values by index ascending (ascending = its reverse).
     Sums are float32 (np.cumsum order); the GPU sums the same values in a parallel order, so a
     top_p boundary within float32 rounding of 1 - top_p may fall differently (never seen in tests).
-    If every entry is removed the arg-max is kept (mlx would sample from an all -inf row)."""
+    The same holds for min_p: lse (np.sum order here, a DPP / wave-ordered sum on the GPU) enters every
+    lp, so an entry within float32 rounding of the min_p threshold may be kept on one side only.
+    If every entry is removed the arg-max is kept (mlx would sample from an all -inf row).
+    Parity of this chain against mlx_lm itself is unpinned (mlx_lm is not importable here and the
+    reference holds no sampler fixture; its generate() samples with plain categorical,
+    generation.py:51-54)."""
     l = logits.astype(F32)
     n = l.shape[-1]
     keep = l >= topk_threshold(l, top_k)

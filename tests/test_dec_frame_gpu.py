@@ -101,31 +101,3 @@ def test_dec_frame_sampled_matches_launch_path_and_oracle(top_k):
     del model
 
 
-def test_dec_frame_table_replicas_identical():
-    """Option tab_rep (workgroup w reads copy w % n of the folded proj_tab / qkv0_tab rows): greedy and
-    temperature-only sampled codes (the per-workgroup Gumbel-max key path) identical with 1 and 4
-    copies, the copies rebuilt after the option changes, the persistent decoder running every frame."""
-    from csm_mlx import _lib
-    from csm_mlx.generation import generate_codes_batch
-    from csm_mlx.models import CSM
-    from csm_mlx.sampling import Sampler
-    from csm_mlx.tokenizers import tokenize_text_segment
-    args, w = csm_weights("1b")
-    model = CSM(args, dtype="bf16")
-    model.load_weights(w)
-    L = _lib.lib()
-    prompt = tokenize_text_segment(prompt_ids(7), 0, 32)
-    out = {}
-    for smp in (Sampler(0.0, 0), Sampler(0.8, 0)):
-        for rep in (1, 4, 1):
-            _lib.check(L.csm_set_option(model.engine, b"tab_rep", rep))
-            ep0 = np.zeros(1, np.uint32)
-            _lib.check(L.csm_debug_read(model.engine, b"dec_frame_epoch", _lib.ptr(ep0), 4, None))
-            h, n, _ = generate_codes_batch(model, [prompt], 6, sampler=smp, seeds=[99])
-            ep1 = np.zeros(1, np.uint32)
-            _lib.check(L.csm_debug_read(model.engine, b"dec_frame_epoch", _lib.ptr(ep1), 4, None))
-            assert int(ep1[0]) - int(ep0[0]) == 6 * 498, f"tab_rep {rep}: the persistent decoder did not run"
-            out.setdefault(smp.temp, []).append(h[: n[0], 0].copy())
-    for t, runs in out.items():
-        assert all(np.array_equal(r, runs[0]) for r in runs), f"temperature {t}: codes differ across table replicas"
-    _lib.check(L.csm_set_option(model.engine, b"tab_rep", 1))

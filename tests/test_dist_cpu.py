@@ -60,14 +60,14 @@ def _gather_worker(rank, world, port, q):
     # ragged per-utterance results: utterance g has g % 4 + 1 frames (one stopped at EOS early)
     codes = [np.full((g % 4 + 1, 5), g, np.int32) + np.arange(5, dtype=np.int32) for g in mine]
     pcm = [np.linspace(g, g + 1, (g % 4 + 1) * 8, dtype=np.float32) for g in mine]
-    c_all, p_all = gather_results(codes, pcm, max_frames=6, frame_samples=8)
-    c_only, none = gather_results(codes, None, max_frames=6, frame_samples=8)
+    c_all, p_all = gather_results(codes, pcm, max_frames=6, frame_samples=8, dst=None)
+    c_only, none = gather_results(codes, None, max_frames=6, frame_samples=8, dst=None)
     q.put((rank, c_all, p_all, c_only, none))
     dist.destroy_process_group()
 
 
 def test_gather_results_world2():
-    """csm_mlx.dist.gather_results over gloo: every rank receives every utterance's codes and PCM in
+    """csm_mlx.dist.gather_results(dst=None) over gloo: every rank receives every utterance's codes and PCM in
     global order with its own length (ragged, padded in transit)."""
     import numpy as np
     ctx = mp.get_context("spawn")
@@ -96,3 +96,81 @@ def test_shard_rejects_uneven_batch():
     assert shard(256, 8, 7) == list(range(224, 256))
     with pytest.raises(ValueError):
         shard(10, 4, 0)
+
+
+def _bench_mod():
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "csm-mlx_amd"), root]
+    import bench
+    return bench
+
+
+def test_bench_self_launch_argv():
+    """``python bench.py --gpus N`` without a launcher starts torch.distributed.run with N ranks on
+    127.0.0.1 as a child, passing its own arguments through unchanged."""
+    import sys
+    bench = _bench_mod()
+    assert bench.resolve_world(None, {}) == (1, False)
+    assert bench.resolve_world(1, {}) == (1, False)
+    assert bench.resolve_world(8, {}) == (8, True)
+    argv = ["--gpus", "8", "--steps", "3", "--warmup", "1"]
+    cmd = bench.launcher_argv(argv, 8, 29512)
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=8" in cmd and "--nnodes=1" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1" and cmd[cmd.index("--master-port") + 1] == "29512"
+    assert cmd[-len(argv) - 1].endswith("bench.py") and cmd[-len(argv):] == argv
+
+
+def test_bench_world_size_mismatch_refused():
+    """Under a launcher, WORLD_SIZE decides; an explicit --gpus that disagrees exits non-zero before
+    anything touches a GPU."""
+    import subprocess
+    import sys
+    bench = _bench_mod()
+    assert bench.resolve_world(None, {"WORLD_SIZE": "4"}) == (4, False)
+    assert bench.resolve_world(4, {"WORLD_SIZE": "4"}) == (4, False)
+    with pytest.raises(SystemExit):
+        bench.resolve_world(8, {"WORLD_SIZE": "4"})
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "4"], cwd=root, env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr
+
+
+def _gather0_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "csm-mlx_amd"), root]
+    import numpy as np
+    import torch.distributed as dist
+    from csm_mlx.dist import gather_results, shard
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    mine = shard(2 * world, world, rank)
+    codes = [np.full((g % 3 + 1, 4), g, np.int32) for g in mine]
+    pcm = [np.full((g % 3 + 1) * 8, g, np.float32) for g in mine]
+    q.put((rank, *gather_results(codes, pcm, max_frames=4, frame_samples=8)))   # default: to rank 0
+    dist.destroy_process_group()
+
+
+def test_gather_results_to_rank0_world3():
+    """The bench's result collection: one gather per kind to rank 0; the other ranks get nothing back."""
+    import numpy as np
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_gather0_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=120) for _ in ps], key=lambda r: r[0])
+    for p in ps:
+        p.join(60)
+    _, c_all, p_all = res[0]
+    assert len(c_all) == len(p_all) == 6
+    for g in range(6):
+        assert np.array_equal(c_all[g], np.full((g % 3 + 1, 4), g, np.int32))
+        assert np.array_equal(p_all[g], np.full((g % 3 + 1) * 8, g, np.float32))
+    for _, c, p in res[1:]:
+        assert c is None and p is None

@@ -166,7 +166,7 @@ def test_csm_1b_bf16_batch_composition_invariance():
         assert np.abs(a - b).max() <= 2e-3 * np.abs(a).max()
 
 
-@pytest.mark.parametrize("B,dtype,bb", [(8, "bf16", 0), (24, "bf16", 0), (24, "q4", 0), (24, "bf16", 1)])
+@pytest.mark.parametrize("B,dtype,bb", [(8, "bf16", 0), (24, "bf16", 0), (24, "q4", 0), (24, "bf16", 1), (24, "q4", 1)])
 def test_streaming_decoder_matches_wide_gemm(B, dtype, bb):
     """The batched depth decoder at codebook steps >= 2 on the streaming matrix-core GEMM over
     pre-split activations (gemm_xs.hip; option gemm_xs, on by default) against the same frames on
