@@ -1778,10 +1778,12 @@ int csm_bench_gemv(csm_engine* e, int which, int M, int iters, float* avg_us, do
     hipEvent_t a, b;
     HIPCHK(hipEventCreate(&a));
     HIPCHK(hipEventCreate(&b));
+    if (xsb) gemm_xs_stamps_report("warm");  // lab builds: clears the stamps of the warm-up launches
     HIPCHK(hipEventRecord(a, e->st));
     for (int i = 0; i < iters; ++i) run1(i);
     HIPCHK(hipEventRecord(b, e->st));
     HIPCHK(hipEventSynchronize(b));
+    if (xsb) gemm_xs_stamps_report((std::string(stack ? "dec" : "bb") + " kind " + std::to_string(kind) + " M " + std::to_string(M)).c_str());
     float ms = 0.f;
     HIPCHK(hipEventElapsedTime(&ms, a, b));
     (void)hipEventDestroy(a);

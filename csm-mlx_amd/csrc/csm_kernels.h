@@ -55,6 +55,7 @@ struct GemvParams {
   float* qkv_tab;       // EPI_QKV table build: rows [M][(Hq + 2 Hkv) hd] instead of q / KV cache
   // MFMA path split-K (set by launch_gemm_mfma from ws): slice partials [ksplit][M][N], sum-of-squares [ksplit][M]
   GemmWs* ws;            // the calling engine's scratch (host pointer; required for split launches)
+  unsigned lab_launch;   // lab builds of gemm_xs (XS_STAMPS): launch index for the phase stamps
   const void* Wt;        // the weight's fragment-tiled copy (looked up in ws->tiled by launch_gemm_mfma)
   float* kpart;          // [tile][m chunk][slice][slab] split-K slice partials (+ sum x^2), written sc1
   unsigned* kticket;     // [tile][m chunk] arrival tickets (zero between launches)
@@ -329,6 +330,7 @@ bool gemm_xs_eligible(int N, int K, int M, int wdt);
 int gemm_xs_tiles(int N, int K, int M, bool head = false);
 void launch_gemm_xs(const GemvParams& p, int epi, hipStream_t st, bool nt = false, int wdt = WDT_BF16);
 bool gemm_xs_reserve(GemmWs& ws, int N, int K, int M);
+void gemm_xs_stamps_report(const char* tag);  // lab builds (-DXS_STAMPS=1): phase breakdown to stderr
 // Fragment-tiled weight copy for the MFMA path: per 32-row tile and 64-K stage, the bytes each lane
 // of a wave loads for v_mfma_f32_32x32x16_bf16's B operand, contiguous (bf16: 4 KB = 4 steps x 64
 // lanes x 16 B; int4: 1 KB of nibbles, then a [tile][stage][32] block of scale|bias words); rows

@@ -82,14 +82,49 @@ __device__ __forceinline__ void combine(__amdgpu_buffer_rsrc_t rs, float (*ct)[N
   }
 }
 
+// Lab build only (tools/variant.sh -DXS_STAMPS=1): per-block clock stamps of the phases, 100 MHz
+// s_memrealtime, for the first XS_ST_BLOCKS blocks of every launch, reported by gemm_xs_stamps_report.
+#ifndef XS_STAMPS
+#define XS_STAMPS 0
+#endif
+constexpr int XS_ST_N = 8, XS_ST_BLOCKS = 1024, XS_ST_LAUNCHES = 64;
+__device__ unsigned long long g_xs_st[XS_ST_LAUNCHES][XS_ST_BLOCKS][XS_ST_N];
+__device__ unsigned g_xs_launch;
+#define XS_STAMP(k) do { if constexpr (XS_STAMPS != 0) { if (threadIdx.x == 0) { \
+    const unsigned bl = blockIdx.x + gridDim.x * blockIdx.y, ln = p.lab_launch % XS_ST_LAUNCHES; \
+    if (bl < XS_ST_BLOCKS) g_xs_st[ln][bl][k] = __builtin_amdgcn_s_memrealtime(); } } } while (0)
+
 template <bool Q4, int MT, int RTW, int PD, bool NT, int XW>
 __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
+  XS_STAMP(0);
   constexpr int NB = 32 * MT, NBR = 32 * RTW, NTH = 64 * XW;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int tile = blockIdx.x, n0 = tile * NBR;
+  // XCD-aware placement.  Blocks are dealt round-robin over the 8 XCDs (linear id % 8 share one L2;
+  // MI355X_MICROARCH.md: observed, speed only), and the split operand of K slice s is read by every
+  // block of slice s: with tile-major ids every XCD held every slice, so each slice crossed into all 8
+  // L2s (the decoder down at 64 rows fetched 25 MB of its 3 MB operand, r4 config-5 PMC pass).  Here the
+  // blocks of one XCD take the same slice(s) -- slices >= 8: XCD x owns slices [x S/8, (x+1) S/8); fewer:
+  // 8/S XCDs share a slice and split its tiles.  Same (tile, slice) work items, same combine order.
+  int tile = blockIdx.x, slice = blockIdx.y;
+  {
+    const int T = gridDim.x, S = gridDim.y, L = blockIdx.x + T * blockIdx.y, xcd = L & 7, j = L >> 3;
+#ifndef XCD_MAP
+#define XCD_MAP 1  // lab: -DXCD_MAP=0 restores the tile-major placement (A/B)
+#endif
+    if (XCD_MAP && (T * S) % 8 == 0) {
+      if (S % 8 == 0) {
+        slice = xcd * (S / 8) + j / T;
+        tile = j % T;
+      } else if (8 % S == 0 && T % (8 / S) == 0) {
+        slice = xcd % S;
+        tile = (xcd / S) * (T / (8 / S)) + j;
+      }
+    }
+  }
+  const int n0 = tile * NBR;
   const int nks = p.K / XK, nt32 = (p.N + 31) / 32;
-  const int ks = p.ksplit, nst = nks / ks, wst = nst / XW, ws0 = blockIdx.y * nst + wave * wst;
+  const int ks = p.ksplit, nst = nks / ks, wst = nst / XW, ws0 = slice * nst + wave * wst;
   const __amdgpu_buffer_rsrc_t wrs = rsrc(p.Wt, 0x7fffffff), ars = rsrc(p.xs_in, 0x7fffffff), zrs = rsrc(p.Wt, 0);
   int wv[RTW], sv[RTW];
 #pragma unroll
@@ -102,7 +137,7 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
   if constexpr (Q4) {  // X_g of this block's stages: the two half-group sums, in order
     for (int e = tid; e < XW * wst * NB; e += NTH) {
       const int w = e / (wst * NB), j = (e / NB) % wst, m = e % NB;
-      const int st = blockIdx.y * nst + w * wst + j;
+      const int st = slice * nst + w * wst + j;
       xg[w][j][m] = p.hs_in[(size_t)(2 * st) * xs::HS_ROWS + m] + p.hs_in[(size_t)(2 * st + 1) * xs::HS_ROWS + m];
     }
     __syncthreads();
@@ -116,7 +151,12 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
   auto load = [&](int j, St& g) {
     const bool live = j < wst;
     const int st = ws0 + (live ? j : 0);
-    const __amdgpu_buffer_rsrc_t wr = live ? wrs : zrs, ar = live ? ars : zrs;
+#ifndef XS_LAB
+#define XS_LAB 0  // lab ablations (tools/variant.sh -DXS_LAB=bits, results invalid): 1 no MFMA, 2 no activation
+                  // traffic, 4 no weight traffic, 8 no split-K exchange / epilogue, 16 stop after the waves'
+                  // reduction
+#endif
+    const __amdgpu_buffer_rsrc_t wr = (live && !(XS_LAB & 4)) ? wrs : zrs, ar = (live && !(XS_LAB & 2)) ? ars : zrs;
 #pragma unroll
     for (int i = 0; i < RTW; ++i) {
       if constexpr (Q4) {
@@ -174,6 +214,7 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
 #pragma unroll
   for (int d = 0; d < PD; ++d) load(d, g[d]);
   asm volatile("" ::: "memory");  // the ring's loads stay where they are issued (no sinking to their use)
+  XS_STAMP(1);
   const int hrow = 4 * (lane >> 5);  // int4 fold: lane (r, h) register jj holds batch row (jj & 3) + 8 (jj >> 2) + 4 h
   for (int j0 = 0; j0 < wst; j0 += PD) {
 #pragma unroll
@@ -216,6 +257,16 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
             }
           }
         }
+      } else if constexpr ((XS_LAB & 1) != 0) {  // lab: operands consumed by one VALU op each, no MFMA
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+#pragma unroll
+          for (int q = 0; q < 3; ++q)
+#pragma unroll
+            for (int t = 0; t < MT; ++t) acc[t][0][s] += __uint_as_float(g[d].a[t][q][s].x ^ g[d].a[t][q][s].w);
+#pragma unroll
+          for (int i = 0; i < RTW; ++i) acc[0][i][4 + s] += __uint_as_float(g[d].w[i][s].y ^ g[d].w[i][s].z);
+        }
       } else {
 #pragma unroll
         for (int s = 0; s < 4; ++s)
@@ -240,7 +291,19 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
   __shared__ float rsc[NB];
   __shared__ float pss[NB][NBR / 8 + 1], phs[NB][NBR / 8 + 1];  // producer: 8-column partial sums
   __shared__ int last;
+  XS_STAMP(2);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the LDS-DMA prefetch too; the barrier below publishes it)
+  if constexpr ((XS_LAB & 8) != 0) {  // lab: the K loop alone (one store keeps it live)
+    float v = 0.f;
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+      for (int i = 0; i < RTW; ++i)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v += acc[t][i][j];
+    if (v == 1.2345f) p.out[tid] = v;
+    return;
+  }
 #pragma unroll
   for (int t = 0; t < MT; ++t)
 #pragma unroll
@@ -257,12 +320,17 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
     ct[ml][c] = v;
   }
   __syncthreads();
+  XS_STAMP(3);
+  if constexpr ((XS_LAB & 16) != 0) {  // lab: stop after the waves' reduction (no exchange, no epilogue)
+    if (ct[tid & 31][0] == 1.2345f) p.out[tid] = 0.f;
+    return;
+  }
   if (ks > 1) {
     // slice partial [NB][NBR] write-through, ticket; the last slice to arrive sums all in slice order
     const int slab_f = NB * NBR;
     float* slab = p.kpart + (size_t)tile * ks * slab_f;
     const __amdgpu_buffer_rsrc_t rs = rsrc(slab, ks * slab_f * 4);
-    const int mine = blockIdx.y * slab_f * 4;
+    const int mine = slice * slab_f * 4;
     for (int q = tid; q < mrows * (NBR / 4); q += NTH) {
       const int ml = q / (NBR / 4), j = (q % (NBR / 4)) * 4;
       const f32x4_t v = {ct[ml][j], ct[ml][j + 1], ct[ml][j + 2], ct[ml][j + 3]};
@@ -270,6 +338,7 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    XS_STAMP(4);
     if (tid == 0) {
       gu32* tk = (gu32*)p.kticket + tile;
       const unsigned old = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -277,6 +346,7 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
       if (last) __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
     }
     __syncthreads();
+    XS_STAMP(5);
     if (!last) return;
     switch (ks) {
       case 2: combine<2, NB, NBR, NTH>(rs, ct, mrows, slab_f, tid); break;
@@ -285,6 +355,7 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
       default: combine<16, NB, NBR, NTH>(rs, ct, mrows, slab_f, tid); break;
     }
     __syncthreads();
+    XS_STAMP(6);
   }
   // ---- epilogue
   if (norm && tid < mrows) {
@@ -364,6 +435,11 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
     }
     p.part[(size_t)tid * p.part_stride + tile] = best;
   }
+  if constexpr (XS_STAMPS != 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    XS_STAMP(7);
+  }
 }
 
 // Launch shape: RTW 2 (64-row tiles) for the wide and the long-K projections and for the heads (the
@@ -406,6 +482,34 @@ size_t xs_need(int N, int K, int M, bool head, size_t& tk) {
 }
 
 }  // namespace
+
+// Lab (XS_STAMPS builds): mean phase durations over the recorded launches, per launch shape, to stderr.
+// Phases: 0 start, 1 ring issued, 2 K loop done, 3 waves reduced, 4 partial published, 5 ticket taken,
+// 6 combined (last slice), 7 end.  No-op in product builds.
+void gemm_xs_stamps_report(const char* tag) {
+  if constexpr (XS_STAMPS == 0) {
+    (void)tag;
+  } else {
+    static unsigned long long h[XS_ST_LAUNCHES][XS_ST_BLOCKS][XS_ST_N];
+    if (hipDeviceSynchronize() != hipSuccess || hipMemcpyFromSymbol(h, HIP_SYMBOL(g_xs_st), sizeof(h)) != hipSuccess) return;
+    double sum[XS_ST_N] = {0};
+    double cnt[XS_ST_N] = {0};
+    for (int l = 0; l < XS_ST_LAUNCHES; ++l) {
+      unsigned long long t0 = ~0ull;
+      for (int b = 0; b < XS_ST_BLOCKS; ++b)
+        if (h[l][b][0]) t0 = std::min(t0, h[l][b][0]);
+      if (t0 == ~0ull) continue;
+      for (int b = 0; b < XS_ST_BLOCKS; ++b)
+        for (int k = 0; k < XS_ST_N; ++k)
+          if (h[l][b][k] >= t0 && h[l][b][0]) { sum[k] += (double)(h[l][b][k] - t0) * 0.01; cnt[k] += 1; }
+    }
+    fprintf(stderr, "xs_stamps %s (us after the launch's first block start, mean over blocks):", tag);
+    for (int k = 0; k < XS_ST_N; ++k) fprintf(stderr, " %d:%.2f(%d)", k, cnt[k] ? sum[k] / cnt[k] : -1.0, (int)cnt[k]);
+    fprintf(stderr, "\n");
+    static unsigned long long z[XS_ST_LAUNCHES][XS_ST_BLOCKS][XS_ST_N];
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_xs_st), z, sizeof(z));
+  }
+}
 
 bool gemm_xs_eligible(int N, int K, int M, int wdt) {
   if (!(wdt == WDT_BF16 || wdt == WDT_Q4) || M < 1 || M > GEMM_XS_MAX_M || N % 2 || K % XK || K / XK < 2) return false;
@@ -488,6 +592,10 @@ void launch_gemm_xs(const GemvParams& p0, int epi, hipStream_t st, bool nt_w, in
   // caches the decoder's weights are re-read from
   const bool nt = epi == EPI_ARGMAX || nt_w;
   const dim3 grid(tiles, ks);
+  if constexpr (XS_STAMPS != 0) {
+    static unsigned n = 0;
+    p.lab_launch = n++;
+  }
 #define GX_W(Q_, MT_, RTW_, PD_, NT_) do { if (xw == 4) hipLaunchKernelGGL((gemm_xs_kernel<Q_, MT_, RTW_, PD_, NT_, 4>), grid, dim3(256), 0, st, p); \
                                              else hipLaunchKernelGGL((gemm_xs_kernel<Q_, MT_, RTW_, PD_, NT_, 2>), grid, dim3(128), 0, st, p); } while (0)
 #define GX_K(Q_, MT_, RTW_, PD_) do { if (nt) GX_W(Q_, MT_, RTW_, PD_, true); else GX_W(Q_, MT_, RTW_, PD_, false); } while (0)

@@ -78,6 +78,7 @@ struct mimi_codec {
   // workspace (grown on demand)
   size_t ws_big = 0, ws_rows = 0;
   float *W0 = nullptr, *W1 = nullptr, *H = nullptr;
+  float* ks_ws = nullptr;  // split-K scratch of the codec GEMMs (MIMI_KS_WS_FLOATS, mimi_kernels.h)
   float *R = nullptr, *Rh = nullptr, *Rqkv = nullptr, *Rq = nullptr, *Ratt = nullptr, *Rf = nullptr;
   int* dcodes = nullptr;
   size_t dcodes_n = 0;
@@ -304,6 +305,7 @@ void run_transformer(mimi_codec* m, std::vector<MTLayer>& T, std::vector<float*>
     MTLayer& L = T[l];
     launch_layernorm_rows(m->R, D, L.n1w, L.n1b, d.norm_eps, m->Rh, M, st);
     LinParams lp{};
+    lp.ks_ws = m->ks_ws;
     lp.x = m->Rh; lp.M = M; lp.K = D; lp.xs = D; lp.W = L.in_w; lp.N = 3 * D; lp.out = m->Rqkv; lp.os = 3 * D;
     lp.epi = EPI_STORE;
     launch_linear(lp, st);
@@ -314,15 +316,18 @@ void run_transformer(mimi_codec* m, std::vector<MTLayer>& T, std::vector<float*>
     a.mode = d.attn_mode == 0 ? ATTN_BLOCK : ATTN_WINDOW;
     launch_attn(a, hd, st);
     lp = LinParams{};
+    lp.ks_ws = m->ks_ws;
     lp.x = m->Ratt; lp.M = M; lp.K = D; lp.xs = D; lp.W = L.out_w; lp.N = D; lp.out = m->R; lp.os = D;
     lp.epi = EPI_ADD; lp.scale = L.ls1;
     launch_linear(lp, st);
     launch_layernorm_rows(m->R, D, L.n2w, L.n2b, d.norm_eps, m->Rh, M, st);
     lp = LinParams{};
+    lp.ks_ws = m->ks_ws;
     lp.x = m->Rh; lp.M = M; lp.K = D; lp.xs = D; lp.W = L.l1; lp.N = F; lp.out = m->Rf; lp.os = F;
     lp.epi = EPI_GELU; lp.gelu_erf = d.gelu_erf;
     launch_linear(lp, st);
     lp = LinParams{};
+    lp.ks_ws = m->ks_ws;
     lp.x = m->Rf; lp.M = M; lp.K = F; lp.xs = F; lp.W = L.l2; lp.N = D; lp.out = m->R; lp.os = D;
     lp.epi = EPI_ADD; lp.scale = L.ls2;
     launch_linear(lp, st);
@@ -345,6 +350,7 @@ void run_window_op(mimi_codec* m, const MOp& o, const float* in, int cs_in, int 
   if (o.kind == 0) {
     const MConv& c = m->convs[o.idx];
     ConvParams p{};
+    p.ks_ws = m->ks_ws;
     p.x = in; p.Cin = c.cin; p.Tin = P + n; p.x_bstride = c.cin * cs_in; p.x_cstride = cs_in; p.x_off = 0;
     p.w = c.w; p.bias = c.b; p.Cout = c.cout; p.k = c.k; p.stride = 1; p.dil = c.dil; p.pad_l = 0;
     p.replicate = 0; p.elu_in = c.elu; p.y = out; p.Tout = n; p.y_bstride = c.cout * cs_out; p.y_cstride = cs_out;
@@ -353,18 +359,21 @@ void run_window_op(mimi_codec* m, const MOp& o, const float* in, int cs_in, int 
   } else if (o.kind == 1) {
     const MConvTr& t = m->convtrs[o.idx];
     ConvTrParams p{};
+    p.ks_ws = m->ks_ws;
     p.x = in; p.Cin = t.cin; p.Tin = P + n; p.x_bstride = t.cin * cs_in; p.x_cstride = cs_in; p.x_off = 0;
     p.wt = t.wt; p.bias = t.b; p.Cout = t.cout; p.s = t.s; p.elu_in = t.elu; p.t_in0 = P; p.n_in = n; p.y = out;
     p.y_bstride = t.cout * cs_out; p.y_cstride = cs_out; p.y_off = P_next; p.B = B;
     launch_convtr(p, st);
   } else {
     const MRes& r = m->res[o.idx];
-    ConvParams p{};  // block.1: ELU -> conv(k, ch -> hid) over the window
+    ConvParams p{};
+    p.ks_ws = m->ks_ws;  // block.1: ELU -> conv(k, ch -> hid) over the window
     p.x = in; p.Cin = r.ch; p.Tin = P + n; p.x_bstride = r.ch * cs_in; p.x_cstride = cs_in; p.x_off = 0;
     p.w = r.c1.w; p.bias = r.c1.b; p.Cout = r.hid; p.k = r.k; p.stride = 1; p.dil = r.dil; p.pad_l = 0;
     p.elu_in = 1; p.y = m->H; p.Tout = n; p.y_bstride = r.hid * n; p.y_cstride = n; p.y_off = 0; p.B = B;
     launch_conv1d(p, st);
-    ConvParams q{};  // block.3: ELU -> conv(1, hid -> ch) + identity skip (true_skip)
+    ConvParams q{};
+    q.ks_ws = m->ks_ws;  // block.3: ELU -> conv(1, hid -> ch) + identity skip (true_skip)
     q.x = m->H; q.Cin = r.hid; q.Tin = n; q.x_bstride = r.hid * n; q.x_cstride = n; q.x_off = 0;
     q.w = r.c2.w; q.bias = r.c2.b; q.Cout = r.ch; q.k = 1; q.stride = 1; q.dil = 1; q.pad_l = 0; q.elu_in = 1;
     q.y = out; q.Tout = n; q.y_bstride = r.ch * cs_out; q.y_cstride = cs_out; q.y_off = P_next;
@@ -461,6 +470,7 @@ int mimi_create(const mimi_dims* dims, int device, int max_batch, int max_frames
       m->hist.push_back(P > 0 ? (float*)m->alloc((size_t)max_batch * m->op_cin(o) * P * 4) : nullptr);
     }
     m->up_hist = (float*)m->alloc((size_t)max_batch * dims->dimension * 4);
+    m->ks_ws = (float*)m->alloc(MIMI_KS_WS_FLOATS * 4);
     HIPCHK(hipDeviceSynchronize());
     *out = m.release();
   }
@@ -563,6 +573,7 @@ int mimi_encode(mimi_codec* m, int B, int N, const float* pcm, int32_t* codes, i
         const int k_eff = (c.k - 1) * c.dil + 1;
         const int64_t Tout = lens[i + 1];
         ConvParams p{};
+        p.ks_ws = m->ks_ws;
         p.x = in; p.Cin = c.cin; p.Tin = (int)Tin; p.x_bstride = c.cin * (int)Tin; p.x_cstride = (int)Tin;
         p.w = c.w; p.bias = c.b; p.Cout = c.cout; p.k = c.k; p.stride = c.stride; p.dil = c.dil;
         p.pad_l = k_eff - c.stride; p.elu_in = c.elu; p.y = out; p.Tout = (int)Tout;
@@ -572,12 +583,14 @@ int mimi_encode(mimi_codec* m, int B, int N, const float* pcm, int32_t* codes, i
       } else {  // resblock on the full sequence (causal, zero left pad)
         const MRes& r = m->res[o.idx];
         ConvParams p{};
+        p.ks_ws = m->ks_ws;
         p.x = in; p.Cin = r.ch; p.Tin = (int)Tin; p.x_bstride = r.ch * (int)Tin; p.x_cstride = (int)Tin;
         p.w = r.c1.w; p.bias = r.c1.b; p.Cout = r.hid; p.k = r.k; p.stride = 1; p.dil = r.dil;
         p.pad_l = (r.k - 1) * r.dil; p.elu_in = 1; p.y = m->H; p.Tout = (int)Tin; p.y_bstride = r.hid * (int)Tin;
         p.y_cstride = (int)Tin; p.B = B;
         launch_conv1d(p, st);
         ConvParams q{};
+        q.ks_ws = m->ks_ws;
         q.x = m->H; q.Cin = r.hid; q.Tin = (int)Tin; q.x_bstride = r.hid * (int)Tin; q.x_cstride = (int)Tin;
         q.w = r.c2.w; q.bias = r.c2.b; q.Cout = r.ch; q.k = 1; q.stride = 1; q.dil = 1; q.elu_in = 1; q.y = out;
         q.Tout = (int)Tin; q.y_bstride = r.ch * (int)Tin; q.y_cstride = (int)Tin; q.resid = in;
@@ -595,6 +608,7 @@ int mimi_encode(mimi_codec* m, int B, int N, const float* pcm, int32_t* codes, i
     // downsample: k = 2s, stride s, replicate pad, no bias
     {
       ConvParams p{};
+      p.ks_ws = m->ks_ws;
       p.x = bufs[cur]; p.Cin = D; p.Tin = (int)T25; p.x_bstride = D * (int)T25; p.x_cstride = (int)T25;
       p.w = m->down_w; p.Cout = D; p.k = 2 * s; p.stride = s; p.dil = 1; p.pad_l = s; p.replicate = 1;
       p.y = bufs[cur ^ 1]; p.Tout = (int)Tf; p.y_bstride = D * (int)Tf; p.y_cstride = (int)Tf; p.B = B;
@@ -607,6 +621,7 @@ int mimi_encode(mimi_codec* m, int B, int N, const float* pcm, int32_t* codes, i
     grow(m->dcodes, m->dcodes_n, (size_t)B * d.n_q * Tf);
     for (int q = 0; q < 2; ++q) {
       LinParams lp{};
+      lp.ks_ws = m->ks_ws;
       lp.x = m->R; lp.M = M; lp.K = D; lp.xs = D; lp.W = m->rvq_in[q]; lp.N = cd; lp.out = m->Rh; lp.os = cd;
       lp.epi = EPI_STORE;
       launch_linear(lp, st);
@@ -630,6 +645,7 @@ static void decode_frames(mimi_codec* m, int B, int F, const int32_t* dcodes, in
   // RVQ decode: semantic + acoustic gathers, output projections summed into conv layout [B][D][F]
   launch_rvq_gather(dcodes, layout, B, F, d.n_q, 0, 1, m->cb, d.bins, cd, m->Rh, st);
   LinParams lp{};
+  lp.ks_ws = m->ks_ws;
   lp.x = m->Rh; lp.M = M; lp.K = cd; lp.xs = cd; lp.W = m->rvq_out[0]; lp.N = D; lp.conv_T = F;
   lp.conv_bstride = D * F; lp.out = m->W1; lp.accumulate = 0;
   launch_linear(lp, st);

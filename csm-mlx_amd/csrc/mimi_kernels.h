@@ -2,6 +2,12 @@
 #pragma once
 #include "csm_kernels.h"
 
+// Split-K scratch of the codec GEMMs (one per codec, mimi_create): partial tiles of up to 512 blocks of
+// 64 x 64 (launches with fewer than 512 blocks split K until they reach it: the streaming decode_step's
+// short-time, wide-channel convs and its 64-row transformer linears), summed in slice order by a
+// second kernel that runs the problem's epilogue.  Null: no split.
+constexpr size_t MIMI_KS_WS_FLOATS = (size_t)512 * 64 * 64;
+
 // Causal Conv1d as implicit GEMM: y[b][co][t] = bias[co] + sum_{ci,j} w[co][ci][j] * act(xv(b,ci,t*stride+j*dil-pad_l))
 // xv outside [0, Tin) is 0 (constant pad) or the edge sample (replicate pad); act = ELU when elu_in.
 struct ConvParams {
@@ -16,6 +22,7 @@ struct ConvParams {
   const float* resid;              // optional, same layout as y (added after bias)
   int r_bstride, r_cstride, r_off;
   int B;
+  float* ks_ws;                    // split-K scratch (MIMI_KS_WS_FLOATS) or null
 };
 
 // ConvTranspose1d with k = 2*s (every Mimi transposed conv): per output phase r = t % s,
@@ -30,6 +37,7 @@ struct ConvTrParams {
   float* y;
   int y_bstride, y_cstride, y_off;
   int B;
+  float* ks_ws;                    // split-K scratch (MIMI_KS_WS_FLOATS) or null
 };
 
 // Row-major linear: out[m][n] = epi( sum_k x[m][k] * W[n][k] )
@@ -47,6 +55,7 @@ struct LinParams {
   int conv_T;       // 0 = row-major store
   int conv_bstride;
   int accumulate;   // conv store: add into existing values
+  float* ks_ws;     // split-K scratch (MIMI_KS_WS_FLOATS) or null
 };
 
 void launch_conv1d(const ConvParams& p, hipStream_t st);

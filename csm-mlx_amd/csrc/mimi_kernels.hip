@@ -10,13 +10,23 @@
 // out(i, j) = sum_kk A(i, kk) * B(kk, j); 64 x 64 tile, K-step 16, 4x4 outputs per thread.
 // Problems supply a(), b(), store(); B_KCONTIG selects the B-tile load mapping (consecutive kk
 // per thread when B's memory is contiguous along kk, else consecutive j).
-template <class P>
-__global__ __launch_bounds__(256) void gemm64_kernel(P p) {
+// SPLIT: blockIdx.z = z * ks + slice; the block sums K range [slice * KD / ks, (slice + 1) * KD / ks)
+// (whole 16-steps) and writes its raw tile to slab[slice][z][i][j]; splitk_reduce_kernel adds the slices
+// in order and runs the problem's epilogue.
+template <class P, bool SPLIT>
+__global__ __launch_bounds__(256) void gemm64_kernel(P p, int ks, float* slab, int Z) {
   __shared__ __attribute__((aligned(16))) float As[16][68];
   __shared__ __attribute__((aligned(16))) float Bs[16][68];
   const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
-  const int i0 = blockIdx.y * 64, j0 = blockIdx.x * 64, z = blockIdx.z;
+  const int i0 = blockIdx.y * 64, j0 = blockIdx.x * 64;
+  const int z = SPLIT ? (int)blockIdx.z / ks : (int)blockIdx.z, sl = SPLIT ? (int)blockIdx.z % ks : 0;
   const int KD = p.kdim();
+  int kb = 0, ke = KD;
+  if constexpr (SPLIT) {
+    const int nst = (KD + 15) / 16;
+    kb = (nst * sl / ks) * 16;
+    ke = min(KD, (nst * (sl + 1) / ks) * 16);
+  }
   float acc[4][4];
 #pragma unroll
   for (int r = 0; r < 4; ++r)
@@ -27,40 +37,40 @@ __global__ __launch_bounds__(256) void gemm64_kernel(P p) {
   float va[4], vb[4];
   auto fetch = [&](int k0) {
     {
-      const int i = tid >> 2, kb = (tid & 3) * 4;
+      const int i = tid >> 2, kq = (tid & 3) * 4;
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        va[e] = (i0 + i < p.M && k0 + kb + e < KD) ? p.a(z, i0 + i, k0 + kb + e) : 0.f;
+        va[e] = (i0 + i < p.M && k0 + kq + e < ke) ? p.a(z, i0 + i, k0 + kq + e) : 0.f;
     }
     if constexpr (P::B_KCONTIG) {
-      const int j = tid >> 2, kb = (tid & 3) * 4;
+      const int j = tid >> 2, kq = (tid & 3) * 4;
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        vb[e] = (j0 + j < p.N && k0 + kb + e < KD) ? p.b(z, k0 + kb + e, j0 + j) : 0.f;
+        vb[e] = (j0 + j < p.N && k0 + kq + e < ke) ? p.b(z, k0 + kq + e, j0 + j) : 0.f;
     } else {
       const int kk = tid >> 4, jb = (tid & 15) * 4;
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        vb[e] = (k0 + kk < KD && j0 + jb + e < p.N) ? p.b(z, k0 + kk, j0 + jb + e) : 0.f;
+        vb[e] = (k0 + kk < ke && j0 + jb + e < p.N) ? p.b(z, k0 + kk, j0 + jb + e) : 0.f;
     }
   };
-  fetch(0);
-  for (int k0 = 0; k0 < KD; k0 += 16) {
+  fetch(kb);
+  for (int k0 = kb; k0 < ke; k0 += 16) {
     {
-      const int i = tid >> 2, kb = (tid & 3) * 4;
+      const int i = tid >> 2, kq = (tid & 3) * 4;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) As[kb + e][i] = va[e];
+      for (int e = 0; e < 4; ++e) As[kq + e][i] = va[e];
     }
     if constexpr (P::B_KCONTIG) {
-      const int j = tid >> 2, kb = (tid & 3) * 4;
+      const int j = tid >> 2, kq = (tid & 3) * 4;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) Bs[kb + e][j] = vb[e];
+      for (int e = 0; e < 4; ++e) Bs[kq + e][j] = vb[e];
     } else {
       const int kk = tid >> 4, jb = (tid & 15) * 4;
       *reinterpret_cast<float4*>(&Bs[kk][jb]) = make_float4(vb[0], vb[1], vb[2], vb[3]);
     }
     __syncthreads();
-    if (k0 + 16 < KD) fetch(k0 + 16);
+    if (k0 + 16 < ke) fetch(k0 + 16);
 #pragma unroll
     for (int kk = 0; kk < 16; ++kk) {
       const float4 a = *reinterpret_cast<const float4*>(&As[kk][ty * 4]);
@@ -78,8 +88,50 @@ __global__ __launch_bounds__(256) void gemm64_kernel(P p) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const int i = i0 + ty * 4 + r, j = j0 + tx * 4 + c;
-      if (i < p.M && j < p.N) p.store(z, i, j, acc[r][c]);
+      if (i < p.M && j < p.N) {
+        if constexpr (SPLIT) slab[(((size_t)sl * Z + z) * p.M + i) * p.N + j] = acc[r][c];
+        else p.store(z, i, j, acc[r][c]);
+      }
     }
+}
+
+// the split-K slices of every output, added in slice order, then the problem's epilogue
+template <class P>
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(P p, const float* slab, int ks, int Z) {
+  const size_t tot = (size_t)Z * p.M * p.N;
+  for (size_t e = (size_t)blockIdx.x * 256 + threadIdx.x; e < tot; e += (size_t)gridDim.x * 256) {
+    float v = slab[e];
+    for (int s = 1; s < ks; ++s) v += slab[(size_t)s * tot + e];
+    const int j = (int)(e % p.N);
+    const size_t r = e / p.N;
+    p.store((int)(r / p.M), (int)(r % p.M), j, v);
+  }
+}
+
+// Split-K slices for a launch whose grid would hold `blocks` 64 x 64 tiles (counted on the batch-folded
+// column space, so a folded and an unfolded launch of the same conv split alike -- same sums): slices
+// double while the grid stays <= CSM_MIMI_KS_BLOCKS (default 512; 0 = never split) and every slice keeps
+// >= 64 of the K dimension.  The streaming decode_step's first conv (1024 x 64 outputs, K 3584) ran on
+// 16 blocks for 500 us (profiles/r04_prof_config3_per_frame.txt).
+static int mimi_splitk(int KD, int blocks, size_t slab_per_slice) {
+  static const int target = [] { const char* e = getenv("CSM_MIMI_KS_BLOCKS"); return e ? atoi(e) : 512; }();
+  int ks = 1;
+  while (blocks * ks * 2 <= target && KD / (ks * 2) >= 64 && ks < 32 && slab_per_slice * ks * 2 <= MIMI_KS_WS_FLOATS) ks *= 2;
+  return ks;
+}
+
+template <class P>
+static void launch_gemm64(const P& pr, dim3 grid, int ks, float* ws, hipStream_t st) {
+  if (ks <= 1 || !ws) {
+    hipLaunchKernelGGL((gemm64_kernel<P, false>), grid, dim3(256), 0, st, pr, 1, nullptr, (int)grid.z);
+    return;
+  }
+  const int Z = (int)grid.z;
+  const dim3 g2(grid.x, grid.y, grid.z * ks);
+  hipLaunchKernelGGL((gemm64_kernel<P, true>), g2, dim3(256), 0, st, pr, ks, ws, Z);
+  const size_t tot = (size_t)Z * pr.M * pr.N;
+  const int rb = (int)std::min<size_t>(2048, (tot + 255) / 256);
+  hipLaunchKernelGGL(splitk_reduce_kernel<P>, dim3(rb), dim3(256), 0, st, pr, ws, ks, Z);
 }
 
 // ---------------------------------------------------------------------------- causal conv1d
@@ -130,7 +182,8 @@ void launch_conv1d(const ConvParams& p, hipStream_t st) {
   const bool fold = p.Tout < 64 && p.B > 1 && conv_fold_enabled();
   ConvProblem pr{p, p.Cout, fold ? p.B * p.Tout : p.Tout, fold ? p.Tout : 0};
   dim3 grid((pr.N + 63) / 64, (p.Cout + 63) / 64, fold ? 1 : p.B);
-  hipLaunchKernelGGL(gemm64_kernel<ConvProblem>, grid, dim3(256), 0, st, pr);
+  const int ks = mimi_splitk(p.Cin * p.k, ((p.B * p.Tout + 63) / 64) * ((p.Cout + 63) / 64), (size_t)p.B * p.Tout * p.Cout);
+  launch_gemm64(pr, grid, ks, p.ks_ws, st);
 }
 
 // ---------------------------------------------------------------------------- transposed conv (k = 2s)
@@ -173,7 +226,9 @@ void launch_convtr(const ConvTrParams& p, hipStream_t st) {
   const bool fold = p.n_in < 64 && p.B > 1 && conv_fold_enabled();
   ConvTrProblem pr{p, p.Cout, fold ? p.B * p.n_in : p.n_in, fold ? p.n_in : 0};
   dim3 grid((pr.N + 63) / 64, (p.Cout + 63) / 64, fold ? p.s : p.B * p.s);
-  hipLaunchKernelGGL(gemm64_kernel<ConvTrProblem>, grid, dim3(256), 0, st, pr);
+  const int ks = mimi_splitk(p.Cin * 2, ((p.B * p.n_in + 63) / 64) * ((p.Cout + 63) / 64) * p.s,
+                             (size_t)p.B * p.n_in * p.s * p.Cout);
+  launch_gemm64(pr, grid, ks, p.ks_ws, st);
 }
 
 // ---------------------------------------------------------------------------- linear (rows x W^T)
@@ -211,10 +266,12 @@ struct LinProblem {
 // decode_step) 2083 -> 2123 frames/s; at 125 rows (one-shot decode of a 10 s utterance) neutral, and
 // 16 rows per weight pass was slower (2001).  Round 3: the codec transformer's rows at B = 32 are 64
 // (two 25 Hz steps per frame), where gemm64 left the N = 512 outputs on 8 workgroups: cutoff 64,
-// config 3 2932 -> 3076 frames/s (profiles/r03_ab_mimi.txt).  CSM_MIMI_GEMV_M sets the largest row
-// count (0 = never).
+// config 3 2932 -> 3076 frames/s (profiles/r03_ab_mimi.txt).  Round 4: above 16 rows the tiled GEMM
+// with split-K (mimi_splitk: 64-512 blocks instead of 8-32) -- the 64-row linears took 40-68 us on the
+// GEMV, which re-reads the weights for every 4-row pass (profiles/r04_prof_config3_per_frame.txt).
+// CSM_MIMI_GEMV_M sets the largest row count on the GEMV (0 = never).
 static int mimi_gemv_rows() {
-  static const int v = [] { const char* e = getenv("CSM_MIMI_GEMV_M"); return e ? atoi(e) : 64; }();
+  static const int v = [] { const char* e = getenv("CSM_MIMI_GEMV_M"); return e ? atoi(e) : 16; }();
   return v;
 }
 
@@ -229,7 +286,8 @@ void launch_linear(const LinParams& p, hipStream_t st) {
   }
   LinProblem pr{p, p.N, p.M};
   dim3 grid((p.M + 63) / 64, (p.N + 63) / 64, 1);
-  hipLaunchKernelGGL(gemm64_kernel<LinProblem>, grid, dim3(256), 0, st, pr);
+  const int ks = mimi_splitk(p.K, (int)(grid.x * grid.y), (size_t)p.M * p.N);
+  launch_gemm64(pr, grid, ks, p.ks_ws, st);
 }
 
 // ============================================================================ LayerNorm rows
