@@ -86,6 +86,7 @@ def lib():
             "csm_frame_c0_logits": ([P, P], I),
             "csm_frame_finish": ([P, P, ctypes.POINTER(I)], I),
             "csm_frame_forced": ([P, P, P, P, P], I),
+            "csm_frame_host_step": ([P, P, P, ctypes.POINTER(I)], I),
             "csm_read_codes": ([P, P, P, P, ctypes.POINTER(I)], I),
             "csm_debug_read": ([P, ctypes.c_char_p, P, I64, ctypes.POINTER(I64)], I),
             "csm_codes_device_ptr": ([P, ctypes.POINTER(P)], I),

@@ -22,19 +22,22 @@ import numpy as np
 
 from . import _lib
 from .models import CSM
-from .sampling import Sampler
+from .sampling import HostSampler, Sampler
 from .segment import Segment
 from .tokenizers import decode_audio, get_audio_tokenizer, tokenize_segment, tokenize_text_segment
 
 default_stream = None  # MLX stream placeholder (generation.py:19); the engine owns its HIP stream
 
 
-def _resolve_sampler(temperature: float, sampler: Optional[Sampler], top_k: int = 0) -> Sampler:
+def _resolve_sampler(temperature: float, sampler, top_k: int = 0):
+    """A Sampler descriptor (runs on the GPU), or any other callable wrapped as a HostSampler (runs
+    on the host for every codebook: csm_frame_host_step)."""
     if sampler is not None:
-        if callable(sampler) and not isinstance(sampler, Sampler):
-            raise NotImplementedError("arbitrary sampler callables cannot run inside the GPU frame graph; "
-                                      "use csm_mlx.sampling.make_sampler(temp, top_k=...)")
-        return sampler
+        if isinstance(sampler, (Sampler, HostSampler)):
+            return sampler
+        if callable(sampler):
+            return HostSampler(sampler)
+        raise TypeError(f"sampler must be a csm_mlx.sampling.Sampler or a callable, got {type(sampler).__name__}")
     return Sampler(float(temperature), int(top_k))
 
 
@@ -126,6 +129,31 @@ class FrameCache:
             c0_history.append(self.last_codes()[:, :1].copy())
         return bool(done.value)
 
+    def run_host_sampled(self, sampler: HostSampler, processors: Sequence[Callable] = (),
+                         c0_history: Optional[list] = None) -> bool:
+        """One frame whose every code comes from a host sampler callable (the reference's sampler=,
+        applied per codebook): c0 logits -> processors -> sampler -> csm_frame_host_step, which feeds
+        the codes forward and returns the next codebook's logits, K times.  Returns whether every
+        utterance is done."""
+        self._check()
+        V, K = self.model.n_audio_vocab, self.model.n_audio_codebooks
+        logits = np.zeros((self.B, V), np.float32)
+        _lib.check(self.L.csm_frame_c0_logits(self.model.engine, _lib.ptr(logits)))
+        hist = np.stack(c0_history, 0) if c0_history else np.zeros((0,), np.int32)
+        for proc in processors:
+            logits = np.ascontiguousarray(np.asarray(proc(hist, logits), np.float32).reshape(self.B, V))
+        done = ctypes.c_int(0)
+        for i in range(K):
+            codes = np.ascontiguousarray(np.clip(sampler(logits), 0, V - 1), np.int32)
+            if i == 0 and c0_history is not None:
+                c0_history.append(codes[:, None].copy())
+            out = np.zeros((self.B, V), np.float32)
+            _lib.check(self.L.csm_frame_host_step(self.model.engine, _lib.ptr(codes),
+                                                  _lib.ptr(out) if i + 1 < K else None, ctypes.byref(done)))
+            logits = out
+        self.frames += 1
+        return bool(done.value)
+
     def codes(self) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
         """(history [F,B,K], n_frames [B], done [B])."""
         self._check()
@@ -182,6 +210,9 @@ def generate_frame(model: CSM, tokens, *, temperature: float = 0.8, token_mask=N
                              f"create the cache with make_frame_cache(model, temperature=..., sampler=...)")
     for b in range(B):
         cache.prefill(b, tokens[b], mask[b])
+    if isinstance(cache.sampler, HostSampler):
+        cache.run_host_sampled(cache.sampler, logits_processors or (), c0_history)
+        return cache.last_codes()
     if logits_processors:
         cache.run_processed(logits_processors, c0_history)
         return cache.last_codes()
@@ -243,7 +274,13 @@ def generate_codes_batch(model: CSM, prompts: Sequence[Tuple[np.ndarray, np.ndar
         cache.prefill(0, *prompts[0])
     t0 = _mark(timings, "prefill", t0, model)
     left = max_audio_frames
-    if logits_processors:
+    if isinstance(sampler, HostSampler):  # a sampler callable: every code from the host, frame by frame
+        c0_history_h: list = []
+        for _ in range(max_audio_frames):
+            if cache.run_host_sampled(sampler, logits_processors or (), c0_history_h):
+                break
+        left = 0
+    elif logits_processors:
         c0_history: list = []                                                    # generation.py:128
         for _ in range(max_audio_frames):
             if cache.run_processed(logits_processors, c0_history):
@@ -332,6 +369,16 @@ def _overlapped_frames(cache: "FrameCache", codec, max_audio_frames: int):
         yield codec.decode_step(prev[0])[:, 0], prev[1]
 
 
+def _host_sampled_frames(cache: "FrameCache", codec, max_audio_frames: int, sampler: HostSampler, processors):
+    """The streaming loop with a host sampler callable (every code from the host; nothing to overlap):
+    EOS is tested before the frame is decoded (generation.py:237-251)."""
+    c0_history: list = []
+    for _ in range(max_audio_frames):
+        if cache.run_host_sampled(sampler, processors or (), c0_history):
+            break
+        yield codec.decode_step(cache.last_codes())[:, 0], cache.done()
+
+
 def _processed_frames(cache: "FrameCache", codec, max_audio_frames: int, processors):
     """The streaming loop with host logits processors: each frame pauses after codebook0_head, so
     there is nothing to overlap; EOS is tested before the frame is decoded (generation.py:237-251)."""
@@ -358,7 +405,10 @@ def stream_generate_batch(model: CSM, prompts: Sequence[Tuple[np.ndarray, np.nda
     cache.prefill_batch([(b, t, m) for b, (t, m) in enumerate(prompts)])
     codec.reset_state(B)
     try:
-        yield from _overlapped_frames(cache, codec, max_audio_frames)
+        if isinstance(smp, HostSampler):
+            yield from _host_sampled_frames(cache, codec, max_audio_frames, smp, None)
+        else:
+            yield from _overlapped_frames(cache, codec, max_audio_frames)
     finally:
         codec.reset_state(B)
 
@@ -379,8 +429,12 @@ def stream_generate(model: CSM, text, speaker: int, context: List[Segment], max_
     cache.prefill(0, t, m)
     codec.reset_state(1)
     try:
-        frames = (_processed_frames(cache, codec, max_audio_frames, logits_processors) if logits_processors
-                  else _overlapped_frames(cache, codec, max_audio_frames))
+        if isinstance(smp, HostSampler):
+            frames = _host_sampled_frames(cache, codec, max_audio_frames, smp, logits_processors)
+        elif logits_processors:
+            frames = _processed_frames(cache, codec, max_audio_frames, logits_processors)
+        else:
+            frames = _overlapped_frames(cache, codec, max_audio_frames)
         for pcm, _ in frames:
             yield pcm[0]
     finally:

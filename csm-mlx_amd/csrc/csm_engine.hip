@@ -82,7 +82,8 @@ struct csm_engine {
   // input row from it instead of running the projection GEMV.
   float* proj_tab = nullptr;
   bool proj_tab_dirty = true;
-  bool c0_pending = false;  // csm_frame_c0_logits ran; csm_frame_finish must follow
+  bool c0_pending = false;  // csm_frame_c0_logits ran; csm_frame_finish (or csm_frame_host_step) must follow
+  int host_piece = 1;       // csm_frame_host_step: the codebook whose code the next call feeds is host_piece - 1
   // decoder layer 0's QKV folded too: qkv0_tab[cb][code] = RoPE'd (q, k | v) of layer 0 for input row
   // proj_tab[cb][code] at position cb + 1 (fp32, built by the same QKV GEMV); codebook steps >= 2 then
   // skip layer 0's QKV launch and its attention gathers the row (AttnParams::g_tab).
@@ -565,13 +566,17 @@ void check_dec_frame(csm_engine* e) {
 // then steps 1..K-1 as in phase 0.
 // phase 3: teacher forcing -- every head stores its logits and the code fed forward is the caller's
 // (e->force [B][K]), as compute_loss feeds the target frame (trainer.py:233-262).
-void enqueue_head_phase(csm_engine* e, hipStream_t st, int phase) {
+// phase 4: one piece of a host-sampled frame (a sampler callable on the host, csm_frame_host_step):
+// piece p feeds the host's code for codebook p - 1 forward (e->force, as teacher forcing) and runs
+// decoder step p + its head (logits stored); piece K feeds the last code and advances the frame.  The
+// c0 head ran as phase 1 (csm_frame_c0_logits).
+void enqueue_head_phase(csm_engine* e, hipStream_t st, int phase, int piece = 0) {
   if (phase == 0 && dec_frame_eligible(e)) {
     enqueue_dec_frame(e, st);
     return;
   }
   const int B = e->B, K = e->K, D = e->D, Dd = e->Dd, V = e->V, Vp = e->Vpad;
-  const bool greedy = e->temperature <= 0.f && phase != 3;
+  const bool greedy = e->temperature <= 0.f && phase != 3 && phase != 4;
   const bool c0_sampled = !greedy || phase == 2;  // c0 published by sample_kernel as a single partial
   const int n0 = head_blocks(Vp, D, B, e->wdt);        // c0-head blocks (partials per row)
   const int ni = head_blocks(Vp, Dd, B, e->head_wdt);  // ci-head blocks
@@ -581,18 +586,20 @@ void enqueue_head_phase(csm_engine* e, hipStream_t st, int phase) {
   sp.frame_ctr = e->frame_ctr; sp.K = K; sp.codes = e->codes; sp.part_stride = e->part_stride;
   sp.use_top_p = e->use_top_p; sp.use_min_p = e->use_min_p; sp.min_keep = e->min_keep;
   sp.top_p_cut = e->top_p_cut; sp.log_min_p = e->log_min_p;
-  sp.forced = phase == 3 ? e->force : nullptr;
+  sp.forced = (phase == 3 || phase == 4) ? e->force : nullptr;
   // c0 = codebook0_head(h_last) (generation.py:42); greedy arg-max fused into the GEMV epilogue
   GemvParams g = gp(e);
   g.W = e->c0_head; g.N = Vp; g.K = D; g.x = e->h_last; g.xs = D; g.M = B; g.out = e->c0_logits; g.os = Vp;
   g.part = part(0); g.part_stride = e->part_stride; g.n_valid = V;
-  if (phase != 2) launch_gemv(g, e->wdt, (greedy && phase == 0) ? EPI_ARGMAX : EPI_STORE, 0, st);
+  if (phase != 2 && phase != 4) launch_gemv(g, e->wdt, (greedy && phase == 0) ? EPI_ARGMAX : EPI_STORE, 0, st);
   if (phase == 1) return;
+  const int cb_first = phase == 4 ? piece - 1 : 0;  // the code fed forward before the first step below
   if (c0_sampled) {
-    sp.logits = e->c0_logits; sp.cb = 0; sp.part = part(0);
+    sp.logits = e->c0_logits; sp.cb = cb_first; sp.part = part(cb_first);
     launch_sample(sp, e->wdt, B, st);
   }
-  for (int i = 1; i < K; ++i) {
+  const int i_lo = phase == 4 ? piece : 1, i_hi = phase == 4 ? std::min(piece + 1, K) : K;
+  for (int i = i_lo; i < i_hi; ++i) {
     const int M = (i == 1) ? 2 * B : B;
     // decoder(projection(decoder_inputs)) (generation.py:74-77): the projection gathers its input
     // rows itself -- [h_last, E_a[c0]] at step 1 (:62-64), E_a[c_{i-1} + V*(i-1)] after (:87-89)
@@ -649,11 +656,12 @@ void enqueue_head_phase(csm_engine* e, hipStream_t st, int phase) {
     } else if (!(ablate() & 64)) {
       launch_gemv(g, e->head_wdt, greedy ? EPI_ARGMAX : EPI_STORE, 1, st);
     }
-    if (!greedy) {
+    if (!greedy && phase != 4) {
       sp.logits = e->ci_logits + (size_t)(i - 1) * B * Vp; sp.cb = i; sp.part = part(i);
       launch_sample(sp, e->wdt, B, st);
     }
   }
+  if (phase == 4 && piece < K) return;  // the frame continues with the host's next code
   AdvanceParams ap{};
   ap.codes = e->codes; ap.hist = e->hist; ap.F_cap = e->F_cap; ap.B = B; ap.K = K; ap.V = V; ap.done = e->done;
   ap.n_frames = e->n_frames; ap.frame_ctr = e->frame_ctr;
@@ -1521,6 +1529,7 @@ int csm_frame_c0_logits(csm_engine* e, float* logits) {
     HIPCHK(hipStreamSynchronize(e->st));
     check_dec_frame(e);  // the backbone row may have run on the persistent step
     e->c0_pending = true;
+    e->host_piece = 1;
   }
   CSM_CATCH
 }
@@ -1546,6 +1555,41 @@ int csm_frame_finish(csm_engine* e, const float* logits, int* all_done) {
       *all_done = all;
     } else {
       HIPCHK(hipStreamSynchronize(e->st));  // the host logits buffer may be released on return
+    }
+    check_dec_frame(e);
+  }
+  CSM_CATCH
+}
+
+int csm_frame_host_step(csm_engine* e, const int32_t* codes, float* logits, int* all_done) {
+  CSM_TRY {
+    if (!e->c0_pending) throw CsmError(CSM_ERR_STATE, "csm_frame_host_step without csm_frame_c0_logits");
+    if (!codes) throw CsmError(CSM_ERR_ARG, "null codes");
+    const int piece = e->host_piece;  // codes are those of codebook piece - 1
+    if (piece < e->K && !logits) throw CsmError(CSM_ERR_ARG, "null logits buffer");
+    for (int b = 0; b < e->B; ++b)
+      if (codes[b] < 0 || codes[b] >= e->V) throw CsmError(CSM_ERR_ARG, "host-sampled code out of range");
+    HIPCHK(hipSetDevice(e->dev));
+    HIPCHK(hipMemcpy2DAsync(e->force + (piece - 1), (size_t)e->K * 4, codes, 4, 4, e->B, hipMemcpyHostToDevice, e->st));
+    enqueue_head_phase(e, e->st, 4, piece);
+    HIPCHK(hipGetLastError());
+    if (piece < e->K) {
+      HIPCHK(hipMemcpy2DAsync(logits, (size_t)e->V * 4, e->ci_logits + (size_t)(piece - 1) * e->B * e->Vpad,
+                              (size_t)e->Vpad * 4, (size_t)e->V * 4, e->B, hipMemcpyDeviceToHost, e->st));
+      HIPCHK(hipStreamSynchronize(e->st));
+      e->host_piece = piece + 1;
+      if (all_done) *all_done = 0;
+    } else {
+      e->c0_pending = false;
+      e->host_piece = 1;
+      e->need_body = true;
+      e->frames_run++;
+      std::vector<uint8_t> d(e->B);
+      HIPCHK(hipMemcpyAsync(d.data(), e->done, e->B, hipMemcpyDeviceToHost, e->st));
+      HIPCHK(hipStreamSynchronize(e->st));
+      int all = 1;
+      for (auto v : d) all &= (v != 0);
+      if (all_done) *all_done = all;
     }
     check_dec_frame(e);
   }

@@ -167,31 +167,12 @@ __global__ __launch_bounds__(256) void gemm_wide_kernel(GemvParams p) {
   const int r = lane & 31, h = lane >> 5, slot = lane + h;
   // grid (row tile, K slice, batch chunk): tiles fastest in dispatch order (measured: the
   // chunk-major order cost configs 4 / 5 3-4 %)
-  // XCD-aware placement (as gemm_xs_kernel, gemm_xs.hip): the blocks of one XCD take the same K
-  // slice(s), so each slice's activation rows reach one L2 instead of all 8 (blocks are dealt
-  // round-robin over the XCDs in linear-id order; every batch-chunk plane holds T * S blocks)
-  int tile = blockIdx.x, slice = blockIdx.y;
-  {
-    const int T = gridDim.x, S = gridDim.y, L = blockIdx.x + T * blockIdx.y, xcd = L & 7, j = L >> 3;
-#ifndef XCD_MAP
-#define XCD_MAP 1  // lab: -DXCD_MAP=0 restores the tile-major placement (A/B)
-#endif
-    if (XCD_MAP && (T * S) % 8 == 0) {
-      if (S % 8 == 0) {
-        slice = xcd * (S / 8) + j / T;
-        tile = j % T;
-      } else if (8 % S == 0 && T % (8 / S) == 0) {
-        slice = xcd % S;
-        tile = (xcd / S) * (T / (8 / S)) + j;
-      }
-    }
-  }
-  const int n0 = tile * NBR;
+  const int tile = blockIdx.x, n0 = tile * NBR;
   const int blin = (blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
   (void)blin;
   GSTAMP(0);
   const int mc = blockIdx.z, m0 = mc * NB, nchunks = gridDim.z;
-  const int Kblk = p.K / p.ksplit, kslice = slice * Kblk, nst = Kblk / GP_KC;
+  const int Kblk = p.K / p.ksplit, kslice = blockIdx.y * Kblk, nst = Kblk / GP_KC;
   const bool norm = p.nw != nullptr;
   const int kh = KW == 2 ? (wave >> 1) : 0;
   const int rt0 = KW == 2 ? (wave & 1) : wave * RTW;
@@ -388,7 +369,7 @@ __global__ __launch_bounds__(256) void gemm_wide_kernel(GemvParams p) {
     const int slab_f = NB * NBR + NB;
     float* slab = p.kpart + ((size_t)(tile * nchunks + mc) * p.ksplit) * slab_f;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(slab, 0, p.ksplit * slab_f * 4, GP_RSRC3);
-    const int mine = slice * slab_f * 4;
+    const int mine = blockIdx.y * slab_f * 4;
     for (int q = tid; q < mrows * (NBR / 4); q += 256) {
       const int ml = q / (NBR / 4), j = (q % (NBR / 4)) * 4;
       const f32x4_t v = {ct[ml][j], ct[ml][j + 1], ct[ml][j + 2], ct[ml][j + 3]};

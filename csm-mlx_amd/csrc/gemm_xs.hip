@@ -100,31 +100,9 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
   constexpr int NB = 32 * MT, NBR = 32 * RTW, NTH = 64 * XW;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // XCD-aware placement.  Blocks are dealt round-robin over the 8 XCDs (linear id % 8 share one L2;
-  // MI355X_MICROARCH.md: observed, speed only), and the split operand of K slice s is read by every
-  // block of slice s: with tile-major ids every XCD held every slice, so each slice crossed into all 8
-  // L2s (the decoder down at 64 rows fetched 25 MB of its 3 MB operand, r4 config-5 PMC pass).  Here the
-  // blocks of one XCD take the same slice(s) -- slices >= 8: XCD x owns slices [x S/8, (x+1) S/8); fewer:
-  // 8/S XCDs share a slice and split its tiles.  Same (tile, slice) work items, same combine order.
-  int tile = blockIdx.x, slice = blockIdx.y;
-  {
-    const int T = gridDim.x, S = gridDim.y, L = blockIdx.x + T * blockIdx.y, xcd = L & 7, j = L >> 3;
-#ifndef XCD_MAP
-#define XCD_MAP 1  // lab: -DXCD_MAP=0 restores the tile-major placement (A/B)
-#endif
-    if (XCD_MAP && (T * S) % 8 == 0) {
-      if (S % 8 == 0) {
-        slice = xcd * (S / 8) + j / T;
-        tile = j % T;
-      } else if (8 % S == 0 && T % (8 / S) == 0) {
-        slice = xcd % S;
-        tile = (xcd / S) * (T / (8 / S)) + j;
-      }
-    }
-  }
-  const int n0 = tile * NBR;
+  const int tile = blockIdx.x, n0 = tile * NBR;
   const int nks = p.K / XK, nt32 = (p.N + 31) / 32;
-  const int ks = p.ksplit, nst = nks / ks, wst = nst / XW, ws0 = slice * nst + wave * wst;
+  const int ks = p.ksplit, nst = nks / ks, wst = nst / XW, ws0 = blockIdx.y * nst + wave * wst;
   const __amdgpu_buffer_rsrc_t wrs = rsrc(p.Wt, 0x7fffffff), ars = rsrc(p.xs_in, 0x7fffffff), zrs = rsrc(p.Wt, 0);
   int wv[RTW], sv[RTW];
 #pragma unroll
@@ -137,7 +115,7 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
   if constexpr (Q4) {  // X_g of this block's stages: the two half-group sums, in order
     for (int e = tid; e < XW * wst * NB; e += NTH) {
       const int w = e / (wst * NB), j = (e / NB) % wst, m = e % NB;
-      const int st = slice * nst + w * wst + j;
+      const int st = blockIdx.y * nst + w * wst + j;
       xg[w][j][m] = p.hs_in[(size_t)(2 * st) * xs::HS_ROWS + m] + p.hs_in[(size_t)(2 * st + 1) * xs::HS_ROWS + m];
     }
     __syncthreads();
@@ -330,7 +308,7 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
     const int slab_f = NB * NBR;
     float* slab = p.kpart + (size_t)tile * ks * slab_f;
     const __amdgpu_buffer_rsrc_t rs = rsrc(slab, ks * slab_f * 4);
-    const int mine = slice * slab_f * 4;
+    const int mine = blockIdx.y * slab_f * 4;
     for (int q = tid; q < mrows * (NBR / 4); q += NTH) {
       const int ml = q / (NBR / 4), j = (q % (NBR / 4)) * 4;
       const f32x4_t v = {ct[ml][j], ct[ml][j + 1], ct[ml][j + 2], ct[ml][j + 3]};

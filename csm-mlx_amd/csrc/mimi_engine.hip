@@ -70,6 +70,11 @@ struct mimi_codec {
   float* rvq_in[2] = {nullptr, nullptr};
   float* rvq_out[2] = {nullptr, nullptr};
   float *cb = nullptr, *c2half = nullptr;  // [n_q][bins][cd], [n_q][bins]
+  float* cbT = nullptr;                    // [n_q][cd][bins]: codebooks dims-major (RVQ encode distance GEMM)
+  float* rvq_r = nullptr;                  // RVQ encode scratch: 2 x [M][cd] residuals, 2 x [M][bins / 256] partials
+  size_t rvq_r_n = 0;
+  unsigned long long* rvq_p = nullptr;
+  size_t rvq_p_n = 0;
   float* rope = nullptr;
   std::map<std::string, Dest> dest;
   std::set<std::string> loaded;
@@ -104,6 +109,8 @@ struct mimi_codec {
     for (void* p : allocs) (void)hipFree(p);
     for (float* p : {W0, W1, H, R, Rh, Rqkv, Rq, Ratt, Rf, dpcm}) if (p) (void)hipFree(p);
     if (dcodes) (void)hipFree(dcodes);
+    if (rvq_r) (void)hipFree(rvq_r);
+    if (rvq_p) (void)hipFree(rvq_p);
     if (st) (void)hipStreamDestroy(st);
   }
   int op_cin(const MOp& o) const {
@@ -230,6 +237,7 @@ void build_layout(mimi_codec* m) {
   }
   m->cb = (float*)m->alloc((size_t)d.n_q * d.bins * cd * 4);
   m->c2half = (float*)m->alloc((size_t)d.n_q * d.bins * 4);
+  m->cbT = (float*)m->alloc((size_t)d.n_q * d.bins * cd * 4);
   m->cb_sum.assign(d.n_q, {});
   m->cb_usage.assign(d.n_q, {});
   for (int k = 0; k < d.n_q; ++k) {
@@ -257,6 +265,10 @@ void finish_codebook(mimi_codec* m, int k) {
     c2[i] = (float)(acc / 2.0);
   }
   HIPCHK(hipMemcpy(m->cb + (size_t)k * bins * cd, e.data(), e.size() * 4, hipMemcpyHostToDevice));
+  std::vector<float> et((size_t)bins * cd);
+  for (int i = 0; i < bins; ++i)
+    for (int j = 0; j < cd; ++j) et[(size_t)j * bins + i] = e[(size_t)i * cd + j];
+  HIPCHK(hipMemcpy(m->cbT + (size_t)k * bins * cd, et.data(), et.size() * 4, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(m->c2half + (size_t)k * bins, c2.data(), c2.size() * 4, hipMemcpyHostToDevice));
 }
 
@@ -626,7 +638,17 @@ int mimi_encode(mimi_codec* m, int B, int N, const float* pcm, int32_t* codes, i
       lp.epi = EPI_STORE;
       launch_linear(lp, st);
       const int k0 = q == 0 ? 0 : 1, k1 = q == 0 ? 1 : d.n_q;
-      if (k1 > k0) launch_rvq_encode(m->Rh, M, (int)Tf, cd, m->cb, m->c2half, d.bins, k0, k1, d.n_q, m->dcodes, st);
+      if (k1 <= k0) continue;
+      // many rows: one distance GEMM launch per codebook (CSM_RVQ_GEMM=0: the tiled / per-row kernels)
+      static const bool gemm_on = [] { const char* e = getenv("CSM_RVQ_GEMM"); return !(e && e[0] == '0'); }();
+      if (gemm_on && M >= 256 && rvq_gemm_eligible(cd, d.bins)) {
+        grow(m->rvq_r, m->rvq_r_n, (size_t)2 * M * cd);
+        grow(m->rvq_p, m->rvq_p_n, 2 * rvq_gemm_parts(M, d.bins));
+        launch_rvq_encode_gemm(m->Rh, M, (int)Tf, cd, m->cb, m->cbT, m->c2half, d.bins, k0, k1, d.n_q, m->dcodes,
+                               m->rvq_r, m->rvq_p, st);
+      } else {
+        launch_rvq_encode(m->Rh, M, (int)Tf, cd, m->cb, m->c2half, d.bins, k0, k1, d.n_q, m->dcodes, st);
+      }
     }
     HIPCHK(hipMemcpyAsync(codes, m->dcodes, (size_t)B * d.n_q * Tf * 4, hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));

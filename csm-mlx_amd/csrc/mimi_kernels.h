@@ -83,6 +83,14 @@ void launch_rvq_gather(const int* codes, int layout, int B, int F, int n_q, int 
 // codes[b][k][t] for m = b*T + t
 void launch_rvq_encode(float* r, int M, int T, int cd, const float* cb, const float* c2half, int bins, int k0, int k1,
                        int n_q, int* codes, hipStream_t st);
+// The same as one distance GEMM launch per codebook (+ a finishing pass): cbT = codebooks dims-major
+// [n_q][cd][bins]; rbuf = 2 x [M][cd] floats, pbuf = 2 x rvq_gemm_parts(M, bins) partials of scratch.
+// Codes and the final residual bit-identical to launch_rvq_encode's.
+bool rvq_gemm_eligible(int cd, int bins);
+size_t rvq_gemm_parts(int M, int bins);
+void launch_rvq_encode_gemm(float* r, int M, int T, int cd, const float* cb, const float* cbT, const float* c2half,
+                            int bins, int k0, int k1, int n_q, int* codes, float* rbuf, unsigned long long* pbuf,
+                            hipStream_t st);
 // copy a [B][C][len] window: dst[b][c][i] = src[b][c][src_off + i]
 void launch_copy_window(const float* src, int B, int C, int src_bstride, int src_cstride, int src_off, float* dst,
                         int dst_bstride, int dst_cstride, int dst_off, int len, hipStream_t st);

@@ -573,6 +573,137 @@ __global__ __launch_bounds__(256) void rvq_encode_tiled_kernel(float* r, int M, 
   }
 }
 
+// Split-RVQ encode as one distance GEMM per codebook (config 5's context encode: 4032 latent rows x 31
+// codebooks per 64 segments; rvq_encode_tiled_kernel streamed every codebook through every 16-row
+// block, 15 ms per launch).  Launch k: block (code tile ct of 256, row tile of 64) first finishes codebook
+// k-1 for its rows -- arg-min over the 8 code-tile partials of k-1 (first minimum), residual r_k = r_{k-1}
+// - c_{k-1}[idx] into LDS (every code tile of a row tile computes the same r_k; tile 0 writes it and the
+// code) -- then scores its 256 codes against the 64 rows: the (row, code) dots are fmaf chains over the
+// dims in order with the code operand first, rvq_encode_kernel's arithmetic, so codes and residuals are
+// bit-identical to it; the codebook arrives dims-major (cbT [k][dim][code], built at load) in 32-dim
+// LDS chunks, double-buffered.  A partial (dist key, code) per (row, code tile) goes to part_cur.
+constexpr int RQ_R = 64, RQ_C = 256, RQ_D = 32, RQ_CDMAX = 256;
+__device__ __forceinline__ unsigned long long rq_key(float dist, int c) {
+  return ((unsigned long long)f2key(dist) << 32) | (unsigned)c;  // min = smallest dist, then smallest code
+}
+
+struct RvqStep {
+  const float* r_in;                 // [M][cd] residual r_{k-1} (or the input latent when part_prev is null)
+  float* r_out;                      // [M][cd] r_k for the next launch
+  const unsigned long long* part_prev;  // [M][nct] partials of codebook k-1, null at the first codebook
+  unsigned long long* part_cur;      // [M][nct] partials of codebook k (null: finishing pass only)
+  const float* cb_prev;              // codebook k-1 [bins][cd]
+  const float* cbT;                  // codebook k dims-major [cd][bins]
+  const float* c2half;               // [bins] of codebook k
+  int* codes;                        // [B][n_q][T]
+  int M, T, cd, bins, nct, k, n_q;
+};
+
+__global__ __launch_bounds__(256) void rvq_step_kernel(RvqStep p) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  __shared__ __attribute__((aligned(16))) float rsT[RQ_CDMAX][RQ_R];      // r_k [dim][row]
+  __shared__ __attribute__((aligned(16))) float Bs[2][RQ_D][RQ_C];        // codebook chunk [dim][code]
+  __shared__ int sidx[RQ_R];
+  const int tid = threadIdx.x, ct = blockIdx.x, m0 = blockIdx.y * RQ_R;
+  const int cd = p.cd;
+  // (1) finish codebook k-1 for the 64 rows
+  if (tid < RQ_R) {
+    int idx = -1;
+    const int m = min(m0 + tid, p.M - 1);
+    if (p.part_prev) {
+      unsigned long long best = ~0ull;
+      for (int j = 0; j < p.nct; ++j) best = min(best, p.part_prev[(size_t)m * p.nct + j]);
+      idx = min(max((int)(unsigned)(best & 0xffffffffu), 0), p.bins - 1);
+      if (ct == 0 && m0 + tid < p.M) p.codes[((size_t)(m / p.T) * p.n_q + (p.k - 1)) * p.T + m % p.T] = idx;
+    }
+    sidx[tid] = idx;
+  }
+  __syncthreads();
+  for (int e = tid; e < RQ_R * cd; e += 256) {
+    const int i = e / cd, d = e % cd, m = min(m0 + i, p.M - 1);
+    float v = p.r_in[(size_t)m * cd + d];
+    if (sidx[i] >= 0) v = v - p.cb_prev[(size_t)sidx[i] * cd + d];
+    rsT[d][i] = v;
+    if (ct == 0 && m0 + i < p.M) p.r_out[(size_t)m * cd + d] = v;
+  }
+  if (!p.part_cur) return;  // finishing pass (after the last codebook)
+  // (2) distances of this tile's 256 codes: thread (ty, tx) -> rows 8 ty .. +8, codes 8 tx .. +8
+  const int tx = tid & 31, ty = tid >> 5, c0 = ct * RQ_C;
+  auto load = [&](int buf, int d0) {
+    for (int e = tid; e < RQ_D * RQ_C / 4; e += 256) {
+      const int dd = e / (RQ_C / 4), c4 = (e % (RQ_C / 4)) * 4;
+      *reinterpret_cast<f4*>(&Bs[buf][dd][c4]) = *reinterpret_cast<const f4*>(p.cbT + (size_t)(d0 + dd) * p.bins + c0 + c4);
+    }
+  };
+  float acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = 0.f;
+  load(0, 0);
+  __syncthreads();
+  const int nch = cd / RQ_D;
+  for (int ch = 0; ch < nch; ++ch) {
+    const int buf = ch & 1;
+    if (ch + 1 < nch) load(buf ^ 1, (ch + 1) * RQ_D);
+#pragma unroll 4
+    for (int dd = 0; dd < RQ_D; ++dd) {
+      const int d = ch * RQ_D + dd;
+      const f4 r0 = *reinterpret_cast<const f4*>(&rsT[d][8 * ty]);
+      const f4 r1 = *reinterpret_cast<const f4*>(&rsT[d][8 * ty + 4]);
+      const f4 b0 = *reinterpret_cast<const f4*>(&Bs[buf][dd][8 * tx]);
+      const f4 b1 = *reinterpret_cast<const f4*>(&Bs[buf][dd][8 * tx + 4]);
+      const float rv[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+      const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[i][j] = fmaf(bv[j], rv[i], acc[i][j]);
+    }
+    __syncthreads();
+  }
+  // (3) per row: first minimum over the tile's codes (keys: dist, then code)
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    unsigned long long best = ~0ull;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int c = c0 + 8 * tx + j;
+      best = min(best, rq_key(p.c2half[c] - acc[i][j], c));
+    }
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) best = min(best, (unsigned long long)__shfl_xor(best, o, 32));
+    const int m = m0 + 8 * ty + i;
+    if (tx == 0 && m < p.M) p.part_cur[(size_t)m * p.nct + ct] = best;
+  }
+}
+
+bool rvq_gemm_eligible(int cd, int bins) { return cd % RQ_D == 0 && cd <= RQ_CDMAX && bins % RQ_C == 0; }
+size_t rvq_gemm_parts(int M, int bins) { return (size_t)M * (bins / RQ_C); }
+
+void launch_rvq_encode_gemm(float* r, int M, int T, int cd, const float* cb, const float* cbT, const float* c2half,
+                            int bins, int k0, int k1, int n_q, int* codes, float* rbuf, unsigned long long* pbuf,
+                            hipStream_t st) {
+  const int nct = bins / RQ_C;
+  const size_t pn = (size_t)M * nct;
+  RvqStep s{};
+  s.M = M; s.T = T; s.cd = cd; s.bins = bins; s.nct = nct; s.n_q = n_q; s.codes = codes;
+  const dim3 grid(nct, (M + RQ_R - 1) / RQ_R);
+  for (int k = k0; k <= k1; ++k) {
+    const int i = k - k0;
+    s.k = k;
+    s.r_in = i == 0 ? r : rbuf + (size_t)(i & 1) * M * cd;
+    s.r_out = k == k1 ? r : rbuf + (size_t)((i + 1) & 1) * M * cd;   // the finishing pass writes r_{k1} back
+    s.part_prev = i == 0 ? nullptr : pbuf + (size_t)((i - 1) & 1) * pn;
+    s.part_cur = k == k1 ? nullptr : pbuf + (size_t)(i & 1) * pn;
+    s.cb_prev = k > k0 ? cb + (size_t)(k - 1) * bins * cd : nullptr;
+    s.cbT = k < k1 ? cbT + (size_t)k * bins * cd : nullptr;
+    s.c2half = k < k1 ? c2half + (size_t)k * bins : nullptr;
+    // the finishing pass needs only code tile 0 (it writes the codes and r); it computes no distances
+    hipLaunchKernelGGL(rvq_step_kernel, k == k1 ? dim3(1, grid.y) : grid, dim3(256), 0, st, s);
+  }
+}
+
 void launch_rvq_encode(float* r, int M, int T, int cd, const float* cb, const float* c2half, int bins, int k0, int k1,
                        int n_q, int* codes, hipStream_t st) {
   const char* env = getenv("CSM_RVQ_TILED");  // read per call (encode is never graph-captured): A/B tests

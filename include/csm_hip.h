@@ -116,6 +116,13 @@ int csm_frame_step(csm_engine* e, int32_t* out_codes, uint8_t* done);
  * (generation.py:44-49) -- called once per frame instead of csm_run_frames. */
 int csm_frame_c0_logits(csm_engine* e, float* logits);
 int csm_frame_finish(csm_engine* e, const float* logits, int* all_done);
+/* A frame sampled on the host by an arbitrary sampler callable (the sampler= keyword the reference CLI
+ * passes, cli/generate.py:168-174, :197-199; upstream csm-mlx applied it to every codebook's logits):
+ * after csm_frame_c0_logits, call csm_frame_host_step K times; call i (1..K) hands the host's codes[B]
+ * of codebook i-1 to the engine, which feeds them forward (as csm_frame_forced does) and runs decoder
+ * step i + its head: logits [B][V] receive codebook i's logits for calls 1..K-1; call K finishes the
+ * frame (history, EOS) and sets *all_done.  Replaces csm_frame_finish for that frame. */
+int csm_frame_host_step(csm_engine* e, const int32_t* codes, float* logits, int* all_done);
 /* Teacher-forced frame (the scoring form of trainer.py:203-318 compute_loss): the backbone step
  * consumes the previous frame, then every head stores its logits while the code fed forward is
  * codes[B][K] (the target frame).  c0_logits [B][V] and ci_logits [K-1][B][V] (optional, may be

@@ -317,10 +317,12 @@ class OracleCSM:
         return np.concatenate([audio, text], axis=-2)
 
     def frame(self, tokens, mask, cache, temperature=0.0, top_k=0, seeds=None, frame_idx=0,
-              processors=None, c0_history=None, top_p=0.0, min_p=0.0, min_keep=1):
+              processors=None, c0_history=None, top_p=0.0, min_p=0.0, min_keep=1, sampler=None):
         """generation.py:21-92.  tokens/mask (B,T,33).  Returns codes (B,K) int32.
         processors: logits processors on c0 (:44-49), called with (stack(c0_history) or zeros((0,)),
-        logits); c0 (B,1) is appended to c0_history when it is a list (:60-61)."""
+        logits); c0 (B,1) is appended to c0_history when it is a list (:60-61).
+        sampler: a callable logits (B, V) -> codes (B,) used for every codebook instead of the built-in
+        greedy / Gumbel sampler (the sampler= keyword of the reference CLI, cli/generate.py:197-199)."""
         B = tokens.shape[0]
         emb = self.embed_tokens(tokens) * mask[..., None].astype(F32)              # :34-35
         x = np.zeros(emb.shape[:2] + emb.shape[3:], F32)
@@ -336,8 +338,11 @@ class OracleCSM:
         self.debug["h_last"] = h_last
         seeds = seeds if seeds is not None else [0] * B
         flt = dict(top_p=top_p, min_p=min_p, min_keep=min_keep)
-        c0 = np.array([sample_one(c0_logits[b], temperature, top_k, seeds[b], frame_idx * self.K, **flt)
-                       for b in range(B)], dtype=np.int64)                        # :51-54
+        if sampler is not None:
+            c0 = np.asarray(sampler(c0_logits), np.int64).reshape(B)
+        else:
+            c0 = np.array([sample_one(c0_logits[b], temperature, top_k, seeds[b], frame_idx * self.K, **flt)
+                           for b in range(B)], dtype=np.int64)                    # :51-54
         out = np.zeros((B, self.K), np.int32)
         out[:, 0] = c0
         if c0_history is not None:
@@ -350,8 +355,11 @@ class OracleCSM:
                              dcache)                                               # :74-77
             logits = np.matmul(z[:, -1, :], self.w["audio_head"][i - 1]).astype(F32)   # :79 (in,out) layout
             ci_logits_all.append(logits)
-            ci = np.array([sample_one(logits[b], temperature, top_k, seeds[b], frame_idx * self.K + i, **flt)
-                           for b in range(B)], dtype=np.int64)
+            if sampler is not None:
+                ci = np.asarray(sampler(logits), np.int64).reshape(B)
+            else:
+                ci = np.array([sample_one(logits[b], temperature, top_k, seeds[b], frame_idx * self.K + i, **flt)
+                               for b in range(B)], dtype=np.int64)
             out[:, i] = ci
             dec_in = self.embed_audio(i, ci)[:, None, :]                          # :87-89
         self.debug["ci_logits"] = np.stack(ci_logits_all, axis=1)
@@ -359,7 +367,7 @@ class OracleCSM:
 
     def generate_codes(self, prompt_tokens: np.ndarray, prompt_mask: np.ndarray, max_frames: int,
                        temperature=0.0, top_k=0, seed=0, max_seq_len=2048, collect_logits=False,
-                       processors=None, top_p=0.0, min_p=0.0, min_keep=1):
+                       processors=None, top_p=0.0, min_p=0.0, min_keep=1, sampler=None):
         """generation.py:95-178 up to (not including) decode_audio.  prompt (L,33).
 
         Returns (codes (F,K) int32 up to EOS, logits list if requested)."""
@@ -372,7 +380,7 @@ class OracleCSM:
         samples, logs, c0_history = [], [], []                                     # :128
         for f in range(max_frames):                                                # :139
             s = self.frame(inp, msk, cache, temperature, top_k, [seed], f, processors, c0_history,
-                           top_p=top_p, min_p=min_p, min_keep=min_keep)
+                           top_p=top_p, min_p=min_p, min_keep=min_keep, sampler=sampler)
             if collect_logits:
                 logs.append((self.debug["c0_logits"][0].copy(), self.debug["ci_logits"][0].copy()))
             if not s.any():                                                        # :151 EOS
