@@ -47,7 +47,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, int bytes)
 // enter the matrix cores as exact bf16 integers, per stage S_g = sum q x (three products per step as
 // for bf16), folded as acc += scale * S_g + bias * X_g with X_g the stage's activation sum per row
 // (the producers' half-group sums, xs.h) -- the arithmetic of gemm_wide_kernel's int4 path.
-constexpr int Q4_WST_MAX = 16;  // stages per wave whose X_g an int4 block stages in LDS
+constexpr int Q4_XG = 64;  // stages per block whose X_g an int4 block stages in LDS (Q4_XG / XW per wave)
 constexpr int SS_MAX = 64 * 64;  // sums-of-squares partials a normed launch stages (tiles x rows)
 
 // Split-K combine by the last slice to arrive: every slice's partial tile read with 16-B sc1 loads, up
@@ -111,7 +111,7 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
     wv[i] = Q4 ? T * nks * 1024 + 16 * lane : (T * nks * 4 * 64 + lane) * 16;
     sv[i] = nt32 * nks * 1024 + (T * nks * 32 + (lane & 31)) * 4;  // int4: the lane's scale|bias words
   }
-  __shared__ __attribute__((aligned(16))) float xg[Q4 ? XW : 1][Q4 ? Q4_WST_MAX : 1][NB];
+  __shared__ __attribute__((aligned(16))) float xg[Q4 ? XW : 1][Q4 ? Q4_XG / XW : 1][NB];
   if constexpr (Q4) {  // X_g of this block's stages: the two half-group sums, in order
     for (int e = tid; e < XW * wst * NB; e += NTH) {
       const int w = e / (wst * NB), j = (e / NB) % wst, m = e % NB;
@@ -263,7 +263,8 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
   }
   // the waves' partial tiles -> ct[batch row][weight row], added in wave order.  Accumulator register
   // j of lane (r, h): batch row (j & 3) + 8 (j >> 2) + 4 h of tile t, weight row r of tile i.
-  __shared__ float red[XW][MT * RTW * 16][64];
+  constexpr int RW = XW > 4 ? 4 : XW;  // reduction slots: 8-wave blocks pre-add waves w + 4 into w
+  __shared__ float red[RW][MT * RTW * 16][64];
   __shared__ float ct[NB][NBR + 1];
   __shared__ float hb[NB][NBR / 2 + 1];
   __shared__ float rsc[NB];
@@ -282,19 +283,41 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
     if (v == 1.2345f) p.out[tid] = v;
     return;
   }
+  if constexpr (XW > 4) {  // waves 4..7 hand their tiles to waves 0..3 (added in registers)
+    if (wave >= 4) {
 #pragma unroll
-  for (int t = 0; t < MT; ++t)
+      for (int t = 0; t < MT; ++t)
 #pragma unroll
-    for (int i = 0; i < RTW; ++i)
+        for (int i = 0; i < RTW; ++i)
 #pragma unroll
-      for (int j = 0; j < 16; ++j) red[wave][(t * RTW + i) * 16 + j][lane] = acc[t][i][j];
+          for (int j = 0; j < 16; ++j) red[wave - 4][(t * RTW + i) * 16 + j][lane] = acc[t][i][j];
+    }
+    __syncthreads();
+    if (wave < 4) {
+#pragma unroll
+      for (int t = 0; t < MT; ++t)
+#pragma unroll
+        for (int i = 0; i < RTW; ++i)
+#pragma unroll
+          for (int j = 0; j < 16; ++j) acc[t][i][j] += red[wave][(t * RTW + i) * 16 + j][lane];
+    }
+    __syncthreads();
+  }
+  if (wave < RW) {
+#pragma unroll
+    for (int t = 0; t < MT; ++t)
+#pragma unroll
+      for (int i = 0; i < RTW; ++i)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) red[wave][(t * RTW + i) * 16 + j][lane] = acc[t][i][j];
+  }
   __syncthreads();
   for (int e = tid; e < NB * NBR; e += NTH) {
     const int ml = e / NBR, c = e % NBR, rr = ml & 31;
     const int idx = ((ml >> 5) * RTW + (c >> 5)) * 16 + (rr & 3) + 4 * (rr >> 3), ln = (c & 31) + 32 * ((rr >> 2) & 1);
     float v = red[0][idx][ln];
 #pragma unroll
-    for (int w = 1; w < XW; ++w) v += red[w][idx][ln];
+    for (int w = 1; w < RW; ++w) v += red[w][idx][ln];
     ct[ml][c] = v;
   }
   __syncthreads();
@@ -439,14 +462,15 @@ void xs_shape(int N, int K, int M, bool head, int& rtw, int& ks, int& pd, int& x
   // occupies) against 2: QKV 9.4 -> 7.2 us and o 8.0 -> 6.8 us at 32 bf16 rows, int4 gate/up 24.7 -> 16.1
   // and down 20.6 -> 16.1 us at 64 rows; config 4 3667 -> 3816, config 5 3501 -> 4035 frames/s
   // (profiles/r04_ab_xs_waves.txt).  Lab knob CSM_XS_WAVES=2 restores the two-wave blocks.
-  static const int waves = [] { const char* v = getenv("CSM_XS_WAVES"); return v && atoi(v) == 2 ? 2 : 4; }();
+  static const int waves = [] { const char* v = getenv("CSM_XS_WAVES"); const int w = v ? atoi(v) : 4; return w == 2 || w == 8 ? w : 4; }();
   xw = nks >= 2 * waves ? waves : 2;
   ks = 1;
   while (tiles * ks < tgt && ks < MAX_SLICES && nks / (ks * 2) >= xw && nks % (ks * 2) == 0) ks *= 2;
   const int wst = nks / ks / xw;
   // ring depth at 64 rows with 64-row tiles (lab knob CSM_XS_PD64, default 1: register budget)
   static const int cap64 = [] { const char* v = getenv("CSM_XS_PD64"); return v ? std::max(1, atoi(v)) : 1; }();
-  const int cap = M > 32 ? (rtw == 2 ? cap64 : 2) : 4;
+  int cap = M > 32 ? (rtw == 2 ? cap64 : 2) : 4;
+  if (xw == 8) cap = std::min(cap, M > 32 ? 1 : 2);  // two waves per SIMD: <= 256 registers, no spills
   pd = 1;
   while (pd * 2 <= cap && wst % (pd * 2) == 0) pd *= 2;
 }
@@ -491,11 +515,11 @@ void gemm_xs_stamps_report(const char* tag) {
 
 bool gemm_xs_eligible(int N, int K, int M, int wdt) {
   if (!(wdt == WDT_BF16 || wdt == WDT_Q4) || M < 1 || M > GEMM_XS_MAX_M || N % 2 || K % XK || K / XK < 2) return false;
-  if (wdt == WDT_Q4)  // the X_g stage table holds <= Q4_WST_MAX stages per wave
+  if (wdt == WDT_Q4)  // the X_g stage table holds <= Q4_XG stages per block
     for (int h = 0; h < 2; ++h) {
       int rtw, ks, pd, xw;
       xs_shape(N, K, M, h == 1, rtw, ks, pd, xw);
-      if (K / XK / ks / xw > Q4_WST_MAX) return false;
+      if (K / XK / ks > Q4_XG) return false;
     }
   return true;
 }
@@ -575,6 +599,7 @@ void launch_gemm_xs(const GemvParams& p0, int epi, hipStream_t st, bool nt_w, in
     p.lab_launch = n++;
   }
 #define GX_W(Q_, MT_, RTW_, PD_, NT_) do { if (xw == 4) hipLaunchKernelGGL((gemm_xs_kernel<Q_, MT_, RTW_, PD_, NT_, 4>), grid, dim3(256), 0, st, p); \
+                                             else if (xw == 8) hipLaunchKernelGGL((gemm_xs_kernel<Q_, MT_, RTW_, PD_, NT_, 8>), grid, dim3(512), 0, st, p); \
                                              else hipLaunchKernelGGL((gemm_xs_kernel<Q_, MT_, RTW_, PD_, NT_, 2>), grid, dim3(128), 0, st, p); } while (0)
 #define GX_K(Q_, MT_, RTW_, PD_) do { if (nt) GX_W(Q_, MT_, RTW_, PD_, true); else GX_W(Q_, MT_, RTW_, PD_, false); } while (0)
 #define GX_P(Q_, MT_, RTW_) do { if (pd == 4) GX_K(Q_, MT_, RTW_, (MT_ == 1 ? 4 : 2)); else if (pd == 2) GX_K(Q_, MT_, RTW_, 2); \
