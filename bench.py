@@ -250,9 +250,15 @@ def _decoder_xs(model, batch: int) -> bool:
     return 8 <= batch <= 64 and model.dtype in ("bf16", "q4") and os.environ.get("CSM_GEMM_XS", "1") != "0"
 
 
+def _backbone_xs(model, batch: int) -> bool:
+    """The batched backbone rows run on the streaming GEMM too (round 4 default; csm_engine.hip
+    bb_xs_eligible, option bb_xs / CSM_BB_XS=0 off)."""
+    return _decoder_xs(model, batch) and os.environ.get("CSM_BB_XS", "1") != "0"
+
+
 def _kernel_name(model, batch: int, stack: str) -> str:
-    if stack == "decoder" and _decoder_xs(model, batch):
-        return (f"gemm_xs_kernel<Q4={'true' if model.dtype == 'q4' else 'false'}> = decoder gate/up + SiLU*up as a "
+    if (stack == "decoder" and _decoder_xs(model, batch)) or (stack == "backbone" and _backbone_xs(model, batch)):
+        return (f"gemm_xs_kernel<Q4={'true' if model.dtype == 'q4' else 'false'}> = {stack} gate/up + SiLU*up as a "
                 f"streaming exact-split MFMA GEMM over {batch} rows (split operands written by the producers)")
     if batch >= 8 and model.dtype in ("bf16", "q4"):
         return (f"gemm_wide_kernel<Q4={'true' if model.dtype == 'q4' else 'false'}> = {stack} RMSNorm + gate/up + "
@@ -290,7 +296,7 @@ def rooflines(model, batch: int):
 
     def gemv(which, stack):
         us, nb = ctypes.c_float(0), ctypes.c_double(0)
-        xs = stack == "decoder" and _decoder_xs(model, batch)      # the kernel the frame runs (| 8: gemm_xs)
+        xs = _decoder_xs(model, batch) if stack == "decoder" else _backbone_xs(model, batch)   # the kernel the frame runs (| 8: gemm_xs)
         _lib.check(L.csm_bench_gemv(model.engine, which | (8 if xs else 0), batch, 400, ctypes.byref(us), ctypes.byref(nb)))
         return entry(us.value, nb.value, _kernel_name(model, batch, stack),
                      f"{stack}_gate_up{'_xs' if xs else ''}/{model.dtype}/B{batch}")

@@ -144,7 +144,10 @@ struct csm_engine {
   bool xs_on = [] { const char* v = getenv("CSM_GEMM_XS"); return !(v && v[0] == '0'); }();
   void *xs_D = nullptr, *xs_A = nullptr, *xs_F = nullptr;
   float* xs_ss = nullptr;
-  bool bb_xs_on = [] { const char* v = getenv("CSM_BB_XS"); return v && v[0] == '1'; }();
+  // the batched backbone on the streaming GEMM too (option bb_xs / CSM_BB_XS=0 off): with 8-wave blocks it
+  // beats gemm_wide on every backbone shape -- int4 at 64 rows gate/up 40.4 -> 22.7, down 28.2 -> 18.9,
+  // QKV 24.8 -> 18.3, o 15.8 -> 11.4 us; bf16 at 32 rows 63 -> 58 us per layer (profiles/r04_ab_xs_waves8.txt)
+  bool bb_xs_on = [] { const char* v = getenv("CSM_BB_XS"); return !(v && v[0] == '0'); }();
   float *hs_D = nullptr, *hs_A = nullptr, *hs_F = nullptr;  // int4 engines: half-group sums of the split rows
   GemmWs ws;         // split-K slabs + tickets of this engine's MFMA launches (ensure_batch sizes them)
   // persistent frame decoder (dec_frame.hip) for batch-1 greedy bf16 frames: hand-off granules, tag
@@ -469,8 +472,7 @@ void enqueue_body(csm_engine* e, hipStream_t st) {
   EmbedParams ep{};
   ep.codes = e->codes; ep.text_emb = e->text_emb; ep.audio_emb = e->audio_emb; ep.V = e->V; ep.K = e->K;
   ep.D = e->D; ep.out = e->x; ep.pos_inc = e->pos;
-  // the backbone's projections measured no faster on gemm_xs than on gemm_wide at 32-64 rows (its
-  // long-K down and QKV slower, profiles/r03_gemm_xs_shapes.txt): opt-in (option bb_xs / CSM_BB_XS=1)
+  // batched backbone rows on the streaming GEMM (round 4 default; option bb_xs / CSM_BB_XS=0: gemm_wide)
   const bool bb_xs = e->bb_xs_on && !bb_step_eligible(e) && bb_xs_eligible(e, B);
   if (bb_xs) {
     ep.xs_out = e->xs_D; ep.xs_nw = e->bb.L[0].n1; ep.ss_out = e->xs_ss; ep.ss_stride = GEMM_XS_MAX_M;

@@ -462,11 +462,12 @@ void xs_shape(int N, int K, int M, bool head, int& rtw, int& ks, int& pd, int& x
   // occupies) against 2: QKV 9.4 -> 7.2 us and o 8.0 -> 6.8 us at 32 bf16 rows, int4 gate/up 24.7 -> 16.1
   // and down 20.6 -> 16.1 us at 64 rows; config 4 3667 -> 3816, config 5 3501 -> 4035 frames/s
   // (profiles/r04_ab_xs_waves.txt).  8 (two per SIMD: one wave's loads / int4 fold overlap the other's
-  // MFMAs) for the long projections: gate/up 13.1 -> 11.6 and down 12.3 -> 11.3 us at 32 bf16 rows, int4
-  // gate/up 16.1 -> 13.8 and down 15.5 -> 13.8 us at 64 rows; the short QKV / o stay at 4 (o 6.8 vs 7.2)
-  // (profiles/r04_ab_xs_waves8.txt).  Lab knob CSM_XS_WAVES=2 / 4 / 8 forces one count everywhere.
+  // MFMAs) everywhere but the depth decoder's QKV / o at <= 32 rows (o 6.8 vs 7.2 us): gate/up 13.1 -> 11.6
+  // and down 12.3 -> 11.3 us at 32 bf16 rows, int4 gate/up 16.1 -> 13.8, down 15.5 -> 13.8, QKV 10.6 ->
+  // 9.8 us at 64 rows, the backbone's projections 4-14 % (profiles/r04_ab_xs_waves8.txt).  Lab knob
+  // CSM_XS_WAVES=2 / 4 / 8 forces one count everywhere.
   static const int waves = [] { const char* v = getenv("CSM_XS_WAVES"); const int w = v ? atoi(v) : 0; return w == 2 || w == 4 || w == 8 ? w : 0; }();
-  const int want = waves ? waves : ((N >= 4096 || K >= 4096) ? 8 : 4);
+  const int want = waves ? waves : (((size_t)N * K <= (size_t)1536 * 1024 && M <= 32) ? 4 : 8);
   xw = nks >= 2 * want ? want : (nks >= 8 ? 4 : 2);
   ks = 1;
   while (tiles * ks < tgt && ks < MAX_SLICES && nks / (ks * 2) >= xw && nks % (ks * 2) == 0) ks *= 2;

@@ -172,7 +172,7 @@ def test_streaming_decoder_matches_wide_gemm(B, dtype, bb):
     pre-split activations (gemm_xs.hip; option gemm_xs, on by default) against the same frames on
     gemm_wide_kernel: identical greedy codes, ci logits within fp32 summation-order noise (both sum
     exact fp32 products), 4 frames, csm_1b bf16 and int4; bb=1 also runs the backbone's projections
-    on it (option bb_xs, opt-in)."""
+    on it (option bb_xs, on by default since round 4; bb=0 keeps it on gemm_wide)."""
     from csm_mlx import _lib
     from csm_mlx.generation import FrameCache
     from csm_mlx.sampling import Sampler
@@ -197,7 +197,7 @@ def test_streaming_decoder_matches_wide_gemm(B, dtype, bb):
         out.append((hist.copy(), n.copy(), logs))
         del cache
     _lib.check(L.csm_set_option(model.engine, b"gemm_xs", 1))
-    _lib.check(L.csm_set_option(model.engine, b"bb_xs", 0))
+    _lib.check(L.csm_set_option(model.engine, b"bb_xs", 1))
     del model
     (h0, n0, l0), (h1, n1, l1) = out
     assert np.array_equal(n0, n1) and np.array_equal(h0, h1), "streaming decoder codes differ from gemm_wide"
