@@ -133,3 +133,30 @@ def test_bad_wav_rejected(tmp_path):
     (tmp_path / "x.wav").write_bytes(b"not a wav file at all")
     with pytest.raises(ValueError):
         read_audio(tmp_path / "x.wav", 24000)
+
+
+def test_sampler_resolution_and_host_sampler():
+    """sampler= accepts the GPU descriptor (make_sampler) and any other callable, which becomes a
+    HostSampler run on every codebook's logits (csm_frame_host_step); logprobs=True hands it
+    logits - logsumexp as mlx_lm samplers expect."""
+    import numpy as np
+    from csm_mlx.generation import _resolve_sampler
+    from csm_mlx.sampling import HostSampler, Sampler, make_sampler
+    assert _resolve_sampler(0.0, None) == Sampler(0.0, 0)
+    s = make_sampler(0.7, top_k=5)
+    assert _resolve_sampler(0.0, s) is s
+    hs = _resolve_sampler(0.0, lambda x: np.argmax(x, -1))
+    assert isinstance(hs, HostSampler) and not hs.greedy
+    logits = np.array([[0.0, 2.0, 1.0], [3.0, -1.0, 3.5]], np.float32)
+    assert hs(logits).tolist() == [1, 2] and hs(logits).dtype == np.int32
+    seen = {}
+
+    def fn(lp):
+        seen["lp"] = lp
+        return np.zeros((lp.shape[0], 1), np.int64)
+    out = HostSampler(fn, logprobs=True)(logits)
+    assert out.shape == (2,) and out.tolist() == [0, 0]
+    np.testing.assert_allclose(np.exp(seen["lp"]).sum(-1), 1.0, rtol=1e-6)
+    import pytest
+    with pytest.raises(TypeError):
+        _resolve_sampler(0.0, 3)
