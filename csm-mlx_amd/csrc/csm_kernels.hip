@@ -808,6 +808,7 @@ __device__ __forceinline__ int block_argmax(T v, int i, T* sv, int* si) {
 // make_sampler(temp, top_k) semantics with the build's counter-based RNG.  The chosen code's
 // audio embedding (embed_audio, models.py:79-80) is gathered into the next decoder input row.
 constexpr int SAMPLE_NPT = 16;  // logits per thread: V <= 4096 (checked at launch)
+constexpr int SAMPLE_CMAX = 512;  // compacted top-k survivors (more ties than this: the in-place loop)
 // The top_k-th largest of a 256-thread block's logits (lv[i] = logit tid + 256 i, i < SAMPLE_NPT):
 // radix select of its order-preserving key, 8 bits per pass; the digit is found by a parallel suffix
 // count over the 256 bins (thread t holds digit 255 - t), not a serial scan.  Every logit >= the
@@ -889,20 +890,72 @@ __global__ __launch_bounds__(256) void sample_kernel(SampleParams p) {
       const int v = tid + 256 * i;
       lv[i] = v < V ? lg[v] : 0.f;
     }
-    const float thr = (p.top_k > 0 && p.top_k < V) ? topk_threshold_256(lv, V, p.top_k, hist, wsum, sh) : -INFINITY;
+    const bool topk = p.top_k > 0 && p.top_k < V;
+    const float thr = topk ? topk_threshold_256(lv, V, p.top_k, hist, wsum, sh) : -INFINITY;
     const uint64_t key = gumbel_key(p.seeds[b], p.frame_ctr[0] * p.K + p.cb);
     const float inv_t = 1.0f / p.temperature;
     double best = -INFINITY;
     int bi = 0x7fffffff;
+    // With a top-k threshold the kept entries (k plus ties, ~2 % of the row) are compacted into LDS
+    // first, so the double-precision Gumbel noise is drawn for them alone: in place, nearly every wave
+    // had a kept entry in nearly every slot and paid the two double logs for all 16 slots.  The
+    // winner is the same -- max perturbed value, lowest index on ties -- whatever the visiting order.
+    __shared__ int cidx[SAMPLE_CMAX];
+    __shared__ float clv[SAMPLE_CMAX];
+    __shared__ int wcnt[4];
+    int kept_n = SAMPLE_CMAX + 1;
+    if (topk) {
+      const int lane = tid & 63, wave = tid >> 6;
+      const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+      uint64_t mk[SAMPLE_NPT];
+      int mine = 0;
 #pragma unroll
-    for (int i = 0; i < SAMPLE_NPT; ++i) {
-      const int v = tid + 256 * i;
-      const float l = lv[i];
-      if (v >= V || !(l >= thr)) continue;
-      const double val = gumbel_perturbed(l, inv_t, key, v);
-      if (val > best) {
-        best = val;
-        bi = v;
+      for (int i = 0; i < SAMPLE_NPT; ++i) {
+        mk[i] = __ballot(tid + 256 * i < V && lv[i] >= thr);
+        mine += __popcll(mk[i]);
+      }
+      if (lane == 0) wcnt[wave] = mine;
+      __syncthreads();
+      int base = 0;
+      kept_n = 0;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        base += w < wave ? wcnt[w] : 0;
+        kept_n += wcnt[w];
+      }
+      if (kept_n <= SAMPLE_CMAX) {
+#pragma unroll
+        for (int i = 0; i < SAMPLE_NPT; ++i) {
+          if ((mk[i] >> lane) & 1ull) {
+            const int at = base + __popcll(mk[i] & below);
+            cidx[at] = tid + 256 * i;
+            clv[at] = lv[i];
+          }
+          base += __popcll(mk[i]);
+        }
+      }
+      __syncthreads();
+    }
+    if (kept_n <= SAMPLE_CMAX) {
+      for (int j = tid; j < kept_n; j += 256) {
+        const int v = cidx[j];
+        const double val = gumbel_perturbed(clv[j], inv_t, key, v);
+        if (val > best || (val == best && v < bi)) {
+          best = val;
+          bi = v;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < SAMPLE_NPT; ++i) {
+        const int v = tid + 256 * i;
+        const float l = lv[i];
+        if (v >= V || !(l >= thr)) continue;
+        const double val = gumbel_perturbed(l, inv_t, key, v);
+        if (val > best) {
+          best = val;
+          bi = v;
+        }
       }
     }
     code = block_argmax<double>(best, bi, sdv, si);
