@@ -754,7 +754,7 @@ void ensure_batch(csm_engine* e, int B) {
     e->xs_A = e->balloc(bA);
     e->xs_F = e->balloc(bF);
     e->xs_ss = (float*)e->balloc((size_t)64 * xm * 4);
-    for (float** h : {&e->hs_D, &e->hs_A, &e->hs_F}) *h = (float*)e->balloc(bF / 6 / xm / 32 * xs::HS_ROWS * 4 + 4096);
+    for (float** h : {&e->hs_D, &e->hs_A, &e->hs_F}) *h = (float*)e->balloc(bF / xs::XS_EB / xm / 32 * xs::HS_ROWS * 4 + 4096);
   }
 }
 

@@ -622,17 +622,21 @@ __device__ __forceinline__ void attn_block(const AttnParams& p, int m, int kvh, 
 }
 
 // Short causal attention (depth decoder: <= 32 cached positions, generation.py:70-77): one wave per
-// (row, q head); lanes (key j, half of the head dims) compute the scores, lane d owns output dims
-// d + 64 i.  Every K half-row and V column slice is loaded up front (16-B / 4-B loads straight to
-// VGPRs) -- one memory round trip instead of attn_block's staged chunk pipeline.  fp32 throughout:
-// scores, softmax (max-subtracted, one pass: all keys fit one wave), P.V in key order.  With g_tab
-// set (decoder layer 0, codebook steps >= 2) the row's q and its key/value at pos come from the
-// folded layer-0 table (see AttnParams).
+// (row, q head); lanes (key j, half of the head dims) compute the scores.  Every K half-row and V row
+// is loaded up front with 16-B loads straight to VGPRs -- one memory round trip instead of
+// attn_block's staged chunk pipeline.  P.V (as dec_frame's DF_PV 2): lane = (key half kv = lane >> 5:
+// keys 16 kv .. 16 kv + 15, dims 4 dq .. 4 dq + 3, dq = lane & 31), so a key's V row is one 16-B load
+// per lane (16 loads per wave instead of 64 of 4 B); each half sums its keys in order and the halves
+// are added once (keys 0-15 first); lanes dq < 32 return dims 4 dq .. 4 dq + 3.  fp32 throughout:
+// scores, softmax (max-subtracted, one pass: all keys fit one wave).  With g_tab set (decoder layer 0,
+// codebook steps >= 2) the row's q and its key/value at pos come from the folded layer-0 table (see
+// AttnParams).
 template <int HD, int NMAX>
 __device__ __forceinline__ void attn_short_head(const AttnParams& p, int m, int h, int lane, float* qsh,
-                                                float (&o)[HD / 64], bool write_kv, bool write_code, bool copy_res,
+                                                float (&o)[4], bool write_kv, bool write_code, bool copy_res,
                                                 int* code_out) {
-  constexpr int V4 = HD / 4, NO = HD / 64;
+  static_assert(HD == 128 && NMAX == 32, "key halves of 16 x 32 lanes x 4 dims");
+  constexpr int V4 = HD / 4;
   const int G = p.Hq / p.Hkv, kvh = h / G;
   const int b = p.rm.b(m), pos = p.rm.pos(m);
   const int n = pos + 1;
@@ -650,11 +654,13 @@ __device__ __forceinline__ void attn_short_head(const AttnParams& p, int m, int 
   const f32x4* ksrc = reinterpret_cast<const f32x4*>(K + (size_t)jl * HD + hh * (HD / 2));
 #pragma unroll
   for (int d4 = 0; d4 < H4; ++d4) kr[d4] = ksrc[d4];
-  float vv[NMAX][NO];
+  const int kv = lane >> 5, dq = lane & 31;
+  f32x4 vv[NMAX / 2];
 #pragma unroll
-  for (int j = 0; j < NMAX; ++j)
-#pragma unroll
-    for (int i = 0; i < NO; ++i) vv[j][i] = (j < jc) ? V[(size_t)j * HD + lane + 64 * i] : 0.f;
+  for (int u = 0; u < NMAX / 2; ++u) {
+    const int j = 16 * kv + u;
+    vv[u] = (j < jc) ? *reinterpret_cast<const f32x4*>(V + (size_t)j * HD + 4 * dq) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
   const float* qrow = p.q + (size_t)m * p.qs;
   if (gath) {
     const unsigned long long best = wave_argmax_partials(p.g_part + (size_t)b * p.g_part_stride, p.g_part_n, lane);
@@ -671,10 +677,8 @@ __device__ __forceinline__ void attn_short_head(const AttnParams& p, int m, int 
       for (int d4 = 0; d4 < H4; ++d4) kr[d4] = t4[d4];
     }
 #pragma unroll
-    for (int j = 0; j < NMAX; ++j)
-      if (j == pos)
-#pragma unroll
-        for (int i = 0; i < NO; ++i) vv[j][i] = tv[lane + 64 * i];
+    for (int u = 0; u < NMAX / 2; ++u)
+      if (16 * kv + u == pos) vv[u] = *reinterpret_cast<const f32x4*>(tv + 4 * dq);
     if (write_kv && h % G == 0) {  // this kv head's K/V row at pos -> cache (read by the later codebook steps)
       float* kd = const_cast<float*>(K) + (size_t)pos * HD;
       float* vd = const_cast<float*>(V) + (size_t)pos * HD;
@@ -716,37 +720,48 @@ __device__ __forceinline__ void attn_short_head(const AttnParams& p, int m, int 
   const float new_m = wave_max(s);
   const float pj = (kj < n) ? expf(s - new_m) : 0.f;
   const float l_run = wave_sum(hh == 0 ? pj : 0.f);
-#pragma unroll
-  for (int i = 0; i < NO; ++i) o[i] = 0.f;
   const int pji = __float_as_int(pj);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int j = 0; j < NMAX; ++j) {
-    if (j < n) {
-      const float pb = __int_as_float(__builtin_amdgcn_readlane(pji, j));
-#pragma unroll
-      for (int i = 0; i < NO; ++i) o[i] = fmaf(pb, vv[j][i], o[i]);
+  for (int u = 0; u < NMAX / 2; ++u) {
+    const float pa = __int_as_float(__builtin_amdgcn_readlane(pji, u));
+    const float pb = __int_as_float(__builtin_amdgcn_readlane(pji, 16 + u));
+    const float pw = kv ? pb : pa;
+    if (16 * kv + u < n) {
+      acc.x = fmaf(pw, vv[u].x, acc.x);
+      acc.y = fmaf(pw, vv[u].y, acc.y);
+      acc.z = fmaf(pw, vv[u].z, acc.z);
+      acc.w = fmaf(pw, vv[u].w, acc.w);
     }
   }
   const float inv = 1.f / l_run;
-#pragma unroll
-  for (int i = 0; i < NO; ++i) o[i] = o[i] * inv;
+  const float t0 = __shfl_xor(acc.x, 32, 64), t1 = __shfl_xor(acc.y, 32, 64), t2 = __shfl_xor(acc.z, 32, 64),
+              t3 = __shfl_xor(acc.w, 32, 64);
+  o[0] = (acc.x + t0) * inv;  // (lanes < 32: keys 0-15 + keys 16-31)
+  o[1] = (acc.y + t1) * inv;
+  o[2] = (acc.z + t2) * inv;
+  o[3] = (acc.w + t3) * inv;
 }
 
 template <int HD, int NMAX>
 __global__ __launch_bounds__(64) void attn_short_kernel(AttnParams p) {
   __shared__ __attribute__((aligned(16))) float qsh[HD];
-  const int m = blockIdx.x / p.Hq, h = blockIdx.x % p.Hq;
-  float o[HD / 64];
-  attn_short_head<HD, NMAX>(p, m, h, threadIdx.x, qsh, o, true, true, true, nullptr);
-  float* out = p.out + (size_t)m * p.os + h * HD;
+  const int m = blockIdx.x / p.Hq, h = blockIdx.x % p.Hq, lane = threadIdx.x, dq = lane & 31;
+  float o[4];
+  attn_short_head<HD, NMAX>(p, m, h, lane, qsh, o, true, true, true, nullptr);
+  // half-group sums for an int4 o_proj: 32 columns = 8 lanes, each lane's 4 in column order, then
+  // the lanes' sums in a butterfly (lanes 32-63 mirror 0-31 and store nothing)
+  float hsum = (o[0] + o[1]) + (o[2] + o[3]);
 #pragma unroll
-  for (int i = 0; i < HD / 64; ++i) out[threadIdx.x + 64 * i] = o[i];
-  if (p.xs_out)  // split for the streaming o_proj GEMM (gemm_xs.hip)
-#pragma unroll
-    for (int i = 0; i < HD / 64; ++i) {
-      xs::store1(p.xs_out, p.xs_K, m, h * HD + threadIdx.x + 64 * i, o[i]);
-      if (p.hs_out) xs_half_sum(p.hs_out, m, h * HD + 64 * i, o[i], threadIdx.x);
+  for (int x = 1; x < 8; x <<= 1) hsum += __shfl_xor(hsum, x, 64);
+  if (lane < 32) {
+    float* out = p.out + (size_t)m * p.os + h * HD + 4 * dq;
+    *reinterpret_cast<float4*>(out) = make_float4(o[0], o[1], o[2], o[3]);
+    if (p.xs_out) {  // the operand of the streaming o_proj GEMM (gemm_xs.hip)
+      xs::store4(p.xs_out, p.xs_K, m, h * HD + 4 * dq, o);
+      if (p.hs_out && (dq & 7) == 0) p.hs_out[(size_t)((h * HD + 4 * dq) / 32) * xs::HS_ROWS + m] = hsum;
     }
+  }
 }
 
 template <int HD>

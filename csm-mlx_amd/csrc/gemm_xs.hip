@@ -6,7 +6,8 @@
 // projections are latency- and VALU-bound there -- every block re-normalises and re-splits the
 // same fp32 activation rows into three bf16 parts through LDS with a barrier per 64-K stage, at one
 // wave per SIMD.  Here the producer of a row block (the previous projection's epilogue, the
-// attention, the row gather) writes it ONCE already split, in MFMA fragment order (xs.h); every
+// attention, the row gather) writes it ONCE in MFMA fragment order (xs.h: fp32, split into the three
+// parts in registers by the consumer); every
 // block then streams both operands straight into registers through a ring of PD stages whose loads
 // are pinned at issue (compiler barrier: no sinking to the use), with no LDS and no barrier in the
 // K loop.  Lab (profiles/r03_lab_gemm_stream.txt): decoder gate/up at 32 rows 8.8 us against
@@ -123,7 +124,16 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
   struct St {
     u32x4_t w[RTW][Q4 ? 1 : 4];
     uint32_t sb[RTW];
-    u32x4_t a[MT][3][4];
+    u32x4_t a[MT][XS_F32 ? 4 : 3][XS_F32 ? 2 : 4];  // XS_F32: [t][s][half] fp32; else [t][part][s]
+  };
+  // the three bf16 parts of row tile t, step s (XS_F32: split here from the fp32 fragment)
+  auto parts = [&](const St& g, int t, int s, u32x4_t (&pt)[3]) {
+    if constexpr (XS_F32 != 0) {
+      xs::split_frag(g.a[t][s][0], g.a[t][s][1], pt);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 3; ++q) pt[q] = g.a[t][q][s];
+    }
   };
   // stage j of this wave (j >= wst: zero-sized descriptors, no traffic) -- straight-line loads
   auto load = [&](int j, St& g) {
@@ -147,12 +157,21 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
       }
     }
 #pragma unroll
-    for (int t = 0; t < MT; ++t)
-#pragma unroll
-      for (int q = 0; q < 3; ++q)
+    for (int t = 0; t < MT; ++t) {
+      if constexpr (XS_F32 != 0) {
 #pragma unroll
         for (int s = 0; s < 4; ++s)
-          g.a[t][q][s] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(ar, lane * 16, ((t * nks + st) * 12 + q * 4 + s) * 1024, 0));
+#pragma unroll
+          for (int hf = 0; hf < 2; ++hf)
+            g.a[t][s][hf] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(ar, lane * 16, (((t * nks + st) * 4 + s) * 2 + hf) * 1024, 0));
+      } else {
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+#pragma unroll
+          for (int s = 0; s < 4; ++s)
+            g.a[t][q][s] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(ar, lane * 16, ((t * nks + st) * 12 + q * 4 + s) * 1024, 0));
+      }
+    }
   };
   f32x16_t acc[MT][RTW];
 #pragma unroll
@@ -208,13 +227,19 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
           bf16x8_t b[RTW];
 #pragma unroll
           for (int i = 0; i < RTW; ++i) b[i] = __builtin_bit_cast(bf16x8_t, xs::q4_word_bf16(g[d].w[i][0][s]));
+          // (row tiles have their own accumulators: t outside q gives every accumulator the same
+          // MFMA sequence as q outside t, with one tile's parts live at a time)
 #pragma unroll
-          for (int q = 0; q < 3; ++q)
+          for (int t = 0; t < MT; ++t) {
+            u32x4_t pt[3];
+            parts(g[d], t, s, pt);
 #pragma unroll
-            for (int t = 0; t < MT; ++t)
+            for (int q = 0; q < 3; ++q)
 #pragma unroll
               for (int i = 0; i < RTW; ++i)
-                gq[t][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, g[d].a[t][q][s]), b[i], gq[t][i], 0, 0, 0);
+                gq[t][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, pt[q]), b[i], gq[t][i], 0, 0, 0);
+            if constexpr (XS_F32 != 0 && MT > 1) __builtin_amdgcn_sched_barrier(0);  // one tile's parts live at a time (no spills)
+          }
         }
         const int jst = j0 + d;
 #pragma unroll
@@ -238,24 +263,31 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
       } else if constexpr ((XS_LAB & 1) != 0) {  // lab: operands consumed by one VALU op each, no MFMA
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
+          u32x4_t pt[MT][3];
+#pragma unroll
+          for (int t = 0; t < MT; ++t) parts(g[d], t, s, pt[t]);
 #pragma unroll
           for (int q = 0; q < 3; ++q)
 #pragma unroll
-            for (int t = 0; t < MT; ++t) acc[t][0][s] += __uint_as_float(g[d].a[t][q][s].x ^ g[d].a[t][q][s].w);
+            for (int t = 0; t < MT; ++t) acc[t][0][s] += __uint_as_float(pt[t][q].x ^ pt[t][q].w);
 #pragma unroll
           for (int i = 0; i < RTW; ++i) acc[0][i][4 + s] += __uint_as_float(g[d].w[i][s].y ^ g[d].w[i][s].z);
         }
       } else {
 #pragma unroll
-        for (int s = 0; s < 4; ++s)
+        for (int s = 0; s < 4; ++s) {
 #pragma unroll
-          for (int q = 0; q < 3; ++q)
+          for (int t = 0; t < MT; ++t) {  // (t outside q: the same MFMA sequence per accumulator)
+            u32x4_t pt[3];
+            parts(g[d], t, s, pt);
 #pragma unroll
-            for (int t = 0; t < MT; ++t)
+            for (int q = 0; q < 3; ++q)
 #pragma unroll
               for (int i = 0; i < RTW; ++i)
-                acc[t][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, g[d].a[t][q][s]),
+                acc[t][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, pt[q]),
                                                                      __builtin_bit_cast(bf16x8_t, g[d].w[i][s]), acc[t][i], 0, 0, 0);
+          }
+        }
       }
       load(j0 + d + PD, g[d]);
       asm volatile("" ::: "memory");
