@@ -86,22 +86,22 @@ __device__ __forceinline__ float row16_sum(float v) {
 constexpr int GP_RSRC3 = 0x00020000;  // buffer descriptor word 3 (raw 32-bit format)
 constexpr int GP_SC1 = 16;            // cache policy: sc1 (agent-coherent, as __hip_atomic_load/store)
 constexpr int GP_NT = 2;              // cache policy: non-temporal
-template <int KS, int NB, int NBR>
+template <int KS, int NB, int NBR, int NTH>
 __device__ __forceinline__ void gp_combine(__amdgpu_buffer_rsrc_t rs, float (*ct)[NBR + 1], float* ssb,
                                            int mrows, bool norm, int slab_f, int tid) {
   constexpr int U = KS >= 16 ? 1 : 16 / KS;
   const int nq = mrows * (NBR / 4);
-  for (int q0 = tid; q0 < nq; q0 += 256 * U) {
+  for (int q0 = tid; q0 < nq; q0 += NTH * U) {
     f32x4_t v[U][KS];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int q = min(q0 + 256 * u, nq - 1);
+      const int q = min(q0 + NTH * u, nq - 1);
 #pragma unroll
       for (int s = 0; s < KS; ++s) v[u][s] = __builtin_amdgcn_raw_buffer_load_b128(rs, q * 16, s * slab_f * 4, GP_SC1);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int q = q0 + 256 * u;
+      const int q = q0 + NTH * u;
       if (q < nq) {
         f32x4_t sum = v[u][0];
 #pragma unroll
@@ -126,15 +126,17 @@ __device__ __forceinline__ void gp_combine(__amdgpu_buffer_rsrc_t rs, float (*ct
   }
 }
 
-// Block = 4 waves over NBR weight rows x 32*MT batch rows x one K slice, stages of 64 K (one int4
-// group).  The activations are the MFMA A operand (rows = batch rows), the weights the B operand
+// Block = NW waves (4; 8 for long prompts: two per SIMD, so one wave's staging / int4 fold runs
+// beside the other's MFMAs) over NBR weight rows x 32*MT batch rows x one K slice, stages of 64 K
+// (one int4 group).  The activations are the MFMA A operand (rows = batch rows), the weights the B operand
 // (columns = weight rows): every lane's 16 accumulators then share ONE weight row, whose int4
 // scale / bias it loaded itself.  Weights go global -> registers in fragment order (no LDS): with
 // the K order permuted inside a stage (step s, half h <-> k = 32h + 8s + j, the same permutation on
 // both operands) lane (r, h) reads 64 contiguous bytes of weight row r per bf16 stage (16 for int4).
 // Activations go global -> registers -> (RMSNorm weight, sum of squares, hi/mid/lo split) -> LDS
-// once per stage and are shared by the block's NBR / 32 row tiles.  NBR = 256: 2 row tiles per
-// wave; 128: one; 64: two waves per row tile split each stage's steps (summed in a fixed order).
+// once per stage and are shared by the block's NBR / 32 row tiles.  4 waves: NBR = 256: 2 row tiles
+// per wave; 128: one; 64: two waves per row tile split each stage's steps (summed in a fixed order);
+// 8 waves: 256: one row tile per wave; 128 / 64: 2 / 4 waves per row tile.
 #ifdef GEMM_STAMPS  // lab build only (tools/variant.sh ... -DGEMM_STAMPS): per-block phase clocks
 __device__ unsigned long long g_gemm_stamps[1024][6];
 #define GSTAMP(i) do { if (threadIdx.x == 0 && blin < 1024) g_gemm_stamps[blin][i] = __builtin_amdgcn_s_memrealtime(); } while (0)
@@ -145,12 +147,16 @@ extern "C" int csm_gemm_stamps(unsigned long long* out, int n) {
 #define GSTAMP(i) do {} while (0)
 #endif
 
-template <bool Q4, int MT, int NBR, int PD, bool NT>
-__global__ __launch_bounds__(256) void gemm_wide_kernel(GemvParams p) {
-  constexpr int NB = MT * 32;
-  constexpr int KW = NBR == 64 ? 2 : 1;    // waves per row tile
-  constexpr int RTW = NBR == 256 ? 2 : 1;  // row tiles per wave
-  constexpr int NS = 4 / KW;               // k-steps per wave per stage
+template <bool Q4, int MT, int NBR, int PD, bool NT, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void gemm_wide_kernel(GemvParams p) {
+  constexpr int NB = MT * 32, NTH = 64 * NW;
+  constexpr int NTILE = NBR / 32;                            // 32-row tiles of the block
+  constexpr int RTW = NTILE > NW ? NTILE / NW : 1;           // row tiles per wave
+  constexpr int KW = NW > NTILE ? NW / NTILE : 1;            // waves per row tile (they split the steps)
+  constexpr int NGRP = NTILE / RTW;                          // wave groups (one per RTW row tiles)
+  constexpr int NS = 4 / KW;                                 // k-steps per wave per stage
+  constexpr int RPT = NTH / 16, NI = NB / RPT;               // activation staging: rows per pass, passes
+  static_assert(NI >= 1 && NS >= 1 && NGRP * KW == NW, "wave layout");
   constexpr int SLOTS = 65;                // 16-B slots per (part, batch tile, step) block: lane l at l + l / 32
   constexpr int XS_BYTES = 2 * 3 * MT * 4 * SLOTS * 16;
   constexpr int CT_BYTES = NB * (NBR + 1) * 4;
@@ -174,8 +180,8 @@ __global__ __launch_bounds__(256) void gemm_wide_kernel(GemvParams p) {
   const int mc = blockIdx.z, m0 = mc * NB, nchunks = gridDim.z;
   const int Kblk = p.K / p.ksplit, kslice = blockIdx.y * Kblk, nst = Kblk / GP_KC;
   const bool norm = p.nw != nullptr;
-  const int kh = KW == 2 ? (wave >> 1) : 0;
-  const int rt0 = KW == 2 ? (wave & 1) : wave * RTW;
+  const int kh = wave / NGRP;
+  const int rt0 = (wave % NGRP) * RTW;
   // this lane's weight bytes in the fragment-tiled copy (gemm_retile): row tile T, stage kst at
   // T * nks + kst blocks of 4 KB (bf16; + 1 KB per step) or 1 KB (int4; scale|bias words after)
   const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.Wt), 0, 0x7fffffff, GP_RSRC3);
@@ -190,13 +196,13 @@ __global__ __launch_bounds__(256) void gemm_wide_kernel(GemvParams p) {
   // activation staging map: thread -> batch row x_c + 16 i, k x_k4 .. x_k4 + 3 of the stage
   const int x_c = tid >> 4, x_k4 = (tid & 15) * 4;
   const int st_h = x_k4 >> 5, st_s = (x_k4 >> 3) & 3, st_j = (x_k4 >> 2) & 1;
-  float ss[NB / 16];
+  float ss[NI];
 #pragma unroll
-  for (int i = 0; i < NB / 16; ++i) ss[i] = 0.f;
+  for (int i = 0; i < NI; ++i) ss[i] = 0.f;
   struct Stage {
     u32x4_t w[RTW][Q4 ? 1 : NS];
     uint32_t sb[RTW];
-    f32x4_t xr[NB / 16];
+    f32x4_t xr[NI];
     f32x4_t nwr;
   };
   Stage sg[PD];
@@ -209,15 +215,15 @@ __global__ __launch_bounds__(256) void gemm_wide_kernel(GemvParams p) {
   const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p.x), 0, 0x7fffffff, GP_RSRC3);
   const __amdgpu_buffer_rsrc_t nrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(nwp), 0, 0x7fffffff, GP_RSRC3);
   const __amdgpu_buffer_rsrc_t zrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.Wt), 0, 0, GP_RSRC3);
-  int xv[NB / 16];
+  int xv[NI];
 #pragma unroll
-  for (int i = 0; i < NB / 16; ++i) xv[i] = (min(m0 + x_c + 16 * i, p.M - 1) * p.xs + x_k4) * 4;
+  for (int i = 0; i < NI; ++i) xv[i] = (min(m0 + x_c + RPT * i, p.M - 1) * p.xs + x_k4) * 4;
   auto load = [&](int st, Stage& g) {
     const bool live = st < nst;
     const int kc = kslice + (live ? st : 0) * GP_KC;
     const __amdgpu_buffer_rsrc_t xr = live ? xrs : zrs, nr = live ? nrs : zrs, wr = live ? wrs : zrs;
 #pragma unroll
-    for (int i = 0; i < NB / 16; ++i) g.xr[i] = __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(xr, xv[i], kc * 4, 0));
+    for (int i = 0; i < NI; ++i) g.xr[i] = __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(xr, xv[i], kc * 4, 0));
     g.nwr = __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(nr, x_k4 * 4, kc * 4, 0));
 #pragma unroll
     for (int i = 0; i < RTW; ++i) {
@@ -232,8 +238,8 @@ __global__ __launch_bounds__(256) void gemm_wide_kernel(GemvParams p) {
   };
   auto store = [&](const Stage& g, int buf, bool live) {
 #pragma unroll
-    for (int i = 0; i < NB / 16; ++i) {
-      const int c = x_c + 16 * i;
+    for (int i = 0; i < NI; ++i) {
+      const int c = x_c + RPT * i;
       float v[4] = {g.xr[i].x, g.xr[i].y, g.xr[i].z, g.xr[i].w};
       if (norm) {
         const float nw4[4] = {g.nwr.x, g.nwr.y, g.nwr.z, g.nwr.w};
@@ -283,8 +289,10 @@ __global__ __launch_bounds__(256) void gemm_wide_kernel(GemvParams p) {
         bf16x8_t b[RTW];
 #pragma unroll
         for (int i = 0; i < RTW; ++i) {
-          if constexpr (Q4) {  // (KW = 2: the wave's half of the 4 words, selected without indexing)
-            const uint32_t word = KW == 2 ? (kh ? g.w[i][0][NS + s] : g.w[i][0][s]) : g.w[i][0][s];
+          if constexpr (Q4) {  // (KW > 1: the wave's share of the 4 words, selected without indexing)
+            uint32_t word = g.w[i][0][s];
+            if constexpr (KW == 2) word = kh ? g.w[i][0][NS + s] : g.w[i][0][s];
+            if constexpr (KW == 4) word = kh == 0 ? g.w[i][0][0] : (kh == 1 ? g.w[i][0][1] : (kh == 2 ? g.w[i][0][2] : g.w[i][0][3]));
             b[i] = __builtin_bit_cast(bf16x8_t, xs::q4_word_bf16(word));
           } else {
             b[i] = __builtin_bit_cast(bf16x8_t, g.w[i][s]);
@@ -338,9 +346,9 @@ __global__ __launch_bounds__(256) void gemm_wide_kernel(GemvParams p) {
   // sum of squares per batch row: the 16 threads of a row share it
   if (norm) {
 #pragma unroll
-    for (int i = 0; i < NB / 16; ++i) {
+    for (int i = 0; i < NI; ++i) {
       const float v = row16_sum(ss[i]);
-      if ((tid & 15) == 0) ssb[x_c + 16 * i] = v;
+      if ((tid & 15) == 0) ssb[x_c + RPT * i] = v;
     }
   }
   // accumulators -> C tile [batch row][weight row]; lane (r, h) register j: batch row
@@ -354,8 +362,9 @@ __global__ __launch_bounds__(256) void gemm_wide_kernel(GemvParams p) {
         for (int j = 0; j < 16; ++j) ct[32 * t + (j & 3) + 8 * (j >> 2) + 4 * h][32 * (rt0 + i) + r] = acc[t][i][j];
   }
   __syncthreads();
-  if constexpr (KW == 2) {  // second half of the steps, added in a fixed order
-    if (kh == 1) {
+#pragma unroll
+  for (int kk = 1; kk < KW; ++kk) {  // the later step shares, added in a fixed order
+    if (kh == kk) {
 #pragma unroll
       for (int t = 0; t < MT; ++t)
 #pragma unroll
@@ -370,7 +379,7 @@ __global__ __launch_bounds__(256) void gemm_wide_kernel(GemvParams p) {
     float* slab = p.kpart + ((size_t)(tile * nchunks + mc) * p.ksplit) * slab_f;
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(slab, 0, p.ksplit * slab_f * 4, GP_RSRC3);
     const int mine = blockIdx.y * slab_f * 4;
-    for (int q = tid; q < mrows * (NBR / 4); q += 256) {
+    for (int q = tid; q < mrows * (NBR / 4); q += NTH) {
       const int ml = q / (NBR / 4), j = (q % (NBR / 4)) * 4;
       const f32x4_t v = {ct[ml][j], ct[ml][j + 1], ct[ml][j + 2], ct[ml][j + 3]};
       __builtin_amdgcn_raw_buffer_store_b128(v, rs, q * 16, mine, GP_SC1);
@@ -388,14 +397,14 @@ __global__ __launch_bounds__(256) void gemm_wide_kernel(GemvParams p) {
     GSTAMP(3);
     if (!last) return;
     switch (p.ksplit) {
-      case 2: gp_combine<2, NB, NBR>(rs, ct, ssb, mrows, norm, slab_f, tid); break;
-      case 4: gp_combine<4, NB, NBR>(rs, ct, ssb, mrows, norm, slab_f, tid); break;
-      case 8: gp_combine<8, NB, NBR>(rs, ct, ssb, mrows, norm, slab_f, tid); break;
-      default: gp_combine<16, NB, NBR>(rs, ct, ssb, mrows, norm, slab_f, tid); break;
+      case 2: gp_combine<2, NB, NBR, NTH>(rs, ct, ssb, mrows, norm, slab_f, tid); break;
+      case 4: gp_combine<4, NB, NBR, NTH>(rs, ct, ssb, mrows, norm, slab_f, tid); break;
+      case 8: gp_combine<8, NB, NBR, NTH>(rs, ct, ssb, mrows, norm, slab_f, tid); break;
+      default: gp_combine<16, NB, NBR, NTH>(rs, ct, ssb, mrows, norm, slab_f, tid); break;
     }
     __syncthreads();
   }
-  for (int e = tid; e < mrows * (NBR / 2); e += 256) {
+  for (int e = tid; e < mrows * (NBR / 2); e += NTH) {
     const int ml = e / (NBR / 2), rp = (e % (NBR / 2)) * 2;
     const int n = n0 + rp;
     float va = ct[ml][rp], vb = ct[ml][rp + 1];
@@ -476,6 +485,15 @@ static size_t gemm_need(int N, int K, int M, bool q4, size_t& tk) {
 
 static constexpr int gemm_pd_cap(bool q4, int mt, int nbr) { return nbr == 256 ? ((q4 && mt == 2) ? 2 : 4) : ((mt == 2 || q4) ? 4 : 8); }
 
+// 8-wave blocks (two waves per SIMD: one wave's activation staging and int4 fold beside the other's
+// MFMAs) for long prompts (>= GEMM_W8_MIN_M rows: the prompt prefill), where the 4-wave block holds
+// 256 VGPRs + AGPRs at one wave per SIMD.  CSM_GEMM_W8=0: always 4 (A/B).
+constexpr int GEMM_W8_MIN_M = 256;
+static bool gemm_w8(int M) {
+  static const bool on = [] { const char* e = getenv("CSM_GEMM_W8"); return !e || atoi(e) != 0; }();
+  return on && M >= GEMM_W8_MIN_M;
+}
+
 void launch_gemm_mfma(const GemvParams& p0, int wdt, bool nt, hipStream_t st) {
   GemvParams p = p0;
   const bool q4 = wdt == WDT_Q4;
@@ -510,8 +528,10 @@ void launch_gemm_mfma(const GemvParams& p0, int wdt, bool nt, hipStream_t st) {
   const int pd_cap = gemm_pd_cap(wdt == WDT_Q4, MT, nbr);
   int pd = 1;  // the deepest ring within the cap that divides the stage count
   while (pd * 2 <= pd_cap && nst % (pd * 2) == 0) pd *= 2;
-#define GW_K(Q_, MT_, NBR_, PD_) do { if (nt) hipLaunchKernelGGL((gemm_wide_kernel<Q_, MT_, NBR_, PD_, true>), g3, dim3(256), 0, st, p); \
-                                      else hipLaunchKernelGGL((gemm_wide_kernel<Q_, MT_, NBR_, PD_, false>), g3, dim3(256), 0, st, p); } while (0)
+  const bool w8 = MT == 2 && gemm_w8(p.M);
+#define GW_W(Q_, MT_, NBR_, PD_, NT_) do { if (w8 && MT_ == 2) hipLaunchKernelGGL((gemm_wide_kernel<Q_, MT_, NBR_, (PD_ > 2 ? 2 : PD_), NT_, 8>), g3, dim3(512), 0, st, p); \
+                                           else hipLaunchKernelGGL((gemm_wide_kernel<Q_, MT_, NBR_, PD_, NT_>), g3, dim3(256), 0, st, p); } while (0)
+#define GW_K(Q_, MT_, NBR_, PD_) do { if (nt) GW_W(Q_, MT_, NBR_, PD_, true); else GW_W(Q_, MT_, NBR_, PD_, false); } while (0)
 #define GW_C(Q_, MT_, NBR_, PD_) (PD_ < gemm_pd_cap(Q_, MT_, NBR_) ? PD_ : gemm_pd_cap(Q_, MT_, NBR_))
 #define GW_P(Q_, MT_, NBR_) do { if (pd == 8) GW_K(Q_, MT_, NBR_, GW_C(Q_, MT_, NBR_, 8)); else if (pd == 4) GW_K(Q_, MT_, NBR_, GW_C(Q_, MT_, NBR_, 4)); \
                                  else if (pd == 2) GW_K(Q_, MT_, NBR_, 2); else GW_K(Q_, MT_, NBR_, 1); } while (0)
@@ -522,6 +542,7 @@ void launch_gemm_mfma(const GemvParams& p0, int wdt, bool nt, hipStream_t st) {
 #undef GW_C
 #undef GW_P
 #undef GW_K
+#undef GW_W
 }
 
 // ---------------------------------------------------------------------------- tiled weight copies

@@ -295,7 +295,11 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
   }
   // the waves' partial tiles -> ct[batch row][weight row], added in wave order.  Accumulator register
   // j of lane (r, h): batch row (j & 3) + 8 (j >> 2) + 4 h of tile t, weight row r of tile i.
-  constexpr int RW = XW > 4 ? 4 : XW;  // reduction slots: 8-wave blocks pre-add waves w + 4 into w
+  // reduction slots: one per wave where the slab fits 64 KB (then every wave stores once and the
+  // ct pass adds (w, w + 4) pairs in the pre-add's order -- one barrier and one LDS round trip
+  // fewer, same sums); else 8-wave blocks pre-add waves w + 4 into w through 4 slots
+  constexpr bool RED_ALL = XW > 4 && MT * RTW * 16 * 64 * 4 * XW <= 65536;
+  constexpr int RW = RED_ALL ? XW : (XW > 4 ? 4 : XW);
   __shared__ float red[RW][MT * RTW * 16][64];
   __shared__ float ct[NB][NBR + 1];
   __shared__ float hb[NB][NBR / 2 + 1];
@@ -315,7 +319,7 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
     if (v == 1.2345f) p.out[tid] = v;
     return;
   }
-  if constexpr (XW > 4) {  // waves 4..7 hand their tiles to waves 0..3 (added in registers)
+  if constexpr (XW > 4 && !RED_ALL) {  // waves 4..7 hand their tiles to waves 0..3 (added in registers)
     if (wave >= 4) {
 #pragma unroll
       for (int t = 0; t < MT; ++t)
@@ -347,9 +351,16 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
   for (int e = tid; e < NB * NBR; e += NTH) {
     const int ml = e / NBR, c = e % NBR, rr = ml & 31;
     const int idx = ((ml >> 5) * RTW + (c >> 5)) * 16 + (rr & 3) + 4 * (rr >> 3), ln = (c & 31) + 32 * ((rr >> 2) & 1);
-    float v = red[0][idx][ln];
+    float v;
+    if constexpr (RED_ALL) {  // ((s0 + s1) + s2) + s3 with s_w = wave w + wave w + 4, as the pre-add
+      v = red[0][idx][ln] + red[4][idx][ln];
 #pragma unroll
-    for (int w = 1; w < RW; ++w) v += red[w][idx][ln];
+      for (int w = 1; w < 4; ++w) v += red[w][idx][ln] + red[w + 4][idx][ln];
+    } else {
+      v = red[0][idx][ln];
+#pragma unroll
+      for (int w = 1; w < RW; ++w) v += red[w][idx][ln];
+    }
     ct[ml][c] = v;
   }
   __syncthreads();
@@ -499,7 +510,10 @@ void xs_shape(int N, int K, int M, bool head, int& rtw, int& ks, int& pd, int& x
   // 9.8 us at 64 rows, the backbone's projections 4-14 % (profiles/r04_ab_xs_waves8.txt).  Lab knob
   // CSM_XS_WAVES=2 / 4 / 8 forces one count everywhere.
   static const int waves = [] { const char* v = getenv("CSM_XS_WAVES"); const int w = v ? atoi(v) : 0; return w == 2 || w == 4 || w == 8 ? w : 0; }();
-  const int want = waves ? waves : (((size_t)N * K <= (size_t)1536 * 1024 && M <= 32) ? 4 : 8);
+  // the heads (arg-max epilogue, 64-row tiles, ~33 of them): fewer waves per block leave room for
+  // more K slices, spreading the head's bytes over more CUs (CSM_XS_HEAD_WAVES lab knob)
+  static const int head_waves = [] { const char* v = getenv("CSM_XS_HEAD_WAVES"); const int w = v ? atoi(v) : 0; return w == 2 || w == 4 || w == 8 ? w : 8; }();
+  const int want = waves ? waves : (head && N % 64 != 0 ? head_waves : (((size_t)N * K <= (size_t)1536 * 1024 && M <= 32) ? 4 : 8));
   xw = nks >= 2 * want ? want : (nks >= 8 ? 4 : 2);
   ks = 1;
   while (tiles * ks < tgt && ks < MAX_SLICES && nks / (ks * 2) >= xw && nks % (ks * 2) == 0) ks *= 2;

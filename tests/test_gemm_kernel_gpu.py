@@ -1,6 +1,6 @@
 """Direct test of the batched MFMA GEMM (csrc/gemm_kernels.hip, gemm_wide_kernel): every csm_1b
 projection shape, bf16 and int4, at 8 / 32 / 64 / 100 rows (one or two batch tiles, one or two
-64-row chunks), against the GEMV's fp32 arithmetic on the same stored weights -- csm_linear with
+64-row chunks) and 300 rows (a prompt-sized launch: 8-wave blocks, gemm_kernels.hip GEMM_W8_MIN_M), against the GEMV's fp32 arithmetic on the same stored weights -- csm_linear with
 and without the "linear_mfma" option.  The two differ only in summation order (the GEMM's products
 are fp32-exact through the hi/mid/lo activation split), so the bar is fp32 rounding."""
 import ctypes
@@ -54,7 +54,7 @@ def test_mfma_gemm_matches_gemv_every_shape(dtype):
     bad = []
     for name in NAMES:
         K = _in_width(model, name)
-        for M in (8, 32, 64, 100):
+        for M in (8, 32, 64, 100, 300):
             x = rng.standard_normal((M, K)).astype(np.float32)
             y0 = _linear(model, name, x, False)
             y1 = _linear(model, name, x, True)
