@@ -132,8 +132,11 @@ __global__ __launch_bounds__(256) void gemm64_mf_kernel(P p, int ks, float* slab
   }
   f32x16_t acc = {};
   float va[4], vb[4];
+  // B staged along kk (runs of taps) for the linears and the strided convs, along the output steps
+  // otherwise
+  const bool bk = P::B_KCONTIG || p.kcontig();
   // (whole runs of four inside the tile take the problem's 4-wide loads: A along kk, B along kk
-  // (B_KCONTIG) or along the output steps; the values are those of the per-element accessors)
+  // or along the output steps; the values are those of the per-element accessors)
   auto fetch = [&](int k0) {
     {
       const int i = tid >> 2, kq = (tid & 3) * 4;
@@ -145,11 +148,9 @@ __global__ __launch_bounds__(256) void gemm64_mf_kernel(P p, int ks, float* slab
           va[e] = (i0 + i < p.M && k0 + kq + e < ke) ? p.a(z, i0 + i, k0 + kq + e) : 0.f;
       }
     }
-    if constexpr (P::B_KCONTIG) {
+    if (bk) {
       const int j = tid >> 2, kq = (tid & 3) * 4;
-      if (j0 + j < p.N && k0 + kq + 3 < ke) {
-        ld4(p.bptr(z, k0 + kq, j0 + j), vb);
-      } else {
+      if (!(j0 + j < p.N && k0 + kq + 3 < ke && p.b4k(z, k0 + kq, j0 + j, vb))) {
 #pragma unroll
         for (int e = 0; e < 4; ++e)
           vb[e] = (j0 + j < p.N && k0 + kq + e < ke) ? p.b(z, k0 + kq + e, j0 + j) : 0.f;
@@ -171,7 +172,7 @@ __global__ __launch_bounds__(256) void gemm64_mf_kernel(P p, int ks, float* slab
 #pragma unroll
       for (int e = 0; e < 4; ++e) As[kq + e][i] = va[e];
     }
-    if constexpr (P::B_KCONTIG) {
+    if (bk) {
       const int j = tid >> 2, kq = (tid & 3) * 4;
 #pragma unroll
       for (int e = 0; e < 4; ++e) Bs[kq + e][j] = vb[e];
@@ -257,6 +258,19 @@ struct ConvProblem {
   __device__ int kdim() const { return c.Cin * c.k; }
   __device__ float a(int, int co, int kk) const { return c.w[(size_t)co * c.Cin * c.k + kk]; }
   __device__ const float* aptr(int, int co, int kk) const { return c.w + (size_t)co * c.Cin * c.k + kk; }
+  // strided convs (the encoder's downsampling): B staged along the taps -- consecutive kk of one input
+  // channel are consecutive input samples
+  __device__ bool kcontig() const { return c.stride > 1 && c.dil == 1 && !fold; }
+  __device__ bool b4k(int z, int kk0, int t, float (&v)[4]) const {
+    const int ci = kk0 / c.k, j = kk0 - ci * c.k;
+    const int u = t * c.stride + j - c.pad_l;
+    if (j + 3 >= c.k || u < 0 || u + 3 >= c.Tin) return false;
+    ld4(c.x + (size_t)z * c.x_bstride + (size_t)ci * c.x_cstride + c.x_off + u, v);
+    if (c.elu_in)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = elu_f(v[e]);
+    return true;
+  }
   // steps t0 .. t0 + 3 of one utterance at stride 1, all inside the input: one 4-wide load
   __device__ bool b4(int z, int kk, int t0, float (&v)[4]) const {
     if (c.stride != 1) return false;
@@ -327,6 +341,8 @@ struct ConvTrProblem {
     return c.wt[((size_t)r * c.Cout + co) * c.Cin * 2 + kk];
   }
   __device__ const float* aptr(int z, int co, int kk) const { return c.wt + ((size_t)(z % c.s) * c.Cout + co) * c.Cin * 2 + kk; }
+  __device__ bool kcontig() const { return false; }
+  __device__ bool b4k(int, int, int, float (&)[4]) const { return false; }
   // inputs i0 .. i0 + 3 of one utterance, all at or after the first: one 4-wide load
   __device__ bool b4(int z, int kk, int i0, float (&v)[4]) const {
     int bb = z / c.s;
@@ -386,7 +402,11 @@ struct LinProblem {
   __device__ float a(int, int n, int kk) const { return c.W[(size_t)n * c.K + kk]; }
   __device__ float b(int, int kk, int m) const { return c.x[(size_t)m * c.xs + kk]; }
   __device__ const float* aptr(int, int n, int kk) const { return c.W + (size_t)n * c.K + kk; }
-  __device__ const float* bptr(int, int kk, int m) const { return c.x + (size_t)m * c.xs + kk; }
+  __device__ bool kcontig() const { return true; }
+  __device__ bool b4k(int, int kk0, int m, float (&v)[4]) const {
+    ld4(c.x + (size_t)m * c.xs + kk0, v);
+    return true;
+  }
   __device__ bool b4(int, int, int, float (&)[4]) const { return false; }
   __device__ void store(int, int n, int m, float v) const {
     if (c.conv_T) {  // conv layout out[b][n][t], m = b*T + t
