@@ -142,6 +142,9 @@ struct csm_engine {
   // half-group sums for int4.  Config 4 3917 vs 3729 frames/s on gemm_wide (r03).
   // csm_set_option "gemm_xs" / CSM_GEMM_XS=0 turn it off.
   bool xs_on = [] { const char* v = getenv("CSM_GEMM_XS"); return !(v && v[0] == '0'); }();
+  // the depth decoder's step 1 (2 rows per utterance) on the streaming GEMM as well (CSM_XS_STEP1=0: on
+  // gemm_wide, the A/B)
+  bool xs_step1 = [] { const char* v = getenv("CSM_XS_STEP1"); return !(v && v[0] == '0'); }();
   void *xs_D = nullptr, *xs_A = nullptr, *xs_F = nullptr;
   float* xs_ss = nullptr;
   // the batched backbone on the streaming GEMM too (option bb_xs / CSM_BB_XS=0 off): with 8-wave blocks it
@@ -313,7 +316,9 @@ bool dec_xs_eligible(csm_engine* e, int M) {
          gemm_xs_tiles(Dd, s.q_dim(), M) <= 64;
 }
 
-void run_dec_xs(csm_engine* e, int M, const RowMap& rm, hipStream_t st, const AttnParams& attn0) {
+// l0_qkv: layer 0 also projects its q | k | v from split rows (step 1, whose rows launch_xs_rows split
+// after the projection) instead of gathering them from the folded table (attn0).
+void run_dec_xs(csm_engine* e, int M, const RowMap& rm, hipStream_t st, const AttnParams& attn0, bool l0_qkv = false) {
   Stack& s = e->dec;
   const csm_llama_dims& d = s.d;
   const int D = d.hidden, F = d.intermediate;
@@ -324,12 +329,12 @@ void run_dec_xs(csm_engine* e, int M, const RowMap& rm, hipStream_t st, const At
   float* hsF = q4 ? e->hs_F : nullptr;
   for (int i = 0; i < d.n_layers; ++i) {
     LayerW& l = s.L[i];
-    if (i > 0) {  // norm1 + QKV + RoPE + KV append from the split rows the previous down wrote
+    if (i > 0 || l0_qkv) {  // norm1 + QKV + RoPE + KV append from the split rows the previous down wrote
       GemvParams g = gp(e);
       g.W = l.wqkv; g.N = s.qkv_rows(); g.K = D; g.M = M; g.nw = l.n1; g.eps = d.eps;
       g.out = e->dq; g.os = s.q_dim(); g.Hq = d.n_heads; g.Hkv = d.n_kv_heads; g.hd = d.head_dim;
       g.S_cap = s.S_cap; g.rope = s.rope; g.kc = l.kc; g.vc = l.vc; g.rm = rm;
-      g.xs_in = e->xs_D; g.ss_in = e->xs_ss; g.ss_n = ss_d; g.ss_stride = GEMM_XS_MAX_M; g.hs_in = hsD;
+      g.xs_in = e->xs_D; g.ss_in = e->xs_ss; g.ss_n = i == 0 ? (D + 511) / 512 : ss_d; g.ss_stride = GEMM_XS_MAX_M; g.hs_in = hsD;
       launch_gemm_xs(g, EPI_QKV, st, false, e->wdt);
     }
     AttnParams a = i == 0 ? attn0 : AttnParams{};
@@ -616,6 +621,9 @@ void enqueue_head_phase(csm_engine* e, hipStream_t st, int phase, int piece = 0)
     RowMap rm = (i == 1) ? RowMap{2, 0, nullptr, 0} : RowMap{1, 0, nullptr, i};
     const bool use_tab = folded && e->use_qkv0_tab && e->qkv0_built && !e->no_tab_batched;
     const bool xs_dec = use_tab && dec_xs_eligible(e, M);  // streaming matrix-core decoder + head
+    // step 1 (two rows per utterance) on the streaming GEMM too: the projected rows split once, layer 0's
+    // QKV projected from them; the head stays on the dense path (it reads one row of each pair)
+    const bool xs_s1 = i == 1 && !folded && e->xs_step1 && dec_xs_eligible(e, M) && Dd % 512 == 0;
     if (!use_tab && (gemm_mfma_eligible(Dd, D, M, e->wdt) || gemm_mfma_eligible(e->dec.qkv_rows(), Dd, M, e->wdt))) {
       // batched: materialise the gathered rows densely, then every projection runs on the matrix cores
       if (!folded) {
@@ -630,7 +638,13 @@ void enqueue_head_phase(csm_engine* e, hipStream_t st, int phase, int piece = 0)
         gr.K = Dd; gr.out = e->dx; gr.os = Dd;
         launch_gather_rows(gr, e->wdt, st);
       }
-      run_stack(e, e->dec, e->dx, M, e->dq, e->datt, e->dmlp, rm, st, nullptr);
+      if (xs_s1) {
+        launch_xs_rows(e->dx, (int)Dd, M, (int)Dd, e->dec.L[0].n1, e->xs_D, e->xs_ss, GEMM_XS_MAX_M,
+                       e->wdt == WDT_Q4 ? e->hs_D : nullptr, st);
+        run_dec_xs(e, M, rm, st, AttnParams{}, true);
+      } else {
+        run_stack(e, e->dec, e->dx, M, e->dq, e->datt, e->dmlp, rm, st, nullptr);
+      }
     } else if (use_tab) {
       // layer 0's q | k | v and input row gathered from the folded tables by the attention (no layer-0
       // QKV projection); at >= 8 rows the other projections run on the matrix cores
@@ -737,7 +751,8 @@ void ensure_batch(csm_engine* e, int B) {
   // the streaming decoder path (gemm_xs): split-row buffers for up to GEMM_XS_MAX_M rows + its scratch
   {
     // (shared by the backbone and the decoder: their launches never overlap)
-    const int xm = GEMM_XS_MAX_M, rows = std::min((int)Bm, xm);
+    // (2 Bm: the depth decoder's step 1 carries two rows per utterance)
+    const int xm = GEMM_XS_MAX_M, rows = std::min(2 * (int)Bm, xm);
     size_t bD = 0, bA = 0, bF = 0;
     for (Stack* s : {&e->bb, &e->dec}) {
       const int Dm = s->d.hidden, F = s->d.intermediate;

@@ -285,6 +285,9 @@ void launch_table_rows(const void* base, int wdt, int Ntot, int K, const int* id
 // dst[i] = float(src[i]) for n elements (n % 8 == 0)
 void launch_to_f32(const void* src, int wdt, float* dst, size_t n, hipStream_t st);
 void launch_attn(const AttnParams& p, int hd, hipStream_t st);
+// dense rows -> the streaming GEMM's operand (x * nw), per-512-column sums of squares, half-group sums
+void launch_xs_rows(const float* x, int xstride, int M, int K, const float* nw, void* xs_out, float* ss_out, int ss_stride,
+                    float* hs_out, hipStream_t st);
 // rows per block of the GEMV launch for (N, K, M): N must be a multiple of it
 int gemv_rows_per_block(int N, int K, int M);
 void launch_rmsnorm_rows(const float* x, int xs, const float* w, float eps, int D, float* out, int os, int M,

@@ -97,6 +97,47 @@ __global__ __launch_bounds__(64) void embed_rows_kernel(EmbedParams p) {
   }
 }
 
+// ============================================================================ split rows
+// The streaming GEMM's operand (xs.h) from dense rows: x[m] * nw in fragment order, per-row sums of
+// squares of x per 512-column block (ss_out[blockIdx.y * ss_stride + m]) and, for int4 consumers, the
+// half-group sums -- the embedding producer's outputs (embed_rows_kernel), for rows another kernel
+// wrote densely (the depth decoder's step-1 rows after the projection).  One wave per 512 columns.
+__global__ __launch_bounds__(64) void xs_rows_kernel(const float* x, int xstride, int K, const float* nw, void* xs_out,
+                                                     float* ss_out, int ss_stride, float* hs_out) {
+  const int m = blockIdx.x, t = threadIdx.x, d0 = (blockIdx.y * 64 + t) * 8;
+  if (d0 >= K) return;
+  const float* xr = x + (size_t)m * xstride + d0;
+  const float4 a = *reinterpret_cast<const float4*>(xr), b = *reinterpret_cast<const float4*>(xr + 4);
+  const float v8[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  float sq = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) sq = fmaf(v8[e], v8[e], sq);
+  sq = wave_sum(sq);
+  if (t == 0) ss_out[(size_t)blockIdx.y * ss_stride + m] = sq;
+  float hsum = 0.f;
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) {
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      v[u] = v8[4 * hf + u] * nw[d0 + 4 * hf + u];
+      hsum += v[u];
+    }
+    xs::store4(xs_out, K, m, d0 + 4 * hf, v);
+  }
+  if (hs_out) {
+    const int b4 = t & ~3;
+    const float h0 = __shfl(hsum, b4, 64), h1 = __shfl(hsum, b4 + 1, 64), h2 = __shfl(hsum, b4 + 2, 64),
+                h3 = __shfl(hsum, b4 + 3, 64);
+    if ((t & 3) == 0) hs_out[(size_t)(d0 / 32) * xs::HS_ROWS + m] = ((h0 + h1) + h2) + h3;
+  }
+}
+
+void launch_xs_rows(const float* x, int xstride, int M, int K, const float* nw, void* xs_out, float* ss_out, int ss_stride,
+                    float* hs_out, hipStream_t st) {
+  hipLaunchKernelGGL(xs_rows_kernel, dim3(M, (K + 511) / 512), dim3(64), 0, st, x, xstride, K, nw, xs_out, ss_out, ss_stride, hs_out);
+}
+
 // ============================================================================ GEMV
 // y[m, n] = sum_k norm(x)[m, k] * W[n, k]   (W row-major [N][K], MLX (out,in) layout)
 //
