@@ -496,13 +496,15 @@ void xs_shape(int N, int K, int M, bool head, int& rtw, int& ks, int& pd, int& x
   static const int rtw_long = [] { const char* v = getenv("CSM_XS_LONGK_RTW"); return v ? atoi(v) : 1; }();
   rtw = (N >= 4096 || head) ? 2 : (K >= 4096 ? rtw_long : 1);
   const int tiles = (N + 32 * rtw - 1) / (32 * rtw);
-  // split-K slices until the grid has >= `target` blocks (CSM_XS_BLOCKS lab knob).  The short-K small
-  // projections at <= 32 rows (the decoder's QKV / o, the backbone's o) take none (target 1,
+  // split-K slices until the grid has >= `target` blocks (CSM_XS_BLOCKS lab knob).  The depth decoder's
+  // small projections at <= 32 rows (QKV / o, N x K <= 1536 x 1024) take none (target 1,
   // CSM_XS_SMALL_BLOCKS): one K slice over 8 waves, no partial exchange -- decoder QKV 7.2 -> 6.3 us,
-  // o 6.7 -> 6.2 us, config 4 4347 -> 4378 frames/s (profiles/r04_ab_step1_small.txt)
+  // o 6.7 -> 6.2 us, config 4 4347 -> 4378 frames/s (profiles/r04_ab_step1_small.txt); the backbone's
+  // o (2048 x 2048) measured ~2 us slower that way and keeps its slices (profiles/r04_prof_config4_per_frame_final.txt)
   static const int target = [] { const char* v = getenv("CSM_XS_BLOCKS"); return v ? atoi(v) : 256; }();
   static const int small_target = [] { const char* v = getenv("CSM_XS_SMALL_BLOCKS"); return v ? atoi(v) : 1; }();
-  const int tgt = (N <= 2048 && K <= 2048 && !head && M <= 32) ? small_target : target;
+  const bool dec_small = (size_t)N * K <= (size_t)1536 * 1024 && M <= 32 && !head;
+  const int tgt = dec_small ? small_target : target;
   // waves per block; the block's K slice is split between them.  4 (one per SIMD of the CU the block
   // occupies) against 2: QKV 9.4 -> 7.2 us and o 8.0 -> 6.8 us at 32 bf16 rows, int4 gate/up 24.7 -> 16.1
   // and down 20.6 -> 16.1 us at 64 rows; config 4 3667 -> 3816, config 5 3501 -> 4035 frames/s
@@ -517,7 +519,7 @@ void xs_shape(int N, int K, int M, bool head, int& rtw, int& ks, int& pd, int& x
   static const int head_waves = [] { const char* v = getenv("CSM_XS_HEAD_WAVES"); const int w = v ? atoi(v) : 0; return w == 2 || w == 4 || w == 8 ? w : 8; }();
   // (the decoder's QKV / o at <= 32 rows: 8 waves now that they take one K slice; 4 with split-K)
   static const int small_waves = [] { const char* v = getenv("CSM_XS_SMALL_WAVES"); const int w = v ? atoi(v) : 0; return w == 2 || w == 4 || w == 8 ? w : 8; }();
-  const int want = waves ? waves : (head && N % 64 != 0 ? head_waves : (((size_t)N * K <= (size_t)1536 * 1024 && M <= 32) ? small_waves : 8));
+  const int want = waves ? waves : (head && N % 64 != 0 ? head_waves : (dec_small ? small_waves : 8));
   xw = nks >= 2 * want ? want : (nks >= 8 ? 4 : 2);
   ks = 1;
   while (tiles * ks < tgt && ks < MAX_SLICES && nks / (ks * 2) >= xw && nks % (ks * 2) == 0) ks *= 2;
