@@ -298,9 +298,13 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
   // reduction slots: one per wave where the slab fits 64 KB (then every wave stores once and the
   // ct pass adds (w, w + 4) pairs in the pre-add's order -- one barrier and one LDS round trip
   // fewer, same sums); else 8-wave blocks pre-add waves w + 4 into w through 4 slots
+  // RED_HALF (8 waves, two row tiles, 128 KB of partials): the same single pass per row tile in turn
+  // -- every wave stores its row tile t partials into its own slot, the ct pass builds rows 32 t ..
+  // 32 t + 31 -- instead of the 4-slot pre-add (whose phases leave half the waves idle)
   constexpr bool RED_ALL = XW > 4 && MT * RTW * 16 * 64 * 4 * XW <= 65536;
-  constexpr int RW = RED_ALL ? XW : (XW > 4 ? 4 : XW);
-  __shared__ float red[RW][MT * RTW * 16][64];
+  constexpr bool RED_HALF = !RED_ALL && XW > 4 && MT == 2 && RTW * 16 * 64 * 4 * XW <= 65536;
+  constexpr int RW = (RED_ALL || RED_HALF) ? XW : (XW > 4 ? 4 : XW);
+  __shared__ float red[RW][(RED_HALF ? 1 : MT) * RTW * 16][64];
   __shared__ float ct[NB][NBR + 1];
   __shared__ float hb[NB][NBR / 2 + 1];
   __shared__ float rsc[NB];
@@ -319,7 +323,26 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
     if (v == 1.2345f) p.out[tid] = v;
     return;
   }
-  if constexpr (XW > 4 && !RED_ALL) {  // waves 4..7 hand their tiles to waves 0..3 (added in registers)
+  if constexpr (RED_HALF) {
+#pragma unroll
+    for (int t = 0; t < MT; ++t) {
+      if (t > 0) __syncthreads();  // row tile t - 1's partials consumed
+#pragma unroll
+      for (int i = 0; i < RTW; ++i)
+#pragma unroll
+        for (int j = 0; j < 16; ++j) red[wave][i * 16 + j][lane] = acc[t][i][j];
+      __syncthreads();
+      for (int e = tid; e < 32 * NBR; e += NTH) {
+        const int rr = e / NBR, c = e % NBR;
+        const int idx = (c >> 5) * 16 + (rr & 3) + 4 * (rr >> 3), ln = (c & 31) + 32 * ((rr >> 2) & 1);
+        float v = red[0][idx][ln] + red[4][idx][ln];  // the 4-slot pre-add's sums, in its order
+#pragma unroll
+        for (int w = 1; w < 4; ++w) v += red[w][idx][ln] + red[w + 4][idx][ln];
+        ct[32 * t + rr][c] = v;
+      }
+    }
+  }
+  if constexpr (XW > 4 && !RED_ALL && !RED_HALF) {  // waves 4..7 hand their tiles to waves 0..3 (added in registers)
     if (wave >= 4) {
 #pragma unroll
       for (int t = 0; t < MT; ++t)
@@ -339,6 +362,7 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
     }
     __syncthreads();
   }
+  if constexpr (!RED_HALF) {
   if (wave < RW) {
 #pragma unroll
     for (int t = 0; t < MT; ++t)
@@ -362,6 +386,7 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
       for (int w = 1; w < RW; ++w) v += red[w][idx][ln];
     }
     ct[ml][c] = v;
+  }
   }
   __syncthreads();
   XS_STAMP(3);
@@ -504,7 +529,9 @@ void xs_shape(int N, int K, int M, bool head, int& rtw, int& ks, int& pd, int& x
   static const int target = [] { const char* v = getenv("CSM_XS_BLOCKS"); return v ? atoi(v) : 256; }();
   static const int small_target = [] { const char* v = getenv("CSM_XS_SMALL_BLOCKS"); return v ? atoi(v) : 1; }();
   const bool dec_small = (size_t)N * K <= (size_t)1536 * 1024 && M <= 32 && !head;
-  const int tgt = dec_small ? small_target : target;
+  // the arg-max heads (N not a multiple of 64: the padded vocabulary): CSM_XS_HEAD_BLOCKS lab knob
+  static const int head_target = [] { const char* v = getenv("CSM_XS_HEAD_BLOCKS"); return v ? atoi(v) : 256; }();
+  const int tgt = dec_small ? small_target : (head && N % 64 != 0 ? head_target : target);
   // waves per block; the block's K slice is split between them.  4 (one per SIMD of the CU the block
   // occupies) against 2: QKV 9.4 -> 7.2 us and o 8.0 -> 6.8 us at 32 bf16 rows, int4 gate/up 24.7 -> 16.1
   // and down 20.6 -> 16.1 us at 64 rows; config 4 3667 -> 3816, config 5 3501 -> 4035 frames/s
