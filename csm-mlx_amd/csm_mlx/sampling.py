@@ -10,6 +10,7 @@ vocab id).  The filter chain's restatement is oracle/csm_oracle.py
 ``filter_keep``; the GPU side is ``sample_filtered_kernel`` (csm_kernels.hip).
 
 An arbitrary callable (``sampler=fn``, as the reference CLI passes mlx_lm's sampler) is honoured too,
+and so is ``make_sampler(xtc_probability=...)`` (XTC has no GPU counterpart: the chain runs there),
 on the host: ``HostSampler`` wraps it, and every frame then hands each codebook's logits (B, V) to
 ``fn`` and feeds the codes it returns forward (csm_frame_host_step; 32 host round trips per frame,
 so a compatibility path, not the fast one).
@@ -38,14 +39,67 @@ class Sampler:
 
 
 def make_sampler(temp: float = 0.0, top_p: float = 0.0, min_p: float = 0.0, min_tokens_to_keep: int = 1,
-                 top_k: int = 0, xtc_probability: float = 0.0, **_unused) -> Sampler:
+                 top_k: int = 0, xtc_probability: float = 0.0, xtc_threshold: float = 0.0,
+                 xtc_special_tokens=(), seed: int = 0, **_unused):
     """mlx_lm.sample_utils.make_sampler (as cli/generate.py:168-174 calls it) as a GPU sampler
-    descriptor.  XTC sampling has no GPU counterpart and raises."""
-    if xtc_probability:
-        raise NotImplementedError("XTC sampling does not run on the GPU sampler")
+    descriptor.  XTC ("exclude top choices", which the reference CLI never passes) has no GPU
+    counterpart: with ``xtc_probability > 0`` and ``temp > 0`` the whole chain runs on the host as a
+    ``HostSampler`` (``xtc_chain``); at ``temp == 0`` mlx_lm ignores XTC and so does this."""
     if not (0.0 <= top_p <= 1.0) or not (0.0 <= min_p <= 1.0) or int(min_tokens_to_keep) < 1:
         raise ValueError("top_p and min_p must lie in [0, 1], min_tokens_to_keep >= 1")
+    if not (0.0 <= xtc_probability <= 1.0) or not (0.0 <= xtc_threshold <= 0.5):
+        raise ValueError("xtc_probability must lie in [0, 1] and xtc_threshold in [0, 0.5]")
+    if xtc_probability > 0.0 and temp != 0:
+        return HostSampler(xtc_chain(float(temp), float(top_p), float(min_p), int(min_tokens_to_keep), int(top_k),
+                                     float(xtc_probability), float(xtc_threshold), tuple(xtc_special_tokens), seed),
+                           logprobs=True)
     return Sampler(float(temp), int(top_k), float(top_p), float(min_p), int(min_tokens_to_keep))
+
+
+def xtc_chain(temp, top_p, min_p, min_tokens_to_keep, top_k, xtc_probability, xtc_threshold,
+              xtc_special_tokens=(), seed: int = 0):
+    """mlx_lm's make_sampler chain with XTC, on host log-probabilities (B, V): top_k (exactly k kept),
+    top_p (cumulative ascending probability > 1 - top_p), min_p (log p >= log p_max + log min_p, the
+    first ``min_tokens_to_keep`` by rank always kept), then XTC -- with probability
+    ``xtc_probability`` per row, every token whose probability exceeds the smallest probability above
+    ``xtc_threshold`` is removed (special tokens exempt) -- then a categorical draw of
+    ``logprobs / temp``.  Restated from mlx_lm's published sample_utils (not in /root/reference, which
+    never enables XTC): parity unpinned."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    special = np.asarray(list(xtc_special_tokens), np.int64)
+
+    def fn(lp):
+        x = np.array(lp, np.float64)
+        ninf = -np.inf
+        if top_k > 0 and top_k < x.shape[-1]:
+            drop = np.argpartition(-x, top_k - 1, axis=-1)[:, top_k:]
+            np.put_along_axis(x, drop, ninf, axis=-1)
+        if 0.0 < top_p < 1.0:
+            order = np.argsort(x, axis=-1, kind="stable")
+            cum = np.cumsum(np.take_along_axis(np.exp(x), order, axis=-1), axis=-1)
+            cp = np.empty_like(cum)
+            np.put_along_axis(cp, order, cum, axis=-1)
+            x = np.where(cp > 1 - top_p, x, ninf)
+        if min_p != 0.0:
+            order = np.argsort(-x, axis=-1, kind="stable")
+            srt = np.take_along_axis(x, order, axis=-1)
+            rem = srt < srt[:, :1] + np.log(min_p)
+            rem[:, :min_tokens_to_keep] = False
+            rm = np.empty_like(rem)
+            np.put_along_axis(rm, order, rem, axis=-1)
+            x = np.where(rm, ninf, x)
+        p = np.exp(x - x.max(axis=-1, keepdims=True))
+        p /= p.sum(axis=-1, keepdims=True)
+        floor = np.where(p > xtc_threshold, p, np.inf).min(axis=-1, keepdims=True)
+        mask = p > floor
+        if special.size:
+            mask[:, special] = False
+        hit = rng.random((x.shape[0], 1)) <= xtc_probability
+        x = np.where(hit & mask, ninf, x)
+        g = -np.log(-np.log(rng.random(x.shape)))
+        return np.argmax(x / temp + g, axis=-1)
+    return fn
 
 
 @dataclass(frozen=True)

@@ -50,10 +50,28 @@ def test_sampler_descriptor():
     f = make_sampler(0.8, top_p=0.9, min_p=0.05, min_tokens_to_keep=3, top_k=40)
     assert (f.top_p, f.min_p, f.min_tokens_to_keep, f.top_k) == (0.9, 0.05, 3, 40) and f.filtered
     assert not make_sampler(0.8, top_p=1.0).filtered                     # mlx_lm: top_p active in (0, 1)
-    with pytest.raises(NotImplementedError):
-        make_sampler(0.8, xtc_probability=0.1)
+    from csm_mlx.sampling import HostSampler
+    assert isinstance(make_sampler(0.8, xtc_probability=0.1), HostSampler)   # XTC: chain on the host
+    assert make_sampler(0.0, xtc_probability=0.1).greedy                     # mlx_lm: temp 0 ignores XTC
     with pytest.raises(ValueError):
         make_sampler(0.8, top_p=1.5)
+
+
+def test_xtc_chain():
+    """XTC on hand-worked rows: p = (0.5, 0.3, 0.15, 0.05), threshold 0.1 -> the smallest probability
+    above it is 0.15, so 0.5 and 0.3 go; a near-zero temperature then takes the best survivor."""
+    from csm_mlx import make_sampler
+    lp = np.log(np.array([[0.5, 0.3, 0.15, 0.05]] * 3, np.float32))
+    s = make_sampler(1e-6, xtc_probability=1.0, xtc_threshold=0.1)
+    assert s(lp).tolist() == [2, 2, 2]
+    s = make_sampler(1e-6, xtc_probability=1.0, xtc_threshold=0.1, xtc_special_tokens=[0])
+    assert s(lp).tolist() == [0, 0, 0]                                        # special tokens exempt
+    s = make_sampler(1e-6, xtc_probability=1.0, xtc_threshold=0.4)           # one token above: nothing goes
+    assert s(lp).tolist() == [0, 0, 0]
+    s = make_sampler(1e-6, top_k=1, xtc_probability=1.0, xtc_threshold=0.1)  # top_k first: one survivor left
+    assert s(lp).tolist() == [0, 0, 0]
+    with pytest.raises(ValueError):
+        make_sampler(0.8, xtc_probability=1.5)
 
 
 def test_filter_chain_restatement():
