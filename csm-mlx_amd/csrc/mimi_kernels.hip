@@ -197,6 +197,137 @@ __global__ __launch_bounds__(256) void gemm64_mf_kernel(P p, int ks, float* slab
   }
 }
 
+// Wide problems (>= 256 columns: whole-utterance encode / decode convs, the codec transformer's
+// linears): BM x 128 tiles, each wave a (BM / WM) x (128 / WN) block of 32 x 32 MFMA tiles (BM 128:
+// 2 x 2 tiles per wave, one A and one B LDS dword per two MFMAs instead of per one; BM 32 / 64 for the
+// 32- / 64-channel convs, which the 64-row tile ran half / fully padded or on one tile row).  Same
+// K-steps and slices as gemm64_mf_kernel, each output one accumulator fed k in order: bit-identical.
+// LDS rows are BM + 32 (or BM when BM % 64 == 32) floats apart, so the two k rows an MFMA operand read
+// touches (lanes h = 0 / 1) land on disjoint halves of the 64 banks.
+template <class P, bool SPLIT, int BM>
+__global__ __launch_bounds__(256) void gemm128_mf_kernel(P p, int ks, float* slab, int Z) {
+  typedef float f32x16_t __attribute__((ext_vector_type(16)));
+  constexpr int BN = 128, WM = BM >= 64 ? 2 : 1, WN = 4 / WM, TM = BM / WM / 32, TN = BN / WN / 32;
+  constexpr int SA = BM % 64 ? BM : BM + 32, SB = BN + 32;
+  constexpr int NA = BM >= 64 ? BM / 64 : 1;  // A groups of four per thread
+  __shared__ __attribute__((aligned(16))) float As[16][SA];
+  __shared__ __attribute__((aligned(16))) float Bs[16][SB];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave / WN, wn = wave % WN;
+  const int i0 = blockIdx.y * BM, j0 = blockIdx.x * BN;
+  const int z = SPLIT ? (int)blockIdx.z / ks : (int)blockIdx.z, sl = SPLIT ? (int)blockIdx.z % ks : 0;
+  const int KD = p.kdim();
+  int kb = 0, ke = KD;
+  if constexpr (SPLIT) {
+    const int nst = (KD + 15) / 16;
+    kb = (nst * sl / ks) * 16;
+    ke = min(KD, (nst * (sl + 1) / ks) * 16);
+  }
+  f32x16_t acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b) acc[a][b] = f32x16_t{};
+  float va[NA][4], vb[2][4];
+  const bool bk = P::B_KCONTIG || p.kcontig();
+  const bool a_on = BM >= 64 || tid < BM * 4;
+  auto fetch = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < NA; ++u) {
+      const int i = u * 64 + (tid >> 2), kq = (tid & 3) * 4;
+      if (a_on && i0 + i < p.M && k0 + kq + 3 < ke) {
+        ld4(p.aptr(z, i0 + i, k0 + kq), va[u]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          va[u][e] = (a_on && i0 + i < p.M && k0 + kq + e < ke) ? p.a(z, i0 + i, k0 + kq + e) : 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int g = tid + 256 * u;
+      if (bk) {
+        const int j = g >> 2, kq = (g & 3) * 4;
+        if (!(j0 + j < p.N && k0 + kq + 3 < ke && p.b4k(z, k0 + kq, j0 + j, vb[u]))) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            vb[u][e] = (j0 + j < p.N && k0 + kq + e < ke) ? p.b(z, k0 + kq + e, j0 + j) : 0.f;
+        }
+      } else {
+        const int kk = g >> 5, jb = (g & 31) * 4;
+        if (!(k0 + kk < ke && j0 + jb + 3 < p.N && p.b4(z, k0 + kk, j0 + jb, vb[u]))) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            vb[u][e] = (k0 + kk < ke && j0 + jb + e < p.N) ? p.b(z, k0 + kk, j0 + jb + e) : 0.f;
+        }
+      }
+    }
+  };
+  fetch(kb);
+  const int r = lane & 31, h = lane >> 5;
+  const int ra = wm * (BM / WM) + r, rb = wn * (BN / WN) + r;
+  for (int k0 = kb; k0 < ke; k0 += 16) {
+#pragma unroll
+    for (int u = 0; u < NA; ++u) {
+      const int i = u * 64 + (tid >> 2), kq = (tid & 3) * 4;
+      if (a_on)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) As[kq + e][i] = va[u][e];
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int g = tid + 256 * u;
+      if (bk) {
+        const int j = g >> 2, kq = (g & 3) * 4;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) Bs[kq + e][j] = vb[u][e];
+      } else {
+        const int kk = g >> 5, jb = (g & 31) * 4;
+        *reinterpret_cast<float4*>(&Bs[kk][jb]) = make_float4(vb[u][0], vb[u][1], vb[u][2], vb[u][3]);
+      }
+    }
+    __syncthreads();
+    if (k0 + 16 < ke) fetch(k0 + 16);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      float a[TM], b[TN];
+#pragma unroll
+      for (int x = 0; x < TM; ++x) a[x] = As[2 * t + h][ra + 32 * x];
+#pragma unroll
+      for (int y = 0; y < TN; ++y) b[y] = Bs[2 * t + h][rb + 32 * y];
+#pragma unroll
+      for (int x = 0; x < TM; ++x)
+#pragma unroll
+        for (int y = 0; y < TN; ++y) acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[x], b[y], acc[x][y], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int x = 0; x < TM; ++x)
+#pragma unroll
+    for (int y = 0; y < TN; ++y)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int i = i0 + wm * (BM / WM) + 32 * x + 8 * (q >> 2) + 4 * h + (q & 3);
+        const int j = j0 + wn * (BN / WN) + 32 * y + r;
+        if (i < p.M && j < p.N) {
+          if constexpr (SPLIT) slab[(((size_t)sl * Z + z) * p.M + i) * p.N + j] = acc[x][y][q];
+          else p.store(z, i, j, acc[x][y][q]);
+        }
+      }
+}
+
+// CSM_MIMI_WIDE=0: every codec GEMM on the 64 x 64 tile (A/B); else >= CSM_MIMI_WIDE_N columns (default
+// 256) take gemm128_mf_kernel
+static int mimi_wide_n() {
+  static const int v = [] {
+    const char* e = getenv("CSM_MIMI_WIDE");
+    if (e && atoi(e) == 0) return 1 << 30;
+    const char* n = getenv("CSM_MIMI_WIDE_N");
+    return n ? atoi(n) : 256;
+  }();
+  return v;
+}
+
 // CSM_MIMI_MFMA=0: the VALU tile (A/B)
 static bool mimi_mfma() {
   static const bool v = [] { const char* e = getenv("CSM_MIMI_MFMA"); return !e || atoi(e) != 0; }();
@@ -228,9 +359,31 @@ static int mimi_splitk(int KD, int blocks, size_t slab_per_slice) {
   return ks;
 }
 
+template <class P, int BM>
+static void launch_wide(const P& pr, dim3 grid, int ks, float* ws, hipStream_t st) {
+  const int Z = (int)grid.z;
+  const dim3 g((pr.N + 127) / 128, (pr.M + BM - 1) / BM, grid.z);
+  if (ks <= 1 || !ws) {
+    hipLaunchKernelGGL((gemm128_mf_kernel<P, false, BM>), g, dim3(256), 0, st, pr, 1, nullptr, Z);
+    return;
+  }
+  hipLaunchKernelGGL((gemm128_mf_kernel<P, true, BM>), dim3(g.x, g.y, g.z * ks), dim3(256), 0, st, pr, ks, ws, Z);
+  const size_t tot = (size_t)Z * pr.M * pr.N;
+  const int rb = (int)std::min<size_t>(2048, (tot + 255) / 256);
+  hipLaunchKernelGGL(splitk_reduce_kernel<P>, dim3(rb), dim3(256), 0, st, pr, ws, ks, Z);
+}
+
+// grid: the 64 x 64 tile grid (its block count also sized the split-K slices, so a wide launch splits
+// exactly as the 64-tile one would: same sums)
 template <class P>
 static void launch_gemm64(const P& pr, dim3 grid, int ks, float* ws, hipStream_t st) {
   const bool mf = mimi_mfma();
+  if (mf && pr.N >= mimi_wide_n()) {
+    if (pr.M <= 32) launch_wide<P, 32>(pr, grid, ks, ws, st);
+    else if (pr.M <= 64) launch_wide<P, 64>(pr, grid, ks, ws, st);
+    else launch_wide<P, 128>(pr, grid, ks, ws, st);
+    return;
+  }
   if (ks <= 1 || !ws) {
     if (mf) hipLaunchKernelGGL((gemm64_mf_kernel<P, false>), grid, dim3(256), 0, st, pr, 1, nullptr, (int)grid.z);
     else hipLaunchKernelGGL((gemm64_kernel<P, false>), grid, dim3(256), 0, st, pr, 1, nullptr, (int)grid.z);
