@@ -187,12 +187,29 @@ __global__ __launch_bounds__(256) void gemm64_mf_kernel(P p, int ks, float* slab
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(As[2 * t + h][32 * qi + r], Bs[2 * t + h][32 * qj + r], acc, 0, 0, 0);
     __syncthreads();
   }
+  // the epilogue's loads (bias, residual, accumulated-onto values) issued four rows at a time before
+  // their stores (which they could alias as far as the compiler knows): 4 memory round trips per tile
+  // instead of 16
+  if constexpr (SPLIT) {
 #pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int i = i0 + 32 * qi + 8 * (q >> 2) + 4 * h + (q & 3), j = j0 + 32 * qj + r;
-    if (i < p.M && j < p.N) {
-      if constexpr (SPLIT) slab[(((size_t)sl * Z + z) * p.M + i) * p.N + j] = acc[q];
-      else p.store(z, i, j, acc[q]);
+    for (int q = 0; q < 16; ++q) {
+      const int i = i0 + 32 * qi + 8 * (q >> 2) + 4 * h + (q & 3), j = j0 + 32 * qj + r;
+      if (i < p.M && j < p.N) slab[(((size_t)sl * Z + z) * p.M + i) * p.N + j] = acc[q];
+    }
+  } else {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {  // four rows at a time (registers: occupancy of the main loop)
+      float2 e[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = i0 + 32 * qi + 8 * g + 4 * h + u, j = j0 + 32 * qj + r;
+        e[u] = (i < p.M && j < p.N) ? p.pre(z, i, j) : make_float2(0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = i0 + 32 * qi + 8 * g + 4 * h + u, j = j0 + 32 * qj + r;
+        if (i < p.M && j < p.N) p.post(z, i, j, acc[4 * g + u], e[u]);
+      }
     }
   }
 }
@@ -301,23 +318,41 @@ __global__ __launch_bounds__(256) void gemm128_mf_kernel(P p, int ks, float* sla
     }
     __syncthreads();
   }
+  // per 32 x 32 tile, four rows at a time: their epilogue loads, then their stores (as gemm64_mf_kernel)
 #pragma unroll
   for (int x = 0; x < TM; ++x)
 #pragma unroll
-    for (int y = 0; y < TN; ++y)
+    for (int y = 0; y < TN; ++y) {
+      const int ib = i0 + wm * (BM / WM) + 32 * x + 4 * h, j = j0 + wn * (BN / WN) + 32 * y + r;
+      if constexpr (SPLIT) {
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int i = i0 + wm * (BM / WM) + 32 * x + 8 * (q >> 2) + 4 * h + (q & 3);
-        const int j = j0 + wn * (BN / WN) + 32 * y + r;
-        if (i < p.M && j < p.N) {
-          if constexpr (SPLIT) slab[(((size_t)sl * Z + z) * p.M + i) * p.N + j] = acc[x][y][q];
-          else p.store(z, i, j, acc[x][y][q]);
+        for (int q = 0; q < 16; ++q) {
+          const int i = ib + 8 * (q >> 2) + (q & 3);
+          if (i < p.M && j < p.N) slab[(((size_t)sl * Z + z) * p.M + i) * p.N + j] = acc[x][y][q];
+        }
+      } else {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          float2 e[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int i = ib + 8 * g + u;
+            e[u] = (i < p.M && j < p.N) ? p.pre(z, i, j) : make_float2(0.f, 0.f);
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int i = ib + 8 * g + u;
+            if (i < p.M && j < p.N) p.post(z, i, j, acc[x][y][4 * g + u], e[u]);
+          }
         }
       }
+    }
 }
 
-// CSM_MIMI_WIDE=0: every codec GEMM on the 64 x 64 tile (A/B); else >= CSM_MIMI_WIDE_N columns (default
-// 256) take gemm128_mf_kernel
+// CSM_MIMI_WIDE=0: every codec GEMM on the 64 x 64 tile (A/B); else launches of >= CSM_MIMI_WIDE_N columns
+// (default 256) and >= 192 wide blocks (fewer left CUs idle: a 4096-column decode conv ran 620 us on 128
+// blocks against 324 on 512 64-tiles), except 1-tap convs, take gemm128_mf_kernel
+// (profiles/r04_ab_mimi_wide.txt)
 static int mimi_wide_n() {
   static const int v = [] {
     const char* e = getenv("CSM_MIMI_WIDE");
@@ -378,7 +413,9 @@ static void launch_wide(const P& pr, dim3 grid, int ks, float* ws, hipStream_t s
 template <class P>
 static void launch_gemm64(const P& pr, dim3 grid, int ks, float* ws, hipStream_t st) {
   const bool mf = mimi_mfma();
-  if (mf && pr.N >= mimi_wide_n()) {
+  const size_t wblocks = (size_t)((pr.N + 127) / 128) * ((pr.M + (pr.M <= 32 ? 31 : pr.M <= 64 ? 63 : 127)) /
+                                                          (pr.M <= 32 ? 32 : pr.M <= 64 ? 64 : 128)) * grid.z;
+  if (mf && pr.wide_ok() && pr.N >= mimi_wide_n() && wblocks >= 192) {
     if (pr.M <= 32) launch_wide<P, 32>(pr, grid, ks, ws, st);
     else if (pr.M <= 64) launch_wide<P, 64>(pr, grid, ks, ws, st);
     else launch_wide<P, 128>(pr, grid, ks, ws, st);
@@ -414,6 +451,8 @@ struct ConvProblem {
   // strided convs (the encoder's downsampling): B staged along the taps -- consecutive kk of one input
   // channel are consecutive input samples
   __device__ bool kcontig() const { return c.stride > 1 && c.dil == 1 && !fold; }
+  // 1-tap convs (K = Cin, memory-bound, mostly with a residual) ran faster on the 64 x 64 tile
+  bool wide_ok() const { return c.k > 1; }
   __device__ bool b4k(int z, int kk0, int t, float (&v)[4]) const {
     const int ci = kk0 / c.k, j = kk0 - ci * c.k;
     const int u = t * c.stride + j - c.pad_l;
@@ -455,15 +494,25 @@ struct ConvProblem {
     const float v = c.x[(size_t)z * c.x_bstride + (size_t)ci * c.x_cstride + c.x_off + u];
     return c.elu_in ? elu_f(v) : v;
   }
-  __device__ void store(int z, int co, int t, float v) const {
+  // epilogue operands (bias, residual), loaded by a tile for all its outputs before its first store
+  __device__ float2 pre(int z, int co, int t) const {
     if (fold) {
       z = t / fold;
       t -= z * fold;
     }
-    if (c.bias) v += c.bias[co];
-    if (c.resid) v += c.resid[(size_t)z * c.r_bstride + (size_t)co * c.r_cstride + c.r_off + t];
+    return make_float2(c.bias ? c.bias[co] : 0.f,
+                       c.resid ? c.resid[(size_t)z * c.r_bstride + (size_t)co * c.r_cstride + c.r_off + t] : 0.f);
+  }
+  __device__ void post(int z, int co, int t, float v, float2 e) const {
+    if (fold) {
+      z = t / fold;
+      t -= z * fold;
+    }
+    if (c.bias) v += e.x;
+    if (c.resid) v += e.y;
     c.y[(size_t)z * c.y_bstride + (size_t)co * c.y_cstride + c.y_off + t] = v;
   }
+  __device__ void store(int z, int co, int t, float v) const { post(z, co, t, v, pre(z, co, t)); }
 };
 
 // CSM_MIMI_CONV_FOLD=0: no batch folding (A/B).  Measured: config 3 (B = 32 streaming decode_step)
@@ -495,6 +544,7 @@ struct ConvTrProblem {
   }
   __device__ const float* aptr(int z, int co, int kk) const { return c.wt + ((size_t)(z % c.s) * c.Cout + co) * c.Cin * 2 + kk; }
   __device__ bool kcontig() const { return false; }
+  bool wide_ok() const { return true; }
   __device__ bool b4k(int, int, int, float (&)[4]) const { return false; }
   // inputs i0 .. i0 + 3 of one utterance, all at or after the first: one 4-wide load
   __device__ bool b4(int z, int kk, int i0, float (&v)[4]) const {
@@ -525,16 +575,18 @@ struct ConvTrProblem {
     const float v = c.x[(size_t)bb * c.x_bstride + (size_t)ci * c.x_cstride + c.x_off + ti];
     return c.elu_in ? elu_f(v) : v;
   }
-  __device__ void store(int z, int co, int i, float v) const {
+  __device__ float2 pre(int, int co, int) const { return make_float2(c.bias ? c.bias[co] : 0.f, 0.f); }
+  __device__ void post(int z, int co, int i, float v, float2 e) const {
     int bb = z / c.s;
     const int r = z % c.s;
     if (fold) {
       bb = i / fold;
       i -= bb * fold;
     }
-    if (c.bias) v += c.bias[co];
+    if (c.bias) v += e.x;
     c.y[(size_t)bb * c.y_bstride + (size_t)co * c.y_cstride + c.y_off + (size_t)i * c.s + r] = v;
   }
+  __device__ void store(int z, int co, int i, float v) const { post(z, co, i, v, pre(z, co, i)); }
 };
 
 void launch_convtr(const ConvTrParams& p, hipStream_t st) {
@@ -556,30 +608,43 @@ struct LinProblem {
   __device__ float b(int, int kk, int m) const { return c.x[(size_t)m * c.xs + kk]; }
   __device__ const float* aptr(int, int n, int kk) const { return c.W + (size_t)n * c.K + kk; }
   __device__ bool kcontig() const { return true; }
+  bool wide_ok() const { return true; }
   __device__ bool b4k(int, int kk0, int m, float (&v)[4]) const {
     ld4(c.x + (size_t)m * c.xs + kk0, v);
     return true;
   }
   __device__ bool b4(int, int, int, float (&)[4]) const { return false; }
-  __device__ void store(int, int n, int m, float v) const {
+  __device__ float* optr(int n, int m) const {
     if (c.conv_T) {  // conv layout out[b][n][t], m = b*T + t
       const int bb = m / c.conv_T, t = m % c.conv_T;
-      float* o = c.out + (size_t)bb * c.conv_bstride + (size_t)n * c.conv_T + t;
-      *o = c.accumulate ? *o + v : v;
+      return c.out + (size_t)bb * c.conv_bstride + (size_t)n * c.conv_T + t;
+    }
+    return c.out + (size_t)m * c.os + n;
+  }
+  // (the value accumulated onto, the layer scale)
+  __device__ float2 pre(int, int n, int m) const {
+    if (c.conv_T) return make_float2(c.accumulate ? *optr(n, m) : 0.f, 0.f);
+    if (c.epi == EPI_ADD) return make_float2(*optr(n, m), c.scale ? c.scale[n] : 0.f);
+    return make_float2(0.f, 0.f);
+  }
+  __device__ void post(int, int n, int m, float v, float2 e) const {
+    float* o = optr(n, m);
+    if (c.conv_T) {
+      *o = c.accumulate ? e.x + v : v;
       return;
     }
-    float* o = c.out + (size_t)m * c.os + n;
     switch (c.epi) {
       case EPI_GELU:
         *o = c.gelu_erf ? gelu_erf_f(v) : gelu_tanh_f(v);
         break;
       case EPI_ADD:
-        *o += c.scale ? c.scale[n] * v : v;
+        *o = e.x + (c.scale ? e.y * v : v);
         break;
       default:
         *o = v;
     }
   }
+  __device__ void store(int z, int n, int m, float v) const { post(z, n, m, v, pre(z, n, m)); }
 };
 
 // Few rows (streaming decode_step: one row per utterance): gemm64's 64 x 64 tiles leave most of the
