@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Codec kernel-trace driver: encode B x S seconds of synthetic PCM twice and decode the codes once
-(synthetic mimi_202407 weights), for rocprofv3 --kernel-trace.  usage: python tools/mimi_prof.py [B] [S]"""
+(synthetic mimi_202407 weights), for rocprofv3 --kernel-trace.  usage: python tools/mimi_prof.py [B] [S] [out.npz]
+(out.npz: the codes and the decoded PCM, for bit-identity checks between settings)"""
 import os
 import sys
 import time
@@ -28,3 +29,5 @@ for it in range(2):
 t0 = time.perf_counter()
 y = codec.decode(codes)
 print(f"decode: {time.perf_counter() - t0:.4f} s  pcm {y.shape}", flush=True)
+if len(sys.argv) > 3:
+    np.savez(sys.argv[3], codes=codes, pcm=y)
