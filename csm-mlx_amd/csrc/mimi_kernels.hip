@@ -986,12 +986,20 @@ struct RvqStep {
   int M, T, cd, bins, nct, k, n_q;
 };
 
+// MF: the scores on the fp32 matrix cores (v_mfma_f32_32x32x2_f32: each (row, code) dot the same
+// k-ordered fmaf chain, the product's operand order immaterial -- bit-identical codes).  Wave w scores
+// codes 64 w .. 64 w + 63 of the tile against all 64 rows (2 x 2 tiles of 32 x 32); odd dims of r_k and
+// of the codebook chunk are stored with the 32-column halves swapped, so the two k rows an operand read
+// touches (lanes h = 0 / 1) sit on disjoint LDS bank halves.
+template <bool MF>
 __global__ __launch_bounds__(256) void rvq_step_kernel(RvqStep p) {
   typedef float f4 __attribute__((ext_vector_type(4)));
   __shared__ __attribute__((aligned(16))) float rsT[RQ_CDMAX][RQ_R];      // r_k [dim][row]
   __shared__ __attribute__((aligned(16))) float Bs[2][RQ_D][RQ_C];        // codebook chunk [dim][code]
   __shared__ int sidx[RQ_R];
+  __shared__ unsigned long long wred[MF ? 4 : 1][RQ_R];
   const int tid = threadIdx.x, ct = blockIdx.x, m0 = blockIdx.y * RQ_R;
+  auto sw = [](int d) { return MF ? (d & 1) * 32 : 0; };  // column swizzle of dim d's row
   const int cd = p.cd;
   // (1) finish codebook k-1 for the 64 rows
   if (tid < RQ_R) {
@@ -1010,7 +1018,7 @@ __global__ __launch_bounds__(256) void rvq_step_kernel(RvqStep p) {
     const int i = e / cd, d = e % cd, m = min(m0 + i, p.M - 1);
     float v = p.r_in[(size_t)m * cd + d];
     if (sidx[i] >= 0) v = v - p.cb_prev[(size_t)sidx[i] * cd + d];
-    rsT[d][i] = v;
+    rsT[d][i ^ sw(d)] = v;
     if (ct == 0 && m0 + i < p.M) p.r_out[(size_t)m * cd + d] = v;
   }
   if (!p.part_cur) return;  // finishing pass (after the last codebook)
@@ -1019,9 +1027,62 @@ __global__ __launch_bounds__(256) void rvq_step_kernel(RvqStep p) {
   auto load = [&](int buf, int d0) {
     for (int e = tid; e < RQ_D * RQ_C / 4; e += 256) {
       const int dd = e / (RQ_C / 4), c4 = (e % (RQ_C / 4)) * 4;
-      *reinterpret_cast<f4*>(&Bs[buf][dd][c4]) = *reinterpret_cast<const f4*>(p.cbT + (size_t)(d0 + dd) * p.bins + c0 + c4);
+      *reinterpret_cast<f4*>(&Bs[buf][dd][c4 ^ sw(dd)]) = *reinterpret_cast<const f4*>(p.cbT + (size_t)(d0 + dd) * p.bins + c0 + c4);
     }
   };
+  const int nch = cd / RQ_D;
+  if constexpr (MF) {
+    typedef float f32x16_t __attribute__((ext_vector_type(16)));
+    const int lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+    f32x16_t acc[2][2];
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int y = 0; y < 2; ++y) acc[x][y] = f32x16_t{};
+    load(0, 0);
+    __syncthreads();
+    for (int ch = 0; ch < nch; ++ch) {
+      const int buf = ch & 1;
+      if (ch + 1 < nch) load(buf ^ 1, (ch + 1) * RQ_D);
+#pragma unroll 4
+      for (int t = 0; t < RQ_D / 2; ++t) {
+        const int dd = 2 * t + h, d = ch * RQ_D + dd;  // (RQ_D even: d and dd share their parity)
+        float a[2], b[2];
+#pragma unroll
+        for (int x = 0; x < 2; ++x) a[x] = rsT[d][(32 * x + r) ^ sw(d)];
+#pragma unroll
+        for (int y = 0; y < 2; ++y) b[y] = Bs[buf][dd][(64 * wave + 32 * y + r) ^ sw(dd)];
+#pragma unroll
+        for (int x = 0; x < 2; ++x)
+#pragma unroll
+          for (int y = 0; y < 2; ++y) acc[x][y] = __builtin_amdgcn_mfma_f32_32x32x2f32(b[y], a[x], acc[x][y], 0, 0, 0);
+      }
+      __syncthreads();
+    }
+    // acc[x][y][q]: code 64 wave + 32 y + 8 (q >> 2) + 4 h + (q & 3), row 32 x + r (B operand = rows)
+    float c2[2][16];
+#pragma unroll
+    for (int y = 0; y < 2; ++y)
+#pragma unroll
+      for (int q = 0; q < 16; ++q) c2[y][q] = p.c2half[c0 + 64 * wave + 32 * y + 8 * (q >> 2) + 4 * h + (q & 3)];
+#pragma unroll
+    for (int x = 0; x < 2; ++x) {
+      unsigned long long best = ~0ull;
+#pragma unroll
+      for (int y = 0; y < 2; ++y)
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+          best = min(best, rq_key(c2[y][q] - acc[x][y][q], c0 + 64 * wave + 32 * y + 8 * (q >> 2) + 4 * h + (q & 3)));
+      best = min(best, (unsigned long long)__shfl_xor(best, 32, 64));  // the other half's codes of this row
+      if (h == 0) wred[wave][32 * x + r] = best;
+    }
+    __syncthreads();
+    if (tid < RQ_R) {
+      const unsigned long long best = min(min(wred[0][tid], wred[1][tid]), min(wred[2][tid], wred[3][tid]));
+      if (m0 + tid < p.M) p.part_cur[(size_t)(m0 + tid) * p.nct + ct] = best;
+    }
+    return;
+  }
   float acc[8][8];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
@@ -1029,7 +1090,6 @@ __global__ __launch_bounds__(256) void rvq_step_kernel(RvqStep p) {
     for (int j = 0; j < 8; ++j) acc[i][j] = 0.f;
   load(0, 0);
   __syncthreads();
-  const int nch = cd / RQ_D;
   for (int ch = 0; ch < nch; ++ch) {
     const int buf = ch & 1;
     if (ch + 1 < nch) load(buf ^ 1, (ch + 1) * RQ_D);
@@ -1065,6 +1125,12 @@ __global__ __launch_bounds__(256) void rvq_step_kernel(RvqStep p) {
   }
 }
 
+// CSM_RVQ_MFMA=0: the VALU scoring tile (A/B)
+static bool rvq_mfma() {
+  static const bool v = [] { const char* e = getenv("CSM_RVQ_MFMA"); return !e || atoi(e) != 0; }();
+  return v;
+}
+
 bool rvq_gemm_eligible(int cd, int bins) { return cd % RQ_D == 0 && cd <= RQ_CDMAX && bins % RQ_C == 0; }
 size_t rvq_gemm_parts(int M, int bins) { return (size_t)M * (bins / RQ_C); }
 
@@ -1087,7 +1153,8 @@ void launch_rvq_encode_gemm(float* r, int M, int T, int cd, const float* cb, con
     s.cbT = k < k1 ? cbT + (size_t)k * bins * cd : nullptr;
     s.c2half = k < k1 ? c2half + (size_t)k * bins : nullptr;
     // the finishing pass needs only code tile 0 (it writes the codes and r); it computes no distances
-    hipLaunchKernelGGL(rvq_step_kernel, k == k1 ? dim3(1, grid.y) : grid, dim3(256), 0, st, s);
+    if (rvq_mfma()) hipLaunchKernelGGL(rvq_step_kernel<true>, k == k1 ? dim3(1, grid.y) : grid, dim3(256), 0, st, s);
+    else hipLaunchKernelGGL(rvq_step_kernel<false>, k == k1 ? dim3(1, grid.y) : grid, dim3(256), 0, st, s);
   }
 }
 
