@@ -445,8 +445,14 @@ __global__ __launch_bounds__(64 * NW) void gemm_wide_kernel(GemvParams p) {
 // whole stages.  CSM_GEMM_NBR / CSM_GEMM_BLOCKS override (lab sweeps).
 static int g_nbr_env = [] { const char* e = getenv("CSM_GEMM_NBR"); return e ? atoi(e) : 0; }();
 static int g_blocks_env = [] { const char* e = getenv("CSM_GEMM_BLOCKS"); return e ? atoi(e) : 0; }();
+// int4 prompt prefill (>= 256 rows, the 8-wave blocks): 256 weight rows per block for every shape (the
+// block's activation staging -- norm, three-part split, group sums -- is shared by twice the columns):
+// config 5's prefill 0.155 -> 0.140 s (profiles/r04_ab_prefill_nbr.txt).  CSM_GEMM_PREFILL_NBR=0: the
+// per-shape widths below.
+static int g_prefill_nbr = [] { const char* e = getenv("CSM_GEMM_PREFILL_NBR"); return e ? atoi(e) : 256; }();
 static int gemm_nbr(int N, int K, int M, bool q4) {
   if (g_nbr_env == 64 || g_nbr_env == 128 || g_nbr_env == 256) return g_nbr_env;
+  if (q4 && M >= 256 && (g_prefill_nbr == 128 || g_prefill_nbr == 256)) return g_prefill_nbr;
   if (q4) {
     if (N >= 8192 && K >= 2048) return 256;
     if (N >= 8192 || (N >= 2048 && (N >= 3072 || K >= 8192))) return 128;
