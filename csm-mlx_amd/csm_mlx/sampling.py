@@ -70,25 +70,8 @@ def xtc_chain(temp, top_p, min_p, min_tokens_to_keep, top_k, xtc_probability, xt
     special = np.asarray(list(xtc_special_tokens), np.int64)
 
     def fn(lp):
-        x = np.array(lp, np.float64)
+        x = mlx_filter(lp, top_k, top_p, min_p, min_tokens_to_keep)
         ninf = -np.inf
-        if top_k > 0 and top_k < x.shape[-1]:
-            drop = np.argpartition(-x, top_k - 1, axis=-1)[:, top_k:]
-            np.put_along_axis(x, drop, ninf, axis=-1)
-        if 0.0 < top_p < 1.0:
-            order = np.argsort(x, axis=-1, kind="stable")
-            cum = np.cumsum(np.take_along_axis(np.exp(x), order, axis=-1), axis=-1)
-            cp = np.empty_like(cum)
-            np.put_along_axis(cp, order, cum, axis=-1)
-            x = np.where(cp > 1 - top_p, x, ninf)
-        if min_p != 0.0:
-            order = np.argsort(-x, axis=-1, kind="stable")
-            srt = np.take_along_axis(x, order, axis=-1)
-            rem = srt < srt[:, :1] + np.log(min_p)
-            rem[:, :min_tokens_to_keep] = False
-            rm = np.empty_like(rem)
-            np.put_along_axis(rm, order, rem, axis=-1)
-            x = np.where(rm, ninf, x)
         p = np.exp(x - x.max(axis=-1, keepdims=True))
         p /= p.sum(axis=-1, keepdims=True)
         floor = np.where(p > xtc_threshold, p, np.inf).min(axis=-1, keepdims=True)
@@ -100,6 +83,32 @@ def xtc_chain(temp, top_p, min_p, min_tokens_to_keep, top_k, xtc_probability, xt
         g = -np.log(-np.log(rng.random(x.shape)))
         return np.argmax(x / temp + g, axis=-1)
     return fn
+
+
+def mlx_filter(lp, top_k, top_p, min_p, min_tokens_to_keep):
+    """mlx_lm's top_k -> top_p -> min_p on host log-probabilities (B, V): the removed entries -inf
+    (float64; top_k keeps exactly k, as mlx's argpartition)."""
+    import numpy as np
+    x = np.array(lp, np.float64)
+    ninf = -np.inf
+    if top_k > 0 and top_k < x.shape[-1]:
+        drop = np.argpartition(-x, top_k - 1, axis=-1)[:, top_k:]
+        np.put_along_axis(x, drop, ninf, axis=-1)
+    if 0.0 < top_p < 1.0:
+        order = np.argsort(x, axis=-1, kind="stable")
+        cum = np.cumsum(np.take_along_axis(np.exp(x), order, axis=-1), axis=-1)
+        cp = np.empty_like(cum)
+        np.put_along_axis(cp, order, cum, axis=-1)
+        x = np.where(cp > 1 - top_p, x, ninf)
+    if min_p != 0.0:
+        order = np.argsort(-x, axis=-1, kind="stable")
+        srt = np.take_along_axis(x, order, axis=-1)
+        rem = srt < srt[:, :1] + np.log(min_p)
+        rem[:, :min_tokens_to_keep] = False
+        rm = np.empty_like(rem)
+        np.put_along_axis(rm, order, rem, axis=-1)
+        x = np.where(rm, ninf, x)
+    return x
 
 
 @dataclass(frozen=True)

@@ -74,6 +74,21 @@ def test_xtc_chain():
         make_sampler(0.8, xtc_probability=1.5)
 
 
+def test_host_filter_matches_oracle_chain():
+    """The host chain's top_k -> top_p -> min_p (csm_mlx.sampling.mlx_filter, under XTC) keeps the same
+    entries as the oracle's filter_keep (the GPU sampler's specification) on tie-free rows."""
+    from csm_mlx.sampling import mlx_filter
+    from oracle.csm_oracle import filter_keep
+    rng = np.random.default_rng(5)
+    for (k, tp, mp, mk) in [(50, 0.9, 0.05, 3), (0, 0.8, 0.0, 1), (40, 0.0, 0.1, 1), (2051, 0.95, 0.02, 5)]:
+        for _ in range(4):
+            logits = (rng.standard_normal(2051) * 3).astype(np.float32)
+            lp = logits.astype(np.float64) - np.log(np.exp(logits.astype(np.float64)).sum())
+            host = np.isfinite(mlx_filter(lp[None], k, tp, mp, mk)[0])
+            ref = filter_keep(logits, k, tp, mp, mk)
+            assert np.array_equal(host, ref), (k, tp, mp, mk, np.flatnonzero(host != ref)[:5])
+
+
 def test_filter_chain_restatement():
     """oracle filter_keep (mlx_lm apply_top_k -> apply_top_p -> apply_min_p) on hand-worked rows."""
     from oracle.csm_oracle import filter_keep
