@@ -460,6 +460,7 @@ static int gemm_nbr(int N, int K, int M, bool q4) {
   }
   return (N >= 8192 && M > 32) ? 128 : 64;
 }
+static int g_prefill_blocks = [] { const char* e = getenv("CSM_GEMM_PREFILL_BLOCKS"); return !e || atoi(e) != 0; }();
 static int gemm_ksplit(int N, int K, int M, bool q4) {
   const int nbr = gemm_nbr(N, K, M, q4);
   const int tiles = (N + nbr - 1) / nbr, chunks = (M + 63) / 64;
@@ -468,7 +469,10 @@ static int gemm_ksplit(int N, int K, int M, bool q4) {
   // 16.2 -> 15.4 and 12.7 -> 12.2) and the int4 backbone QKV (30.5 -> 25.2 us); every other
   // csm_1b shape is slower so
   const bool half = (size_t)N * K <= (size_t)1536 * 1024 || (q4 && N == 3072 && K == 2048);
-  const int target = g_blocks_env > 0 ? g_blocks_env : (half ? 128 : 256);
+  // the int4 prompt prefill (>= 256 rows on 256-row blocks): 128 too (its o / down at 248 blocks then run
+  // unsplit; profiles/r04_ab_prefill_blocks.txt)
+  const bool prefill = q4 && M >= 256 && g_prefill_blocks;
+  const int target = g_blocks_env > 0 ? g_blocks_env : ((half || prefill) ? 128 : 256);
   int ks = 1;
   while (tiles * chunks * ks < target && ks < GK_MAX_SLICES && K % (GP_KC * ks * 2) == 0) ks *= 2;
   return ks;
