@@ -144,7 +144,10 @@ class FrameCache:
             logits = np.ascontiguousarray(np.asarray(proc(hist, logits), np.float32).reshape(self.B, V))
         done = ctypes.c_int(0)
         for i in range(K):
-            codes = np.ascontiguousarray(np.clip(sampler(logits), 0, V - 1), np.int32)
+            raw = np.asarray(sampler(logits)).reshape(self.B)
+            if raw.size and (raw.min() < 0 or raw.max() >= V):   # no silent clamp: -1 -> 0 would read as EOS
+                raise ValueError(f"sampler returned a code outside [0, {V}): {raw.min()} .. {raw.max()}")
+            codes = np.ascontiguousarray(raw, np.int32)
             if i == 0 and c0_history is not None:
                 c0_history.append(codes[:, None].copy())
             out = np.zeros((self.B, V), np.float32)

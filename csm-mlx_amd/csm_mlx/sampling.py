@@ -60,11 +60,14 @@ def xtc_chain(temp, top_p, min_p, min_tokens_to_keep, top_k, xtc_probability, xt
               xtc_special_tokens=(), seed: int = 0):
     """mlx_lm's make_sampler chain with XTC, on host log-probabilities (B, V): top_k (exactly k kept),
     top_p (cumulative ascending probability > 1 - top_p), min_p (log p >= log p_max + log min_p, the
-    first ``min_tokens_to_keep`` by rank always kept), then XTC -- with probability
-    ``xtc_probability`` per row, every token whose probability exceeds the smallest probability above
-    ``xtc_threshold`` is removed (special tokens exempt) -- then a categorical draw of
-    ``logprobs / temp``.  Restated from mlx_lm's published sample_utils (not in /root/reference, which
-    never enables XTC): parity unpinned."""
+    first ``min_tokens_to_keep`` by rank always kept), then XTC as mlx_lm's ``apply_xtc`` -- ONE
+    uniform draw per call (for the whole batch) decides whether XTC applies, and the floor is ONE
+    minimum over the whole (B, V) array of the probabilities above ``xtc_threshold`` (``.min()`` with
+    no axis); every token whose probability exceeds that floor is removed (special tokens exempt) --
+    then a categorical draw of ``logprobs / temp``.  At B = 1 the per-call and per-row forms agree; at
+    B > 1 this keeps mlx_lm's batch-global form.  Restated from mlx_lm's published sample_utils (not in
+    /root/reference, which never enables XTC): parity unpinned; the arithmetic is pinned on hand-worked
+    rows in tests/test_abi_cpu.py."""
     import numpy as np
     rng = np.random.default_rng(seed)
     special = np.asarray(list(xtc_special_tokens), np.int64)
@@ -74,12 +77,12 @@ def xtc_chain(temp, top_p, min_p, min_tokens_to_keep, top_k, xtc_probability, xt
         ninf = -np.inf
         p = np.exp(x - x.max(axis=-1, keepdims=True))
         p /= p.sum(axis=-1, keepdims=True)
-        floor = np.where(p > xtc_threshold, p, np.inf).min(axis=-1, keepdims=True)
+        floor = np.where(p > xtc_threshold, p, np.inf).min()          # batch-global, as mlx_lm
         mask = p > floor
         if special.size:
             mask[:, special] = False
-        hit = rng.random((x.shape[0], 1)) <= xtc_probability
-        x = np.where(hit & mask, ninf, x)
+        if not rng.random() > xtc_probability:                          # one draw per call
+            x = np.where(mask, ninf, x)
         g = -np.log(-np.log(rng.random(x.shape)))
         return np.argmax(x / temp + g, axis=-1)
     return fn

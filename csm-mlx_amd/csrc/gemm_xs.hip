@@ -548,8 +548,13 @@ void xs_shape(int N, int K, int M, bool head, int& rtw, int& ks, int& pd, int& x
   static const int small_waves = [] { const char* v = getenv("CSM_XS_SMALL_WAVES"); const int w = v ? atoi(v) : 0; return w == 2 || w == 4 || w == 8 ? w : 8; }();
   const int want = waves ? waves : (head && N % 64 != 0 ? head_waves : (dec_small ? small_waves : 8));
   xw = nks >= 2 * want ? want : (nks >= 8 ? 4 : 2);
+  // every wave takes wst = nks / ks / xw whole stages: the waves must divide the slice's stages (K = 640:
+  // 10 stages -> 2 waves), or the leftover stages would never be computed (gemm_xs_eligible rejects a
+  // shape whose stage count no wave count divides)
+  while (xw > 2 && nks % xw != 0) xw /= 2;
   ks = 1;
-  while (tiles * ks < tgt && ks < MAX_SLICES && nks / (ks * 2) >= xw && nks % (ks * 2) == 0) ks *= 2;
+  while (tiles * ks < tgt && ks < MAX_SLICES && nks / (ks * 2) >= xw && nks % (ks * 2) == 0 && (nks / (ks * 2)) % xw == 0)
+    ks *= 2;
   const int wst = nks / ks / xw;
   // ring depth at 64 rows with 64-row tiles (lab knob CSM_XS_PD64, default 1: register budget)
   static const int cap64 = [] { const char* v = getenv("CSM_XS_PD64"); return v ? std::max(1, atoi(v)) : 1; }();
@@ -599,13 +604,22 @@ void gemm_xs_stamps_report(const char* tag) {
 
 bool gemm_xs_eligible(int N, int K, int M, int wdt) {
   if (!(wdt == WDT_BF16 || wdt == WDT_Q4) || M < 1 || M > GEMM_XS_MAX_M || N % 2 || K % XK || K / XK < 2) return false;
-  if (wdt == WDT_Q4)  // the X_g stage table holds <= Q4_XG stages per block
-    for (int h = 0; h < 2; ++h) {
-      int rtw, ks, pd, xw;
-      xs_shape(N, K, M, h == 1, rtw, ks, pd, xw);
-      if (K / XK / ks > Q4_XG) return false;
-    }
+  for (int h = 0; h < 2; ++h) {
+    int rtw, ks, pd, xw;
+    xs_shape(N, K, M, h == 1, rtw, ks, pd, xw);
+    if ((K / XK) % ks != 0 || (K / XK / ks) % xw != 0) return false;  // every stage on exactly one wave
+    if (wdt == WDT_Q4 && K / XK / ks > Q4_XG) return false;            // the X_g stage table holds <= Q4_XG stages
+  }
   return true;
+}
+
+// Host-side shape query (csm_hip_prof.h csm_xs_shape): the launch geometry gemm_xs would use, for the
+// CPU tests of the stage-coverage rule.
+extern "C" int csm_xs_shape(int N, int K, int M, int head, int* out) {
+  int rtw, ks, pd, xw;
+  xs_shape(N, K, M, head != 0, rtw, ks, pd, xw);
+  out[0] = rtw; out[1] = ks; out[2] = pd; out[3] = xw;
+  return gemm_xs_eligible(N, K, M, WDT_BF16) ? 1 : 0;
 }
 
 int gemm_xs_tiles(int N, int K, int M, bool head) {

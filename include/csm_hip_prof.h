@@ -49,6 +49,12 @@ int csm_bench_bb_step(csm_engine* e, int iters, float* avg_us, double* bytes);
  * Process-wide lab knobs are environment variables read once (CSM_NT_MASK, CSM_GEMV_XL, CSM_XS_*). */
 int csm_set_option(csm_engine* e, const char* key, int value);
 
+/* Launch geometry the streaming matrix-core GEMM (gemm_xs.hip) would use for an (N, K) projection at M
+ * rows (head != 0: an arg-max / SiLU launch): out[4] = {weight-row tiles of 32 per block, K slices,
+ * ring depth, waves per block}.  Returns 1 if the shape is eligible (every 64-deep K stage falls on
+ * exactly one wave of one slice), else 0.  Host-only (no device call). */
+int csm_xs_shape(int N, int K, int M, int head, int* out);
+
 #ifdef __cplusplus
 }
 #endif

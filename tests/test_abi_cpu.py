@@ -74,6 +74,24 @@ def test_xtc_chain():
         make_sampler(0.8, xtc_probability=1.5)
 
 
+def test_xtc_batch_global():
+    """mlx_lm's apply_xtc at B > 1: ONE floor over the whole array and ONE coin per call.  Rows
+    p = (0.5, 0.3, 0.15, 0.05) and (0.7, 0.12, 0.1, 0.08), threshold 0.1: the probabilities above it are
+    0.5, 0.3, 0.15 and 0.7, 0.12, so the batch floor is 0.12 -- row 0 loses 0.5, 0.3 AND 0.15 (survivor
+    index 3; a per-row floor of 0.15 would leave index 2), row 1 loses 0.7 (survivor index 1)."""
+    from csm_mlx import make_sampler
+    lp = np.log(np.array([[0.5, 0.3, 0.15, 0.05], [0.7, 0.12, 0.1, 0.08]], np.float32))
+    assert make_sampler(1e-6, xtc_probability=1.0, xtc_threshold=0.1)(lp).tolist() == [3, 1]
+    # one coin for the batch: identical rows either all lose their top tokens or none does
+    rows = np.log(np.array([[0.5, 0.3, 0.15, 0.05]] * 4, np.float32))
+    seen = set()
+    for seed in range(40):
+        out = make_sampler(1e-6, xtc_probability=0.5, xtc_threshold=0.1, seed=seed)(rows).tolist()
+        assert len(set(out)) == 1, out
+        seen.add(out[0])
+    assert seen == {0, 2}
+
+
 def test_host_filter_matches_oracle_chain():
     """The host chain's top_k -> top_p -> min_p (csm_mlx.sampling.mlx_filter, under XTC) keeps the same
     entries as the oracle's filter_keep (the GPU sampler's specification) on tie-free rows."""
@@ -133,3 +151,28 @@ def test_weights_loading_rejects_bad_shapes_without_gpu():
     m = CSM(csm_tiny(), dtype="float32")
     with pytest.raises(Exception):
         m.load_weights({"projection.weight": np.zeros((3, 3), np.float32)})
+
+
+def test_xs_shape_covers_every_stage():
+    """gemm_xs launch geometry (host code, no GPU): every eligible shape gives each wave of each K slice
+    the same whole number of 64-deep stages, so none is dropped -- K = 640 (10 stages) and 1280 (20)
+    included, which once picked 4 / 8 waves and silently skipped 2 / 4 stages."""
+    import ctypes
+    from csm_mlx import _lib
+    L = _lib.lib()
+    out = (ctypes.c_int * 4)()
+    seen = 0
+    for K in range(128, 8192 + 1, 64):
+        for N in (256, 1024, 1536, 2056, 16384):
+            for M in (8, 32, 64):
+                for head in (0, 1):
+                    ok = L.csm_xs_shape(N, K, M, head, out)
+                    rtw, ks, pd, xw = list(out)
+                    nks = K // 64
+                    if ok:
+                        seen += 1
+                        assert nks % ks == 0 and (nks // ks) % xw == 0 and xw in (2, 4, 8), (N, K, M, head, list(out))
+                        assert (nks // ks // xw) % pd == 0
+    assert seen > 0
+    out640 = (ctypes.c_int * 4)()
+    assert L.csm_xs_shape(1024, 640, 32, 0, out640) == 1 and (10 // out640[1]) % out640[3] == 0
