@@ -101,6 +101,25 @@ def aggregate(frames_local: float, dt_local: float, world: int, device=None):
     return float(f.item()), float(m.item())
 
 
+def rank_report(frames_local: float, dt_local: float, steps: int, world: int, device_index: int, device=None):
+    """What the communicator saw: backend, world size, and per rank its GPU index, its own
+    ms per step and frames -- all-gathered, so a scaling line shows which rank was slowest."""
+    me = [float(device_index), dt_local / max(1, steps) * 1000.0, frames_local]
+    if world == 1 and "WORLD_SIZE" not in os.environ:
+        return {"backend": None, "world_size_seen": 1,
+                "ranks": [{"rank": 0, "device": device_index, "ms_per_step": round(me[1], 3), "frames": int(me[2])}],
+                "slowest_rank": 0}
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor(me, dtype=torch.float64, device=device)
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    rows = [o.cpu().tolist() for o in out]
+    ranks = [{"rank": r, "device": int(v[0]), "ms_per_step": round(v[1], 3), "frames": int(v[2])} for r, v in enumerate(rows)]
+    return {"backend": dist.get_backend(), "world_size_seen": dist.get_world_size(), "ranks": ranks,
+            "slowest_rank": max(range(len(ranks)), key=lambda r: ranks[r]["ms_per_step"])}
+
+
 def build_codec(seed=0, device=None, model_name="csm_1b"):
     from csm_mlx.config import MIMI_CONFIGURATION
     from csm_mlx.mimi import MimiCodec
@@ -278,7 +297,7 @@ def _traffic(key: str):
     return (ent["bytes"], ent["source"]) if ent else (None, None)
 
 
-def rooflines(model, batch: int):
+def rooflines(model, batch: int, iters: int = 400):
     """Live HIP-event rooflines on the engine stream.  ``dominant``: the persistent frame decoder
     (dec_frame_kernel, one launch per frame) when it runs the frame's head -- batch 1 bf16 --
     else the decoder gate/up projection at this batch; ``backbone_gate_up`` beside it: the persistent
@@ -295,21 +314,23 @@ def rooflines(model, batch: int):
                 "avg_us": round(us, 3), "bytes_per_launch": int(nb), "kernel": kernel}
 
     def gemv(which, stack):
+        if iters <= 0:   # (PMC passes: counters on the frame's own launches only, no replays)
+            return None
         us, nb = ctypes.c_float(0), ctypes.c_double(0)
         xs = _decoder_xs(model, batch) if stack == "decoder" else _backbone_xs(model, batch)   # the kernel the frame runs (| 8: gemm_xs)
-        _lib.check(L.csm_bench_gemv(model.engine, which | (8 if xs else 0), batch, 400, ctypes.byref(us), ctypes.byref(nb)))
+        _lib.check(L.csm_bench_gemv(model.engine, which | (8 if xs else 0), batch, iters, ctypes.byref(us), ctypes.byref(nb)))
         return entry(us.value, nb.value, _kernel_name(model, batch, stack),
                      f"{stack}_gate_up{'_xs' if xs else ''}/{model.dtype}/B{batch}")
 
     us, nb = ctypes.c_float(0), ctypes.c_double(0)
-    if batch == 1 and L.csm_bench_bb_step(model.engine, 20, ctypes.byref(us), ctypes.byref(nb)) == 0:
+    if batch == 1 and iters > 0 and L.csm_bench_bb_step(model.engine, 20, ctypes.byref(us), ctypes.byref(nb)) == 0:
         out = {"backbone_gate_up": entry(us.value, nb.value, "bb_step_kernel = persistent backbone step: the 16 "
                                          "backbone blocks + final norm of one decode row, one launch",
                                          f"bb_step/{model.dtype}/B1")}
     else:
         out = {"backbone_gate_up": gemv(0, "backbone")}
     us, nb = ctypes.c_float(0), ctypes.c_double(0)
-    if batch == 1 and L.csm_bench_dec_frame(model.engine, 20, ctypes.byref(us), ctypes.byref(nb)) == 0:
+    if batch == 1 and iters > 0 and L.csm_bench_dec_frame(model.engine, 20, ctypes.byref(us), ctypes.byref(nb)) == 0:
         out["dominant"] = entry(us.value, nb.value, "dec_frame_kernel = persistent frame decoder: codebook0_head + "
                                 "31 decoder steps (4 layers + audio_head slice each) of one frame, one launch",
                                 f"dec_frame/{model.dtype}/B1")
@@ -335,6 +356,9 @@ def main():
     ap.add_argument("--config", type=int, default=0, choices=[0, 2, 3, 4, 5, 6, 7],
                     help="run BASELINE.json configs[N-1] (batch, dtype, sampling, streaming, context) instead of "
                          "the default configs[1] line; the metric stays audio frames/s")
+    ap.add_argument("--roofline-iters", type=int, default=400,
+                    help="replays of the batched roofline projection after the timed steps (0: none, for PMC passes "
+                         "whose per-kernel averages must cover the frame's own launches only)")
     ap.add_argument("--phases", action="store_true",
                     help="add phases_s_per_step: wall seconds of Mimi encode / prefill / frames / Mimi decode per "
                          "step (the engine is synchronized at each boundary)")
@@ -479,8 +503,9 @@ def main():
     barrier_sync()
     dt = time.perf_counter() - t0
     total_frames, max_dt = aggregate(float(frames), dt, world, dev)
+    dist_info = rank_report(float(frames), dt, args.steps, world, device, dev)
 
-    roof = rooflines(model, args.batch)
+    roof = rooflines(model, args.batch, args.roofline_iters)
     fb = frame_weight_bytes(model)
     frame_steps_per_s = total_frames / max_dt / max(1, args.batch * world)   # engine frame steps / s per GPU
     ach_f = fb * frame_steps_per_s / 1e9
@@ -525,6 +550,7 @@ def main():
                        "parallelism": f"dp{world}", "rtf": round(total_frames / max_dt / 12.5, 2),
                        "weights": weights_info,
                        "results": results_info},
+            "dist": dist_info,
             "roofline": roof["dominant"],
             "roofline_backbone": roof["backbone_gate_up"],
             "roofline_frame": roof_frame,

@@ -67,11 +67,11 @@ DECODER_CONFIGURATION = {
         num_hidden_layers=2, num_attention_heads=2, num_key_value_heads=1, head_dim=128,
         intermediate_size=512, hidden_size=256,
     ),
-    # test-only: a non-power-of-two MLP width (down_proj K = 640 = 10 stages of 64) for the streaming
+    # test-only: a non-power-of-two MLP width (down_proj K = 1280 = 20 stages of 64) for the streaming
     # GEMM's stage-coverage rule (tests/test_gemm_gpu.py)
-    "tiny_f640": LlamaArgs(
+    "tiny_f1280": LlamaArgs(
         num_hidden_layers=2, num_attention_heads=2, num_key_value_heads=1, head_dim=128,
-        intermediate_size=640, hidden_size=256,
+        intermediate_size=1280, hidden_size=256,
     ),
 }
 

@@ -130,12 +130,107 @@ def mimi_golden():
     return out
 
 
+# ----------------------------------------------------------------------------- batched, full length
+# configs[3]'s per-GPU shard (B = 32 bf16 greedy, 125 frames) and configs[2] (B = 32, temperature 0.8,
+# top-k 50, streamed) on the EOS-capable rig of the seed-0 weights (tests/helpers.py eos_rig): prompts
+# as bench.py's prompt_ids(g), g = 0..31; sampling seeds 1234 + g.
+B32_FRAMES = (0, 64, 100, 124)      # frames whose logits are kept (past the backbone's first 64-key chunk)
+B32_CI = (1, 16, 31)                # codebooks whose ci logits are kept
+B32_LOGIT_UTTS = 4                  # logits kept for the first 4 utterances that run all frames (size)
+B32_PROJ = 4                        # random unit vectors per streamed chunk's projection statistics
+
+
+def _b32_prompts():
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from helpers import prompt_ids
+    return [text_frame(prompt_ids(1 if g == 0 else 1000 + g), 32) for g in range(32)]
+
+
+def _b32_run(frames, temperature=0.0, top_k=0, keep_logits=True):
+    """One (32, L, 33) batch through the oracle frame by frame (utterances are independent, so each one's
+    codes up to its EOS frame are those of a run alone, generation.py:139-161).  Returns codes (32, F, K),
+    n_frames (first all-zero frame, or F), c0 (F, 32, V), ci (F, 32, K-1, V) logits."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from helpers import eos_weights, oracle_for
+    args, w = eos_weights("1b")
+    o = oracle_for(args, w, bf16=True)
+    prompts = _b32_prompts()
+    toks = np.stack([t for t, _ in prompts]).astype(np.int64)
+    msk = np.stack([m for _, m in prompts]).astype(bool)
+    seeds = [1234 + g for g in range(32)]
+    cache = o.new_backbone_cache()
+    codes, c0s, cis = [], [], []
+    for f in range(frames):
+        s = o.frame(toks, msk, cache, temperature, top_k, seeds, f)
+        codes.append(s)
+        if keep_logits:
+            c0s.append(o.debug["c0_logits"].copy())
+            cis.append(o.debug["ci_logits"].copy())
+        toks = np.concatenate([s, np.zeros((32, 1), np.int32)], 1)[:, None, :].astype(np.int64)
+        msk = np.concatenate([np.ones_like(s, bool), np.zeros((32, 1), bool)], 1)[:, None, :]
+        print("frame", f, "zero frames so far", int((~np.stack(codes, 1).any(-1)).any(-1).sum()), flush=True)
+    codes = np.stack(codes, 1)
+    zero = ~codes.any(-1)                                        # (32, F) all-zero frames
+    n = np.array([int(np.argmax(z)) if z.any() else frames for z in zero], np.int32)
+    return codes, n, (np.stack(c0s) if keep_logits else None), (np.stack(cis) if keep_logits else None)
+
+
+def config4_b32_golden():
+    """configs[3]'s shard: B = 32 bf16 greedy, 125 frames; codes up to each utterance's EOS; c0 logits at
+    B32_FRAMES and ci logits of B32_CI for every utterance still running there (and at each EOS frame)."""
+    codes, n, c0, ci = _b32_run(125)
+    print("n_frames", n.tolist(), flush=True)
+    out = dict(codes=codes, n_frames=n, frames=np.array(B32_FRAMES), ci_codebooks=np.array(B32_CI))
+    utts = [b for b in range(32) if n[b] == 125][:B32_LOGIT_UTTS]
+    out["logit_utts"] = np.array(utts, np.int32)
+    out["c0"] = np.stack([c0[f][utts] for f in B32_FRAMES])                      # (4 frames, 4 utts, V)
+    out["ci"] = np.stack([ci[f][utts][:, [c - 1 for c in B32_CI]] for f in B32_FRAMES])   # (4, 4, 3, V)
+    eos = [b for b in range(32) if n[b] < 125]
+    out["eos_utts"] = np.array(eos, np.int32)
+    out["eos_c0"] = np.stack([c0[n[b], b] for b in eos]) if eos else np.zeros((0, c0.shape[-1]), np.float32)
+    return out
+
+
+def config3_b32_golden(frames=64):
+    """configs[2]: B = 32, temperature 0.8, top-k 50 (the oracle's restatement of the engine's counter-based
+    RNG), 32 frames; the Mimi oracle's streaming decode_step of every frame: per (utterance, frame) RMS,
+    mean and B32_PROJ projections on seeded unit vectors, and the whole PCM of utterance 0 and of every
+    utterance that ends (frames before its EOS)."""
+    from csm_mlx.weights import synthetic_mimi_weights
+    codes, n, _, _ = _b32_run(frames, 0.8, 50, keep_logits=False)
+    print("n_frames", n.tolist(), flush=True)
+    m = MIMI_CONFIGURATION["mimi_202407"]
+    om = OracleMimi(m, synthetic_mimi_weights(m, 0))
+    om.reset_state()
+    vec = np.random.default_rng(5).standard_normal((B32_PROJ, 1920))
+    vec /= np.linalg.norm(vec, axis=1, keepdims=True)
+    keep = [0] + [b for b in range(32) if n[b] < frames]
+    rms, mean, proj = [], [], []
+    pcm = {b: [] for b in keep}
+    for f in range(frames):
+        y = om.decode_step(np.ascontiguousarray(codes[:, f, :, None]))[:, 0].astype(np.float64)   # (32, 1920)
+        rms.append(np.sqrt(np.mean(y ** 2, axis=1)))
+        mean.append(y.mean(axis=1))
+        proj.append(y @ vec.T)
+        for b in keep:
+            if f < n[b]:
+                pcm[b].append(y[b].astype(np.float32))
+        print("mimi frame", f, flush=True)
+    out = dict(codes=codes, n_frames=n, rms=np.stack(rms, 1), mean=np.stack(mean, 1), proj=np.stack(proj, 1),
+               proj_vec=vec, pcm_utts=np.array(keep, np.int32))
+    for b in keep:
+        out[f"pcm_{b}"] = np.stack(pcm[b]) if pcm[b] else np.zeros((0, 1920), np.float32)
+    return out
+
+
 FIXTURES = {
     "csm_tiny_oracle.npz": csm_golden,
     "mimi_tiny_oracle.npz": mimi_golden,
     "tiny_long_prompt.npz": tiny_long_golden,
     "csm_1b_greedy_125.npz": csm_1b_long_golden,
     "config0_plumbing.npz": config0_golden,
+    "config4_b32_greedy_125.npz": config4_b32_golden,
+    "config3_b32_stream_64.npz": config3_b32_golden,
 }
 
 if __name__ == "__main__":

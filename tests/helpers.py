@@ -127,3 +127,47 @@ def oracle_batch(o, prompts, frames, collect_logits=False, temperature=0.0, top_
             else:
                 out[i] = (codes[j], [(c0[j], ci[j]) for c0, ci in logs] if collect_logits else None)
     return out
+
+
+# ----------------------------------------------------------------------------- EOS-capable weights
+EOS_RIG = dict(alpha=2.5, emb_norm=20.0, head_gain=0.5, seed=77)
+
+
+def eos_rig(args, w, alpha=EOS_RIG["alpha"], emb_norm=EOS_RIG["emb_norm"], head_gain=EOS_RIG["head_gain"],
+            seed=EOS_RIG["seed"]):
+    """Seeded synthetic weights in which an utterance CAN end (test infrastructure).
+
+    The reference stops an utterance at the first all-zero frame (generation.py:151).  With plain random
+    weights all 32 codes are never 0 together, so EOS is never exercised.  The rig (documented here and
+    in DESIGN.md; nothing else changes):
+      * audio_embeddings row ``0 + V*j`` (code 0 of codebook j, j < K-1) = ``emb_norm`` x a seeded unit
+        vector u_j -- ~20x a normal row, so when c_j = 0 the decoder's residual stream at the next step
+        is dominated by projection(u_j);
+      * audio_head[j][:, 0] (code 0 of codebook j+1) = ``head_gain`` x the unit direction of
+        projection(u_j) -- logit 0 then leads by ~10 whenever c_j = 0: a zero code chains to the end of
+        the frame (greedy and sampled alike);
+      * codebook0_head row 0 scaled by ``alpha`` -- c0 = 0 (and so the all-zero frame) becomes an
+        occasional event whose timing depends on the utterance.
+    Returns a new dict (the input is not modified)."""
+    V, K = args.n_audio_vocab, args.n_audio_codebooks
+    rng = np.random.default_rng(seed)
+    out = dict(w)
+    emb = np.array(w["audio_embeddings.weight"], np.float32)
+    ah = np.array(w["audio_head"], np.float32)
+    wp = np.asarray(w["projection.weight"], np.float32)
+    for j in range(K - 1):
+        u = rng.standard_normal(emb.shape[1]).astype(np.float32)
+        u *= emb_norm / np.linalg.norm(u)
+        emb[j * V] = u
+        d = wp @ u
+        ah[j][:, 0] = head_gain * d / np.linalg.norm(d)
+    c0 = np.array(w["codebook0_head.weight"], np.float32)
+    c0[0] *= alpha
+    out["audio_embeddings.weight"], out["audio_head"], out["codebook0_head.weight"] = emb, ah, c0
+    return out
+
+
+@functools.lru_cache(maxsize=2)
+def eos_weights(args_key="1b", seed=0):
+    args, w = csm_weights(args_key, seed)
+    return args, eos_rig(args, w)

@@ -1,0 +1,129 @@
+"""Batched configs at full length against committed oracle fixtures (tests/golden/make_golden.py):
+
+* configs[3]'s per-GPU shard -- csm_1b bf16 B = 32 greedy, all 125 frames (the backbone's batched
+  attention past one 64-key chunk), codes of every utterance up to its EOS, c0 logits and the ci logits
+  of codebooks 1 / 16 / 31 at frames 0 / 64 / 100 / 124 for four utterances that run all 125 frames,
+  and the c0 logits of each early utterance's EOS frame;
+* configs[2] -- B = 32, temperature 0.8, top-k 50, ``stream_generate_batch`` over 64 frames: codes
+  (the oracle's restatement of the engine's counter-based RNG) and, per (utterance, frame) before its
+  EOS, the streamed chunk's RMS, mean and projections on four seeded unit vectors against the Mimi
+  oracle's ``decode_step``, plus whole chunks of utterance 0 and of every utterance that ends.
+
+Both run on the EOS-capable rig of the seed-0 weights (tests/helpers.py eos_rig), so utterances end at
+different frames (per-utterance EOS at B > 1, generation.py:139-161).  Bars: codes and frame counts
+bit-exact; logits within 2e-3 x max|logit|; chunks within 1e-4 RMS (statistics: within what a 1e-4
+RMS error allows)."""
+import os
+
+import numpy as np
+import pytest
+
+from helpers import eos_weights, first_divergence
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _fixture(name):
+    return np.load(os.path.join(GOLDEN, name), allow_pickle=False)
+
+
+def _prompts():
+    from csm_mlx.tokenizers import tokenize_text_segment
+    from helpers import prompt_ids
+    return [tokenize_text_segment(prompt_ids(1 if g == 0 else 1000 + g), 0, 32) for g in range(32)]
+
+
+def _model(args, w, B):
+    from csm_mlx.models import CSM
+    m = CSM(args, dtype="bf16", max_batch=B)
+    m.load_weights(w)
+    return m
+
+
+def _check_codes(hist, n, z):
+    ref_n = z["n_frames"]
+    assert (ref_n < z["codes"].shape[1]).any(), "the fixture has no utterance that ends early"
+    bad = []
+    for b in range(len(ref_n)):
+        want = z["codes"][b, : ref_n[b]]
+        got = hist[: n[b], b]
+        div = first_divergence(got, want)
+        if div is not None or n[b] != ref_n[b]:
+            bad.append(f"utterance {b}: {n[b]} vs {ref_n[b]} frames, first divergence {div}")
+    assert not bad, "; ".join(bad)
+
+
+def test_config4_shard_b32_greedy_125_frames():
+    from csm_mlx.generation import FrameCache
+    from csm_mlx.sampling import Sampler
+    z = _fixture("config4_b32_greedy_125.npz")
+    args, w = eos_weights("1b")
+    B, K, V = 32, args.n_audio_codebooks, args.n_audio_vocab
+    Vp = (V + 7) // 8 * 8
+    model = _model(args, w, B)
+    cache = FrameCache(model, B, Sampler(0.0, 0), [0] * B)
+    cache.prefill_batch([(b, t, m) for b, (t, m) in enumerate(_prompts())])
+    keep = {int(f): i for i, f in enumerate(z["frames"])}
+    ref_n = z["n_frames"]
+    eos_at = {int(ref_n[b]): [] for b in z["eos_utts"]}
+    for b in z["eos_utts"]:
+        eos_at[int(ref_n[b])].append(int(b))
+    cis = [c - 1 for c in z["ci_codebooks"]]
+    errs = []
+    for f in range(125):
+        cache.run(1)
+        if f in keep or f in eos_at:
+            c0 = cache.debug("c0_logits", (B, Vp))[:, :V]
+        if f in keep:
+            ci = cache.debug("ci_logits", (K - 1, B, Vp))[:, :, :V]
+            i = keep[f]
+            for j, b in enumerate(z["logit_utts"]):            # (utterances that run all 125 frames)
+                for got, want in ((c0[b], z["c0"][i, j]), (ci[cis, b], z["ci"][i, j])):
+                    err = float(np.abs(got - want).max())
+                    if err > 2e-3 * float(np.abs(want).max()):
+                        errs.append(f"frame {f} utterance {b}: logits err {err:.3e}")
+        for b in eos_at.get(f, []):
+            j = list(z["eos_utts"]).index(b)
+            err = float(np.abs(c0[b] - z["eos_c0"][j]).max())
+            if err > 2e-3 * float(np.abs(z["eos_c0"][j]).max()):
+                errs.append(f"EOS frame {f} utterance {b}: c0 logits err {err:.3e}")
+    hist, n, _ = cache.codes()
+    del model
+    _check_codes(hist, n, z)
+    assert not errs, "; ".join(errs[:10])
+
+
+def test_config3_stream_b32_sampled_64_frames():
+    from csm_mlx.generation import stream_generate_batch
+    from test_configs_gpu import _codec, _engine_codes
+    z = _fixture("config3_b32_stream_64.npz")
+    args, w = eos_weights("1b")
+    B, frames = 32, int(z["codes"].shape[1])
+    model = _model(args, w, B)
+    _codec(B)
+    chunks = [pcm.copy() for pcm, _ in stream_generate_batch(model, _prompts(), frames * 80, temperature=0.8,
+                                                             top_k=50, seeds=[1234 + g for g in range(B)])]
+    hist, n = _engine_codes(model, B)
+    del model
+    _check_codes(hist, n, z)
+    ref_n = z["n_frames"]
+    assert len(chunks) >= int(ref_n.max())
+    vec = z["proj_vec"]
+    bad = []
+    for f in range(int(ref_n.max())):
+        y = chunks[f].astype(np.float64)
+        for b in range(B):
+            if f >= ref_n[b]:
+                continue
+            rms = float(np.sqrt(np.mean(y[b] ** 2)))
+            if abs(rms - z["rms"][b, f]) > 1e-4 or abs(float(y[b].mean()) - z["mean"][b, f]) > 1e-4 or \
+                    np.abs(y[b] @ vec.T - z["proj"][b, f]).max() > 1e-4 * np.sqrt(1920):
+                bad.append(f"utterance {b} frame {f}")
+    for b in z["pcm_utts"]:
+        ref = z[f"pcm_{b}"]
+        got = np.stack([chunks[f][b] for f in range(len(ref))]) if len(ref) else ref
+        err = float(np.sqrt(np.mean((got.astype(np.float64) - ref) ** 2))) if len(ref) else 0.0
+        if err > 1e-4:
+            bad.append(f"utterance {b}: chunk RMS error {err:.3e}")
+    assert not bad, "; ".join(bad[:10])

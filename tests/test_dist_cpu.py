@@ -174,3 +174,36 @@ def test_gather_results_to_rank0_world3():
         assert np.array_equal(p_all[g], np.full((g % 3 + 1) * 8, g, np.float32))
     for _, c, p in res[1:]:
         assert c is None and p is None
+
+
+def _report_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "csm-mlx_amd"), root]
+    import torch.distributed as dist
+    import bench
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rep = bench.rank_report(125.0 * (rank + 1), 2.0 + rank, 4, world, device_index=rank % 1)
+    q.put((rank, rep))
+    dist.destroy_process_group()
+
+
+def test_rank_report_world2():
+    """bench.py's self-describing multi-rank line: backend and world size as the communicator saw them,
+    every rank's device, ms per step and frames on every rank, and the slowest rank named."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_report_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(60)
+    for rank, rep in res.items():
+        assert rep["backend"] == "gloo" and rep["world_size_seen"] == 2
+        assert [r["rank"] for r in rep["ranks"]] == [0, 1]
+        assert [r["ms_per_step"] for r in rep["ranks"]] == [500.0, 750.0]
+        assert [r["frames"] for r in rep["ranks"]] == [125, 250]
+        assert rep["slowest_rank"] == 1

@@ -35,10 +35,10 @@ def _free_port():
 
 
 def _bench(tmp_path, nproc, batch_per_rank, frames, name, backend="gloo", launcher=False, model="tiny",
-           dtype="float32"):
+           dtype="float32", steps=1):
     out = tmp_path / f"{name}.npz"
     args = [os.path.join(ROOT, "bench.py"), "--gpus", str(nproc), "--model", model, "--dtype", dtype,
-            "--batch", str(batch_per_rank), "--frames", str(frames), "--steps", "1", "--warmup", "0",
+            "--batch", str(batch_per_rank), "--frames", str(frames), "--steps", str(steps), "--warmup", "0",
             "--dist-backend", backend, "--no-cpu-baseline", "--dump", str(out)]
     if launcher:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
@@ -82,3 +82,20 @@ def test_rccl_world1_broadcast_and_gather(tmp_path):
     for g in range(3):
         assert np.array_equal(codes_n[g], codes1[g]), f"utterance {g} codes"
         assert np.array_equal(pcm_n[g], pcm1[g]), f"utterance {g} PCM"
+
+
+def test_rccl_world1_persistent_kernels(tmp_path):
+    """The headline path under a live RCCL communicator: csm_1b bf16 B = 1 greedy (the persistent backbone
+    step and frame decoder, which need every CU of the device) inside ``torch.distributed.run`` on the
+    nccl group, two timed steps with the per-step gather to rank 0 between them: codes identical to the
+    plain single-process run, and the line names what the communicator saw."""
+    line_n, codes_n, _ = _bench(tmp_path, 1, 1, 24, "nccl_pk", backend="nccl", launcher=True, model="csm_1b",
+                                dtype="bf16", steps=2)
+    assert line_n["dist"]["backend"] == "nccl" and line_n["dist"]["world_size_seen"] == 1
+    assert len(line_n["dist"]["ranks"]) == 1 and line_n["dist"]["ranks"][0]["frames"] == 2 * 24
+    assert line_n["roofline"]["kernel"].startswith("dec_frame_kernel"), line_n["roofline"]["kernel"]
+    assert line_n["roofline_backbone"]["kernel"].startswith("bb_step_kernel"), line_n["roofline_backbone"]["kernel"]
+    line_1, codes_1, _ = _bench(tmp_path, 1, 1, 24, "plain_pk", model="csm_1b", dtype="bf16", steps=2)
+    assert line_1["dist"]["backend"] is None
+    assert len(codes_n) == len(codes_1) == 1
+    assert np.array_equal(codes_n[0], codes_1[0]), "codes under the RCCL group differ from the plain run"

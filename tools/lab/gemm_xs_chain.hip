@@ -1,3 +1,13 @@
+// LAB (not built, not product; it needs csm_kernels.hip's attn_short_head in a header, attn_short.h): round 5's prototype of the chained batched decoder launches --
+// gemm_xs.hip refactored into a body function (xs_body) with its LDS in one struct, plus
+// dec_attn_o_kernel (short attention + o_proj in one launch) and dec_mlp_kernel (gate/up + SiLU*up ->
+// down split-K in one launch), the later step's blocks issuing their weight ring, then waiting on
+// counters the earlier step's blocks publish (release/acquire at agent scope; lower-block-index
+// dependencies only).  Driven from csm_engine.hip run_dec_xs behind CSM_XS_CHAIN (bit 0 attention+o,
+// bit 1 MLP); bit-exact (tests/test_gemm_gpu.py + tests/test_configs_gpu.py: 23 passed) but SLOWER:
+// config 4 4304 -> 3985 (attn+o) / 3871 (MLP) / 3571 (both) frames/s; without the fences (invalid)
+// 3881; dec_mlp_kernel 30.1 us against 12.3 + 8.9 us for the two launches, dec_attn_o_kernel 18.4 us
+// against 6.1 + 8.9 (profiles/r05_ab_chain.txt).  Kept for the record; the product keeps separate launches.
 // Streaming matrix-core GEMM for the batched depth decoder: y[m, n] = sum_k A[m, k] W[n, k] at
 // M <= 64 batch rows (generation.py:72-90 at batch B: the projection, QKV / o / gate-up / down of
 // every decoder layer and the audio_head slices, once per codebook step).
@@ -23,6 +33,7 @@
 #include <cstdio>
 #include <cstdlib>
 
+#include "attn_short.h"
 #include "csm_kernels.h"
 #include "xs.h"
 
@@ -95,37 +106,95 @@ __device__ unsigned g_xs_launch;
     const unsigned bl = blockIdx.x + gridDim.x * blockIdx.y, ln = p.lab_launch % XS_ST_LAUNCHES; \
     if (bl < XS_ST_BLOCKS) g_xs_st[ln][bl][k] = __builtin_amdgcn_s_memrealtime(); } } } while (0)
 
-// ROLE: a name tag only (1 QKV, 2 o_proj, 3 down): the decoder's small projections share one shape at
-// 32 bf16 / 64 int4 rows, and a tagged instantiation per role lets a rocprofv3 counter pass attribute
-// FETCH_SIZE to each (launch_gemm_xs); the code is identical.
-template <bool Q4, int MT, int RTW, int PD, bool NT, int XW, int ROLE = 0>
-__global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
+// Geometry / reduction layout of one block shape.
+template <bool Q4, int MT, int RTW, int XW>
+struct XsCfg {
+  static constexpr int NB = 32 * MT, NBR = 32 * RTW, NTH = 64 * XW;
+  // reduction slots: one per wave where the slab fits 64 KB (then every wave stores once and the
+  // ct pass adds (w, w + 4) pairs in the pre-add's order -- one barrier and one LDS round trip
+  // fewer, same sums); else 8-wave blocks pre-add waves w + 4 into w through 4 slots
+  // RED_HALF (8 waves, two row tiles, 128 KB of partials): the same single pass per row tile in turn
+  // -- every wave stores its row tile t partials into its own slot, the ct pass builds rows 32 t ..
+  // 32 t + 31 -- instead of the 4-slot pre-add (whose phases leave half the waves idle)
+  static constexpr bool RED_ALL = XW > 4 && MT * RTW * 16 * 64 * 4 * XW <= 65536;
+  static constexpr bool RED_HALF = !RED_ALL && XW > 4 && MT == 2 && RTW * 16 * 64 * 4 * XW <= 65536;
+  static constexpr int RW = (RED_ALL || RED_HALF) ? XW : (XW > 4 ? 4 : XW);
+};
+
+// The block's LDS (one struct, so a chained launch can overlay the LDS of its roles).
+template <bool Q4, int MT, int RTW, int XW>
+struct __attribute__((aligned(16))) XsLds {
+  using C = XsCfg<Q4, MT, RTW, XW>;
+  // (largest first, the reduction slots at offset 0: the slot pairs (w, w + 4) stay within one
+  // ds_read2st64's offset range, as with separately declared arrays)
+  float red[C::RW][(C::RED_HALF ? 1 : MT) * RTW * 16][64];
+  float sss[SS_MAX + 2 * 64 * XW];                    // [t][NB] partial sums of squares
+  float xg[Q4 ? XW : 1][Q4 ? Q4_XG / XW : 1][C::NB];  // int4: X_g of this block's stages
+  float res[C::NB * C::NBR + 64 * XW];                // [NB][NBR] residual rows (EPI_ADD)
+  float ct[C::NB][C::NBR + 1];
+  float hb[C::NB][C::NBR / 2 + 1];
+  float pss[C::NB][C::NBR / 8 + 1], phs[C::NB][C::NBR / 8 + 1];  // producer: 8-column partial sums
+  float nws[64];                                      // xs_nw[col0 .. col0 + ncol)
+  float rsc[C::NB];
+  int last;
+};
+
+// In-launch hand-off of a chained launch (dec_attn_o_kernel / dec_mlp_kernel below): the block waits
+// until *wait_ctr >= wait_target before it loads anything an earlier role of the same launch produced
+// (its weight ring is issued before the wait), and a tile whose outputs are final adds 1 to *sig_ctr.
+// Producer: every wave's stores drained (vmcnt(0)), workgroup barrier, one lane's agent-scope release
+// fence (the L2 written back) + vmcnt(0), then the counter add; consumer: one lane polls the counter
+// (relaxed agent-scope loads, s_sleep), agent-scope acquire fence, workgroup barrier, then plain loads
+// (MI355X_MICROARCH.md hand-off rules).  A wait past its spin limit raises *err and proceeds.
+// Progress: a block only waits on roles of blocks with LOWER block indices, which the dispatcher has
+// already placed (in-order dispatch per XCD), so the chain cannot deadlock on residency.
+struct XsChain {
+  const unsigned* wait_ctr;
+  unsigned wait_target;
+  unsigned* sig_ctr;
+  int* err;
+};
+
+#ifndef CHAIN_LAB
+#define CHAIN_LAB 0  // lab (tools/variant.sh -DCHAIN_LAB=bits, results invalid): 1 no acquire fence, 2 no release fence
+#endif
+__device__ __forceinline__ void chain_wait(const XsChain* ch, int tid) {
+  if (!ch || !ch->wait_ctr) return;
+  if (tid == 0) {
+    unsigned spins = 0;
+    while (__hip_atomic_load(ch->wait_ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < ch->wait_target) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1u << 24)) {
+        if (ch->err) __hip_atomic_store(ch->err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    if constexpr ((CHAIN_LAB & 1) == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ void chain_signal(unsigned* ctr, int tid) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    if constexpr ((CHAIN_LAB & 2) == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the compiler may drop the fence's own wait)
+    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+template <bool Q4, int MT, int RTW, int PD, bool NT, int XW>
+__device__ __forceinline__ void xs_body(const GemvParams& p, const int tile, const int kslice, XsLds<Q4, MT, RTW, XW>& L,
+                                        const XsChain* ch) {
   XS_STAMP(0);
-  constexpr int NB = 32 * MT, NBR = 32 * RTW, NTH = 64 * XW;
+  using C = XsCfg<Q4, MT, RTW, XW>;
+  constexpr int NB = C::NB, NBR = C::NBR, NTH = C::NTH;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // XCD-aware (tile, slice) placement for the int4 64-row launches with >= 8 K slices (the decoder's QKV
-  // and down at configs[4]'s B = 64): blocks are dealt round-robin over the 8 XCDs (linear id % 8 share
-  // one L2; MI355X_MICROARCH.md, placement is speed only, never correctness), and with tile-major ids
-  // every XCD read every slice of the 64-row fp32 operand -- its 2 MB (down) crossed into all 8 L2s,
-  // 3.7x the launch's algorithmic bytes (round-4 PMC pass).  Here the blocks of XCD x take slices
-  // [x S/8, (x + 1) S/8), so each operand slice reaches one L2.  Same (tile, slice) work items, same
-  // combine order: outputs unchanged.  (At 32 bf16 rows the operand is half the size and the tile-major
-  // order, which keeps a tile's slices and its combine inside one XCD, measured faster: r04_ab_xcd_map.)
-#ifndef XS_XCD_Q4
-#define XS_XCD_Q4 1  // lab: 0 keeps the tile-major placement (A/B)
-#endif
-  int tile = blockIdx.x, slice = blockIdx.y;
-  if constexpr (Q4 && MT == 2 && XS_XCD_Q4 != 0) {
-    const int T = gridDim.x, S = gridDim.y, L = blockIdx.x + T * blockIdx.y;
-    if (S % 8 == 0) {
-      slice = (L & 7) * (S / 8) + (L >> 3) / T;
-      tile = (L >> 3) % T;
-    }
-  }
   const int n0 = tile * NBR;
   const int nks = p.K / XK, nt32 = (p.N + 31) / 32;
-  const int ks = p.ksplit, nst = nks / ks, wst = nst / XW, ws0 = slice * nst + wave * wst;
+  const int ks = p.ksplit, nst = nks / ks, wst = nst / XW, ws0 = kslice * nst + wave * wst;
   const __amdgpu_buffer_rsrc_t wrs = rsrc(p.Wt, 0x7fffffff), ars = rsrc(p.xs_in, 0x7fffffff), zrs = rsrc(p.Wt, 0);
   int wv[RTW], sv[RTW];
 #pragma unroll
@@ -134,15 +203,17 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
     wv[i] = Q4 ? T * nks * 1024 + 16 * lane : (T * nks * 4 * 64 + lane) * 16;
     sv[i] = nt32 * nks * 1024 + (T * nks * 32 + (lane & 31)) * 4;  // int4: the lane's scale|bias words
   }
-  __shared__ __attribute__((aligned(16))) float xg[Q4 ? XW : 1][Q4 ? Q4_XG / XW : 1][NB];
-  if constexpr (Q4) {  // X_g of this block's stages: the two half-group sums, in order
-    for (int e = tid; e < XW * wst * NB; e += NTH) {
-      const int w = e / (wst * NB), j = (e / NB) % wst, m = e % NB;
-      const int st = slice * nst + w * wst + j;
-      xg[w][j][m] = p.hs_in[(size_t)(2 * st) * xs::HS_ROWS + m] + p.hs_in[(size_t)(2 * st + 1) * xs::HS_ROWS + m];
-    }
-    __syncthreads();
-  }
+  auto& xg = L.xg;
+  auto& sss = L.sss;
+  auto& res = L.res;
+  auto& nws = L.nws;
+  auto& red = L.red;
+  auto& ct = L.ct;
+  auto& hb = L.hb;
+  auto& rsc = L.rsc;
+  auto& pss = L.pss;
+  auto& phs = L.phs;
+  auto& last = L.last;
   struct St {
     u32x4_t w[RTW][Q4 ? 1 : 4];
     uint32_t sb[RTW];
@@ -158,15 +229,15 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
     }
   };
   // stage j of this wave (j >= wst: zero-sized descriptors, no traffic) -- straight-line loads
-  auto load = [&](int j, St& g) {
-    const bool live = j < wst;
-    const int st = ws0 + (live ? j : 0);
 #ifndef XS_LAB
 #define XS_LAB 0  // lab ablations (tools/variant.sh -DXS_LAB=bits, results invalid): 1 no MFMA, 2 no activation
                   // traffic, 4 no weight traffic, 8 no split-K exchange / epilogue, 16 stop after the waves'
                   // reduction
 #endif
-    const __amdgpu_buffer_rsrc_t wr = (live && !(XS_LAB & 4)) ? wrs : zrs, ar = (live && !(XS_LAB & 2)) ? ars : zrs;
+  auto load_w = [&](int j, St& g) {
+    const bool live = j < wst;
+    const int st = ws0 + (live ? j : 0);
+    const __amdgpu_buffer_rsrc_t wr = (live && !(XS_LAB & 4)) ? wrs : zrs;
 #pragma unroll
     for (int i = 0; i < RTW; ++i) {
       if constexpr (Q4) {
@@ -178,6 +249,11 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
           g.w[i][s] = __builtin_bit_cast(u32x4_t, __builtin_amdgcn_raw_buffer_load_b128(wr, wv[i], (st * 4 + s) * 1024, NT ? 2 : 0));
       }
     }
+  };
+  auto load_a = [&](int j, St& g) {
+    const bool live = j < wst;
+    const int st = ws0 + (live ? j : 0);
+    const __amdgpu_buffer_rsrc_t ar = (live && !(XS_LAB & 2)) ? ars : zrs;
 #pragma unroll
     for (int t = 0; t < MT; ++t) {
       if constexpr (XS_F32 != 0) {
@@ -195,20 +271,37 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
       }
     }
   };
+  auto load = [&](int j, St& g) {
+    load_w(j, g);
+    load_a(j, g);
+  };
   f32x16_t acc[MT][RTW];
 #pragma unroll
   for (int t = 0; t < MT; ++t)
 #pragma unroll
     for (int i = 0; i < RTW; ++i) acc[t][i] = f32x16_t{};
-  // Epilogue operands prefetched into LDS by LDS-DMA before the first weight stage (no registers held
-  // across the K loop, no dependent global round trips after it): the RMSNorm sums-of-squares partials,
-  // the residual rows of an EPI_ADD tile, the producer's norm-weight columns.
-  __shared__ float sss[SS_MAX + 2 * 64 * XW];  // [t][NB] partial sums of squares
-  __shared__ float res[NB * NBR + 64 * XW];    // [NB][NBR] residual rows (EPI_ADD)
-  __shared__ float nws[64];                    // xs_nw[col0 .. col0 + ncol)
   const bool norm = p.nw != nullptr;
   const bool silu = p.epi == EPI_SILU_MUL;
   const int mrows = min(NB, p.M);
+  St g[PD];
+  const bool chained = ch && ch->wait_ctr;
+  if (chained) {  // the weight ring first (independent of the earlier roles), then the hand-off wait
+#pragma unroll
+    for (int d = 0; d < PD; ++d) load_w(d, g[d]);
+    asm volatile("" ::: "memory");
+    chain_wait(ch, tid);
+  }
+  if constexpr (Q4) {  // X_g of this block's stages: the two half-group sums, in order
+    for (int e = tid; e < XW * wst * NB; e += NTH) {
+      const int w = e / (wst * NB), j = (e / NB) % wst, m = e % NB;
+      const int st = kslice * nst + w * wst + j;
+      xg[w][j][m] = p.hs_in[(size_t)(2 * st) * xs::HS_ROWS + m] + p.hs_in[(size_t)(2 * st + 1) * xs::HS_ROWS + m];
+    }
+    __syncthreads();
+  }
+  // Epilogue operands prefetched into LDS by LDS-DMA before the first weight stage (no registers held
+  // across the K loop, no dependent global round trips after it): the RMSNorm sums-of-squares partials,
+  // the residual rows of an EPI_ADD tile, the producer's norm-weight columns.
   {
     if (norm) {
       const int tot = p.ss_n * NB;
@@ -229,10 +322,27 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
       __builtin_amdgcn_global_load_lds(p.xs_nw + min(col0 + min(lane, ncol - 1), colN - 1), &nws[0], 4, 0, 0);
     }
   }
-  St g[PD];
+  if (chained) {
 #pragma unroll
-  for (int d = 0; d < PD; ++d) load(d, g[d]);
+    for (int d = 0; d < PD; ++d) load_a(d, g[d]);
+  } else {
+#pragma unroll
+    for (int d = 0; d < PD; ++d) load(d, g[d]);
+  }
   asm volatile("" ::: "memory");  // the ring's loads stay where they are issued (no sinking to their use)
+  // EPI_QKV: the RoPE cos / sin of this tile's columns at every row's position, by LDS-DMA behind the
+  // ring (the epilogue then reads LDS instead of making a dependent global round trip after the K loop).
+  // A tile never straddles a head (NBR <= head_dim, heads aligned), so its pairs are one contiguous run.
+  const int qn = p.Hq * p.hd, kn = p.Hkv * p.hd;
+  const bool rope_lds = p.epi == EPI_QKV && n0 < qn + kn;
+  float* const ropes = res;  // (EPI_QKV has no residual rows)
+  if (rope_lds) {
+    const int d0 = (n0 < qn ? n0 : n0 - qn) % p.hd, tot = mrows * NBR;
+    for (int i0 = wave * 64; i0 < tot; i0 += NTH) {
+      const int i = min(i0 + lane, tot - 1), m = i / NBR, j = i % NBR;
+      __builtin_amdgcn_global_load_lds(p.rope + ((size_t)p.rm.pos(m) * (p.hd >> 1) + (d0 >> 1)) * 2 + j, &ropes[i0], 4, 0, 0);
+    }
+  }
   XS_STAMP(1);
   const int hrow = 4 * (lane >> 5);  // int4 fold: lane (r, h) register jj holds batch row (jj & 3) + 8 (jj >> 2) + 4 h
   for (int j0 = 0; j0 < wst; j0 += PD) {
@@ -317,21 +427,9 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
   }
   // the waves' partial tiles -> ct[batch row][weight row], added in wave order.  Accumulator register
   // j of lane (r, h): batch row (j & 3) + 8 (j >> 2) + 4 h of tile t, weight row r of tile i.
-  // reduction slots: one per wave where the slab fits 64 KB (then every wave stores once and the
-  // ct pass adds (w, w + 4) pairs in the pre-add's order -- one barrier and one LDS round trip
-  // fewer, same sums); else 8-wave blocks pre-add waves w + 4 into w through 4 slots
-  // RED_HALF (8 waves, two row tiles, 128 KB of partials): the same single pass per row tile in turn
-  // -- every wave stores its row tile t partials into its own slot, the ct pass builds rows 32 t ..
-  // 32 t + 31 -- instead of the 4-slot pre-add (whose phases leave half the waves idle)
-  constexpr bool RED_ALL = XW > 4 && MT * RTW * 16 * 64 * 4 * XW <= 65536;
-  constexpr bool RED_HALF = !RED_ALL && XW > 4 && MT == 2 && RTW * 16 * 64 * 4 * XW <= 65536;
-  constexpr int RW = (RED_ALL || RED_HALF) ? XW : (XW > 4 ? 4 : XW);
-  __shared__ float red[RW][(RED_HALF ? 1 : MT) * RTW * 16][64];
-  __shared__ float ct[NB][NBR + 1];
-  __shared__ float hb[NB][NBR / 2 + 1];
-  __shared__ float rsc[NB];
-  __shared__ float pss[NB][NBR / 8 + 1], phs[NB][NBR / 8 + 1];  // producer: 8-column partial sums
-  __shared__ int last;
+  // (reduction slots: XsCfg)
+  constexpr bool RED_ALL = C::RED_ALL, RED_HALF = C::RED_HALF;
+  constexpr int RW = C::RW;
   XS_STAMP(2);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the LDS-DMA prefetch too; the barrier below publishes it)
   if constexpr ((XS_LAB & 8) != 0) {  // lab: the K loop alone (one store keeps it live)
@@ -421,7 +519,7 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
     const int slab_f = NB * NBR;
     float* slab = p.kpart + (size_t)tile * ks * slab_f;
     const __amdgpu_buffer_rsrc_t rs = rsrc(slab, ks * slab_f * 4);
-    const int mine = slice * slab_f * 4;
+    const int mine = kslice * slab_f * 4;
     for (int q = tid; q < mrows * (NBR / 4); q += NTH) {
       const int ml = q / (NBR / 4), j = (q % (NBR / 4)) * 4;
       const f32x4_t v = {ct[ml][j], ct[ml][j + 1], ct[ml][j + 2], ct[ml][j + 3]};
@@ -475,7 +573,23 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
       if (p.out) p.out[(size_t)ml * p.os + (n >> 1)] = hv;
       hb[ml][rp >> 1] = hv;
     } else {
-      gemv_epilogue_pair(p, ml, n, va, vb);
+      if (p.epi == EPI_QKV) {  // gemv_epilogue_pair's EPI_QKV with cos / sin from LDS (attention.py:157-177)
+        const int bb = p.rm.b(ml), pos = p.rm.pos(ml);
+        const int nn = n < qn ? n : (n < qn + kn ? n - qn : n - qn - kn), d = nn % p.hd;
+        if (rope_lds) {
+          const float cs = ropes[ml * NBR + rp], sn = ropes[ml * NBR + rp + 1];
+          const float y0 = va * cs - vb * sn, y1 = vb * cs + va * sn;
+          va = y0;
+          vb = y1;
+        }
+        float* o;
+        if (p.qkv_tab) o = p.qkv_tab + (size_t)ml * (qn + 2 * kn) + n;
+        else if (n < qn) o = p.out + (size_t)ml * p.os + n;
+        else o = (n < qn + kn ? p.kc : p.vc) + (((size_t)bb * p.Hkv + nn / p.hd) * p.S_cap + pos) * p.hd + d;
+        *reinterpret_cast<float2*>(o) = make_float2(va, vb);
+      } else {
+        gemv_epilogue_pair(p, ml, n, va, vb);
+      }
     }
     ct[ml][rp] = va;
     ct[ml][rp + 1] = vb;
@@ -526,11 +640,94 @@ __global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
     }
     p.part[(size_t)tid * p.part_stride + tile] = best;
   }
+  if (ch && ch->sig_ctr) chain_signal(ch->sig_ctr, tid);  // this tile's outputs are final
   if constexpr (XS_STAMPS != 0) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     XS_STAMP(7);
   }
+}
+
+template <bool Q4, int MT, int RTW, int PD, bool NT, int XW>
+__global__ __launch_bounds__(64 * XW) void gemm_xs_kernel(GemvParams p) {
+  __shared__ XsLds<Q4, MT, RTW, XW> L;
+  xs_body<Q4, MT, RTW, PD, NT, XW>(p, blockIdx.x, blockIdx.y, L, nullptr);
+}
+
+// ---------------------------------------------------------------------------- chained launches
+// Two dependent steps of a batched decoder layer in ONE launch (generation.py:72-90 at batch B): the
+// later step's blocks issue their weight ring, wait on a counter the earlier step's blocks publish
+// (XsChain), and only then load the earlier step's outputs.  What a launch boundary costs is the
+// drain of the first kernel, the dispatch of the second and its first weight round trip (the stamps:
+// 1.3-4 us before a block's ring is even issued); here the second step's weights are in flight while
+// the first finishes.  ctl.ctr[0 .. CHAIN_NCTR) are the launch's counters and ctl.ctr[CHAIN_NCTR] its
+// exit ticket: the last block out resets them all (zero again for the next launch on the stream).
+constexpr int CHAIN_NCTR = 16;
+
+__device__ __forceinline__ void chain_exit(const ChainCtl& c, int tid) {
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned nb = gridDim.x * gridDim.y;
+    const unsigned old = __hip_atomic_fetch_add(c.ctr + CHAIN_NCTR, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == nb - 1) {
+      for (int i = 0; i <= CHAIN_NCTR; ++i) __hip_atomic_store(c.ctr + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// Attention + o_proj: blocks 0 .. M-1 run the short attention of row m (wave h = q head h: Hq = 8,
+// head_dim 128), publish their rows (split operand of the o_proj) and add to ctr[0]; blocks M .. run
+// the o_proj tiles (32 weight rows x 8 waves, K slices as xs_shape), each waiting for ctr[0] == M.
+template <bool Q4, int MT, int PD>
+__global__ __launch_bounds__(512) void dec_attn_o_kernel(AttnParams a, GemvParams p, ChainCtl c) {
+  __shared__ union {
+    XsLds<Q4, MT, 1, 8> g;
+    float qsh[8][128];
+  } L;
+  const int tid = threadIdx.x;
+  const int natt = a.M;
+  if ((int)blockIdx.x < natt) {
+    attn_short_row<128, 32>(a, blockIdx.x, tid >> 6, tid & 63, L.qsh[tid >> 6]);
+    chain_signal(c.ctr + 0, tid);
+  } else {
+    const int b = blockIdx.x - natt;
+    const XsChain ch{c.ctr + 0, (unsigned)natt, nullptr, c.err};
+    xs_body<Q4, MT, 1, PD, false, 8>(p, b / p.ksplit, b % p.ksplit, L.g, &ch);
+  }
+  chain_exit(c, tid);
+}
+
+// Gate/up + SiLU*up -> down + residual: blocks 0 .. TG-1 run gate/up tile b (64 interleaved rows ->
+// h columns 32 b .. 32 b + 31) and add to ctr[b / G], G = TG / ks the gate/up tiles feeding one
+// down K slice; down item (tile c, slice s) waits for ctr[s] == G.  It runs on block (s + 1) G + c
+// (after that block's own gate/up tile, so only blocks after every producer wait: TD <= G), or, when
+// TD > G, on extra blocks TG + s TD + c.  The down's split-K exchange is gemm_xs's (ticket, last slice
+// combines in slice order), so every sum is the unchained launch's.
+template <bool Q4, int MT, int PD>
+__global__ __launch_bounds__(512) void dec_mlp_kernel(GemvParams pg, GemvParams pd, ChainCtl c) {
+  __shared__ union {
+    XsLds<Q4, MT, 2, 8> g;
+    XsLds<Q4, MT, 1, 8> d;
+  } L;
+  const int tid = threadIdx.x, b = blockIdx.x;
+  const int TG = (pg.N + 63) / 64, TD = (pd.N + 31) / 32, ks = pd.ksplit, G = TG / ks;
+  if (b < TG) {
+    const XsChain ch{nullptr, 0u, c.ctr + b / G, c.err};
+    xs_body<Q4, MT, 2, PD, false, 8>(pg, b, 0, L.g, &ch);
+    __syncthreads();  // (LDS reused by the down role)
+  }
+  int tile = -1, sl = 0;
+  if (TD <= G) {
+    const int r = b - G;  // blocks G .. TG + TD - 1 carry items (s, c): r = s G + c, c < TD
+    if (r >= 0 && r % G < TD) { sl = r / G; tile = r % G; }
+  } else if (b >= TG) {
+    sl = (b - TG) / TD; tile = (b - TG) % TD;
+  }
+  if (tile >= 0) {
+    const XsChain ch{c.ctr + sl, (unsigned)G, nullptr, c.err};
+    xs_body<Q4, MT, 1, PD, false, 8>(pd, tile, sl, L.d, &ch);
+  }
+  chain_exit(c, tid);
 }
 
 // Launch shape: RTW 2 (64-row tiles) for the wide and the long-K projections and for the heads (the
@@ -726,24 +923,73 @@ void launch_gemm_xs(const GemvParams& p0, int epi, hipStream_t st, bool nt_w, in
                                  else GX_K(Q_, MT_, RTW_, 1); } while (0)
 #define GX_M(Q_) do { if (p.M > 32) { if (rtw == 2) GX_P(Q_, 2, 2); else GX_P(Q_, 2, 1); } \
                       else { if (rtw == 2) GX_P(Q_, 1, 2); else GX_P(Q_, 1, 1); } } while (0)
-  const int role = p.epi == EPI_QKV ? 1 : (p.epi == EPI_ADD ? (p.K > p.N ? 3 : 2) : 0);
-#ifndef XS_ROLES
-#define XS_ROLES 1  // lab: 0 launches the untagged instantiations (A/B)
-#endif
-  if (XS_ROLES && role && !nt && xw == 8 && rtw == 1 && ((wdt == WDT_Q4 && p.M > 32 && pd == 1) || (wdt == WDT_BF16 && p.M <= 32 && pd == 2))) {
-#define GX_R(Q_, MT_, PD_) do { if (role == 1) hipLaunchKernelGGL((gemm_xs_kernel<Q_, MT_, 1, PD_, false, 8, 1>), grid, dim3(512), 0, st, p); \
-                                else if (role == 2) hipLaunchKernelGGL((gemm_xs_kernel<Q_, MT_, 1, PD_, false, 8, 2>), grid, dim3(512), 0, st, p); \
-                                else hipLaunchKernelGGL((gemm_xs_kernel<Q_, MT_, 1, PD_, false, 8, 3>), grid, dim3(512), 0, st, p); } while (0)
-    if (wdt == WDT_Q4) GX_R(true, 2, 1);
-    else GX_R(false, 1, 2);
-#undef GX_R
-  } else if (wdt == WDT_Q4) {
-    GX_M(true);
-  } else {
-    GX_M(false);
-  }
+  if (wdt == WDT_Q4) GX_M(true);
+  else GX_M(false);
 #undef GX_M
 #undef GX_P
 #undef GX_K
 #undef GX_W
+}
+
+// ---- chained launches (host)
+// The o_proj / gate-up / down geometry a chained launch takes must be what launch_gemm_xs would pick
+// (same tiles, slices, ring, 8 waves): then every output is bit-identical to the separate launches.
+static bool xs_params_for(GemvParams& p, int epi, int wdt, int want_rtw, int& pd) {
+  p.epi = epi;
+  p.Wt = nullptr;
+  if (p.ws) {
+    const auto ti = p.ws->tiled.find(p.W);
+    if (ti != p.ws->tiled.end()) p.Wt = ti->second;
+  }
+  if (!p.Wt || !p.xs_in || p.M > GEMM_XS_MAX_M || p.scale || (wdt == WDT_Q4 && !p.hs_in) || !gemm_xs_eligible(p.N, p.K, p.M, wdt))
+    return false;
+  const bool head = epi == EPI_ARGMAX || epi == EPI_SILU_MUL;
+  int rtw, ks, xw;
+  xs_shape(p.N, p.K, p.M, head, rtw, ks, pd, xw);
+  if (wdt == WDT_Q4 && rtw == 2 && pd > 2) pd = 2;
+  if (rtw != want_rtw || xw != 8) return false;
+  p.ksplit = ks;
+  if (ks > 1) {
+    size_t tk = 0;
+    const size_t need = xs_need(p.N, p.K, p.M, head, tk);
+    if (!p.ws || need > p.ws->bytes || tk > p.ws->n) return false;
+    p.kpart = p.ws->kpart;
+    p.kticket = p.ws->tickets;
+  }
+  return true;
+}
+
+bool launch_dec_attn_o(const AttnParams& a, const GemvParams& o0, const ChainCtl& c, int wdt, hipStream_t st) {
+  GemvParams p = o0;
+  int pd = 0;
+  if (!c.ctr || a.Hq != 8 || a.Hkv < 1 || a.S_cap > 32 || a.mode != ATTN_CAUSAL || a.M != p.M || !a.xs_out ||
+      !xs_params_for(p, EPI_ADD, wdt, 1, pd))
+    return false;
+  const int want_pd = p.M > 32 ? 1 : 2;
+  if (pd != want_pd) return false;
+  const int tiles = (p.N + 31) / 32;
+  const dim3 grid(a.M + tiles * p.ksplit);
+#define DAO(Q_, MT_, PD_) hipLaunchKernelGGL((dec_attn_o_kernel<Q_, MT_, PD_>), grid, dim3(512), 0, st, a, p, c)
+  if (wdt == WDT_Q4) { if (p.M > 32) DAO(true, 2, 1); else DAO(true, 1, 2); }
+  else { if (p.M > 32) DAO(false, 2, 1); else DAO(false, 1, 2); }
+#undef DAO
+  return true;
+}
+
+bool launch_dec_mlp(const GemvParams& gu0, const GemvParams& dn0, const ChainCtl& c, int wdt, hipStream_t st) {
+  GemvParams pg = gu0, pdn = dn0;
+  int pd1 = 0, pd2 = 0;
+  if (!c.ctr || !xs_params_for(pg, EPI_SILU_MUL, wdt, 2, pd1) || !xs_params_for(pdn, EPI_ADD, wdt, 1, pd2)) return false;
+  const int want_pd = pg.M > 32 ? 1 : 2;
+  const int TG = (pg.N + 63) / 64, TD = (pdn.N + 31) / 32, ks = pdn.ksplit;
+  if (pg.ksplit != 1 || pd1 != want_pd || pd2 != want_pd || pg.M != pdn.M || ks > CHAIN_NCTR || TG % ks != 0 ||
+      pdn.K != pg.N / 2)
+    return false;
+  const int G = TG / ks;
+  const dim3 grid(TD <= G ? TG + TD : TG + ks * TD);
+#define DML(Q_, MT_, PD_) hipLaunchKernelGGL((dec_mlp_kernel<Q_, MT_, PD_>), grid, dim3(512), 0, st, pg, pdn, c)
+  if (wdt == WDT_Q4) { if (pg.M > 32) DML(true, 2, 1); else DML(true, 1, 2); }
+  else { if (pg.M > 32) DML(false, 2, 1); else DML(false, 1, 2); }
+#undef DML
+  return true;
 }
