@@ -194,8 +194,8 @@ def config4_b32_golden():
 def config3_b32_golden(frames=64):
     """configs[2]: B = 32, temperature 0.8, top-k 50 (the oracle's restatement of the engine's counter-based
     RNG), 32 frames; the Mimi oracle's streaming decode_step of every frame: per (utterance, frame) RMS,
-    mean and B32_PROJ projections on seeded unit vectors, and the whole PCM of utterance 0 and of every
-    utterance that ends (frames before its EOS)."""
+    mean and B32_PROJ projections on seeded unit vectors, and whole chunks: utterance 0's first 8 and
+    each ending utterance's last 4 before its EOS."""
     from csm_mlx.weights import synthetic_mimi_weights
     codes, n, _, _ = _b32_run(frames, 0.8, 50, keep_logits=False)
     print("n_frames", n.tolist(), flush=True)
@@ -218,8 +218,11 @@ def config3_b32_golden(frames=64):
         print("mimi frame", f, flush=True)
     out = dict(codes=codes, n_frames=n, rms=np.stack(rms, 1), mean=np.stack(mean, 1), proj=np.stack(proj, 1),
                proj_vec=vec, pcm_utts=np.array(keep, np.int32))
-    for b in keep:
-        out[f"pcm_{b}"] = np.stack(pcm[b]) if pcm[b] else np.zeros((0, 1920), np.float32)
+    for b in keep:   # (size) utterance 0's first 8 chunks; an ending utterance's last 4 before its EOS
+        st = 0 if b == 0 else max(0, len(pcm[b]) - 4)
+        sl = pcm[b][:8] if b == 0 else pcm[b][st:]
+        out[f"pcm_{b}"] = np.stack(sl) if sl else np.zeros((0, 1920), np.float32)
+        out[f"pcm_start_{b}"] = np.array(st, np.int32)
     return out
 
 

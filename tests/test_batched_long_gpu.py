@@ -7,7 +7,8 @@
 * configs[2] -- B = 32, temperature 0.8, top-k 50, ``stream_generate_batch`` over 64 frames: codes
   (the oracle's restatement of the engine's counter-based RNG) and, per (utterance, frame) before its
   EOS, the streamed chunk's RMS, mean and projections on four seeded unit vectors against the Mimi
-  oracle's ``decode_step``, plus whole chunks of utterance 0 and of every utterance that ends.
+  oracle's ``decode_step``, plus whole chunks (utterance 0's first 8, each ending utterance's last 4
+  before its EOS frame).
 
 Both run on the EOS-capable rig of the seed-0 weights (tests/helpers.py eos_rig), so utterances end at
 different frames (per-utterance EOS at B > 1, generation.py:139-161).  Bars: codes and frame counts
@@ -121,8 +122,8 @@ def test_config3_stream_b32_sampled_64_frames():
                     np.abs(y[b] @ vec.T - z["proj"][b, f]).max() > 1e-4 * np.sqrt(1920):
                 bad.append(f"utterance {b} frame {f}")
     for b in z["pcm_utts"]:
-        ref = z[f"pcm_{b}"]
-        got = np.stack([chunks[f][b] for f in range(len(ref))]) if len(ref) else ref
+        ref, st = z[f"pcm_{b}"], int(z[f"pcm_start_{b}"])
+        got = np.stack([chunks[st + f][b] for f in range(len(ref))]) if len(ref) else ref
         err = float(np.sqrt(np.mean((got.astype(np.float64) - ref) ** 2))) if len(ref) else 0.0
         if err > 1e-4:
             bad.append(f"utterance {b}: chunk RMS error {err:.3e}")
