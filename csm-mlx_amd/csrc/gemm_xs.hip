@@ -564,8 +564,10 @@ void xs_shape(int N, int K, int M, bool head, int& rtw, int& ks, int& pd, int& x
   // CSM_XS_WAVES=2 / 4 / 8 forces one count everywhere.
   static const int waves = [] { const char* v = getenv("CSM_XS_WAVES"); const int w = v ? atoi(v) : 0; return w == 2 || w == 4 || w == 8 ? w : 0; }();
   // the heads (arg-max epilogue, 64-row tiles, ~33 of them): fewer waves per block leave room for
-  // more K slices, spreading the head's bytes over more CUs (CSM_XS_HEAD_WAVES lab knob)
-  static const int head_waves = [] { const char* v = getenv("CSM_XS_HEAD_WAVES"); const int w = v ? atoi(v) : 0; return w == 2 || w == 4 || w == 8 ? w : 8; }();
+  // more K slices, spreading the head's bytes over more CUs (CSM_XS_HEAD_WAVES lab knob).  4 waves (4 K
+  // slices, 132 blocks at 32 rows) against 8 (2 slices, 66 blocks): config 4 4383-4409 -> 4496 frames/s,
+  // config 5 5408 -> 5413; 2 waves 4352-4435 (profiles/r05_ab_head_waves.txt)
+  static const int head_waves = [] { const char* v = getenv("CSM_XS_HEAD_WAVES"); const int w = v ? atoi(v) : 0; return w == 2 || w == 4 || w == 8 ? w : 4; }();
   // (the decoder's QKV / o at <= 32 rows: 8 waves now that they take one K slice; 4 with split-K)
   static const int small_waves = [] { const char* v = getenv("CSM_XS_SMALL_WAVES"); const int w = v ? atoi(v) : 0; return w == 2 || w == 4 || w == 8 ? w : 8; }();
   const int want = waves ? waves : (head && N % 64 != 0 ? head_waves : (dec_small ? small_waves : 8));
