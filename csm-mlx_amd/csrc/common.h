@@ -126,6 +126,10 @@ struct RowMap {
   // ragged batched prefill: per-row utterance and position tables (device), overriding the above
   const int* row_b = nullptr;
   const int* row_pos = nullptr;
+  // prompt-prefill attention (attn_prefill_kernel): runs of <= 64 rows of one utterance at consecutive
+  // positions, {first row, rows} (device; null: attn_block per row)
+  const int2* tiles = nullptr;
+  int ntiles = 0;
   __device__ __forceinline__ int b(int m) const { return row_b ? row_b[m] : b_off + m / T; }
   __device__ __forceinline__ int pos(int m) const {
     if (row_pos) return row_pos[m];

@@ -104,6 +104,8 @@ struct csm_engine {
   int32_t* tok = nullptr;
   uint8_t* msk = nullptr;
   int *row_b = nullptr, *row_pos = nullptr;  // [M_cap] batched-prefill row tables
+  int2* ptiles = nullptr;  // [M_cap / 64 + B_max + 2] prompt-prefill attention tiles (RowMap::tiles)
+  bool attn_tiles_on = true;  // csm_set_option "attn_prefill": 0 = attn_block per row (A/B, tests)
   // per-batch state
   int *codes = nullptr, *hist = nullptr, *pos = nullptr, *n_frames = nullptr, *frame_ctr = nullptr;
   unsigned long long* part = nullptr;  // [K][B_max][part_stride] arg-max partials of the heads
@@ -1011,6 +1013,7 @@ int csm_engine_create(const csm_dims* dims, int device, int weight_dtype, int ma
     e->Dd = d.hidden;
     const int S = dims->max_seq_len;
     e->M_cap = std::max(S, 2 * max_batch);
+    if (const char* v = getenv("CSM_ATTN_PREFILL")) e->attn_tiles_on = atoi(v) != 0;  // lab: 0 = per-row prompt attention (A/B)
     HIPCHK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
     alloc_stack(e.get(), e->bb, b, S, "backbone");
     alloc_stack(e.get(), e->dec, d, e->K, "decoder");
@@ -1036,6 +1039,7 @@ int csm_engine_create(const csm_dims* dims, int device, int weight_dtype, int ma
     e->msk = (uint8_t*)e->alloc(M * (K + 1));
     e->row_b = (int*)e->alloc(M * 4);
     e->row_pos = (int*)e->alloc(M * 4);
+    e->ptiles = (int2*)e->alloc((M / 64 + (size_t)max_batch + 2) * sizeof(int2));
     e->frame_ctr = (int*)e->alloc(16);
     e->df_gbuf = e->alloc(dec_frame_gbuf_bytes());
     e->df_epoch = (unsigned*)e->alloc(16);
@@ -1361,6 +1365,14 @@ int csm_prefill(csm_engine* e, int b, int T, const int32_t* tokens, const uint8_
     ep.K = K; ep.D = e->D; ep.out = e->x;
     embed(e, ep, T, e->st);
     RowMap rm{T, b, nullptr, start};
+    if (e->attn_tiles_on) {  // attention tiles: <= 64 consecutive rows
+      std::vector<int2> tl;
+      for (int t0 = 0; t0 < T; t0 += 64) tl.push_back(make_int2(t0, std::min(64, T - t0)));
+      HIPCHK(hipMemcpyAsync(e->ptiles, tl.data(), tl.size() * sizeof(int2), hipMemcpyHostToDevice, e->st));
+      HIPCHK(hipStreamSynchronize(e->st));  // (pageable source)
+      rm.tiles = e->ptiles;
+      rm.ntiles = (int)tl.size();
+    }
     run_stack(e, e->bb, e->x, T, e->q, e->att, e->mlp, rm, e->st);
     launch_rmsnorm_rows(e->x + (size_t)(T - 1) * e->D, e->D, e->bb.norm, e->bb.d.eps, e->D,
                         e->h_last + (size_t)b * e->D, e->D, 1, e->st);
@@ -1396,6 +1408,7 @@ int csm_prefill_batch(csm_engine* e, int n, const int32_t* utts, const int32_t* 
     // utterances in groups of at most M_cap rows: one pass of every projection per group (the
     // weights stream once for all of the group's rows), rows mapped to (utterance, position)
     std::vector<int> rb, rp;
+    std::vector<int2> tl;
     for (int i0 = 0; i0 < n;) {
       int i1 = i0;
       while (i1 < n && row0[i1 + 1] - row0[i0] <= cap) ++i1;
@@ -1412,6 +1425,10 @@ int csm_prefill_batch(csm_engine* e, int n, const int32_t* utts, const int32_t* 
       HIPCHK(hipMemcpyAsync(e->msk, masks + row0[i0] * (K + 1), (size_t)R * (K + 1), hipMemcpyHostToDevice, e->st));
       HIPCHK(hipMemcpyAsync(e->row_b, rb.data(), (size_t)R * 4, hipMemcpyHostToDevice, e->st));
       HIPCHK(hipMemcpyAsync(e->row_pos, rp.data(), (size_t)R * 4, hipMemcpyHostToDevice, e->st));
+      tl.clear();  // attention tiles: <= 64 consecutive rows of one utterance
+      for (int i = i0; i < i1; ++i)
+        for (int t0 = 0; t0 < Ts[i]; t0 += 64) tl.push_back(make_int2((int)(row0[i] - row0[i0]) + t0, std::min(64, Ts[i] - t0)));
+      HIPCHK(hipMemcpyAsync(e->ptiles, tl.data(), tl.size() * sizeof(int2), hipMemcpyHostToDevice, e->st));
       EmbedParams ep{};
       ep.tok = e->tok; ep.mask = e->msk; ep.text_emb = e->text_emb; ep.audio_emb = e->audio_emb; ep.V = e->V;
       ep.K = K; ep.D = e->D; ep.out = e->x;
@@ -1419,6 +1436,10 @@ int csm_prefill_batch(csm_engine* e, int n, const int32_t* utts, const int32_t* 
       RowMap rm{1, 0, nullptr, 0};
       rm.row_b = e->row_b;
       rm.row_pos = e->row_pos;
+      if (e->attn_tiles_on) {
+        rm.tiles = e->ptiles;
+        rm.ntiles = (int)tl.size();
+      }
       run_stack(e, e->bb, e->x, R, e->q, e->att, e->mlp, rm, e->st);
       for (int i = i0; i < i1; ++i) {  // h_last = norm(last row) of each utterance
         const size_t last = row0[i + 1] - 1 - row0[i0];
@@ -1974,6 +1995,10 @@ int csm_set_option(csm_engine* e, const char* key, int value) {
     else if (k == "qkv0_tab_batched") {
       if (!e) throw CsmError(CSM_ERR_ARG, "qkv0_tab_batched needs an engine");
       e->no_tab_batched = value == 0;
+    }
+    else if (k == "attn_prefill") {
+      if (!e) throw CsmError(CSM_ERR_ARG, "attn_prefill needs an engine");
+      e->attn_tiles_on = value != 0;
     }
     else if (k == "prefill_rows") {
       if (!e || value < 0) throw CsmError(CSM_ERR_ARG, "prefill_rows needs an engine and a row count >= 0");

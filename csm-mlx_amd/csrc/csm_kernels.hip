@@ -811,6 +811,157 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnParams p) {
   attn_block<HD>(p, blockIdx.x / p.Hkv, blockIdx.x % p.Hkv, L);
 }
 
+// Prompt-prefill causal attention on the fp32 matrix cores (v_mfma_f32_32x32x2f32).  A prompt's rows
+// are one utterance at consecutive positions, so one 256-thread block takes a tile of <= 64 of them
+// and one kv head; wave w = q head kvh*G + w over the tile's two 32-row MFMA tiles.  Keys 0 .. the
+// tile's last position stream through LDS in 64-key chunks, the next chunk's loads in flight in
+// registers while this one is scored (as attn_block).  Scores are computed transposed, S^T = K Q^T:
+// accumulator register r of lane (c, hh) is query row c against key (r & 3) + 8 (r >> 2) + 4 hh, so
+// a row's online-softmax max / sum are the lane's own registers plus one swap with lane ^ 32, and the
+// same registers are the B operand of O^T = V^T P^T once the MFMA K steps walk the keys in that order
+// (step s, half hh <-> key (s & 3) + 8 (s >> 2) + 4 hh; the score steps walk dims 32 hh + s).  fp32
+// products and fp32 accumulation as attn_block, summed in another order.  attn_block runs one
+// (row, kv head) per block: config 5's 15,872 prompt rows were 127k blocks and ~26 ms of latency
+// chains (profiles/r04_prof_config5_prefill_codec.txt).
+template <int HD>
+__global__ __launch_bounds__(256) void attn_prefill_kernel(AttnParams p) {
+  static_assert(HD == 64, "one 64-dim head per wave: 32 K steps over dims, two 32-dim output tiles");
+  constexpr int KP = HD + 4, V4 = HD / 4, PER = 64 * V4 / 256;
+  __shared__ __attribute__((aligned(16))) float Ks[64 * KP];
+  __shared__ __attribute__((aligned(16))) float Vs[64 * HD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, c32 = lane & 31, hh = lane >> 5;
+  const int kvh = blockIdx.x % p.Hkv, tile = blockIdx.x / p.Hkv;
+  const int2 tl = p.rm.tiles[tile];
+  const int m0 = tl.x, n = tl.y;
+  const int G = p.Hq / p.Hkv;
+  const bool head_ok = wave < G;
+  const int h = kvh * G + min(wave, G - 1);
+  const int b = p.rm.b(m0), pos0 = p.rm.pos(m0), kmax = pos0 + n - 1;
+  const float* K = p.kc + ((size_t)b * p.Hkv + kvh) * p.S_cap * HD;
+  const float* V = p.vc + ((size_t)b * p.Hkv + kvh) * p.S_cap * HD;
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  typedef float f32x16 __attribute__((ext_vector_type(16)));
+  f32x4 kk[PER], vv[PER];
+  auto fetch = [&](int c_) {
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int t = u * 256 + tid, j = min(c_ + t / V4, kmax), d4 = t % V4;
+      kk[u] = *reinterpret_cast<const f32x4*>(K + (size_t)j * HD + d4 * 4);
+      vv[u] = *reinterpret_cast<const f32x4*>(V + (size_t)j * HD + d4 * 4);
+    }
+  };
+  fetch(0);
+  // this lane's query rows (clamped: rows past the tile repeat its last row, never stored), scaled,
+  // dims 32 hh .. 32 hh + 31 (the score steps' B operand)
+  float qv[2][HD / 2];
+  int rpos[2];
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt) {
+    const int r = min(32 * rt + c32, n - 1);
+    rpos[rt] = pos0 + r;
+    const f32x4* qp = reinterpret_cast<const f32x4*>(p.q + (size_t)(m0 + r) * p.qs + h * HD + 32 * hh);
+#pragma unroll
+    for (int s4 = 0; s4 < HD / 8; ++s4) {
+      const f32x4 v = qp[s4];
+      qv[rt][4 * s4] = v.x * p.scale;
+      qv[rt][4 * s4 + 1] = v.y * p.scale;
+      qv[rt][4 * s4 + 2] = v.z * p.scale;
+      qv[rt][4 * s4 + 3] = v.w * p.scale;
+    }
+  }
+  f32x16 o[2][2];
+  float m_run[2] = {-INFINITY, -INFINITY}, l_run[2] = {0.f, 0.f};
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt)
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt) o[rt][dt] = f32x16{};
+  for (int c = 0; c <= kmax; c += 64) {
+    __syncthreads();  // the previous chunk consumed
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int t = u * 256 + tid, j = t / V4, d4 = t % V4;
+      *reinterpret_cast<f32x4*>(&Ks[j * KP + d4 * 4]) = kk[u];
+      *reinterpret_cast<f32x4*>(&Vs[j * HD + d4 * 4]) = vv[u];
+    }
+    __syncthreads();
+    fetch(min(c + 64, kmax));  // (clamped: unconditional)
+    if (!head_ok) continue;
+    f32x16 sc[2][2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      float ka[HD / 2];
+#pragma unroll
+      for (int s4 = 0; s4 < HD / 8; ++s4) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(&Ks[(32 * kt + c32) * KP + 32 * hh + 4 * s4]);
+        ka[4 * s4] = v.x; ka[4 * s4 + 1] = v.y; ka[4 * s4 + 2] = v.z; ka[4 * s4 + 3] = v.w;
+      }
+#pragma unroll
+      for (int rt = 0; rt < 2; ++rt) sc[rt][kt] = f32x16{};
+#pragma unroll
+      for (int s = 0; s < HD / 2; ++s)
+#pragma unroll
+        for (int rt = 0; rt < 2; ++rt) sc[rt][kt] = __builtin_amdgcn_mfma_f32_32x32x2f32(ka[s], qv[rt][s], sc[rt][kt], 0, 0, 0);
+    }
+    // online softmax per query row (this lane's column), causal mask key > row position
+#pragma unroll
+    for (int rt = 0; rt < 2; ++rt) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = c + 32 * kt + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          if (key > rpos[rt]) sc[rt][kt][r] = -INFINITY;
+          mx = fmaxf(mx, sc[rt][kt][r]);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float new_m = fmaxf(m_run[rt], mx);
+      const float alpha = (m_run[rt] == -INFINITY) ? 0.f : expf(m_run[rt] - new_m);
+      float rs = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float pj = expf(sc[rt][kt][r] - new_m);
+          sc[rt][kt][r] = pj;
+          rs += pj;
+        }
+      rs += __shfl_xor(rs, 32, 64);
+      l_run[rt] = l_run[rt] * alpha + rs;
+      m_run[rt] = new_m;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) o[rt][dt] *= alpha;
+    }
+    // O^T[dim][row] += V[key][dim] P[row][key], K steps in the score registers' key order
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int s = 0; s < 16; ++s) {
+        const int key = 32 * kt + (s & 3) + 8 * (s >> 2) + 4 * hh;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+          const float va = Vs[key * HD + 32 * dt + c32];
+#pragma unroll
+          for (int rt = 0; rt < 2; ++rt) o[rt][dt] = __builtin_amdgcn_mfma_f32_32x32x2f32(va, sc[rt][kt][s], o[rt][dt], 0, 0, 0);
+        }
+      }
+  }
+  if (!head_ok) return;
+#pragma unroll
+  for (int rt = 0; rt < 2; ++rt) {
+    const int r = 32 * rt + c32;
+    if (r >= n) continue;
+    const float inv = 1.f / l_run[rt];
+    float* out = p.out + (size_t)(m0 + r) * p.os + h * HD;
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+      for (int r4 = 0; r4 < 4; ++r4)
+        *reinterpret_cast<f32x4*>(out + 32 * dt + 8 * r4 + 4 * hh) =
+            f32x4{o[rt][dt][4 * r4] * inv, o[rt][dt][4 * r4 + 1] * inv, o[rt][dt][4 * r4 + 2] * inv, o[rt][dt][4 * r4 + 3] * inv};
+  }
+}
+
 // ============================================================================ rmsnorm rows
 // out[m] = rmsnorm(x[row(m)]) ; optionally also scatter to dec_in[2m] (decoder step-1 rows).
 __global__ __launch_bounds__(256) void rmsnorm_rows_kernel(const float* x, int xs, const float* w, float eps, int D,
@@ -1370,6 +1521,12 @@ void launch_attn(const AttnParams& p, int hd, hipStream_t st) {
   }
   if ((g_attn_short || (p.xs_out && p.g_tab)) && hd == 128 && p.mode == ATTN_CAUSAL && p.S_cap <= 32) {  // depth decoder
     hipLaunchKernelGGL((attn_short_kernel<128, 32>), dim3(p.M * p.Hq), dim3(64), 0, st, p);
+    return;
+  }
+  // prompt rows with a tile table (csm_prefill / csm_prefill_batch) of >= 16 rows a tile on average
+  if (p.rm.tiles && p.rm.ntiles > 0 && p.M >= 16 * p.rm.ntiles && hd == 64 && p.mode == ATTN_CAUSAL && !p.g_tab &&
+      !p.xs_out && p.Hq / p.Hkv <= 4) {
+    hipLaunchKernelGGL(attn_prefill_kernel<64>, dim3(p.rm.ntiles * p.Hkv), dim3(256), 0, st, p);
     return;
   }
   const int blocks = p.M * p.Hkv;
