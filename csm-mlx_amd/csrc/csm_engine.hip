@@ -1365,7 +1365,7 @@ int csm_prefill(csm_engine* e, int b, int T, const int32_t* tokens, const uint8_
     ep.K = K; ep.D = e->D; ep.out = e->x;
     embed(e, ep, T, e->st);
     RowMap rm{T, b, nullptr, start};
-    if (e->attn_tiles_on) {  // attention tiles: <= 64 consecutive rows
+    if (e->attn_tiles_on && T >= 16) {  // attention tiles: <= 64 consecutive rows (launch_attn's >= 16-row bar)
       std::vector<int2> tl;
       for (int t0 = 0; t0 < T; t0 += 64) tl.push_back(make_int2(t0, std::min(64, T - t0)));
       HIPCHK(hipMemcpyAsync(e->ptiles, tl.data(), tl.size() * sizeof(int2), hipMemcpyHostToDevice, e->st));

@@ -29,7 +29,7 @@ for step in "$@"; do
       out=gpurun_out/${TAG}_b$n.json
       env "${envs[@]}" timeout -k 10 "$T" python -u bench.py $args > "$out" 2> "${out%.json}.err" \
         || { tail -20 "${out%.json}.err"; echo "STEP $n FAILED: $step"; exit 1; }
-      python3 -c "import json,sys; d=json.loads(open('$out').read().strip().splitlines()[-1]); print('$TAG b$n ${envs[*]}', d['value'], d['ms_per_step'], d.get('roofline', {}).get('frac'), d.get('phases_s_per_step'))" ;;
+      python3 -c "import json,sys; d=json.loads(open('$out').read().strip().splitlines()[-1]); print('$TAG b$n ${envs[*]}', d['value'], d['ms_per_step'], (d.get('roofline') or {}).get('frac'), d.get('phases_s_per_step'))" ;;
     prof)
       name=${rest%%:*}; args=${rest#*:}
       timeout -k 10 "$T" bash tools/prof.sh "$name" $args || { echo "STEP $n FAILED: $step"; exit 1; } ;;
