@@ -147,6 +147,11 @@ extern "C" int csm_gemm_stamps(unsigned long long* out, int n) {
 #define GSTAMP(i) do {} while (0)
 #endif
 
+#ifndef GW_LAB
+#define GW_LAB 0  // lab ablations (tools/variant.sh -DGW_LAB=bits, results invalid): 1 staging without norm / split /
+                  // group sums, 2 no int4 scale / bias fold, 4 no MFMA (operands consumed by one VALU op), 8 no int4
+                  // -> bf16 expansion, 16 no LDS reads of the activation fragments
+#endif
 template <bool Q4, int MT, int NBR, int PD, bool NT, int NW = 4>
 __global__ __launch_bounds__(64 * NW) void gemm_wide_kernel(GemvParams p) {
   constexpr int NB = MT * 32, NTH = 64 * NW;
@@ -241,6 +246,15 @@ __global__ __launch_bounds__(64 * NW) void gemm_wide_kernel(GemvParams p) {
     for (int i = 0; i < NI; ++i) {
       const int c = x_c + RPT * i;
       float v[4] = {g.xr[i].x, g.xr[i].y, g.xr[i].z, g.xr[i].w};
+      if constexpr ((GW_LAB & 1) != 0) {  // the same LDS stores of raw bits: the staging's memory side only
+        const u32x2_t raw = {__float_as_uint(v[0]) ^ __float_as_uint(g.nwr.x), __float_as_uint(v[2])};
+        const int sl = (c & 31) + 33 * st_h;
+        *(reinterpret_cast<u32x2_t*>(&Xs(buf, 0, c >> 5, st_s)[sl]) + st_j) = raw;
+        *(reinterpret_cast<u32x2_t*>(&Xs(buf, 1, c >> 5, st_s)[sl]) + st_j) = raw;
+        *(reinterpret_cast<u32x2_t*>(&Xs(buf, 2, c >> 5, st_s)[sl]) + st_j) = raw;
+        if (live && (tid & 15) == 0) xsum[buf][c] = v[1];
+        continue;
+      }
       if (norm) {
         const float nw4[4] = {g.nwr.x, g.nwr.y, g.nwr.z, g.nwr.w};
 #pragma unroll
@@ -293,7 +307,8 @@ __global__ __launch_bounds__(64 * NW) void gemm_wide_kernel(GemvParams p) {
             uint32_t word = g.w[i][0][s];
             if constexpr (KW == 2) word = kh ? g.w[i][0][NS + s] : g.w[i][0][s];
             if constexpr (KW == 4) word = kh == 0 ? g.w[i][0][0] : (kh == 1 ? g.w[i][0][1] : (kh == 2 ? g.w[i][0][2] : g.w[i][0][3]));
-            b[i] = __builtin_bit_cast(bf16x8_t, xs::q4_word_bf16(word));
+            if constexpr ((GW_LAB & 8) != 0) b[i] = __builtin_bit_cast(bf16x8_t, u32x4_t{word, word ^ 1u, word ^ 2u, word ^ 3u});
+            else b[i] = __builtin_bit_cast(bf16x8_t, xs::q4_word_bf16(word));
           } else {
             b[i] = __builtin_bit_cast(bf16x8_t, g.w[i][s]);
           }
@@ -302,10 +317,12 @@ __global__ __launch_bounds__(64 * NW) void gemm_wide_kernel(GemvParams p) {
         for (int t = 0; t < MT; ++t)
 #pragma unroll
           for (int part = 0; part < 3; ++part) {
-            const bf16x8_t a = __builtin_bit_cast(bf16x8_t, Xs(buf, part, t, step)[slot]);
+            const bf16x8_t a = (GW_LAB & 16) != 0 ? __builtin_bit_cast(bf16x8_t, u32x4_t{(uint32_t)slot, (uint32_t)part, (uint32_t)t, (uint32_t)(step + it)})
+                                                  : __builtin_bit_cast(bf16x8_t, Xs(buf, part, t, step)[slot]);
 #pragma unroll
             for (int i = 0; i < RTW; ++i) {
-              if constexpr (Q4) gq[t][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b[i], gq[t][i], 0, 0, 0);
+              if constexpr ((GW_LAB & 4) != 0) gq[t][i][part] += __builtin_bit_cast(float, __builtin_bit_cast(u32x4_t, a).x ^ __builtin_bit_cast(u32x4_t, b[i]).y);
+              else if constexpr (Q4) gq[t][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b[i], gq[t][i], 0, 0, 0);
               else acc[t][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b[i], acc[t][i], 0, 0, 0);
             }
           }
@@ -324,6 +341,7 @@ __global__ __launch_bounds__(64 * NW) void gemm_wide_kernel(GemvParams p) {
             const float sc = bf16_lo(g.sb[i]), bi = bf16_hi(g.sb[i]);
 #pragma unroll
             for (int j = 0; j < 16; ++j) {
+              if constexpr ((GW_LAB & 2) != 0) { acc[t][i][j] += gq[t][i][j]; continue; }
               acc[t][i][j] = fmaf(sc, gq[t][i][j], acc[t][i][j]);
               acc[t][i][j] = fmaf(bi, xs[j], acc[t][i][j]);
             }
