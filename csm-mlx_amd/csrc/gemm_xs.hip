@@ -23,6 +23,8 @@
 #include <cstdio>
 #include <cstdlib>
 
+#include "../../include/csm_hip.h"
+#include "../../include/csm_hip_prof.h"
 #include "csm_kernels.h"
 #include "xs.h"
 
@@ -644,6 +646,27 @@ extern "C" int csm_xs_shape(int N, int K, int M, int head, int* out) {
   xs_shape(N, K, M, head != 0, rtw, ks, pd, xw);
   out[0] = rtw; out[1] = ks; out[2] = pd; out[3] = xw;
   return gemm_xs_eligible(N, K, M, WDT_BF16) ? 1 : 0;
+}
+
+__global__ void q4_expand_kernel(const uint32_t* w, int n, u32x4_t* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = xs::q4_word_bf16(w[i]);
+}
+
+extern "C" int csm_q4_expand(const uint32_t* words, int n, uint32_t* out) {
+  if (!words || !out || n <= 0) return CSM_ERR_ARG;
+  uint32_t* dw = nullptr;
+  u32x4_t* dout = nullptr;
+  int rc = CSM_ERR_HIP;
+  if (hipMalloc(&dw, (size_t)n * 4) == hipSuccess && hipMalloc(&dout, (size_t)n * 16) == hipSuccess &&
+      hipMemcpy(dw, words, (size_t)n * 4, hipMemcpyHostToDevice) == hipSuccess) {
+    hipLaunchKernelGGL(q4_expand_kernel, dim3((n + 255) / 256), dim3(256), 0, 0, dw, n, dout);
+    if (hipGetLastError() == hipSuccess && hipMemcpy(out, dout, (size_t)n * 16, hipMemcpyDeviceToHost) == hipSuccess)
+      rc = CSM_OK;
+  }
+  if (dw) (void)hipFree(dw);
+  if (dout) (void)hipFree(dout);
+  return rc;
 }
 
 int gemm_xs_tiles(int N, int K, int M, bool head) {

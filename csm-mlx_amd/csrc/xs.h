@@ -130,16 +130,33 @@ __device__ __forceinline__ void store1(void* base, int K, int m, int k, float v)
 // sums hs[k / 32][HS_ROWS] (32 columns, summed in column order), the consumer adds the two halves.
 constexpr int HS_ROWS = 64;
 
-// one uint32 of MLX int4 nibbles (k = 8s .. 8s+7, low nibble first) -> 8 exact bf16 (u32x4 of pairs):
-// bytes of the even / odd nibbles through v_cvt_f32_ubyte*, the floats' high halves paired by v_perm
+// one uint32 of MLX int4 nibbles (k = 8s .. 8s+7, low nibble first) -> 8 exact bf16 (u32x4 of pairs).
+// The even / odd nibbles' bytes are interleaved by v_perm and decoded as fp8 e4m3: a byte q in 0..15 is
+// q x 2^-9 there exactly (exponent field q >> 3 = 0 (subnormal) or 1, mantissa q & 7: (q & 7) / 8 x 2^-6
+// and (1 + (q & 7) / 8) x 2^-6), and v_cvt_scalef32_pk_bf16_fp8 with the power-of-two scale 2^9 returns q
+// itself -- 9 vector ops a word instead of 15 (8 v_cvt_f32_ubyte + 4 v_perm + masks).  Q4_FP8=0: the
+// byte -> float path (lab A/B).
+#ifndef Q4_FP8
+#define Q4_FP8 1
+#endif
 __device__ __forceinline__ u32x4_t q4_word_bf16(uint32_t u) {
   const uint32_t a = u & 0x0F0F0F0Fu, b = (u >> 4) & 0x0F0F0F0Fu;
   u32x4_t o;
+  if constexpr (Q4_FP8 != 0) {
+    typedef __bf16 v2bf16_t __attribute__((ext_vector_type(2)));
+    const uint32_t x0 = __builtin_amdgcn_perm(b, a, 0x05010400u);  // {a0, b0, a1, b1}
+    const uint32_t x1 = __builtin_amdgcn_perm(b, a, 0x07030602u);  // {a2, b2, a3, b3}
+    o[0] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(x0, 512.0f, false));
+    o[1] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(x0, 512.0f, true));
+    o[2] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(x1, 512.0f, false));
+    o[3] = __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(x1, 512.0f, true));
+  } else {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const uint32_t fa = __float_as_uint((float)((a >> (8 * i)) & 0xFFu));
-    const uint32_t fb = __float_as_uint((float)((b >> (8 * i)) & 0xFFu));
-    o[i] = __builtin_amdgcn_perm(fb, fa, 0x07060302u);  // {hi16(fa), hi16(fb)}
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t fa = __float_as_uint((float)((a >> (8 * i)) & 0xFFu));
+      const uint32_t fb = __float_as_uint((float)((b >> (8 * i)) & 0xFFu));
+      o[i] = __builtin_amdgcn_perm(fb, fa, 0x07060302u);  // {hi16(fa), hi16(fb)}
+    }
   }
   return o;
 }

@@ -55,6 +55,11 @@ int csm_set_option(csm_engine* e, const char* key, int value);
  * exactly one wave of one slice), else 0.  Host-only (no device call). */
 int csm_xs_shape(int N, int K, int M, int head, int* out);
 
+/* The matrix-core GEMMs' int4 -> bf16 expansion (xs.h q4_word_bf16) of n uint32 words of MLX nibbles, on
+ * the current device: out[4 n] = the bf16 pairs (low half first) of the nibbles in order.  Test hook
+ * (tests/test_gemm_kernel_gpu.py checks every nibble value at every position).  Returns CSM_OK or an error. */
+int csm_q4_expand(const uint32_t* words, int n, uint32_t* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -64,3 +64,21 @@ def test_mfma_gemm_matches_gemv_every_shape(dtype):
                 bad.append(f"{name} M={M}: max err {err:.3e} (max |y| {scale:.3e})")
     del model
     assert not bad, "\n".join(bad)
+
+
+def test_q4_expansion_every_nibble():
+    """The int4 -> bf16 expansion the matrix-core GEMMs feed their MFMAs (xs.h q4_word_bf16: the nibbles as
+    fp8 e4m3 bytes through v_cvt_scalef32_pk_bf16_fp8 at scale 2^9) against the bf16 bits of the integers:
+    every nibble value at every one of the 8 positions, plus random words."""
+    from csm_mlx import _lib
+    L = _lib.lib()
+    words = [sum(v << (4 * j) for j in range(8)) for v in range(16)]                  # v everywhere
+    words += [v << (4 * j) for v in range(16) for j in range(8)]                       # v at j, zeros around
+    words += [int(x) for x in np.random.default_rng(3).integers(0, 2 ** 32, 4096, dtype=np.uint64)]
+    w = np.array(words, np.uint32)
+    out = np.zeros((len(w), 4), np.uint32)
+    _lib.check(L.csm_q4_expand(w.ctypes.data, len(w), out.ctypes.data))
+    nib = (w[:, None] >> (4 * np.arange(8, dtype=np.uint32))[None, :]) & 0xF           # (n, 8) in k order
+    bits = (nib.astype(np.float32).view(np.uint32) >> 16).astype(np.uint32)            # bf16 of the integers
+    want = bits[:, 0::2] | (bits[:, 1::2] << 16)                                       # pairs, low half first
+    assert np.array_equal(out, want)
