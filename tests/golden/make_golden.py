@@ -226,6 +226,65 @@ def config3_b32_golden(frames=64):
     return out
 
 
+C5_UTTS = 8                         # configs[4] utterances pinned at full length (of the GPU test's B = 64)
+C5_LOGIT_FRAMES = (0, 64, 124)      # frames whose c0 / ci logits are kept, for utterances 0 and C5_UTTS - 1
+C5_CI = (1, 16, 31)
+
+
+def config5_q4_prompts(utts=C5_UTTS):
+    """configs[4]'s prompts for utterances 0 .. utts-1 (bench.py context_prompts): 3 context Segments (speaker
+    seg % 2, 12 text ids, 5 s of bench.context_audio Mimi-encoded -- here by the codec oracle, whose codes the
+    GPU encode matches bit for bit, tests/test_mimi_gpu.py) + the 12-id text row."""
+    import bench
+    from bench import prompt_ids
+    from csm_mlx.tokenizers import audio_codes_to_frames, tokenize_text_segment
+    m = MIMI_CONFIGURATION["mimi_202407"]
+    om = OracleMimi(m, synthetic_mimi_weights(m, 0))
+    prompts = []
+    for g in range(utts):
+        parts = []
+        for seg in range(3):
+            parts.append(tokenize_text_segment(prompt_ids(10_000 + 10 * g + seg), seg % 2, 32))
+            parts.append(audio_codes_to_frames(om.encode(bench.context_audio(g, seg)[None, None])[0]))
+        parts.append(tokenize_text_segment(prompt_ids(g), 0, 32))
+        prompts.append((np.concatenate([t for t, _ in parts]).astype(np.int32), np.concatenate([mm for _, mm in parts])))
+        print("prompt", g, prompts[-1][0].shape, flush=True)
+    return prompts
+
+
+def config5_q4_golden(utts=C5_UTTS, frames=125):
+    """configs[4] at full length for its first 8 utterances: int4 group-64 weights (nn.quantize of the seed-0
+    weights; the oracle on the dequantized weights), the Mimi-encoded 3-segment contexts (248 rows), 125 greedy
+    frames.  Codes, frame counts, the prompts, and c0 / ci logit slices at C5_LOGIT_FRAMES for the first and
+    last utterance."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from helpers import csm_weights, oracle_batch, oracle_for
+    prompts = config5_q4_prompts(utts)
+    args, w = csm_weights("1b")
+    ref = oracle_batch(oracle_for(args, w, q4=True), prompts, frames, collect_logits=True)
+    n = np.array([r[0].shape[0] for r in ref], np.int32)
+    print("n_frames", n.tolist(), flush=True)
+    codes = np.zeros((utts, frames, 32), np.int32)
+    for b, r in enumerate(ref):
+        codes[b, :n[b]] = r[0]
+    # the oracle's own top-2 margin of every code (relative to max|logit|): where it is at fp32 resolution
+    # (~1e-6) another summation order may pick the other code, and the GPU test says so instead of failing
+    margin = np.ones((utts, frames, 32), np.float32)
+    for b, r in enumerate(ref):
+        for f in range(n[b]):
+            lg = [r[1][f][0]] + [r[1][f][1][k] for k in range(31)]
+            for k, l in enumerate(lg):
+                top = np.sort(l)[-2:]
+                margin[b, f, k] = (top[1] - top[0]) / max(float(np.abs(l).max()), 1e-30)
+    print("codes with a relative top-2 margin < 1e-5:", int((margin < 1e-5).sum()), flush=True)
+    keep = [0, utts - 1]
+    c0 = np.stack([[ref[b][1][f][0] for f in C5_LOGIT_FRAMES] for b in keep])                     # (2, 3, V)
+    ci = np.stack([[ref[b][1][f][1][[c - 1 for c in C5_CI]] for f in C5_LOGIT_FRAMES] for b in keep])  # (2, 3, 3, V)
+    return dict(codes=codes, n_frames=n, tokens=np.stack([t for t, _ in prompts]),
+                masks=np.stack([m for _, m in prompts]), logit_utts=np.array(keep, np.int32),
+                frames=np.array(C5_LOGIT_FRAMES), ci_codebooks=np.array(C5_CI), c0=c0, ci=ci, margin=margin)
+
+
 FIXTURES = {
     "csm_tiny_oracle.npz": csm_golden,
     "mimi_tiny_oracle.npz": mimi_golden,
@@ -234,6 +293,7 @@ FIXTURES = {
     "config0_plumbing.npz": config0_golden,
     "config4_b32_greedy_125.npz": config4_b32_golden,
     "config3_b32_stream_64.npz": config3_b32_golden,
+    "config5_q4_b8_greedy_125.npz": config5_q4_golden,
 }
 
 if __name__ == "__main__":

@@ -10,7 +10,10 @@
   oracle's ``decode_step``, plus whole chunks (utterance 0's first 8, each ending utterance's last 4
   before its EOS frame).
 
-Both run on the EOS-capable rig of the seed-0 weights (tests/helpers.py eos_rig), so utterances end at
+* configs[4] -- csm_1b int4 B = 64 with Mimi-encoded 3-segment contexts (248-row prompts), 125 greedy
+  frames, utterances 0-7 against the oracle on the dequantized weights (plain seed-0 weights: no early EOS).
+
+The first two run on the EOS-capable rig of the seed-0 weights (tests/helpers.py eos_rig), so utterances end at
 different frames (per-utterance EOS at B > 1, generation.py:139-161).  Bars: codes and frame counts
 bit-exact; logits within 2e-3 x max|logit|; chunks within 1e-4 RMS (statistics: within what a 1e-4
 RMS error allows)."""
@@ -23,6 +26,7 @@ from helpers import eos_weights, first_divergence
 
 pytestmark = pytest.mark.gpu
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+NEAR_TIE = 1e-5   # oracle top-2 logit margin / max|logit| below which a code is a tie at fp32 resolution
 
 
 def _fixture(name):
@@ -128,3 +132,79 @@ def test_config3_stream_b32_sampled_64_frames():
         if err > 1e-4:
             bad.append(f"utterance {b}: chunk RMS error {err:.3e}")
     assert not bad, "; ".join(bad[:10])
+
+
+def test_config5_q4_b64_greedy_125_frames():
+    """configs[4] at full length: B = 64 int4 (nn.quantize) prompts of 3 Mimi-encoded context Segments (the GPU
+    codec, as bench.py --config 5) + the text row, 248 rows each through csm_prefill_batch (the matrix-core
+    prefill and its attention), 125 greedy frames.  Utterances 0-7 against tests/golden/config5_q4_b8_greedy_125.npz
+    (the codec and CSM oracles on the dequantized weights): the GPU-encoded prompts equal the fixture's, codes
+    and frame counts bit-exact, c0 / ci logits of utterances 0 and 7 at frames 0 / 64 / 124 within 1e-3 x
+    max|logit| (the int4 bar of test_gemm_gpu.py).  One exception, reported: a code whose oracle top-2 margin is
+    below NEAR_TIE (fp32 resolution; the fixture stores every code's margin) may part, and that utterance is
+    compared up to it."""
+    import bench
+    from csm_mlx.generation import FrameCache
+    from csm_mlx.models import CSM
+    from csm_mlx.sampling import Sampler
+    from helpers import csm_weights
+    from test_configs_gpu import _codec
+    z = _fixture("config5_q4_b8_greedy_125.npz")
+    args, w = csm_weights("1b")
+    B, K, V = 64, args.n_audio_codebooks, args.n_audio_vocab
+    Vp = (V + 7) // 8 * 8
+    model = CSM(args, dtype="q4", max_batch=B)
+    model.load_weights(w)
+    _codec(3 * B)
+    mine = list(range(B))
+    prompts = bench.context_prompts(mine, bench.context_segments(mine))
+    U = int(z["codes"].shape[0])
+    # the prompts both sides consume: text rows identical; the Mimi-encoded code rows are reported (the GPU
+    # codec's fp32 latents and the oracle's differ in summation order, so an RVQ near-tie can pick the other
+    # code -- then the rest of that frame's codebooks follow the other residual) and the frames below start
+    # from the oracle's prompt, so they pin the CSM path alone
+    flips = []
+    for b in range(U):
+        assert np.array_equal(prompts[b][1], z["masks"][b]), f"utterance {b}: prompt masks differ"
+        d = np.argwhere(prompts[b][0] != z["tokens"][b])
+        assert not (d[:, 1] == K).any(), f"utterance {b}: text rows differ"
+        flips += [(b, int(r)) for r in np.unique(d[:, 0])]
+        prompts[b] = (z["tokens"][b], z["masks"][b])
+    print("config 5 context frames whose Mimi codes differ from the oracle's (utterance, row):", flips, flush=True)
+    assert len(flips) <= 2, f"Mimi encode: {len(flips)} context frames differ from the oracle's: {flips}"
+    cache = FrameCache(model, B, Sampler(0.0, 0), [0] * B)
+    cache.prefill_batch([(b, t, m) for b, (t, m) in enumerate(prompts)])
+    keep = {int(f): i for i, f in enumerate(z["frames"])}
+    cis = [c - 1 for c in z["ci_codebooks"]]
+    errs = []
+    for f in range(125):
+        cache.run(1)
+        if f in keep:
+            c0 = cache.debug("c0_logits", (B, Vp))[:, :V]
+            ci = cache.debug("ci_logits", (K - 1, B, Vp))[:, :, :V]
+            for j, b in enumerate(z["logit_utts"]):
+                for got, want in ((c0[b], z["c0"][j, keep[f]]), (ci[cis, b], z["ci"][j, keep[f]])):
+                    err = float(np.abs(got - want).max())
+                    if err > 1e-3 * float(np.abs(want).max()):
+                        errs.append(f"frame {f} utterance {b}: logits err {err:.3e}")
+    hist, n, _ = cache.codes()
+    del model
+    # codes bit-exact, except that a code whose oracle top-2 margin is at fp32 resolution (< NEAR_TIE x
+    # max|logit|, stored with the fixture) may go the other way under another summation order: then the
+    # utterance is compared up to that code and the tie is reported
+    bad, ties = [], []
+    for b in range(U):
+        nb = int(z["n_frames"][b])
+        div = first_divergence(hist[: n[b], b], z["codes"][b, :nb])
+        if div is None and n[b] == nb:
+            continue
+        if div is not None and div < min(n[b], nb):
+            k = int(np.argmax(hist[div, b] != z["codes"][b, div]))
+            if z["margin"][b, div, k] < NEAR_TIE:
+                ties.append((b, div, k, float(z["margin"][b, div, k])))
+                continue
+        bad.append(f"utterance {b}: {n[b]} vs {nb} frames, first divergence {div}")
+    print("config 5 near-tie codes (utterance, frame, codebook, oracle margin):", ties, flush=True)
+    assert not bad, "; ".join(bad)
+    assert len(ties) <= 2, f"{len(ties)} of {U} utterances part at a near-tie: {ties}"
+    assert not errs, "; ".join(errs[:10])
