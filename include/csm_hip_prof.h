@@ -45,7 +45,9 @@ int csm_bench_bb_step(csm_engine* e, int iters, float* avg_us, double* bytes);
  * runs the batched frame's MFMA GEMM at >= 8 rows instead of the GEMV, default 0: the GEMM's kernel
  * tests), "gemm_xs" (the batched depth decoder on the streaming matrix-core GEMM, gemm_xs.hip,
  * default 1), "bb_xs" (the batched backbone on it too, default 1), "prefill_rows" (row cap of one
- * csm_prefill_batch group, 0 = the engine's capacity), "inject_handoff_error" (test hook).
+ * csm_prefill_batch group, 0 = the engine's capacity), "attn_prefill" (prompt attention on the fp32 matrix
+ * cores, a block per 64-row prompt run and kv head, default 1; 0 = one block per row, tests), "inject_handoff_error"
+ * (test hook).
  * Process-wide lab knobs are environment variables read once (CSM_NT_MASK, CSM_GEMV_XL, CSM_XS_*). */
 int csm_set_option(csm_engine* e, const char* key, int value);
 
