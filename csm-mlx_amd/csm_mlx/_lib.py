@@ -82,6 +82,7 @@ def lib():
             "csm_prefill": ([P, I, I, P, P], I),
             "csm_prefill_batch": ([P, I, P, P, P, P], I),
             "csm_run_frames": ([P, I, ctypes.POINTER(I)], I),
+            "csm_run_frames_ahead": ([P, I, ctypes.POINTER(I)], I),
             "csm_frame_step": ([P, P, P], I),
             "csm_frame_c0_logits": ([P, P], I),
             "csm_frame_finish": ([P, P, ctypes.POINTER(I)], I),

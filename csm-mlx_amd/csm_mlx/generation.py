@@ -110,6 +110,16 @@ class FrameCache:
         self.frames += nframes
         return bool(done.value)
 
+    def run_ahead(self, nframes: int) -> Optional[bool]:
+        """Enqueue nframes frames and return whether every utterance had hit EOS by the end of the
+        PREVIOUS chunk run this way (None for the first): the EOS poll one chunk behind, so the GPU never
+        waits on the host (csm_run_frames_ahead)."""
+        self._check()
+        prev = ctypes.c_int(-1)
+        _lib.check(self.L.csm_run_frames_ahead(self.model.engine, nframes, ctypes.byref(prev)))
+        self.frames += nframes
+        return None if prev.value < 0 else bool(prev.value)
+
     def run_processed(self, processors: Sequence[Callable], c0_history: Optional[list]) -> bool:
         """One frame with host ``logits_processors`` applied to the c0 logits (generation.py:42-61):
         the engine stops after codebook0_head, each processor maps (stack(c0_history) or zeros((0,)),
@@ -259,7 +269,7 @@ def _mark(timings: Optional[dict], key: str, t0: float, model: Optional[CSM] = N
 
 
 def generate_codes_batch(model: CSM, prompts: Sequence[Tuple[np.ndarray, np.ndarray]], max_audio_frames: int, *,
-                         sampler: Sampler, seeds=None, chunk: int = 16,
+                         sampler: Sampler, seeds=None, chunk: int = 8,
                          logits_processors: Optional[List[Callable]] = None, timings: Optional[dict] = None):
     """Run the frame loop for B prompts.  Returns (hist [F,B,K], n_frames [B], cache).  With
     ``logits_processors`` every frame pauses after codebook0_head for them (generation.py:44-49).
@@ -289,11 +299,12 @@ def generate_codes_batch(model: CSM, prompts: Sequence[Tuple[np.ndarray, np.ndar
             if cache.run_processed(logits_processors, c0_history):
                 break
         left = 0
+    ahead = os.environ.get("CSM_EOS_AHEAD", "1") != "0"   # lab: 0 = poll each chunk after it ends (A/B)
     while left > 0:
-        n = min(chunk, left)
-        all_done = cache.run(n)                                                  # EOS poll (generation.py:151)
-        left -= n
-        if all_done:
+        n = min(chunk if ahead else 2 * chunk, left)
+        ended = cache.run_ahead(n) if ahead else cache.run(n)   # EOS poll (generation.py:151); ahead: of the
+        left -= n                                               # previous chunk, while this one runs
+        if ended:                           # (this chunk's frames then change no returned code)
             break
     hist, n_frames, _ = cache.codes()
     _mark(timings, "frames", t0, model)

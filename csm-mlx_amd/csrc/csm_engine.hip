@@ -105,6 +105,13 @@ struct csm_engine {
   uint8_t* msk = nullptr;
   int *row_b = nullptr, *row_pos = nullptr;  // [M_cap] batched-prefill row tables
   int2* ptiles = nullptr;  // [M_cap / 64 + B_max + 2] prompt-prefill attention tiles (RowMap::tiles)
+  // csm_run_frames_ahead: each chunk's done flags and the persistent kernels' error flags are copied to
+  // pinned host memory behind its frames, with an event; a call waits for the previous chunk's only
+  uint8_t* ahead_pin = nullptr;  // [2][ahead_bytes()]
+  hipEvent_t ahead_ev[2] = {nullptr, nullptr};
+  int ahead_slot = 0;
+  bool ahead_pending = false;
+  size_t ahead_bytes() const { return (size_t)(B_max + 7) / 8 * 8 + 8; }
   bool attn_tiles_on = true;  // csm_set_option "attn_prefill": 0 = attn_block per row (A/B, tests)
   // per-batch state
   int *codes = nullptr, *hist = nullptr, *pos = nullptr, *n_frames = nullptr, *frame_ctr = nullptr;
@@ -198,6 +205,9 @@ struct csm_engine {
       }
   }
   ~csm_engine() {
+    for (hipEvent_t ev : ahead_ev)
+      if (ev) (void)hipEventDestroy(ev);
+    if (ahead_pin) (void)hipHostFree(ahead_pin);
     if (g_body) (void)hipGraphExecDestroy(g_body);
     if (g_head) (void)hipGraphExecDestroy(g_head);
     for (void* p : allocs) (void)hipFree(p);
@@ -1302,6 +1312,10 @@ int csm_quantize(csm_engine* e, int group_size, int bits) {
 int csm_begin(csm_engine* e, int B, const uint64_t* seeds, float temperature, int top_k) {
   CSM_TRY {
     e->c0_pending = false;
+    if (e->ahead_pending) {  // the last chunk's pinned copies land before the slots are reused
+      HIPCHK(hipStreamSynchronize(e->st));
+      e->ahead_pending = false;
+    }
     if (B <= 0) throw CsmError(CSM_ERR_ARG, "batch size out of range");
     if (temperature < 0.f) throw CsmError(CSM_ERR_ARG, "temperature must be >= 0");
     HIPCHK(hipSetDevice(e->dev));
@@ -1522,6 +1536,43 @@ int csm_run_frames(csm_engine* e, int nframes, int* all_done) {
       for (auto v : d) all &= (v != 0);
       *all_done = all;
     }
+  }
+  CSM_CATCH
+}
+
+int csm_run_frames_ahead(csm_engine* e, int nframes, int* prev_all_done) {
+  if (!e || !prev_all_done) { csm_set_error("null engine or result pointer"); return CSM_ERR_ARG; }
+  const int rc = csm_run_frames(e, nframes, nullptr);  // enqueued, no wait
+  if (rc != CSM_OK) return rc;
+  CSM_TRY {
+    if (!e->ahead_pin) {
+      HIPCHK(hipHostMalloc((void**)&e->ahead_pin, 2 * e->ahead_bytes(), hipHostMallocDefault));
+      for (hipEvent_t& ev : e->ahead_ev) HIPCHK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    }
+    const int s = e->ahead_slot;
+    uint8_t* pin = e->ahead_pin + s * e->ahead_bytes();
+    int* perr = reinterpret_cast<int*>(pin + e->ahead_bytes() - 8);
+    perr[0] = perr[1] = 0;  // (slot s was last read two chunks ago, after its event)
+    HIPCHK(hipMemcpyAsync(pin, e->done, e->B, hipMemcpyDeviceToHost, e->st));
+    if (e->df_err) HIPCHK(hipMemcpyAsync(perr, e->df_err, 4, hipMemcpyDeviceToHost, e->st));
+    if (e->bb_err) HIPCHK(hipMemcpyAsync(perr + 1, e->bb_err, 4, hipMemcpyDeviceToHost, e->st));
+    HIPCHK(hipEventRecord(e->ahead_ev[s], e->st));
+    int res = -1;
+    if (e->ahead_pending) {
+      const int q = s ^ 1;
+      HIPCHK(hipEventSynchronize(e->ahead_ev[q]));
+      const uint8_t* pq = e->ahead_pin + q * e->ahead_bytes();
+      const int* qerr = reinterpret_cast<const int*>(pq + e->ahead_bytes() - 8);
+      if (qerr[0] || qerr[1]) {
+        HIPCHK(hipStreamSynchronize(e->st));
+        check_dec_frame(e);  // resets the device flags and raises
+      }
+      res = 1;
+      for (int b = 0; b < e->B; ++b) res &= pq[b] != 0;
+    }
+    e->ahead_slot = s ^ 1;
+    e->ahead_pending = true;
+    *prev_all_done = res;
   }
   CSM_CATCH
 }

@@ -104,6 +104,13 @@ int csm_prefill_batch(csm_engine* e, int n, const int32_t* utts, const int32_t* 
 /* Generate up to nframes frames for the whole batch (one HIP graph replay per frame).
  * *all_done (optional) = 1 when every utterance hit EOS. */
 int csm_run_frames(csm_engine* e, int nframes, int* all_done);
+/* csm_run_frames without waiting on this chunk: enqueues nframes frames, then waits for the PREVIOUS
+ * chunk enqueued by this call (not for the frames just enqueued) and sets *prev_all_done = 1 when every
+ * utterance had hit EOS by its end, 0 when not, -1 when there was no previous chunk.  The generation loop
+ * (generation.py:139-161) thus tests EOS one chunk behind while the next chunk already runs, so the GPU
+ * never idles on the host's poll; frames enqueued past an all-EOS chunk change no returned code or frame
+ * count.  CSM_ERR_HIP if a persistent kernel's hand-off timed out in the polled chunk. */
+int csm_run_frames_ahead(csm_engine* e, int nframes, int* prev_all_done);
 /* One frame (generation.py:21-92 + the EOS test :151) with its result handed back: out_codes [B][K]
  * int32 = the frame's codes (the `sample` generate_frame returns), done [B] = utterances past EOS.
  * Either pointer may be NULL.  Equivalent to csm_run_frames(e, 1, NULL) followed by a read of the

@@ -208,3 +208,27 @@ def test_config5_q4_b64_greedy_125_frames():
     assert not bad, "; ".join(bad)
     assert len(ties) <= 2, f"{len(ties)} of {U} utterances part at a near-tie: {ties}"
     assert not errs, "; ".join(errs[:10])
+
+
+def test_generate_loop_polls_eos_one_chunk_behind():
+    """generate_codes_batch's frame loop (csm_run_frames_ahead: each chunk enqueued before the previous
+    chunk's EOS poll returns) on the config-4 fixture's early-ending utterances alone (EOS at frames 5-102,
+    so the whole batch ends and the loop leaves early), then on all 32: codes and frame counts equal the
+    fixture's, whatever frames ran past the batch's end."""
+    from csm_mlx.generation import generate_codes_batch
+    from csm_mlx.sampling import Sampler
+    z = _fixture("config4_b32_greedy_125.npz")
+    args, w = eos_weights("1b")
+    prompts = _prompts()
+    early = [int(b) for b in z["eos_utts"]]
+    for utts in (early, list(range(32))):
+        model = _model(args, w, len(utts))
+        hist, n, cache = generate_codes_batch(model, [prompts[b] for b in utts], 125, sampler=Sampler(0.0, 0))
+        ran = cache.frames
+        del cache, model
+        if utts is early:
+            assert ran < 125, "the loop did not leave after every utterance ended"
+        for j, b in enumerate(utts):
+            nb = int(z["n_frames"][b])
+            assert n[j] == nb, f"utterance {b}: {n[j]} vs {nb} frames"
+            assert first_divergence(hist[: n[j], j], z["codes"][b, :nb]) is None, f"utterance {b}: codes differ"
