@@ -167,7 +167,15 @@ __global__ __launch_bounds__(64 * NW) void gemm_wide_kernel(GemvParams p) {
   constexpr int CT_BYTES = NB * (NBR + 1) * 4;
   constexpr int SM = XS_BYTES > CT_BYTES ? XS_BYTES : CT_BYTES;
   __shared__ __attribute__((aligned(16))) unsigned char smem[SM];
-  __shared__ __attribute__((aligned(16))) float xsum[2][NB];  // int4: the stage's sum of x per batch row
+  // GW_QB: the int4 bias term sum_g bias_g[n] X_g[m] on the matrix cores, 16 stages at a time (X_g split in
+  // three exact bf16 parts, the bf16 biases as the B operand: three MFMAs per tile pair) instead of an fmaf per
+  // accumulator per stage; X_g and the biases wait in 32-stage rings
+#ifndef GW_QB
+#define GW_QB 1
+#endif
+  constexpr bool QB = Q4 && GW_QB != 0;
+  __shared__ __attribute__((aligned(16))) float xsum[QB ? 32 : 2][NB];  // int4: the stage's sum of x per batch row
+  __shared__ uint16_t bsh[QB ? 32 : 1][QB ? NBR : 1];
   __shared__ float ssb[NB];
   __shared__ int last;
   auto Xs = [&](int buf, int part, int t, int s) {
@@ -241,7 +249,8 @@ __global__ __launch_bounds__(64 * NW) void gemm_wide_kernel(GemvParams p) {
       }
     }
   };
-  auto store = [&](const Stage& g, int buf, bool live) {
+  auto store = [&](const Stage& g, int buf, bool live, int st) {
+    const int xslot = QB ? (st & 31) : buf;
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       const int c = x_c + RPT * i;
@@ -252,7 +261,7 @@ __global__ __launch_bounds__(64 * NW) void gemm_wide_kernel(GemvParams p) {
         *(reinterpret_cast<u32x2_t*>(&Xs(buf, 0, c >> 5, st_s)[sl]) + st_j) = raw;
         *(reinterpret_cast<u32x2_t*>(&Xs(buf, 1, c >> 5, st_s)[sl]) + st_j) = raw;
         *(reinterpret_cast<u32x2_t*>(&Xs(buf, 2, c >> 5, st_s)[sl]) + st_j) = raw;
-        if (live && (tid & 15) == 0) xsum[buf][c] = v[1];
+        if (live && (tid & 15) == 0) xsum[xslot][c] = v[1];
         continue;
       }
       if (norm) {
@@ -265,7 +274,7 @@ __global__ __launch_bounds__(64 * NW) void gemm_wide_kernel(GemvParams p) {
       }
       if constexpr (Q4) {  // sum of the group's 64 values of row c: 16 threads x 4, fixed order
         const float sum = row16_sum((v[0] + v[1]) + (v[2] + v[3]));
-        if ((tid & 15) == 0) xsum[buf][c] = sum;
+        if ((tid & 15) == 0) xsum[xslot][c] = sum;
       }
       u32x2_t hi, mid, lo;
       split3_4(v, hi, mid, lo);
@@ -282,7 +291,7 @@ __global__ __launch_bounds__(64 * NW) void gemm_wide_kernel(GemvParams p) {
     for (int i = 0; i < RTW; ++i) acc[t][i] = f32x16_t{};
 #pragma unroll
   for (int d = 0; d < PD; ++d) load(d, sg[d]);
-  store(sg[0], 0, true);
+  store(sg[0], 0, true, 0);
   __syncthreads();
   GSTAMP(1);
   for (int it0 = 0; it0 < nst; it0 += PD) {
@@ -327,7 +336,47 @@ __global__ __launch_bounds__(64 * NW) void gemm_wide_kernel(GemvParams p) {
             }
           }
       }
-      if constexpr (Q4) {  // acc += scale * S_g + bias * X_g: this lane's weight row, 16 batch rows
+      if constexpr (QB) {  // acc += scale * S_g; the biases to their ring, their products every 16 stages
+        if (kh == 0 && lane < 32)
+#pragma unroll
+          for (int i = 0; i < RTW; ++i) bsh[it & 31][32 * (rt0 + i) + lane] = (uint16_t)(g.sb[i] >> 16);
+#pragma unroll
+        for (int t = 0; t < MT; ++t)
+#pragma unroll
+          for (int i = 0; i < RTW; ++i) {
+            const float sc = bf16_lo(g.sb[i]);
+#pragma unroll
+            for (int j = 0; j < 16; ++j) acc[t][i][j] = fmaf(sc, gq[t][i][j], acc[t][i][j]);
+          }
+        if (kh == 0 && ((it & 15) == 15 || it == nst - 1)) {
+          const int c0 = it & ~15;
+#pragma unroll
+          for (int t = 0; t < MT; ++t) {
+            uint32_t xa[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+              const int gi = c0 + 8 * h + k;
+              xa[k] = gi <= it ? __float_as_uint(xsum[gi & 31][32 * t + r]) : 0u;
+            }
+            u32x4_t pa[3];
+            xs::split_frag(u32x4_t{xa[0], xa[1], xa[2], xa[3]}, u32x4_t{xa[4], xa[5], xa[6], xa[7]}, pa);
+#pragma unroll
+            for (int i = 0; i < RTW; ++i) {
+              u32x4_t bw;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const int gi = c0 + 8 * h + 2 * e;
+                const uint32_t lo = gi <= it ? bsh[gi & 31][32 * (rt0 + i) + r] : 0u;
+                const uint32_t hi = gi + 1 <= it ? bsh[(gi + 1) & 31][32 * (rt0 + i) + r] : 0u;
+                bw[e] = lo | (hi << 16);
+              }
+#pragma unroll
+              for (int q = 0; q < 3; ++q)
+                acc[t][i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, pa[q]), __builtin_bit_cast(bf16x8_t, bw), acc[t][i], 0, 0, 0);
+            }
+          }
+        }
+      } else if constexpr (Q4) {  // acc += scale * S_g + bias * X_g: this lane's weight row, 16 batch rows
 #pragma unroll
         for (int t = 0; t < MT; ++t) {
           float xs[16];
@@ -351,10 +400,10 @@ __global__ __launch_bounds__(64 * NW) void gemm_wide_kernel(GemvParams p) {
       if constexpr (PD == 1) {  // one slot (mostly one-stage slices): refill it first, nothing to protect
         if (it + 1 < nst) {
           load(it + 1, sg[0]);
-          store(sg[0], buf ^ 1, true);
+          store(sg[0], buf ^ 1, true, it + 1);
         }
       } else {
-        store(sg[(d + 1) % PD], buf ^ 1, it + 1 < nst);  // past the slice: zeros into the idle buffer
+        store(sg[(d + 1) % PD], buf ^ 1, it + 1 < nst, it + 1);  // past the slice: zeros into the idle buffer
         load(it + PD, sg[d]);
       }
       __syncthreads();
