@@ -101,23 +101,30 @@ def aggregate(frames_local: float, dt_local: float, world: int, device=None):
     return float(f.item()), float(m.item())
 
 
-def rank_report(frames_local: float, dt_local: float, steps: int, world: int, device_index: int, device=None):
+def rank_report(frames_local: float, dt_local: float, steps: int, world: int, device_index: int, device=None,
+                gather_s: float = 0.0):
     """What the communicator saw: backend, world size, and per rank its GPU index, its own
-    ms per step and frames -- all-gathered, so a scaling line shows which rank was slowest."""
-    me = [float(device_index), dt_local / max(1, steps) * 1000.0, frames_local]
+    ms per step, the part of it spent in the per-step result gather (gather_results, inside the timed
+    region) and the rest (generation), and frames -- all-gathered, so a scaling line shows which rank was
+    slowest and what the result collection cost it."""
+    ms = dt_local / max(1, steps) * 1000.0
+    g_ms = gather_s / max(1, steps) * 1000.0
+    me = [float(device_index), ms, frames_local, g_ms]
+
+    def row(r, v):
+        return {"rank": r, "device": int(v[0]), "ms_per_step": round(v[1], 3), "gather_ms_per_step": round(v[3], 3),
+                "generate_ms_per_step": round(v[1] - v[3], 3), "frames": int(v[2])}
     if world == 1 and "WORLD_SIZE" not in os.environ:
-        return {"backend": None, "world_size_seen": 1,
-                "ranks": [{"rank": 0, "device": device_index, "ms_per_step": round(me[1], 3), "frames": int(me[2])}],
-                "slowest_rank": 0}
+        return {"backend": None, "world_size_seen": 1, "ranks": [row(0, me)], "slowest_rank": 0}
     import torch
     import torch.distributed as dist
     t = torch.tensor(me, dtype=torch.float64, device=device)
     out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
     dist.all_gather(out, t)
-    rows = [o.cpu().tolist() for o in out]
-    ranks = [{"rank": r, "device": int(v[0]), "ms_per_step": round(v[1], 3), "frames": int(v[2])} for r, v in enumerate(rows)]
+    ranks = [row(r, o.cpu().tolist()) for r, o in enumerate(out)]
     return {"backend": dist.get_backend(), "world_size_seen": dist.get_world_size(), "ranks": ranks,
-            "slowest_rank": max(range(len(ranks)), key=lambda r: ranks[r]["ms_per_step"])}
+            "slowest_rank": max(range(len(ranks)), key=lambda r: ranks[r]["ms_per_step"]),
+            "max_gather_ms_per_step": max(r["gather_ms_per_step"] for r in ranks)}
 
 
 def build_codec(seed=0, device=None, model_name="csm_1b"):
@@ -195,6 +202,12 @@ CONFIGS = {
     7: dict(batch=1, dtype="bf16", temperature=0.8, top_k=0, stream=False, context=False,
             workload="configs[1] with the reference's default sampler (generate(temperature=0.8), "
                      "generation.py:102), B=1, 10 s + Mimi decode"),
+    # the reference demo's path (run_streaming_csm_mlx.py:811-818, :844-852): nn.quantize(model, 64, 4) then
+    # stream_generate, one utterance; and configs[1] with fp32 weights (the random-init model's arithmetic class)
+    8: dict(batch=1, dtype="q4", temperature=0.0, top_k=0, stream=True, context=False,
+            workload="int4 g64 (nn.quantize) csm_1b stream_generate, B=1, greedy, 10 s (per-frame Mimi decode_step)"),
+    9: dict(batch=1, dtype="float32", temperature=0.0, top_k=0, stream=False, context=False,
+            workload="configs[1] with fp32 weights (MLX's random-init arithmetic class), B=1 greedy, 10 s + Mimi decode"),
 }
 
 
@@ -353,7 +366,7 @@ def main():
     ap.add_argument("--no-decode", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=96, help="oracle frames timed for cpu_baseline (~10 s on 16 cores)")
-    ap.add_argument("--config", type=int, default=0, choices=[0, 2, 3, 4, 5, 6, 7],
+    ap.add_argument("--config", type=int, default=0, choices=[0, 2, 3, 4, 5, 6, 7, 8, 9],
                     help="run BASELINE.json configs[N-1] (batch, dtype, sampling, streaming, context) instead of "
                          "the default configs[1] line; the metric stays audio frames/s")
     ap.add_argument("--roofline-iters", type=int, default=400,
@@ -487,12 +500,16 @@ def main():
             codes, pcm_l = out if decode else (out, None)
             n = sum(len(c) for c in codes)
         if use_dist:    # result collection: one gather per kind to rank 0 (RCCL over xGMI / gloo)
+            t_g = time.perf_counter()
             codes, pcm_l = gather_results(codes, pcm_l, args.frames, FRAME_SAMPLES, dev, dst=0)
+            gather_t[0] += time.perf_counter() - t_g
         last["codes"], last["pcm"] = codes, pcm_l
         return n
 
+    gather_t = [0.0]
     for _ in range(args.warmup):
         step()
+    gather_t[0] = 0.0
     if phases is not None:
         phases.clear()
     barrier_sync()
@@ -503,7 +520,7 @@ def main():
     barrier_sync()
     dt = time.perf_counter() - t0
     total_frames, max_dt = aggregate(float(frames), dt, world, dev)
-    dist_info = rank_report(float(frames), dt, args.steps, world, device, dev)
+    dist_info = rank_report(float(frames), dt, args.steps, world, device, dev, gather_t[0])
 
     roof = rooflines(model, args.batch, args.roofline_iters)
     fb = frame_weight_bytes(model)
@@ -519,7 +536,8 @@ def main():
     if use_dist:
         up = args.batch * ((1 + args.frames * K) * 4 + (args.frames * FRAME_SAMPLES * 4 if decode else 0))
         results_info = {"collection": f"{args.dist_backend} gather to rank 0 per step (codes + lengths int32"
-                                      f"{', PCM float32' if decode else ''}), inside the timed region",
+                                      f"{', PCM float32' if decode else ''}), inside the timed region (its time per "
+                                      "rank: dist.ranks[].gather_ms_per_step)",
                         "host_bytes_per_rank_up": int(up), "host_bytes_rank0_down": int(up * world)}
     if rank == 0 and args.dump:
         z = {f"codes_{i}": c for i, c in enumerate(last["codes"])}

@@ -95,7 +95,8 @@ def lib():
             "csm_linear": ([P, ctypes.c_char_p, I, P, P], I),
             "csm_synchronize": ([P], I),
             "csm_set_option": ([P, ctypes.c_char_p, I], I),
-            "csm_xs_shape": ([I, I, I, I, ctypes.POINTER(I)], I),
+            "csm_xs_shape": ([I, I, I, I, I, ctypes.POINTER(I)], I),
+            "csm_q4_gemv_shape": ([I, I, ctypes.POINTER(I)], I),
             "csm_q4_expand": ([P, I, P], I),
             "csm_bench_gemv": ([P, I, I, I, ctypes.POINTER(F), ctypes.POINTER(ctypes.c_double)], I),
             "csm_bench_dec_frame": ([P, I, ctypes.POINTER(F), ctypes.POINTER(ctypes.c_double)], I),

@@ -108,6 +108,7 @@ struct csm_engine {
   // csm_run_frames_ahead: each chunk's done flags and the persistent kernels' error flags are copied to
   // pinned host memory behind its frames, with an event; a call waits for the previous chunk's only
   uint8_t* ahead_pin = nullptr;  // [2][ahead_bytes()]
+  int2* ptiles_pin = nullptr;     // pinned staging of a single prompt's attention tiles (csm_prefill)
   hipEvent_t ahead_ev[2] = {nullptr, nullptr};
   int ahead_slot = 0;
   bool ahead_pending = false;
@@ -208,6 +209,7 @@ struct csm_engine {
     for (hipEvent_t ev : ahead_ev)
       if (ev) (void)hipEventDestroy(ev);
     if (ahead_pin) (void)hipHostFree(ahead_pin);
+    if (ptiles_pin) (void)hipHostFree(ptiles_pin);
     if (g_body) (void)hipGraphExecDestroy(g_body);
     if (g_head) (void)hipGraphExecDestroy(g_head);
     for (void* p : allocs) (void)hipFree(p);
@@ -1380,12 +1382,14 @@ int csm_prefill(csm_engine* e, int b, int T, const int32_t* tokens, const uint8_
     embed(e, ep, T, e->st);
     RowMap rm{T, b, nullptr, start};
     if (e->attn_tiles_on && T >= 16) {  // attention tiles: <= 64 consecutive rows (launch_attn's >= 16-row bar)
-      std::vector<int2> tl;
-      for (int t0 = 0; t0 < T; t0 += 64) tl.push_back(make_int2(t0, std::min(64, T - t0)));
-      HIPCHK(hipMemcpyAsync(e->ptiles, tl.data(), tl.size() * sizeof(int2), hipMemcpyHostToDevice, e->st));
-      HIPCHK(hipStreamSynchronize(e->st));  // (pageable source)
+      // staged in pinned memory: the copy stays asynchronous (this call's closing synchronize is what
+      // makes the staging reusable by the next csm_prefill)
+      const int nt = (T + 63) / 64;
+      if (!e->ptiles_pin) HIPCHK(hipHostMalloc((void**)&e->ptiles_pin, (e->M_cap / 64 + 1) * sizeof(int2), hipHostMallocDefault));
+      for (int t = 0; t < nt; ++t) e->ptiles_pin[t] = make_int2(64 * t, std::min(64, T - 64 * t));
+      HIPCHK(hipMemcpyAsync(e->ptiles, e->ptiles_pin, nt * sizeof(int2), hipMemcpyHostToDevice, e->st));
       rm.tiles = e->ptiles;
-      rm.ntiles = (int)tl.size();
+      rm.ntiles = nt;
     }
     run_stack(e, e->bb, e->x, T, e->q, e->att, e->mlp, rm, e->st);
     launch_rmsnorm_rows(e->x + (size_t)(T - 1) * e->D, e->D, e->bb.norm, e->bb.d.eps, e->D,
@@ -1564,7 +1568,11 @@ int csm_run_frames_ahead(csm_engine* e, int nframes, int* prev_all_done) {
       const uint8_t* pq = e->ahead_pin + q * e->ahead_bytes();
       const int* qerr = reinterpret_cast<const int*>(pq + e->ahead_bytes() - 8);
       if (qerr[0] || qerr[1]) {
+        // the chunk just enqueued has written slot s behind its event: drain the stream and forget both
+        // slots, so a later call (with or without csm_begin) never polls a stale done state
         HIPCHK(hipStreamSynchronize(e->st));
+        e->ahead_pending = false;
+        e->ahead_slot = 0;
         check_dec_frame(e);  // resets the device flags and raises
       }
       res = 1;

@@ -641,11 +641,12 @@ bool gemm_xs_eligible(int N, int K, int M, int wdt) {
 
 // Host-side shape query (csm_hip_prof.h csm_xs_shape): the launch geometry gemm_xs would use, for the
 // CPU tests of the stage-coverage rule.
-extern "C" int csm_xs_shape(int N, int K, int M, int head, int* out) {
+extern "C" int csm_xs_shape(int N, int K, int M, int head, int wdt, int* out) {
   int rtw, ks, pd, xw;
   xs_shape(N, K, M, head != 0, rtw, ks, pd, xw);
   out[0] = rtw; out[1] = ks; out[2] = pd; out[3] = xw;
-  return gemm_xs_eligible(N, K, M, WDT_BF16) ? 1 : 0;
+  const int w = wdt == CSM_Q4 ? WDT_Q4 : (wdt == CSM_BF16 ? WDT_BF16 : -1);
+  return w >= 0 && gemm_xs_eligible(N, K, M, w) ? 1 : 0;
 }
 
 __global__ void q4_expand_kernel(const uint32_t* w, int n, u32x4_t* out) {

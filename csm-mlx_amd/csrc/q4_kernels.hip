@@ -8,6 +8,7 @@
 // is common.h's q4 layout.
 #include <climits>
 
+#include "../../include/csm_hip_prof.h"
 #include "csm_kernels.h"
 #include "xs.h"
 
@@ -225,7 +226,9 @@ __global__ __launch_bounds__(256) void gemv_q4_kernel(GemvParams p) {
   uint32_t sb[KS][RPT];
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
-    const int k = gt * 32 + s * G * 32;
+    // K need not fill the group's G x 32 span (K = 1280: G = 64, lanes gt >= 40 idle): a lane past K
+    // holds zero weights and skips its dot products
+    const int k = min(gt * 32 + s * G * 32, K - 32);
 #pragma unroll
     for (int r = 0; r < RPT; ++r) {
       const size_t row = (size_t)min(row0 + r, p.N - 1);  // partial last block: re-read a valid row
@@ -304,6 +307,7 @@ __global__ __launch_bounds__(256) void gemv_q4_kernel(GemvParams p) {
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       const int k = gt * 32 + s * G * 32;
+      if (k >= K) continue;  // (idle lane of a K that does not fill the span)
       float qf[RPT][32];
 #pragma unroll
       for (int r = 0; r < RPT; ++r) {
@@ -437,14 +441,12 @@ __global__ __launch_bounds__(256) void gemv_q4_kernel(GemvParams p) {
   }
 }
 
-// Tiling: one K step per thread (G = K / 32, capped at 256; K = 8192 runs G = 256); RPT = 2.
+// Tiling: one K step per thread (G = K / 32 rounded up to a power of two >= 8, capped at 256; K = 8192
+// runs G = 256; K = 1280 runs G = 64 with lanes 40..63 of each group idle); RPT = 2.
 static void q4_tiling(int K, int& G, int& KS) {
-  G = K / 32;
-  KS = 1;
-  if (G > 256) {
-    KS = G / 256;
-    G = 256;
-  }
+  G = 8;
+  while (G < K / 32 && G < 256) G *= 2;
+  KS = (K / 32 + G - 1) / G;
 }
 
 int gemv_q4_rows_per_block(int N, int K, int M) {
@@ -459,8 +461,15 @@ int gemv_q4_rows_per_block(int N, int K, int M) {
 bool gemv_q4_supported(int N, int K) {
   int G, KS;
   q4_tiling(K, G, KS);
-  return K % Q4_GROUP == 0 && N % 2 == 0 && (G == 8 || G == 16 || G == 32 || G == 64 || G == 128 || G == 256) &&
-         KS == 1;
+  return K % Q4_GROUP == 0 && K >= Q4_GROUP && N % 2 == 0 && KS == 1;
+}
+
+extern "C" int csm_q4_gemv_shape(int N, int K, int* out) {
+  if (K <= 0 || N <= 0) return 0;
+  int G, KS;
+  q4_tiling(K, G, KS);
+  out[0] = G; out[1] = KS; out[2] = (256 / G) * 2;
+  return gemv_q4_supported(N, K) ? 1 : 0;
 }
 
 template <int G, bool NT>

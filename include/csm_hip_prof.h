@@ -52,10 +52,15 @@ int csm_bench_bb_step(csm_engine* e, int iters, float* avg_us, double* bytes);
 int csm_set_option(csm_engine* e, const char* key, int value);
 
 /* Launch geometry the streaming matrix-core GEMM (gemm_xs.hip) would use for an (N, K) projection at M
- * rows (head != 0: an arg-max / SiLU launch): out[4] = {weight-row tiles of 32 per block, K slices,
- * ring depth, waves per block}.  Returns 1 if the shape is eligible (every 64-deep K stage falls on
- * exactly one wave of one slice), else 0.  Host-only (no device call). */
-int csm_xs_shape(int N, int K, int M, int head, int* out);
+ * rows (head != 0: an arg-max / SiLU launch) with weights of dtype wdt (CSM_BF16 or CSM_Q4): out[4] =
+ * {weight-row tiles of 32 per block, K slices, ring depth, waves per block}.  Returns 1 if the shape is
+ * eligible for that dtype (every 64-deep K stage falls on exactly one wave of one slice; int4: at most
+ * Q4_XG stages per slice), else 0.  Host-only (no device call). */
+int csm_xs_shape(int N, int K, int M, int head, int wdt, int* out);
+
+/* The int4 GEMV's tiling for an [N][K] matrix (q4_kernels.hip): out[3] = {threads per row group G, K
+ * steps per thread, rows per 256-thread block}.  Returns 1 if the shape is supported, else 0.  Host-only. */
+int csm_q4_gemv_shape(int N, int K, int* out);
 
 /* The matrix-core GEMMs' int4 -> bf16 expansion (xs.h q4_word_bf16) of n uint32 words of MLX nibbles, on
  * the current device: out[4 n] = the bf16 pairs (low half first) of the nibbles in order.  Test hook

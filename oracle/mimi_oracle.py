@@ -205,13 +205,40 @@ class OracleMimi:
         dot = np.matmul(x_btd, cb.T).astype(F32)
         return np.argmin(c2 - dot, axis=-1)
 
-    def rvq_encode(self, q, x_bct, cbs):
+    @staticmethod
+    def vq_margin(x_btd, cb, ref_norm=None):
+        """Sensitivity margin of the nearest-code choice (test bookkeeping, not part of the codec): with
+        d_j = |c_j|^2/2 - x.c_j, best j1 and runner-up j2, (d_j2 - d_j1) / (|h| |c_j1 - c_j2|), |h| =
+        ref_norm (the quantizer's projected latent at that frame; default |x|).  Perturbing the latent by
+        delta moves the gap by at most |delta| |c_j1 - c_j2|, so a choice can flip under another summation
+        order of the latent only where this is below that order's relative error |delta| / |h|.
+        Returns (margin (B,T), runner-up index (B,T))."""
+        d = ((cb * cb).sum(-1, dtype=F32) / F32(2) - np.matmul(x_btd, cb.T).astype(F32)).astype(np.float64)
+        order = np.argsort(d, axis=-1, kind="stable")
+        j1, j2 = order[..., 0], order[..., 1]
+        gap = np.take_along_axis(d, j2[..., None], -1)[..., 0] - np.take_along_axis(d, j1[..., None], -1)[..., 0]
+        hn = np.linalg.norm(x_btd.astype(np.float64), axis=-1) if ref_norm is None else ref_norm
+        den = hn * np.linalg.norm(cb[j1].astype(np.float64) - cb[j2].astype(np.float64), axis=-1)
+        return gap / np.maximum(den, 1e-30), j2
+
+    def rvq_encode(self, q, x_bct, cbs, margins=None, force=None):
+        """margins: a list that receives each codebook's (margin, runner-up) (vq_margin); force: {(b, t, k)}
+        of codes to take as the runner-up instead of the nearest code (the other outcome of a near-tie,
+        for the parity tests' variant prompts); the residual chain then continues from that choice."""
         w = self.w
         h = np.matmul(w[f"quantizer.{q}.input_proj.weight"][:, :, 0], x_bct).astype(F32)   # (B,cd,T)
         r = h.transpose(0, 2, 1).copy()
+        hn = np.linalg.norm(r.astype(np.float64), axis=-1)
         codes = []
-        for cb in cbs:
+        for k, cb in enumerate(cbs):
             idx = self.vq_encode(r, cb)
+            if margins is not None or force:
+                mg, j2 = self.vq_margin(r, cb, hn)
+                if margins is not None:
+                    margins.append((mg, j2))
+                for (b, t, kk) in (force or ()):
+                    if kk == k:
+                        idx[b, t] = j2[b, t]
             r = (r - cb[idx]).astype(F32)
             codes.append(idx)
         return np.stack(codes, axis=1).astype(np.int32)                                      # (B,nq,T)
@@ -234,15 +261,20 @@ class OracleMimi:
                                 self.m.downsample_stride, groups=x.shape[1])
 
     # ------------------------------------------------------------------ public
-    def encode(self, pcm_b1n: np.ndarray) -> np.ndarray:
-        """Mimi.encode: (B,1,N) -> (B,n_q,Tf) int32."""
+    def encode(self, pcm_b1n: np.ndarray, with_margins: bool = False, force=()) -> np.ndarray:
+        """Mimi.encode: (B,1,N) -> (B,n_q,Tf) int32.  with_margins: also return each code's RVQ margin
+        (B,n_q,Tf) (vq_margin); force: codes (b, codebook, t) taken as the runner-up (rvq_encode)."""
         x = self._seanet(self.enc_layout, pcm_b1n.astype(F32))
         x = self.enc_tr(x, self.enc_tr.new_cache())
         x = conv1d(x, self.w["downsample.conv.conv.conv.weight"], None, self.m.downsample_stride, 1, "replicate")
         self.debug_latent = x
-        sem = self.rvq_encode("rvq_first", x, self.cb_first)
-        ac = self.rvq_encode("rvq_rest", x, self.cb_rest)
-        return np.concatenate([sem, ac], axis=1)
+        ms = [] if with_margins else None
+        sem = self.rvq_encode("rvq_first", x, self.cb_first, ms, {(b, t, 0) for b, k, t in force if k == 0})
+        ac = self.rvq_encode("rvq_rest", x, self.cb_rest, ms, {(b, t, k - 1) for b, k, t in force if k > 0})
+        codes = np.concatenate([sem, ac], axis=1)
+        if with_margins:
+            return codes, np.stack([m for m, _ in ms], axis=1)
+        return codes
 
     def decode(self, codes_bkf: np.ndarray) -> np.ndarray:
         """Mimi.decode: (B,n_q,F) -> (B,1,F*frame_size)."""
@@ -256,20 +288,28 @@ class OracleMimi:
         self._hist = None
         self._emitted = 0
 
-    def decode_step(self, codes_bk1: np.ndarray) -> np.ndarray:
+    def decode_step(self, codes_bk1: np.ndarray, window: int = 0) -> np.ndarray:
         """Mimi.decode_step on one frame (B,n_q,1) -> (B,1,frame_size).
 
         The causal convs (upsample, SEANet) are evaluated on the whole history,
         which equals their streaming state machine exactly; the transformer keeps
-        a real KV cache so the "mlx" attention mode sees the keys streaming sees."""
+        a real KV cache so the "mlx" attention mode sees the keys streaming sees.
+        window > 0: the SEANet decoder runs on the last `window` frames of history
+        only (its receptive field is < 5 frames, so for window >= 8 the new frame's
+        samples are the same values up to BLAS summation order -- checked in
+        tests/test_oracle_cpu.py); linear instead of quadratic in the frames."""
         q = self.quantizer_decode(codes_bk1)
         self._qhist = q if self._qhist is None else np.concatenate([self._qhist, q], axis=2)
         s = self.m.downsample_stride
-        new = self.upsample(self._qhist)[:, :, -s:]
+        new = self.upsample(self._qhist[:, :, -2:])[:, :, -s:]   # (depthwise k = 2 s: the last two frames)
         y = self.dec_tr(new, self._tr_cache)
         self._hist = y if self._hist is None else np.concatenate([self._hist, y], axis=2)
-        pcm = self._seanet(self.dec_layout, self._hist)
         fs = self.m.frame_size
-        out = pcm[:, :, self._emitted: self._emitted + fs]
+        if window > 0:
+            pcm = self._seanet(self.dec_layout, self._hist[:, :, -window * s:])
+            out = pcm[:, :, -fs:]
+        else:
+            pcm = self._seanet(self.dec_layout, self._hist)
+            out = pcm[:, :, self._emitted: self._emitted + fs]
         self._emitted += fs
         return out

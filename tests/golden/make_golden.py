@@ -191,9 +191,9 @@ def config4_b32_golden():
     return out
 
 
-def config3_b32_golden(frames=64):
+def config3_b32_golden(frames=125):
     """configs[2]: B = 32, temperature 0.8, top-k 50 (the oracle's restatement of the engine's counter-based
-    RNG), 32 frames; the Mimi oracle's streaming decode_step of every frame: per (utterance, frame) RMS,
+    RNG), all 125 frames; the Mimi oracle's streaming decode_step of every frame: per (utterance, frame) RMS,
     mean and B32_PROJ projections on seeded unit vectors, and whole chunks: utterance 0's first 8 and
     each ending utterance's last 4 before its EOS."""
     from csm_mlx.weights import synthetic_mimi_weights
@@ -208,7 +208,7 @@ def config3_b32_golden(frames=64):
     rms, mean, proj = [], [], []
     pcm = {b: [] for b in keep}
     for f in range(frames):
-        y = om.decode_step(np.ascontiguousarray(codes[:, f, :, None]))[:, 0].astype(np.float64)   # (32, 1920)
+        y = om.decode_step(np.ascontiguousarray(codes[:, f, :, None]), window=12)[:, 0].astype(np.float64)  # (32, 1920)
         rms.append(np.sqrt(np.mean(y ** 2, axis=1)))
         mean.append(y.mean(axis=1))
         proj.append(y @ vec.T)
@@ -226,63 +226,153 @@ def config3_b32_golden(frames=64):
     return out
 
 
-C5_UTTS = 8                         # configs[4] utterances pinned at full length (of the GPU test's B = 64)
-C5_LOGIT_FRAMES = (0, 64, 124)      # frames whose c0 / ci logits are kept, for utterances 0 and C5_UTTS - 1
+C5_UTTS = tuple(range(8)) + tuple(range(56, 64))   # configs[4] utterances pinned at full length (of the GPU
+#                     test's B = 64): both 32-row tiles of the 64-row int4 GEMMs
+C5_LOGIT_FRAMES = (0, 64, 124)      # frames whose c0 / ci logits are kept, for the first and last pinned utterance
 C5_CI = (1, 16, 31)
+RVQ_TIE = 3e-6                      # RVQ margin (oracle vq_margin: gap / (|latent| |c1 - c2|)) below which a context
+#                                     code is a near-tie: the fixture carries the oracle's other outcome (a variant
+#                                     prompt) and its frames.  The oracle's own latents move by 1.2-1.4e-6 (relative)
+#                                     between two BLAS call shapes (one segment vs 24 per call), so a margin this small
+#                                     is decided by summation order, not by the codec
+RVQ_LIST = 1e-5                     # context codes with a margin below this are listed in the fixture (report)
 
 
-def config5_q4_prompts(utts=C5_UTTS):
-    """configs[4]'s prompts for utterances 0 .. utts-1 (bench.py context_prompts): 3 context Segments (speaker
-    seg % 2, 12 text ids, 5 s of bench.context_audio Mimi-encoded -- here by the codec oracle, whose codes the
-    GPU encode matches bit for bit, tests/test_mimi_gpu.py) + the 12-id text row."""
+def config5_q4_contexts(utts=C5_UTTS):
+    """configs[4]'s context codes for utterances `utts` (bench.py context_segments: 3 Segments, 5 s of
+    bench.context_audio each) by the codec oracle, with every code's RVQ margin (OracleMimi.vq_margin).
+    Returns codes (U, 3, 32, 63), margins (U, 3, 32, 63)."""
     import bench
-    from bench import prompt_ids
-    from csm_mlx.tokenizers import audio_codes_to_frames, tokenize_text_segment
     m = MIMI_CONFIGURATION["mimi_202407"]
     om = OracleMimi(m, synthetic_mimi_weights(m, 0))
-    prompts = []
-    for g in range(utts):
-        parts = []
-        for seg in range(3):
-            parts.append(tokenize_text_segment(prompt_ids(10_000 + 10 * g + seg), seg % 2, 32))
-            parts.append(audio_codes_to_frames(om.encode(bench.context_audio(g, seg)[None, None])[0]))
-        parts.append(tokenize_text_segment(prompt_ids(g), 0, 32))
-        prompts.append((np.concatenate([t for t, _ in parts]).astype(np.int32), np.concatenate([mm for _, mm in parts])))
-        print("prompt", g, prompts[-1][0].shape, flush=True)
-    return prompts
+    # one segment per encode call (a variant prompt re-encodes its segment alone: the same BLAS call shapes, so
+    # the same latents bit for bit)
+    pcm = np.stack([bench.context_audio(g, seg) for g in utts for seg in range(3)])[:, None]
+    codes, mg = [], []
+    for i in range(len(pcm)):
+        c, mm = om.encode(pcm[i:i + 1], with_margins=True)
+        codes.append(c)
+        mg.append(mm)
+    print("encoded", len(pcm), "segments", flush=True)
+    U = len(utts)
+    codes = np.concatenate(codes).reshape(U, 3, 32, -1)
+    return codes, np.concatenate(mg).reshape(U, 3, 32, -1), om
 
 
-def config5_q4_golden(utts=C5_UTTS, frames=125):
-    """configs[4] at full length for its first 8 utterances: int4 group-64 weights (nn.quantize of the seed-0
-    weights; the oracle on the dequantized weights), the Mimi-encoded 3-segment contexts (248 rows), 125 greedy
-    frames.  Codes, frame counts, the prompts, and c0 / ci logit slices at C5_LOGIT_FRAMES for the first and
-    last utterance."""
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    from helpers import csm_weights, oracle_batch, oracle_for
-    prompts = config5_q4_prompts(utts)
-    args, w = csm_weights("1b")
-    ref = oracle_batch(oracle_for(args, w, q4=True), prompts, frames, collect_logits=True)
-    n = np.array([r[0].shape[0] for r in ref], np.int32)
-    print("n_frames", n.tolist(), flush=True)
-    codes = np.zeros((utts, frames, 32), np.int32)
+def config5_q4_prompt(g, seg_codes):
+    """One configs[4] prompt (bench.py context_prompts): per context Segment the text row of 12 ids (speaker
+    seg % 2) and its audio frames (tokenize_audio: codes + the EOS zero frame), then the utterance's text."""
+    from bench import prompt_ids
+    from csm_mlx.tokenizers import audio_codes_to_frames, tokenize_text_segment
+    parts = []
+    for seg in range(3):
+        parts.append(tokenize_text_segment(prompt_ids(10_000 + 10 * g + seg), seg % 2, 32))
+        parts.append(audio_codes_to_frames(seg_codes[seg]))
+    parts.append(tokenize_text_segment(prompt_ids(g), 0, 32))
+    return np.concatenate([t for t, _ in parts]).astype(np.int32), np.concatenate([mm for _, mm in parts])
+
+
+def _margins(ref):
+    """The oracle's top-2 logit margin of every code, relative to max|logit| (U, F, 32): where it is at fp32
+    resolution (~1e-7) another summation order may pick the other code."""
+    F = max(r[0].shape[0] for r in ref)
+    margin = np.ones((len(ref), F, 32), np.float32)
     for b, r in enumerate(ref):
-        codes[b, :n[b]] = r[0]
-    # the oracle's own top-2 margin of every code (relative to max|logit|): where it is at fp32 resolution
-    # (~1e-6) another summation order may pick the other code, and the GPU test says so instead of failing
-    margin = np.ones((utts, frames, 32), np.float32)
-    for b, r in enumerate(ref):
-        for f in range(n[b]):
+        for f in range(r[0].shape[0]):
             lg = [r[1][f][0]] + [r[1][f][1][k] for k in range(31)]
             for k, l in enumerate(lg):
                 top = np.sort(l)[-2:]
                 margin[b, f, k] = (top[1] - top[0]) / max(float(np.abs(l).max()), 1e-30)
-    print("codes with a relative top-2 margin < 1e-5:", int((margin < 1e-5).sum()), flush=True)
-    keep = [0, utts - 1]
+    return margin
+
+
+def config5_q4_golden(utts=C5_UTTS, frames=125):
+    """configs[4] at full length for 16 of its 64 utterances (0-7 and 56-63: both 32-row tiles of the batched
+    int4 GEMMs): int4 group-64 weights (nn.quantize of the seed-0 weights; the oracle on the dequantized weights),
+    the Mimi-encoded 3-segment contexts (248 rows), 125 greedy frames.  Stored: the prompts, the context codes'
+    RVQ near-ties (margin < RVQ_LIST: utterance, segment, codebook, frame, margin), codes, frame counts, every
+    code's top-2 logit margin, c0 / ci logit slices at C5_LOGIT_FRAMES for the first and last utterance; and for
+    every context code with an RVQ margin below RVQ_TIE the oracle's OTHER outcome -- the runner-up code there, the
+    residual chain continued from it (OracleMimi.encode force=) -- as a variant prompt with its own 125 frames and
+    margins, so a GPU encode that takes the other side of such a tie is still checked frame for frame."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from helpers import csm_weights, oracle_batch, oracle_for
+    import bench
+    ctx, cmg, om = config5_q4_contexts(utts)
+    prompts = [config5_q4_prompt(g, ctx[u]) for u, g in enumerate(utts)]
+    near = np.argwhere(cmg < RVQ_LIST)
+    ties = [tuple(int(v) for v in x) for x in np.argwhere(cmg < RVQ_TIE)]           # (u, seg, k, t)
+    print("context codes below RVQ_LIST:", len(near), "below RVQ_TIE:", ties, flush=True)
+    var_prompts, var_meta = [], []
+    for (u, seg, k, t) in ties:
+        g = utts[u]
+        vc = om.encode(bench.context_audio(g, seg)[None, None], force=[(0, k, t)])[0]
+        assert (vc != ctx[u, seg]).any(), "the forced runner-up changed nothing"
+        sc = [ctx[u, s] if s != seg else vc for s in range(3)]
+        var_prompts.append(config5_q4_prompt(g, sc))
+        var_meta.append((u, seg, k, t))
+    args, w = csm_weights("1b")
+    o = oracle_for(args, w, q4=True)
+    ref = oracle_batch(o, prompts + var_prompts, frames, collect_logits=True)
+    n = np.array([r[0].shape[0] for r in ref], np.int32)
+    print("n_frames", n.tolist(), flush=True)
+    codes = np.zeros((len(ref), frames, 32), np.int32)
+    for b, r in enumerate(ref):
+        codes[b, :n[b]] = r[0]
+    margin = _margins(ref)
+    U = len(utts)
+    print("codes with a relative top-2 margin < 1e-5:", [tuple(int(v) for v in x) for x in np.argwhere(margin < 1e-5)],
+          flush=True)
+    keep = [0, U - 1]
     c0 = np.stack([[ref[b][1][f][0] for f in C5_LOGIT_FRAMES] for b in keep])                     # (2, 3, V)
     ci = np.stack([[ref[b][1][f][1][[c - 1 for c in C5_CI]] for f in C5_LOGIT_FRAMES] for b in keep])  # (2, 3, 3, V)
-    return dict(codes=codes, n_frames=n, tokens=np.stack([t for t, _ in prompts]),
-                masks=np.stack([m for _, m in prompts]), logit_utts=np.array(keep, np.int32),
-                frames=np.array(C5_LOGIT_FRAMES), ci_codebooks=np.array(C5_CI), c0=c0, ci=ci, margin=margin)
+    nv = len(var_prompts)
+    return dict(utts=np.array(utts, np.int32), codes=codes[:U], n_frames=n[:U],
+                tokens=np.stack([t for t, _ in prompts]), masks=np.stack([m for _, m in prompts]),
+                logit_utts=np.array(keep, np.int32), frames=np.array(C5_LOGIT_FRAMES), ci_codebooks=np.array(C5_CI),
+                c0=c0, ci=ci, margin=margin[:U],
+                rvq_near=near.astype(np.int32).reshape(-1, 4),
+                rvq_near_margin=cmg[tuple(near.T)].astype(np.float64) if len(near) else np.zeros(0),
+                rvq_tie=np.array(RVQ_TIE), var_of=np.array(var_meta, np.int32).reshape(nv, 4),
+                var_margin=np.array([cmg[x] for x in var_meta], np.float64),
+                var_tokens=np.stack([t for t, _ in var_prompts]) if nv else np.zeros((0,) + prompts[0][0].shape, np.int32),
+                var_codes=codes[U:], var_n_frames=n[U:], var_frame_margin=margin[U:])
+
+
+def csm_1b_q4_stream_golden(frames=125):
+    """The reference demo's path (run_streaming_csm_mlx.py:811-818, :844-852: nn.quantize(model, 64, 4), then
+    stream_generate) at configs[1]'s utterance, greedy: csm_1b int4 g64 B = 1, 125 frames, the oracle on the
+    dequantized weights; codes, every code's top-2 logit margin, c0 / ci logit slices at C5_LOGIT_FRAMES, and
+    per frame the Mimi oracle's streaming decode_step chunk (RMS, mean, 4 projections; the first 8 and last 4
+    chunks whole)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from helpers import csm_weights, oracle_for
+    from csm_mlx.models import csm_1b  # noqa: F401
+    args, w = csm_weights("1b")
+    o = oracle_for(args, w, q4=True)
+    codes, logs = o.generate_codes(*text_frame(CONFIG1_IDS, 32), frames, collect_logits=True)
+    margin = _margins([(codes, logs)])[0]
+    print("q4 B=1 codes", codes.shape, "margins < 1e-5:", [tuple(int(v) for v in x) for x in np.argwhere(margin < 1e-5)],
+          flush=True)
+    m = MIMI_CONFIGURATION["mimi_202407"]
+    om = OracleMimi(m, synthetic_mimi_weights(m, 0))
+    om.reset_state()
+    vec = np.random.default_rng(5).standard_normal((B32_PROJ, 1920))
+    vec /= np.linalg.norm(vec, axis=1, keepdims=True)
+    rms, mean, proj, whole = [], [], [], {}
+    F = codes.shape[0]
+    for f in range(F):
+        y = om.decode_step(np.ascontiguousarray(codes[None, f, :, None]), window=12)[0, 0].astype(np.float64)
+        rms.append(np.sqrt(np.mean(y ** 2)))
+        mean.append(y.mean())
+        proj.append(y @ vec.T)
+        if f < 8 or f >= F - 4:
+            whole[f] = y.astype(np.float32)
+    return dict(ids=np.array(CONFIG1_IDS, np.int32), codes=codes, margin=margin, frames=np.array(C5_LOGIT_FRAMES),
+                ci_codebooks=np.array(C5_CI), c0=np.stack([logs[f][0] for f in C5_LOGIT_FRAMES]),
+                ci=np.stack([logs[f][1][[c - 1 for c in C5_CI]] for f in C5_LOGIT_FRAMES]),
+                rms=np.array(rms), mean=np.array(mean), proj=np.stack(proj), proj_vec=vec,
+                pcm_frames=np.array(sorted(whole), np.int32), pcm=np.stack([whole[f] for f in sorted(whole)]))
 
 
 FIXTURES = {
@@ -292,8 +382,9 @@ FIXTURES = {
     "csm_1b_greedy_125.npz": csm_1b_long_golden,
     "config0_plumbing.npz": config0_golden,
     "config4_b32_greedy_125.npz": config4_b32_golden,
-    "config3_b32_stream_64.npz": config3_b32_golden,
-    "config5_q4_b8_greedy_125.npz": config5_q4_golden,
+    "config3_b32_stream_125.npz": config3_b32_golden,
+    "config5_q4_b16_greedy_125.npz": config5_q4_golden,
+    "csm_1b_q4_stream_125.npz": csm_1b_q4_stream_golden,
 }
 
 if __name__ == "__main__":

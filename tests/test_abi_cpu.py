@@ -153,26 +153,59 @@ def test_weights_loading_rejects_bad_shapes_without_gpu():
         m.load_weights({"projection.weight": np.zeros((3, 3), np.float32)})
 
 
-def test_xs_shape_covers_every_stage():
+Q4_XG = 64   # gemm_xs.hip: stages of 64 one int4 block's X_g table holds
+
+
+@pytest.mark.parametrize("wdt", ["bf16", "q4"])
+def test_xs_shape_covers_every_stage(wdt):
     """gemm_xs launch geometry (host code, no GPU): every eligible shape gives each wave of each K slice
     the same whole number of 64-deep stages, so none is dropped -- K = 640 (10 stages) and 1280 (20)
-    included, which once picked 4 / 8 waves and silently skipped 2 / 4 stages."""
+    included, which once picked 4 / 8 waves and silently skipped 2 / 4 stages; int4 slices also hold at
+    most Q4_XG stages (the X_g table).  Every csm_1b / tiny_f1280 projection the batched decoder runs is
+    eligible in both dtypes."""
     import ctypes
     from csm_mlx import _lib
     L = _lib.lib()
+    code = {"bf16": 1, "q4": 2}[wdt]        # include/csm_hip.h csm_dtype
     out = (ctypes.c_int * 4)()
     seen = 0
     for K in range(128, 8192 + 1, 64):
         for N in (256, 1024, 1536, 2056, 16384):
             for M in (8, 32, 64):
                 for head in (0, 1):
-                    ok = L.csm_xs_shape(N, K, M, head, out)
+                    ok = L.csm_xs_shape(N, K, M, head, code, out)
                     rtw, ks, pd, xw = list(out)
                     nks = K // 64
                     if ok:
                         seen += 1
                         assert nks % ks == 0 and (nks // ks) % xw == 0 and xw in (2, 4, 8), (N, K, M, head, list(out))
                         assert (nks // ks // xw) % pd == 0
+                        if wdt == "q4":
+                            assert nks // ks <= Q4_XG, (N, K, M, head, list(out))
     assert seen > 0
     out640 = (ctypes.c_int * 4)()
-    assert L.csm_xs_shape(1024, 640, 32, 0, out640) == 1 and (10 // out640[1]) % out640[3] == 0
+    assert L.csm_xs_shape(1024, 640, 32, 0, code, out640) == 1 and (10 // out640[1]) % out640[3] == 0
+    # the decoder projections (QKV, o, gate/up, down) of csm_1b (D 1024, F 8192) and tiny_f1280 (D 256,
+    # F 1280, QKV 4 x 128 rows)
+    for D, F, qkv in ((1024, 8192, 1536), (256, 1280, 512)):
+        for N, K, head in ((qkv, D, 0), (D, D, 0), (2 * F, D, 1), (D, F, 0)):
+            for M in (8, 32, 64):
+                assert L.csm_xs_shape(N, K, M, head, code, out) == 1, (wdt, N, K, M, head)
+    assert L.csm_xs_shape(1024, 1024, 32, 0, 0, out) == 0      # fp32 weights never take the streaming GEMM
+
+
+def test_q4_gemv_shapes():
+    """The int4 GEMV's tiling (host code): every K that is a multiple of 64 up to 8192 is supported -- a K
+    whose 32-wide steps are not a power of two (1280: 40 steps) runs a 64-lane group with the tail lanes
+    idle -- and each lane covers at most one 32-wide step."""
+    import ctypes
+    from csm_mlx import _lib
+    L = _lib.lib()
+    out = (ctypes.c_int * 3)()
+    for K in range(64, 8192 + 1, 64):
+        assert L.csm_q4_gemv_shape(1024, K, out) == 1, K
+        G, KS, rpb = list(out)
+        assert KS == 1 and G * 32 >= K and (G == 8 or G * 16 < K) and rpb == 512 // G, (K, list(out))
+    assert L.csm_q4_gemv_shape(1024, 1280, out) == 1 and list(out) == [64, 1, 8]
+    assert L.csm_q4_gemv_shape(1023, 1024, out) == 0            # the pair epilogue needs even N
+    assert L.csm_q4_gemv_shape(1024, 96, out) == 0              # K a multiple of the group

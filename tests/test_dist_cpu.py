@@ -184,7 +184,7 @@ def _report_worker(rank, world, port, q):
     import bench
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    rep = bench.rank_report(125.0 * (rank + 1), 2.0 + rank, 4, world, device_index=rank % 1)
+    rep = bench.rank_report(125.0 * (rank + 1), 2.0 + rank, 4, world, device_index=rank % 1, gather_s=0.1 * (rank + 1))
     q.put((rank, rep))
     dist.destroy_process_group()
 
@@ -205,5 +205,67 @@ def test_rank_report_world2():
         assert rep["backend"] == "gloo" and rep["world_size_seen"] == 2
         assert [r["rank"] for r in rep["ranks"]] == [0, 1]
         assert [r["ms_per_step"] for r in rep["ranks"]] == [500.0, 750.0]
+        assert [r["gather_ms_per_step"] for r in rep["ranks"]] == [25.0, 50.0]
+        assert [r["generate_ms_per_step"] for r in rep["ranks"]] == [475.0, 700.0]
         assert [r["frames"] for r in rep["ranks"]] == [125, 250]
-        assert rep["slowest_rank"] == 1
+        assert rep["slowest_rank"] == 1 and rep["max_gather_ms_per_step"] == 50.0
+
+
+def _c4_worker(rank, world, port, q):
+    """configs[3] at its real shape on one rank: 32 of the 256 utterances (bench.shard), 125 frames x 32 codes
+    and 125 x 1920 PCM samples each (30.7 MB of PCM per rank), ragged by a per-utterance EOS, gathered to
+    rank 0 with bench.py's call; returns rank 0's result checks and this rank's gather seconds."""
+    import sys
+    import time
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, "csm-mlx_amd"), root]
+    import numpy as np
+    import torch.distributed as dist
+    import bench
+    from csm_mlx.dist import gather_results
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    mine = bench.shard(256, world, rank)
+    assert len(mine) == 32
+    F, S = 125, bench.FRAME_SAMPLES
+    nf = [F - (g * 7) % 40 if g % 5 == 0 else F for g in mine]                   # some utterances end early
+    codes = [(np.arange(n * 32, dtype=np.int32).reshape(n, 32) + g) % 2051 for g, n in zip(mine, nf)]
+    pcm = [np.full(n * S, g / 256.0, np.float32) for g, n in zip(mine, nf)]
+    dist.barrier()
+    t0 = time.perf_counter()
+    c_all, p_all = gather_results(codes, pcm, F, S, dst=0)
+    dt = time.perf_counter() - t0
+    ok = None
+    if rank == 0:
+        ok = len(c_all) == len(p_all) == 256
+        for g in range(256):
+            n = F - (g * 7) % 40 if g % 5 == 0 else F
+            ok = ok and c_all[g].shape == (n, 32) and int(c_all[g][0, 0]) == g % 2051
+            ok = ok and p_all[g].shape == (n * S,) and float(p_all[g][-1]) == g / 256.0
+    rep = bench.rank_report(float(sum(nf)), 1.0, 1, world, rank, gather_s=dt)
+    q.put((rank, ok, c_all is None, dt, rep))
+    dist.destroy_process_group()
+
+
+def test_config4_shape_gather_world8():
+    """bench.py's 8-rank result path at configs[3]'s shape, over gloo on CPU: B = 256 sharded 32 per rank
+    (contiguous, every utterance once), each rank's 32 ragged code + PCM results (30.7 MB PCM) gathered to
+    rank 0 in global utterance order (245.8 MB into rank 0), nothing back on the others, and each rank's
+    dist entry carrying its gather time apart from generation.  The GPU run moves the same bytes by RCCL."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_c4_worker, args=(r, 8, port, q)) for r in range(8)]
+    for p in ps:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in ps], key=lambda r: r[0])
+    for p in ps:
+        p.join(60)
+    assert res[0][1] is True
+    assert all(none for _, _, none, _, _ in res[1:])
+    rep = res[0][4]
+    assert rep["world_size_seen"] == 8 and [r["rank"] for r in rep["ranks"]] == list(range(8))
+    for r, (_, _, _, dt, _) in zip(rep["ranks"], res):
+        assert abs(r["gather_ms_per_step"] - dt * 1000.0) < 1e-3 and r["gather_ms_per_step"] > 0
+        assert abs(r["generate_ms_per_step"] + r["gather_ms_per_step"] - 1000.0) < 1e-3
+    print("gloo gather of configs[3]'s results to rank 0, ms per rank:", [r["gather_ms_per_step"] for r in rep["ranks"]])

@@ -68,12 +68,13 @@ def test_tiny_bf16_batched_mfma(B):
     _batch_vs_oracle(args, w, id_sets, 6, 2e-3)
 
 
-@pytest.mark.parametrize("dtype", ["bf16"])   # (the int4 GEMV of step 1 takes no 1280-wide MLP)
+@pytest.mark.parametrize("dtype", ["bf16", "q4"])
 def test_tiny_f1280_streaming_gemm_stage_coverage(dtype):
     """A decoder MLP of width 1280 (the engine takes multiples of 256): the streaming GEMM's down
     projection has K = 1280 = 20 stages of 64, which an 8-wave block does not divide (the shape rule now
     picks 4 waves; the 8-wave block once skipped 4 of the 20 stages).  B = 8 greedy, 5 frames, bit-exact
-    against the oracle."""
+    against the oracle.  q4: the int4 GEMV (decoder step 1's rows, the head at B = 1) also takes K = 1280
+    (a 64-lane group with lanes 40..63 idle; round 5 refused the shape)."""
     import dataclasses
     from csm_mlx.models import csm_tiny
     from csm_mlx.weights import synthetic_csm_weights

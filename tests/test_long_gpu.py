@@ -117,3 +117,45 @@ def test_config0_generate_plumbing():
     rms = float(np.sqrt(np.mean((audio.astype(np.float64) - ref) ** 2)))
     assert rms <= 1e-4, f"waveform RMS error {rms:.3e}"
     del model
+
+
+def test_csm_1b_q4_stream_generate_125_frames():
+    """The reference demo's path (run_streaming_csm_mlx.py:811-818, :844-852): nn.quantize(model, 64, 4), then
+    stream_generate -- here csm_1b int4 g64 at B = 1, configs[1]'s utterance, greedy, 10 s -- against
+    tests/golden/csm_1b_q4_stream_125.npz (the oracle on the dequantized weights + the Mimi oracle's decode_step):
+    codes bit-exact over all 125 frames (the fixture stores every code's top-2 margin; none may part), c0 / ci
+    logits at frames 0 / 64 / 124 within 1e-3 x max|logit| (read from a frame-loop run of the same engine),
+    every streamed chunk's RMS / mean / projections within what 1e-4 RMS allows, whole chunks <= 1e-4 RMS."""
+    from csm_mlx import nn, stream_generate
+    from csm_mlx.config import MIMI_CONFIGURATION
+    from csm_mlx.mimi import MimiCodec
+    from csm_mlx.tokenizers import set_audio_tokenizer, tokenize_text_segment
+    from csm_mlx.weights import synthetic_mimi_weights
+    z = _fixture("csm_1b_q4_stream_125.npz")
+    from csm_mlx.models import CSM
+    args, w = csm_weights("1b")
+    model = CSM(args, dtype="bf16", max_batch=1)
+    nn.quantize(model, group_size=64, bits=4)      # before the load: the fp32 weights quantize on the device,
+    model.load_weights(w)                          # as the oracle's quantize -> dequantize of the same weights
+    mc = MIMI_CONFIGURATION["mimi_202407"]
+    codec = MimiCodec(mc, max_batch=1)
+    codec.load_weights(synthetic_mimi_weights(mc, 0))
+    set_audio_tokenizer(codec, 32)
+    ids = z["ids"].tolist()
+    chunks = [np.asarray(c, np.float32) for c in stream_generate(model, ids, 0, [], 10_000, temperature=0.0)]
+    t, m = tokenize_text_segment(ids, 0, 32)
+    codes, c0, ci = _run_collect(model, t, m, 125, set(z["frames"].tolist()), z["ci_codebooks"].tolist())
+    del model
+    _check(codes, c0, ci, z["codes"], z["c0"], z["ci"], 1e-3)
+    assert len(chunks) == len(z["codes"]) == 125
+    bad = []
+    for f, y in enumerate(chunks):
+        y = y.astype(np.float64)
+        if abs(np.sqrt(np.mean(y ** 2)) - z["rms"][f]) > 1e-4 or abs(y.mean() - z["mean"][f]) > 1e-4 or \
+                np.abs(y @ z["proj_vec"].T - z["proj"][f]).max() > 1e-4 * np.sqrt(1920):
+            bad.append(f)
+    for f, ref in zip(z["pcm_frames"], z["pcm"]):
+        err = float(np.sqrt(np.mean((chunks[int(f)].astype(np.float64) - ref) ** 2)))
+        if err > 1e-4:
+            bad.append((int(f), err))
+    assert not bad, f"streamed chunks off the Mimi oracle: {bad[:10]}"

@@ -188,3 +188,45 @@ def test_csm_1b_long_fixtures_regenerate():
         assert np.array_equal(codes, g[key][:3])
     assert g0["ids"][0] == 128000 and g0["ids"][-1] == 128001 and int(g0["n_samples"]) == 125 * 1920
     assert np.isfinite(g0["pcm_rms"]) and 0 < float(g0["pcm_rms"]) < 1
+
+
+def test_mimi_oracle_windowed_decode_step():
+    """decode_step(window=12) (the config-3 fixture's streaming oracle: the SEANet decoder over the last 12
+    frames of history instead of all of it) gives the full-history samples of every frame, mimi_202407,
+    20 frames (past the window) -- within BLAS summation order."""
+    from csm_mlx.config import MIMI_CONFIGURATION
+    from csm_mlx.weights import synthetic_mimi_weights
+    from oracle.mimi_oracle import OracleMimi
+    m = MIMI_CONFIGURATION["mimi_202407"]
+    o = OracleMimi(m, synthetic_mimi_weights(m, 0))
+    codes = np.random.default_rng(4).integers(0, 2048, (1, 32, 20)).astype(np.int32)
+    outs = []
+    for window in (0, 12):
+        o.reset_state()
+        outs.append(np.concatenate([o.decode_step(codes[:, :, f: f + 1], window=window) for f in range(20)], axis=2))
+    assert outs[0].shape == outs[1].shape == (1, 1, 20 * 1920)
+    assert float(np.abs(outs[0] - outs[1]).max()) <= 1e-6 * max(1.0, float(np.abs(outs[0]).max()))
+
+
+def test_mimi_oracle_rvq_margin_and_forced_runner_up():
+    """OracleMimi.vq_margin / encode(force=): the margin is positive and scale-free (the same for x and c
+    scaled together up to rounding); forcing the runner-up of a code changes that code to the runner-up and
+    leaves every earlier codebook and every other frame unchanged (the residual chain is per frame)."""
+    from csm_mlx.config import MIMI_CONFIGURATION
+    from csm_mlx.weights import synthetic_mimi_weights
+    from golden.make_golden import pcm_fixture
+    from oracle.mimi_oracle import OracleMimi
+    rng = np.random.default_rng(0)
+    x, cb = rng.standard_normal((2, 5, 16)).astype(np.float32), rng.standard_normal((64, 16)).astype(np.float32)
+    mg, j2 = OracleMimi.vq_margin(x, cb)
+    assert (mg > 0).all() and (j2 != OracleMimi.vq_encode(x, cb)).all()
+    mg2, _ = OracleMimi.vq_margin(4 * x, 4 * cb)
+    np.testing.assert_allclose(mg2, mg, rtol=1e-4)       # gap and |x| |c1 - c2| both scale as s^2
+    m = MIMI_CONFIGURATION["tiny"]
+    o = OracleMimi(m, synthetic_mimi_weights(m, 0))
+    codes, margins = o.encode(pcm_fixture()[None, None], with_margins=True)
+    assert margins.shape == codes.shape and (margins >= 0).all()
+    k, t = 2, 3
+    forced = o.encode(pcm_fixture()[None, None], force=[(0, k, t)])
+    d = np.argwhere(forced != codes)
+    assert len(d) and (d[:, 2] == t).all() and d[:, 1].min() == k

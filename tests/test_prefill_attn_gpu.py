@@ -76,3 +76,44 @@ def test_prefill_attention_tiles_vs_per_row(dtype):
     ref = oracle_batch(oracle_for(args, w, bf16=(dtype == "bf16")), prompts, FRAMES)
     for b in range(B):
         assert ref_n[b] == FRAMES and first_divergence(runs["batch"][1][:, b], ref[b][0]) is None, f"utterance {b} vs oracle"
+
+
+def test_prefill_attention_tiles_csm_1b_gqa4():
+    """csm_1b's layout (32 query heads over 8 kv heads, G = 4, hd 64: all four waves of attn_prefill_kernel
+    busy, which the tiny backbone's G = 2 never reaches) with single-prompt prefills long enough for the tile
+    path (70 and 130 rows: 2 and 3 tiles, the last partial): tiles vs the per-row attention on the same engine
+    (h_last within 1e-5 of max|h|, codes identical) and codes bit-exact against the oracle."""
+    from csm_mlx import _lib
+    from csm_mlx.generation import FrameCache
+    from csm_mlx.models import CSM
+    from csm_mlx.sampling import Sampler
+    from csm_mlx.tokenizers import tokenize_text_segment
+    from helpers import prompt_ids
+    args, w = csm_weights("1b")
+    K = args.n_audio_codebooks
+    prompts = [tokenize_text_segment(prompt_ids(900 + i, n - 2), 0, K) for i, n in enumerate((70, 130))]
+    B = len(prompts)
+    model = CSM(args, dtype="bf16", max_batch=B)
+    model.load_weights(w)
+    L = _lib.lib()
+    D = model.backbone.args.hidden_size
+
+    def run(tiles):
+        _lib.check(L.csm_set_option(model.engine, b"attn_prefill", 1 if tiles else 0))
+        cache = FrameCache(model, B, Sampler(0.0, 0), [0] * B)
+        for b, (t, m) in enumerate(prompts):
+            cache.prefill(b, t, m)
+        h = cache.debug("h_last", (B, D))
+        cache.run(2)
+        hist, n, _ = cache.codes()
+        return h, hist[:2], n
+
+    ref_h, ref_c, ref_n = run(False)
+    h, c, n = run(True)
+    del model
+    err = (np.abs(h - ref_h).max(axis=1) / np.abs(ref_h).max(axis=1)).max()
+    assert err <= 1e-5, f"h_last {err:.2e} x max|h| from the per-row attention"
+    assert np.array_equal(c, ref_c) and np.array_equal(n, ref_n), "codes differ from the per-row attention"
+    ref = oracle_batch(oracle_for(args, w, bf16=True), prompts, 2)
+    for b in range(B):
+        assert first_divergence(c[:, b], ref[b][0]) is None, f"utterance {b} vs oracle"
