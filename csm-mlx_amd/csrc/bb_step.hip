@@ -60,11 +60,17 @@ struct Lds {
   float red[8][NWG];     // reduce-scatter staging [row][producer]
   float wsum[8][8];      // per-wave partial dots
   float sq[8];           // per-wave partial sums of squares of the gathered x (folded RMSNorm)
-  float hb[32];          // this WG's SiLU*up columns
+  alignas(16) float hb[32];  // this WG's SiLU*up columns
   float2 rope[HD / 2];   // (cos, sin) at the step's position
   float q[HD], kn[HD], vn[HD];          // attention WGs: the head's q and the new k / v row
   float am[8], al[8], ao[8][HD];        // attention WGs: per-wave online-softmax partials
   float Ks[128][HD + 4], Vs[128][HD];   // attention WGs: one pass of 128 keys (K rows padded)
+  // int4 kernel (bb_step_q4_kernel): projection inputs in the padded half-group layout (handoff.h q4p)
+  // with their half-group sums: x * norm weight (QKV / gate-up input) and the attention output (o_proj)
+  alignas(16) float xq[D / 32][36];
+  float xh[D / 32];
+  alignas(16) float aq[D / 32][36];
+  float ah[D / 32];
 };
 
 struct Ctx {
@@ -547,6 +553,257 @@ __device__ __forceinline__ void phase_reduce(Ctx& c) {
   }
 }
 
+// ============================================================================ int4 weights
+// The step of an nn.quantize'd engine (int4 g64, run_streaming_csm_mlx.py:811-818): the hand-offs, the
+// attention and the reduce-scatter are the bf16 kernel's; every projection reads its weight rows as 16-B
+// chunks of 32 nibbles -- one per lane, so a wave covers one 2048-wide row -- plus the half group's
+// {scale, bias} word, against activations staged in the padded layout (q4p) with their half-group sums
+// (handoff.h q4dot32: the int4 GEMV's per-half-group arithmetic).  Per workgroup: QKV wave v rows
+// 12w + v and 12w + 8 + (v & 3) (waves 4-7 load a duplicate they do not use: no branch around a load);
+// o_proj wave v row 8w + v; gate/up wave v rows 64w + 8v .. + 7 (SiLU*up columns 4v .. 4v + 3); down
+// this workgroup's 32 columns (one half group) of rows t + 512 k from the chunk-major copy (q4_down_cm:
+// nibbles [F/32][D][16 B], affine words [F/64][D]).  The RMSNorm is folded as in the bf16 kernel
+// (staged x * nw, the row scale after the dot product), layer 0 included.
+struct WQ4 { u32x4_t a[2]; unsigned s[2]; };
+struct WO4 { u32x4_t a; unsigned s; };
+struct WM4 { u32x4_t g[8]; unsigned gs[8]; u32x4_t d[4]; unsigned ds[4]; };
+constexpr int RB = D / 2, SBR = D / 64 * 4;              // bytes of a row's nibbles / affine words (K = D)
+constexpr int SB_QKV = QKV * RB, SB_O = D * RB, SB_GU = 2 * F * RB, SB_DN = D * F / 2;
+
+__device__ __forceinline__ void load_q4(Ctx& c, int l, WQ4& r) {
+  const char* W = reinterpret_cast<const char*>(c.p.wqkv[l]);
+  const int r0 = 12 * c.w, va = c.wave * RB + c.lane * 16, vb = (8 + (c.wave & 3)) * RB + c.lane * 16;
+  r.a[0] = bload<2>(W, va, r0 * RB);
+  r.a[1] = bload<2>(W, vb, r0 * RB);
+  const int sa = c.wave * SBR + (c.lane >> 1) * 4, sb = (8 + (c.wave & 3)) * SBR + (c.lane >> 1) * 4;
+  r.s[0] = bload4(W, sa, SB_QKV + r0 * SBR);
+  r.s[1] = bload4(W, sb, SB_QKV + r0 * SBR);
+}
+__device__ __forceinline__ void load_o4(Ctx& c, int l, WO4& r) {
+  const char* W = reinterpret_cast<const char*>(c.p.wo[l]);
+  r.a = bload<2>(W, c.wave * RB + c.lane * 16, 8 * c.w * RB);
+  r.s = bload4(W, c.wave * SBR + (c.lane >> 1) * 4, SB_O + 8 * c.w * SBR);
+}
+__device__ __forceinline__ void load_m4(Ctx& c, int l, WM4& r) {
+  const char* G = reinterpret_cast<const char*>(c.p.wgu[l]);
+  const int r0 = 64 * c.w + 8 * c.wave;  // (wave-dependent: in the lane offset, not the scalar one)
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    r.g[i] = bload<2>(G, 8 * c.wave * RB + c.lane * 16, (64 * c.w + i) * RB);
+    r.gs[i] = bload4(G, 8 * c.wave * SBR + (c.lane >> 1) * 4, SB_GU + (64 * c.w + i) * SBR);
+  }
+  (void)r0;
+  const char* Dn = reinterpret_cast<const char*>(c.p.wdc[l]);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    r.d[k] = bload<2>(Dn, c.tid * 16, (c.w * D + k * NT) * 16);
+    r.ds[k] = bload4(Dn, c.tid * 4, SB_DN + ((c.w >> 1) * D + k * NT) * 4);
+  }
+}
+
+// half-group sums of the staged pair (2t, 2t + 1) of each half: the 16 threads of a half group in order
+__device__ __forceinline__ void half_group_sums(Ctx& c, const float (&pair)[2], float* out) {
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    float v = pair[h];
+    v += __shfl_xor(v, 1, 64);
+    v += __shfl_xor(v, 2, 64);
+    v += __shfl_xor(v, 4, 64);
+    v += __shfl_xor(v, 8, 64);
+    if ((c.tid & 15) == 0) out[(h * (D / 2) + 2 * c.tid) >> 5] = v;
+  }
+}
+// an x hand-off (E3 / E5) -> x, xq = x * nw (padded), xh, per-wave sums of squares (folded RMSNorm)
+__device__ __forceinline__ void gather_x4(Ctx& c, const u64* buf, const Nw& nw) {
+  const int poff[2] = {2 * c.tid, D / 2 + 2 * c.tid};
+  float sq = 0.f, pr[2];
+  poll_pairs<2, BB_PROBE_DELAY, 1>(buf, 0x7fffffff, poff, c.tag(), [&](unsigned spin) { return spin_fail(c, spin); },
+                                   [&](const u32x4_t (&g)[2]) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float v0 = __uint_as_float(g[h].x), v1 = __uint_as_float(g[h].z);
+      const float a = v0 * nw.v[2 * h], b = v1 * nw.v[2 * h + 1];
+      *reinterpret_cast<float2*>(&c.L.x[poff[h]]) = make_float2(v0, v1);
+      *reinterpret_cast<float2*>(&c.L.xq[0][0] + q4p(poff[h])) = make_float2(a, b);
+      sq = fmaf(v0, v0, sq);
+      sq = fmaf(v1, v1, sq);
+      pr[h] = a + b;
+    }
+  });
+  c.stamp(c.e + 1);
+  half_group_sums(c, pr, c.L.xh);
+  sq = wave_sum(sq);
+  if (c.lane == 0) c.L.sq[c.wave] = sq;
+  __syncthreads();
+}
+// the same staging from L.x (the embedded row, layer 0)
+__device__ __forceinline__ void stage_x4(Ctx& c, const Nw& nw) {
+  float sq = 0.f, pr[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int k = h * (D / 2) + 2 * c.tid;
+    const float v0 = c.L.x[k], v1 = c.L.x[k + 1];
+    const float a = v0 * nw.v[2 * h], b = v1 * nw.v[2 * h + 1];
+    *reinterpret_cast<float2*>(&c.L.xq[0][0] + q4p(k)) = make_float2(a, b);
+    sq = fmaf(v0, v0, sq);
+    sq = fmaf(v1, v1, sq);
+    pr[h] = a + b;
+  }
+  half_group_sums(c, pr, c.L.xh);
+  sq = wave_sum(sq);
+  if (c.lane == 0) c.L.sq[c.wave] = sq;
+  __syncthreads();
+}
+// the attention output hand-off (E2) -> aq (padded), ah
+template <int DELAY = BB_PROBE_DELAY>
+__device__ __forceinline__ void gather_att4(Ctx& c, const u64* buf) {
+  const int poff[2] = {2 * c.tid, D / 2 + 2 * c.tid};
+  float pr[2];
+  poll_pairs<2, DELAY, 1>(buf, 0x7fffffff, poff, c.tag(), [&](unsigned spin) { return spin_fail(c, spin); },
+                          [&](const u32x4_t (&g)[2]) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float v0 = __uint_as_float(g[h].x), v1 = __uint_as_float(g[h].z);
+      *reinterpret_cast<float2*>(&c.L.aq[0][0] + q4p(poff[h])) = make_float2(v0, v1);
+      pr[h] = v0 + v1;
+    }
+  });
+  c.stamp(c.e + 1);
+  half_group_sums(c, pr, c.L.ah);
+  __syncthreads();
+}
+
+// QKV rows 12w.. (folded norm: the row scale after the dot; RoPE at pos) -> E1, k / v rows to the cache
+__device__ __forceinline__ void phase_qkv4(Ctx& c, int l, int pos, const WQ4& W) {
+  const float* xa = c.L.xq[c.lane];
+  const float hs = c.L.xh[c.lane];
+  float s0 = q4dot32(W.a[0], xa, W.s[0], hs), s1 = q4dot32(W.a[1], xa, W.s[1], hs);
+  s0 = wave_sum(s0);
+  s1 = wave_sum(s1);
+  if (c.lane == 0) { c.L.wsum[c.wave][0] = s0; c.L.wsum[c.wave][1] = s1; }
+  __syncthreads();
+  if (c.tid < 6) {  // pair j: rows i0, i0 + 1 of the slice (row i: wave i & 7, slot i >> 3)
+    const int i0 = 2 * c.tid, n = 12 * c.w + i0;
+    const float rs = row_rs(c);
+    float a = c.L.wsum[i0 & 7][i0 >> 3] * rs, b = c.L.wsum[(i0 + 1) & 7][(i0 + 1) >> 3] * rs;
+    if (n < (HQ + HKV) * HD) {
+      const float2 cs = c.L.rope[(n % HD) / 2];
+      const float y0 = a * cs.x - b * cs.y, y1 = b * cs.x + a * cs.y;
+      a = y0;
+      b = y1;
+    }
+    u64* g = c.buf(G_QKV, QKV);
+    gput(g + n, a, c.tag());
+    gput(g + n + 1, b, c.tag());
+    if (n >= HQ * HD) {  // KVCache.update_and_fetch: the new row at pos
+      const int nn = n < (HQ + HKV) * HD ? n - HQ * HD : n - (HQ + HKV) * HD;
+      float* cache = n < (HQ + HKV) * HD ? c.p.kc[l] : c.p.vc[l];
+      *reinterpret_cast<float2*>(cache + ((size_t)(nn / HD) * c.p.S_cap + pos) * HD + nn % HD) = make_float2(a, b);
+    }
+  }
+}
+// o_proj rows 8w + v (+ residual) -> E3
+__device__ __forceinline__ void phase_o4(Ctx& c, const WO4& W) {
+  float s = q4dot32(W.a, c.L.aq[c.lane], W.s, c.L.ah[c.lane]);
+  s = wave_sum(s);
+  if (c.lane == 0) c.L.wsum[c.wave][0] = s;
+  __syncthreads();
+  if (c.tid < 8 * REP) {
+    const int q = c.tid / REP, n = 8 * c.w + q;
+    c.put(G_X, D, n, c.L.x[n] + c.L.wsum[q][0], c.tid % REP);
+  }
+}
+// gate/up (8 rows per wave -> 4 SiLU*up columns), then the down partials of rows t + 512 k over the
+// workgroup's 32 columns
+__device__ __forceinline__ void phase_m4(Ctx& c, const WM4& W, float (&acc)[4], float rs) {
+  const float* xa = c.L.xq[c.lane];
+  const float hs = c.L.xh[c.lane];
+  float t[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) t[i] = wave_sum(q4dot32(W.g[i], xa, W.gs[i], hs));
+  if (c.lane < 4) {  // pair j = lane: rows 2j (gate), 2j + 1 (up) of the wave's 8
+    const float gt = rs * (c.lane == 0 ? t[0] : (c.lane == 1 ? t[2] : (c.lane == 2 ? t[4] : t[6])));
+    const float up = rs * (c.lane == 0 ? t[1] : (c.lane == 1 ? t[3] : (c.lane == 2 ? t[5] : t[7])));
+    c.L.hb[4 * c.wave + c.lane] = silu_f(gt) * up;
+  }
+  __syncthreads();
+  float hsum = 0.f;
+#pragma unroll
+  for (int j = 0; j < 32; j += 4) {
+    const float4 v = *reinterpret_cast<const float4*>(&c.L.hb[j]);
+    hsum += (v.x + v.y) + (v.z + v.w);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) acc[k] = q4dot32(W.d[k], c.L.hb, W.ds[k], hsum);
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(NT, 1) void bb_step_q4_kernel(BbStepArgs p) {
+  __shared__ __attribute__((aligned(16))) Lds L;
+  Ctx c{p, L, (int)blockIdx.x, (int)threadIdx.x, (int)(threadIdx.x & 63), (int)(threadIdx.x >> 6), 0u, 0};
+  c.tag0 = __hip_atomic_load(p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  c.stamp(0);
+  const int pos = p.pos[0];
+  WQ4 wq;
+  WO4 wo;
+  WM4 wm;
+  load_q4(c, 0, wq);
+  Nw nw1 = nw_fetch(c, p.n1[0]);
+  for (int k = c.tid; k < D; k += NT) L.x[k] = p.x[k];
+  if (c.tid < HD / 2) L.rope[c.tid] = reinterpret_cast<const float2*>(p.rope)[(size_t)pos * (HD / 2) + c.tid];
+  __syncthreads();
+  stage_x4(c, nw1);
+  for (int l = 0; l < NL; ++l) {
+    c.refresh();
+    phase_qkv4(c, l, pos, wq);                        // -> E1
+    ++c.e;
+    const bool attn_wg = c.w < NATT;
+    if (!attn_wg) {                                   // (the attention WGs fetch after their attention)
+      load_o4(c, l, wo);
+      load_m4(c, l, wm);
+    }
+    const Nw nw2 = nw_fetch(c, p.n2[l]);
+    if (attn_wg) {
+      KvPass kp;
+      attn_begin(c, l, pos, kp);
+      attn_rest(c, l, pos, kp);                       // -> E2
+      load_o4(c, l, wo);
+      load_m4(c, l, wm);
+    }
+    if (attn_wg) gather_att4(c, c.rbuf(G_ATT, D));   // E2
+    else gather_att4<BB_DELAY_E2>(c, c.rbuf(G_ATT, D));
+    ++c.e;
+    c.refresh();
+    phase_o4(c, wo);                                  // -> E3
+    if (l + 1 < NL) load_q4(c, l + 1, wq);
+    gather_x4(c, c.rbuf(G_X, D), nw2);                // E3 -> x, xq = x * n2
+    const float rs2 = row_rs(c);
+    ++c.e;
+    c.refresh();
+    float acc[4];
+    phase_m4(c, wm, acc, rs2);
+    {
+      u64* g = c.buf(G_PART, (size_t)NWG * D) + (size_t)c.w * D;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) gput(g + c.tid + NT * k, acc[k], c.tag());   // -> E4
+    }
+    nw1 = nw_fetch(c, l + 1 < NL ? p.n1[l + 1] : p.norm);
+    c.refresh();
+    phase_reduce(c);                                  // waits E4, -> E5
+    gather_x4(c, c.rbuf(G_X, D), nw1);                // E5 -> x, xq = x * (next n1 | final norm)
+    ++c.e;
+  }
+  c.refresh();
+  if (c.w == 0) {
+    const float rs = row_rs(c);
+    for (int k = c.tid; k < D; k += NT) p.h_last[k] = (&L.xq[0][0])[q4p(k)] * rs;
+  }
+  c.stamp(BB_STEP_STAMPS - 1);
+  if (c.w == 0 && c.tid == 0) __hip_atomic_store(p.epoch, c.tag0 - 1u + (unsigned)c.e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+namespace {
 }  // namespace
 
 __global__ __launch_bounds__(NT, 1) void bb_step_kernel(BbStepArgs p) {
@@ -658,8 +915,11 @@ __global__ __launch_bounds__(NT, 1) void bb_step_kernel(BbStepArgs p) {
 
 size_t bb_step_gbuf_bytes() { return G_TOTAL * sizeof(u64); }
 
-void launch_bb_step(const BbStepArgs& p, hipStream_t st) {
-  hipLaunchKernelGGL(bb_step_kernel, dim3(NWG), dim3(NT), 0, st, p);
+void launch_bb_step(const BbStepArgs& p, hipStream_t st, bool q4) {
+  if (q4) hipLaunchKernelGGL(bb_step_q4_kernel, dim3(NWG), dim3(NT), 0, st, p);
+  else hipLaunchKernelGGL(bb_step_kernel, dim3(NWG), dim3(NT), 0, st, p);
 }
 
-const void* bb_step_kernel_ptr() { return reinterpret_cast<const void*>(&bb_step_kernel); }
+const void* bb_step_kernel_ptr(bool q4) {
+  return q4 ? reinterpret_cast<const void*>(&bb_step_q4_kernel) : reinterpret_cast<const void*>(&bb_step_kernel);
+}

@@ -35,6 +35,8 @@ struct LayerW {
   void* wgu = nullptr;   // [2F][D] rows interleaved gate_j, up_j
   void* wd = nullptr;    // [D][F]
   void* wdc = nullptr;   // bf16 engines: down_proj re-laid chunk-major [F/R][D][R] for the fused MLP
+  void* wdq = nullptr;   // int4 engines: the persistent kernels' chunk-major down copy (q4_down_cm), derived:
+                         // rebuilt by build_tiled after any weight change, not a weight buffer
   float* n1 = nullptr;
   float* n2 = nullptr;
   float* kc = nullptr;   // [B][Hkv][S][hd]
@@ -177,7 +179,7 @@ struct csm_engine {
   unsigned* bb_epoch = nullptr;
   int* bb_err = nullptr;
   bool bb_step = [] { const char* v = getenv("CSM_BB_STEP"); return !(v && v[0] == '0'); }();
-  int bb_hw = -1;
+  int bb_hw = -1, bb_hw_q4 = -1;
   unsigned long long* bb_stamps = nullptr;  // csm_set_option "bb_step_stamps": per-hand-off clock stamps
 
   void* balloc(size_t bytes) {
@@ -455,22 +457,25 @@ int head_blocks(int N, int K, int M, int wdt) { return gemv_partials(N, K, M, wd
 // engine has csm_1b's backbone shapes in bf16 (with the chunk-major down copies) and the device has
 // the 256 CUs its one-workgroup-per-CU grid assumes (every workgroup must be resident).
 bool bb_step_eligible(csm_engine* e) {
-  if (!e->bb_step || !e->bb_gbuf || e->B != 1 || e->wdt != WDT_BF16) return false;
+  if (!e->bb_step || !e->bb_gbuf || e->B != 1 || (e->wdt != WDT_BF16 && e->wdt != WDT_Q4)) return false;
+  const bool q4 = e->wdt == WDT_Q4;
   const csm_llama_dims& d = e->bb.d;
   if (d.hidden != 2048 || d.intermediate != 8192 || d.n_heads != 32 || d.n_kv_heads != 8 || d.head_dim != 64 ||
       d.n_layers != BB_STEP_LAYERS)
     return false;
   for (const LayerW& l : e->bb.L)
-    if (!l.wdc) return false;
-  if (e->bb_hw < 0) {
+    if (!(q4 ? l.wdq : l.wdc)) return false;
+  if (q4 && e->tiled_dirty) return false;  // (the int4 down copies are rebuilt at csm_begin)
+  int& hw = q4 ? e->bb_hw_q4 : e->bb_hw;
+  if (hw < 0) {
     hipDeviceProp_t prop;
     int per_cu = 0;
-    e->bb_hw = hipGetDeviceProperties(&prop, e->dev) == hipSuccess && prop.multiProcessorCount == BB_STEP_WGS &&
-                       hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bb_step_kernel_ptr(), BB_STEP_THREADS, 0) ==
-                           hipSuccess && per_cu >= 1
-                   ? 1 : 0;
+    hw = hipGetDeviceProperties(&prop, e->dev) == hipSuccess && prop.multiProcessorCount == BB_STEP_WGS &&
+                 hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, bb_step_kernel_ptr(q4), BB_STEP_THREADS, 0) ==
+                     hipSuccess && per_cu >= 1
+             ? 1 : 0;
   }
-  return e->bb_hw == 1;
+  return hw == 1;
 }
 
 void enqueue_bb_step(csm_engine* e, hipStream_t st) {
@@ -478,12 +483,12 @@ void enqueue_bb_step(csm_engine* e, hipStream_t st) {
   for (int l = 0; l < BB_STEP_LAYERS; ++l) {
     const LayerW& w = e->bb.L[l];
     a.wqkv[l] = (const bf16_t*)w.wqkv; a.wo[l] = (const bf16_t*)w.wo; a.wgu[l] = (const bf16_t*)w.wgu;
-    a.wdc[l] = (const bf16_t*)w.wdc; a.n1[l] = w.n1; a.n2[l] = w.n2; a.kc[l] = w.kc; a.vc[l] = w.vc;
+    a.wdc[l] = (const bf16_t*)(e->wdt == WDT_Q4 ? w.wdq : w.wdc); a.n1[l] = w.n1; a.n2[l] = w.n2; a.kc[l] = w.kc; a.vc[l] = w.vc;
   }
   a.norm = e->bb.norm; a.rope = e->bb.rope; a.S_cap = e->bb.S_cap; a.eps = e->bb.d.eps;
   a.x = e->x; a.pos = e->pos; a.h_last = e->h_last;
   a.gbuf = (unsigned long long*)e->bb_gbuf; a.epoch = e->bb_epoch; a.err = e->bb_err; a.stamps = e->bb_stamps;
-  launch_bb_step(a, st);
+  launch_bb_step(a, st, e->wdt == WDT_Q4);
 }
 
 void enqueue_body(csm_engine* e, hipStream_t st) {
@@ -815,6 +820,14 @@ void build_tiled(csm_engine* e) {
     }
   one(e->proj, e->Dd, e->D, e->wdt);
   one(e->c0_head, e->Vpad, e->D, e->wdt);
+  if (e->wdt == WDT_Q4)  // the persistent kernels' chunk-major down copies (bb_step_q4 / dec_frame_q4)
+    for (Stack* s : {&e->bb, &e->dec})
+      for (LayerW& l : s->L) {
+        const int D = s->d.hidden, F = s->d.intermediate;
+        if (F % 64) continue;
+        if (pass == 0) { if (!l.wdq) l.wdq = e->alloc(q4_bytes(D, F)); }
+        else launch_q4_down_cm(l.wd, D, F, l.wdq, e->st);
+      }
   if (e->head_wdt == WDT_BF16)
     for (int cb = 0; cb < e->K - 1; ++cb) one((const char*)e->audio_head + (size_t)cb * e->Vpad * e->Dd * 2, e->Vpad, e->Dd, WDT_BF16);
   HIPCHK(hipDeviceSynchronize());
@@ -1056,7 +1069,7 @@ int csm_engine_create(const csm_dims* dims, int device, int weight_dtype, int ma
     e->df_gbuf = e->alloc(dec_frame_gbuf_bytes());
     e->df_epoch = (unsigned*)e->alloc(16);
     e->df_err = (int*)e->alloc(16);
-    if (e->wdt == WDT_BF16 && b.hidden == 2048 && b.n_layers == BB_STEP_LAYERS) {
+    if ((e->wdt == WDT_BF16 || e->wdt == WDT_Q4) && b.hidden == 2048 && b.n_layers == BB_STEP_LAYERS) {
       e->bb_gbuf = e->alloc(bb_step_gbuf_bytes());
       e->bb_epoch = (unsigned*)e->alloc(16);
       e->bb_err = (int*)e->alloc(16);
@@ -1988,7 +2001,9 @@ int csm_bench_bb_step(csm_engine* e, int iters, float* avg_us, double* bytes) {
     const double D = d.hidden, F = d.intermediate, QKV = e->bb.qkv_rows(), HKV = d.n_kv_heads, HD = d.head_dim;
     double nb = D * 4 * 2;                                                     // x in, h_last out
     for (int l = 0; l < d.n_layers; ++l) {
-      nb += (QKV * D + D * D + 2 * F * D + D * F) * 2 + 2 * D * 4;              // weights, norm weights
+      nb += (double)e->wbytes((size_t)QKV, (size_t)D) + (double)e->wbytes((size_t)D, (size_t)D) +   // weights in
+            (double)e->wbytes(2 * (size_t)F, (size_t)D) + (double)e->wbytes((size_t)D, (size_t)F) +     // their storage
+            2 * D * 4;                                                          // format; norm weights
       nb += 2 * HKV * (double)pos * HD * 4 + 2 * HKV * HD * 4;                  // K/V history read + append
     }
     for (int i = 0; i < 2; ++i) enqueue_bb_step(e, e->st);

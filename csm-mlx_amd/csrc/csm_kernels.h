@@ -318,6 +318,8 @@ void launch_embed_q4(const EmbedParams& p, int n_text_rows, int M, hipStream_t s
 void launch_gemv_q4(const GemvParams& p, bool nt, hipStream_t st);
 int gemv_q4_rows_per_block(int N, int K, int M);
 bool gemv_q4_supported(int N, int K);
+// the persistent kernels' chunk-major copy of an int4 [D][F] down_proj (q4_bytes(D, F) bytes)
+void launch_q4_down_cm(const void* src, int D, int F, void* dst, hipStream_t st);
 
 // ---- batched projections on MFMA (gemm_kernels.hip)
 constexpr int GEMM_MFMA_MIN_M = 8;  // rows at which a bf16 projection leaves the GEMV for the matrix cores
@@ -355,7 +357,7 @@ struct BbStepArgs {
   const bf16_t* wqkv[BB_STEP_LAYERS];
   const bf16_t* wo[BB_STEP_LAYERS];
   const bf16_t* wgu[BB_STEP_LAYERS];     // gate/up rows interleaved
-  const bf16_t* wdc[BB_STEP_LAYERS];     // down_proj chunk-major [F/8][D][8]
+  const bf16_t* wdc[BB_STEP_LAYERS];     // down_proj chunk-major [F/8][D][8] (int4: q4_down_cm's copy)
   const float* n1[BB_STEP_LAYERS];
   const float* n2[BB_STEP_LAYERS];
   float* kc[BB_STEP_LAYERS];             // [Hkv][S_cap][HD] of utterance 0
@@ -374,8 +376,9 @@ struct BbStepArgs {
 };
 constexpr int BB_STEP_STAMPS = 128;
 size_t bb_step_gbuf_bytes();
-void launch_bb_step(const BbStepArgs& p, hipStream_t st);
-const void* bb_step_kernel_ptr();
+// q4: the int4 kernel (wqkv / wo / wgu in the common.h int4 layout, wdc the q4_down_cm copy)
+void launch_bb_step(const BbStepArgs& p, hipStream_t st, bool q4 = false);
+const void* bb_step_kernel_ptr(bool q4 = false);
 
 constexpr int DEC_FRAME_LAYERS = 4;
 struct DecFrameArgs {

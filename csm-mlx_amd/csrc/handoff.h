@@ -142,6 +142,60 @@ __device__ __forceinline__ void poll_pairs(const u64* base, int bytes, const int
   use(g);
 }
 
+// ---- int4 (MLX affine, group 64; common.h layout) weight chunks for the persistent kernels
+// 4-B raw buffer load (an int4 group's {scale, bias} word), descriptor as bload
+template <int AUX = 0>
+__device__ __forceinline__ unsigned bload4(const void* base, int voff, int soff) {
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+  return __builtin_amdgcn_raw_buffer_load_b32(rs, voff, soff, AUX);
+}
+// One 16-B chunk of 32 nibbles (a half group: word i holds elements 8i .. 8i + 7, byte b elements 8i + 2b
+// (low nibble) and 8i + 2b + 1) against 32 consecutive fp32 activations x (LDS), with that half group's
+// affine word sb and activation sum hs: scale * sum_j q_j x_j + bias * sum_j x_j (the int4 GEMV's
+// per-half-group arithmetic, q4_kernels.hip gemv_q4_kernel).
+__device__ __forceinline__ float q4dot32(const u32x4_t w, const float* x, unsigned sb, float hs) {
+  float d0 = 0.f, d1 = 0.f, d2 = 0.f, d3 = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const unsigned u = w[i], lo = u & 0x0F0F0F0Fu, hi = (u >> 4) & 0x0F0F0F0Fu;
+    const float4 a = *reinterpret_cast<const float4*>(x + 8 * i), b = *reinterpret_cast<const float4*>(x + 8 * i + 4);
+    d0 = fmaf((float)(lo & 0xFFu), a.x, d0);
+    d1 = fmaf((float)(hi & 0xFFu), a.y, d1);
+    d2 = fmaf((float)((lo >> 8) & 0xFFu), a.z, d2);
+    d3 = fmaf((float)((hi >> 8) & 0xFFu), a.w, d3);
+    d0 = fmaf((float)((lo >> 16) & 0xFFu), b.x, d0);
+    d1 = fmaf((float)((hi >> 16) & 0xFFu), b.y, d1);
+    d2 = fmaf((float)(lo >> 24), b.z, d2);
+    d3 = fmaf((float)(hi >> 24), b.w, d3);
+  }
+  return fmaf(bf16_lo(sb), (d0 + d1) + (d2 + d3), bf16_hi(sb) * hs);
+}
+// 8 nibbles of one word (elements j < 8, low nibble of byte b = element 2b) against x[0..7]
+__device__ __forceinline__ float q4dot8(unsigned u, const float* x) {
+  const unsigned lo = u & 0x0F0F0F0Fu, hi = (u >> 4) & 0x0F0F0F0Fu;
+  const float4 a = *reinterpret_cast<const float4*>(x), b = *reinterpret_cast<const float4*>(x + 4);
+  float s = (float)(lo & 0xFFu) * a.x;
+  s = fmaf((float)(hi & 0xFFu), a.y, s);
+  s = fmaf((float)((lo >> 8) & 0xFFu), a.z, s);
+  s = fmaf((float)((hi >> 8) & 0xFFu), a.w, s);
+  s = fmaf((float)((lo >> 16) & 0xFFu), b.x, s);
+  s = fmaf((float)((hi >> 16) & 0xFFu), b.y, s);
+  s = fmaf((float)(lo >> 24), b.z, s);
+  s = fmaf((float)(hi >> 24), b.w, s);
+  return s;
+}
+// Padded LDS layout of an int4 kernel's activation row: each 32-element half group 36 floats apart, so
+// the 64 lanes' 16-B reads of their own half groups fall on distinct banks (gemv_q4_kernel's layout)
+__device__ __forceinline__ int q4p(int k) { return (k >> 5) * 36 + (k & 31); }
+// sums of lanes 0-31 and of lanes 32-63 (wave_sum's DPP row reductions, rows combined per half)
+__device__ __forceinline__ float2 half_sums(float v) {
+  v += dpp_f<0x128>(v);
+  v += dpp_f<0x124>(v);
+  v += dpp_f<0x4E>(v);
+  v += dpp_f<0xB1>(v);
+  return make_float2(lane_f(v, 0) + lane_f(v, 16), lane_f(v, 32) + lane_f(v, 48));
+}
+
 // threadIdx.x through an opaque move: lane-dependent addresses derived from it inside the frame loop
 // are recomputed per iteration instead of being hoisted out of the loop and held (spilled) for the
 // whole frame.

@@ -118,6 +118,29 @@ void launch_q4_to_f32(const void* base, int Ntot, int K, int r0, int n, float* d
                      Ntot, K, r0, n, dst);
 }
 
+// [D][F] quantized down_proj -> the persistent kernels' chunk-major copy: nibbles [F/32][D][16 B] (columns
+// 32c .. 32c + 31 of row n, the 16 bytes of the standard layout, contiguous per column chunk), then the
+// affine words [F/64][D] -- a workgroup's 32-column slice of every row is one contiguous stream.
+__global__ __launch_bounds__(256) void q4_down_cm_kernel(const uint8_t* src, int D, int F, uint8_t* dst) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const size_t nch = (size_t)(F / 32) * D;
+  if (i < nch) {
+    const size_t c = i / D, n = i % D;
+    *reinterpret_cast<uint4*>(dst + i * 16) = *reinterpret_cast<const uint4*>(src + n * (F / 2) + c * 16);
+  }
+  if (i < (size_t)(F / Q4_GROUP) * D) {
+    const size_t g = i / D, n = i % D;
+    reinterpret_cast<uint32_t*>(dst + (size_t)D * F / 2)[i] =
+        reinterpret_cast<const uint32_t*>(src + q4_sb_offset(D, F))[n * (F / Q4_GROUP) + g];
+  }
+}
+
+void launch_q4_down_cm(const void* src, int D, int F, void* dst, hipStream_t st) {
+  const size_t n = (size_t)(F / 32) * D;
+  hipLaunchKernelGGL(q4_down_cm_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, (const uint8_t*)src, D, F,
+                     (uint8_t*)dst);
+}
+
 // ============================================================================ embedding (QuantizedEmbedding)
 // embed_rows_kernel with dequantized rows: x[m] = sum_j mask * (scale * q + bias) of row tok + V*j of
 // the audio table, then the text column (generation.py:32-36 order).

@@ -115,3 +115,40 @@ def test_handoff_timeout_reported_by_every_frame_entry(model_1b):
             else:
                 _lib.check(L.csm_frame_finish(model.engine, _lib.ptr(logits), None))
         _lib.check(L.csm_synchronize(model.engine))       # the flag was consumed by the report
+
+
+@pytest.fixture(scope="module")
+def model_1b_q4():
+    from csm_mlx.models import CSM
+    args, w = csm_weights("1b")
+    model = CSM(args, dtype="q4")
+    model.load_weights(w)
+    yield args, w, model
+    del model
+
+
+def test_bb_step_q4_matches_launch_path_and_oracle(model_1b_q4):
+    """The int4 persistent backbone step (bb_step_q4_kernel: nn.quantize'd weights read as nibbles + group
+    affine words, the bf16 kernel's hand-offs) against the int4 GEMV launch path on the same engine (codes
+    identical, c0 logits within 2e-3 x max) and the oracle on the dequantized weights (codes), 12 frames;
+    deterministic run to run."""
+    from csm_mlx.generation import generate_codes_batch
+    from csm_mlx.sampling import Sampler
+    from csm_mlx.tokenizers import tokenize_text_segment
+    args, w, model = model_1b_q4
+    prompt = tokenize_text_segment(prompt_ids(31), 0, 32)
+    got = _compare(model, prompt, 12)
+    h1, n1, _ = generate_codes_batch(model, [prompt], 40, sampler=Sampler(0.0, 0))
+    h2, n2, _ = generate_codes_batch(model, [prompt], 40, sampler=Sampler(0.0, 0))
+    assert np.array_equal(h1, h2) and np.array_equal(n1, n2)
+    assert first_divergence(h1[:12, 0], got) is None
+    orc = oracle_for(args, w, q4=True).generate_codes(*prompt, 12)
+    assert first_divergence(got, orc) is None
+
+
+def test_bb_step_q4_long_context(model_1b_q4):
+    from csm_mlx.tokenizers import tokenize_text_segment
+    args, w, model = model_1b_q4
+    rng = np.random.default_rng(7)
+    prompt = tokenize_text_segment([int(t) for t in rng.integers(1000, 120000, 600)], 0, 32)
+    _compare(model, prompt, 4)
