@@ -180,6 +180,7 @@ struct csm_engine {
   int* bb_err = nullptr;
   bool bb_step = [] { const char* v = getenv("CSM_BB_STEP"); return !(v && v[0] == '0'); }();
   int bb_hw = -1, bb_hw_q4 = -1;
+  int df_hw_q4 = -1;
   unsigned long long* bb_stamps = nullptr;  // csm_set_option "bb_step_stamps": per-hand-off clock stamps
 
   void* balloc(size_t bytes) {
@@ -522,7 +523,8 @@ void enqueue_body(csm_engine* e, hipStream_t st) {
 // csm_1b's decoder shapes in bf16 and the folded tables, and the device has the 256 CUs its grid of
 // one workgroup per CU assumes (every workgroup must be resident: the hand-offs spin).
 bool dec_frame_eligible(csm_engine* e) {
-  if (!e->dec_frame || e->B != 1 || e->wdt != WDT_BF16 || e->head_wdt != WDT_BF16) return false;
+  if (!e->dec_frame || e->B != 1 || (e->wdt != WDT_BF16 && e->wdt != WDT_Q4) || e->head_wdt != WDT_BF16) return false;
+  const bool q4 = e->wdt == WDT_Q4;
   if (e->temperature > 0.f && (e->use_top_p || e->use_min_p)) return false;  // filters: sample_filtered_kernel
   const csm_llama_dims& d = e->dec.d;
   if (d.hidden != 1024 || d.intermediate != 8192 || d.n_heads != 8 || d.n_kv_heads != 2 || d.head_dim != 128 ||
@@ -530,17 +532,19 @@ bool dec_frame_eligible(csm_engine* e) {
       e->dec.S_cap != e->K)
     return false;
   for (const LayerW& l : e->dec.L)
-    if (!l.wdc) return false;
+    if (!(q4 ? l.wdq : l.wdc)) return false;
+  if (q4 && e->tiled_dirty) return false;  // (the int4 down copies are rebuilt at csm_begin)
   if (!e->proj_tab || !e->fold_proj || !e->use_qkv0_tab || !e->qkv0_built || e->proj_tab_dirty) return false;
-  if (e->df_hw < 0) {
+  int& hw = q4 ? e->df_hw_q4 : e->df_hw;
+  if (hw < 0) {
     hipDeviceProp_t prop;
     int per_cu = 0;
-    e->df_hw = hipGetDeviceProperties(&prop, e->dev) == hipSuccess && prop.multiProcessorCount == DEC_FRAME_WGS &&
-                       hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dec_frame_kernel_ptr(), DEC_FRAME_THREADS, 0) ==
-                           hipSuccess && per_cu >= 1
-                   ? 1 : 0;
+    hw = hipGetDeviceProperties(&prop, e->dev) == hipSuccess && prop.multiProcessorCount == DEC_FRAME_WGS &&
+                 hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dec_frame_kernel_ptr(q4), DEC_FRAME_THREADS, 0) ==
+                     hipSuccess && per_cu >= 1
+             ? 1 : 0;
   }
-  return e->df_hw == 1;
+  return hw == 1;
 }
 
 void enqueue_dec_frame_only(csm_engine* e, hipStream_t st) {
@@ -548,7 +552,7 @@ void enqueue_dec_frame_only(csm_engine* e, hipStream_t st) {
   for (int l = 0; l < DEC_FRAME_LAYERS; ++l) {
     const LayerW& w = e->dec.L[l];
     a.wqkv[l] = (const bf16_t*)w.wqkv; a.wo[l] = (const bf16_t*)w.wo; a.wgu[l] = (const bf16_t*)w.wgu;
-    a.wdc[l] = (const bf16_t*)w.wdc; a.n1[l] = w.n1; a.n2[l] = w.n2; a.kc[l] = w.kc; a.vc[l] = w.vc;
+    a.wdc[l] = (const bf16_t*)(e->wdt == WDT_Q4 ? w.wdq : w.wdc); a.n1[l] = w.n1; a.n2[l] = w.n2; a.kc[l] = w.kc; a.vc[l] = w.vc;
   }
   a.norm = e->dec.norm; a.rope = e->dec.rope; a.S_cap = e->dec.S_cap; a.eps = e->dec.d.eps;
   a.c0_head = (const bf16_t*)e->c0_head; a.proj = (const bf16_t*)e->proj; a.audio_head = (const bf16_t*)e->audio_head;
@@ -559,7 +563,7 @@ void enqueue_dec_frame_only(csm_engine* e, hipStream_t st) {
   static const int hnt = [] { const char* v = getenv("CSM_DF_HNT"); return v ? atoi(v) : 1; }();
   a.wnt = wnt; a.hnt = hnt;
   a.temperature = e->temperature; a.top_k = e->top_k; a.seeds = e->seeds; a.frame_ctr = e->frame_ctr;
-  launch_dec_frame(a, st);
+  launch_dec_frame(a, st, e->wdt == WDT_Q4);
 }
 
 void enqueue_dec_frame(csm_engine* e, hipStream_t st) {
@@ -1958,12 +1962,14 @@ int csm_bench_dec_frame(csm_engine* e, int iters, float* avg_us, double* bytes) 
     // decoder K/V rows are written again (the advance launch is not replayed).
     const size_t D = e->Dd, DB = e->D, V = e->V, F = e->dec.d.intermediate, QKV = e->dec.qkv_rows();
     const size_t HKV = e->dec.d.n_kv_heads, HD = e->dec.d.head_dim;
-    double nb = (double)V * DB * 2 + DB * 4 + (double)D * DB * 2;    // codebook0_head, h_last, projection
+    // every weight in its storage format (bf16, or int4 nibbles + affine words); audio_head stays bf16
+    auto wb = [&](size_t n, size_t k) { return (double)e->wbytes(n, k); };
+    double nb = wb(V, DB) + DB * 4 + wb(D, DB);                       // codebook0_head, h_last, projection
     for (int step = 1; step < e->K; ++step) {
       const int rows = step == 1 ? 2 : 1, pos = step == 1 ? 1 : step;
       for (int l = 0; l < DEC_FRAME_LAYERS; ++l) {
-        nb += (l == 0 && step > 1) ? (double)QKV * 4 : (double)QKV * D * 2;  // folded qkv0 table row / QKV
-        nb += (double)D * D * 2 + 2.0 * F * D * 2 + (double)F * D * 2;       // o, gate/up, down
+        nb += (l == 0 && step > 1) ? (double)QKV * 4 : wb(QKV, D);          // folded qkv0 table row / QKV
+        nb += wb(D, D) + wb(2 * F, D) + wb(D, F);                           // o, gate/up, down
         nb += 2.0 * HKV * (pos + 1) * HD * 4 + 2.0 * HKV * rows * HD * 4;    // K/V history read + append
       }
       nb += (double)V * D * 2 + D * 4;                                      // audio_head[step-1], next x row

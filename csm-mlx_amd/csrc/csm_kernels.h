@@ -419,5 +419,7 @@ struct DecFrameArgs {
 constexpr int DEC_FRAME_STAMPS = 1024;
 size_t dec_frame_gbuf_bytes();
 constexpr int DEC_FRAME_WGS = 256, DEC_FRAME_THREADS = 512;
-void launch_dec_frame(const DecFrameArgs& p, hipStream_t st);
-const void* dec_frame_kernel_ptr();  // for the occupancy query
+// q4: the int4 kernel (wqkv / wo / wgu / c0_head / proj in the common.h int4 layout, wdc the q4_down_cm copy;
+// audio_head bf16)
+void launch_dec_frame(const DecFrameArgs& p, hipStream_t st, bool q4 = false);
+const void* dec_frame_kernel_ptr(bool q4 = false);  // for the occupancy query

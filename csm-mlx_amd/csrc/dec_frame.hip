@@ -32,6 +32,8 @@
 // Arithmetic: fp32 accumulation of bf16 weights x fp32 activations, RMSNorm as the oracle
 // (x * rsqrt(mean(x^2) + eps) * w), RoPE on interleaved pairs from the cos/sin table, softmax with
 // max subtraction, reductions in fixed orders (deterministic run to run).
+#include <type_traits>
+
 #include "csm_kernels.h"
 #include "handoff.h"
 
@@ -89,15 +91,27 @@ struct Lds {
   float att[MAXM][D];      // attention output
   float qs[HQ][HD];        // scaled query of one row per head
   float2 rope[MAXM][HD / 2];// (cos, sin) of this step's positions, staged once per step
-  float hb[MAXM][32];      // this WG's h columns
+  alignas(16) float hb[MAXM][32];  // this WG's h columns
   float red[4 * MAXM][256];// reduce-scatter staging [row][producer]
   float wsum[8][MAXM * 8]; // per-wave partial dots
   float sq[8][MAXM];       // per-wave partial sums of squares of the gathered x rows (folded RMSNorm)
-  float Ks[HKV][32][HD + 4];// cached keys of this layer (rows padded: conflict-free row-parallel reads)
+  union {
+    float Ks[HKV][32][HD + 4];// cached keys of this layer (rows padded: conflict-free row-parallel reads)
+    struct {                  // int4 kernel, frame start only (before any step's K history): h_last in the
+      float hq[DB / 32][36];  // padded half-group layout (handoff.h q4p) with its half-group sums
+      float hh[DB / 32];
+    } h0;
+  };
   float Vs[HKV][32][HD];    // cached values
   float lg[VMAX];          // sampling: the head's logits, gathered from every workgroup
   int code;                // last arg-max
   int flag;
+  // int4 kernel: projection inputs in the padded layout with their half-group sums -- x * norm weight
+  // (QKV / gate-up / head input) and the attention output (o_proj input)
+  alignas(16) float xq[MAXM][D / 32][36];
+  float xh[MAXM][D / 32];
+  alignas(16) float aq[MAXM][D / 32][36];
+  float ah[MAXM][D / 32];
 };
 
 }  // namespace
@@ -426,8 +440,69 @@ __device__ __forceinline__ void load_head(Ctx& c, const bf16_t* W, int K, WHd& r
   }
 }
 
+// ---- int4 weight slices (an nn.quantize'd engine: dec_frame_kernel<true>).  A 16-B chunk holds 32
+// nibbles (a half group), so one 1024-wide decoder row is 32 lanes: each wave covers two rows, lanes 0-31
+// the first, 32-63 the second (half_sums reduces them apart); every chunk comes with its half group's
+// affine word (handoff.h q4dot32).  Down reads the chunk-major copy (q4_down_cm: nibbles [F/32][D][16 B],
+// affine words [F/64][D]) -- the WG's 32 columns are one half group of every row.
+constexpr int RB = D / 2, SBR = D / 64 * 4;             // a 1024-wide row: nibble bytes, affine-word bytes
+constexpr int RBH = DB / 2, SBRH = DB / 64 * 4;         // a 2048-wide row (codebook0_head, projection)
+constexpr int SB_QKV = QKV * RB, SB_O = D * RB, SB_GU = 2 * F * RB, SB_DN = D * F / 2, SB_PROJ = D * RBH;
+struct WQkv4 { u32x4_t a; unsigned s; };       // waves 0-2: rows 6w + 2v (lanes 0-31), 6w + 2v + 1 (32-63)
+struct WO4 { u32x4_t a; unsigned s; };         // waves 0-1: rows 4w + 2v, + 1
+struct WGu4 { u32x4_t a[4]; unsigned s[4]; };  // load i: rows 64w + 8v + 2i (gate, lanes 0-31), + 1 (up)
+struct WDn4 { u32x4_t a[2]; unsigned s[2]; };  // rows 2t, 2t + 1 over the WG's 32 columns
+__device__ __forceinline__ int hrow(const Ctx& c) { return c.lane >> 5; }  // which row of the wave's two
+__device__ __forceinline__ int hgi(const Ctx& c) { return c.lane & 31; }   // the lane's half group
+
+__device__ __forceinline__ void load_qkv4(Ctx& c, int l, WQkv4& r) {
+  if (c.wave < 3) {
+    const char* W = reinterpret_cast<const char*>(c.p.wqkv[l]);
+    const int row = 2 * c.wave + hrow(c);
+    r.a = bload(W, row * RB + hgi(c) * 16, 6 * c.w * RB);
+    r.s = bload4(W, row * SBR + (hgi(c) >> 1) * 4, SB_QKV + 6 * c.w * SBR);
+  }
+}
+__device__ __forceinline__ void load_o4(Ctx& c, int l, WO4& r) {
+  if (c.wave < 2) {
+    const char* W = reinterpret_cast<const char*>(c.p.wo[l]);
+    const int row = 2 * c.wave + hrow(c);
+    r.a = bload(W, row * RB + hgi(c) * 16, 4 * c.w * RB);
+    r.s = bload4(W, row * SBR + (hgi(c) >> 1) * 4, SB_O + 4 * c.w * SBR);
+  }
+}
+template <int I0, int I1>
+__device__ __forceinline__ void load_gu4(Ctx& c, int l, WGu4& r) {
+  const char* W = reinterpret_cast<const char*>(c.p.wgu[l]);
+  const int row = 8 * c.wave + hrow(c);
+#pragma unroll
+  for (int i = I0; i < I1; ++i) {
+    r.a[i] = bload(W, row * RB + hgi(c) * 16, (64 * c.w + 2 * i) * RB);
+    r.s[i] = bload4(W, row * SBR + (hgi(c) >> 1) * 4, SB_GU + (64 * c.w + 2 * i) * SBR);
+  }
+}
+__device__ __forceinline__ void load_dn4(Ctx& c, int l, WDn4& r) {
+  const char* W = reinterpret_cast<const char*>(c.p.wdc[l]);
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    r.a[k] = bload(W, (2 * c.tid + k) * 16, c.w * D * 16);
+    r.s[k] = bload4(W, (2 * c.tid + k) * 4, SB_DN + (c.w >> 1) * D * 4);
+  }
+}
+
+// half-group sums of the pair (2t, 2t + 1) of one 1024-wide row: the 16 threads of a half group in order
+__device__ __forceinline__ void half_group_sum16(const Ctx& c, float v, float* out) {
+  v += __shfl_xor(v, 1, 64);
+  v += __shfl_xor(v, 2, 64);
+  v += __shfl_xor(v, 4, 64);
+  v += __shfl_xor(v, 8, 64);
+  if ((c.tid & 15) == 0) out[c.tid >> 4] = v;
+}
+
 // ---- phases
 // QKV rows of this WG for M rows at positions pos0..pos0+M-1 (RoPE), published to E1.
+template <int M, bool SC>
+__device__ __forceinline__ void qkv_publish(Ctx& c, int pos0);
 template <int M, bool SC>
 __device__ __forceinline__ void phase_qkv(Ctx& c, int pos0, const WQkv& W) {
   if (c.wave < 6) {
@@ -439,6 +514,24 @@ __device__ __forceinline__ void phase_qkv(Ctx& c, int pos0, const WQkv& W) {
     if (c.lane == 0) { c.L.wsum[c.wave][0] = s0; if constexpr (M == 2) c.L.wsum[c.wave][1] = s1; }
   }
   __syncthreads();
+  qkv_publish<M, SC>(c, pos0);
+}
+// int4: waves 0-2, the wave's two rows from its two lane halves (row 2v + h -> wsum[2v + h], as above)
+template <int M, bool SC>
+__device__ __forceinline__ void phase_qkv4(Ctx& c, int pos0, const WQkv4& W) {
+  if (c.wave < 3) {
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const float2 h = half_sums(q4dot32(W.a, c.L.xq[m][hgi(c)], W.s, c.L.xh[m][hgi(c)]));
+      if (c.lane == 0) { c.L.wsum[2 * c.wave][m] = h.x; c.L.wsum[2 * c.wave + 1][m] = h.y; }
+    }
+  }
+  __syncthreads();
+  qkv_publish<M, SC>(c, pos0);
+}
+// the WG's 6 rows (wsum[r][m]) -> folded row scale, RoPE pairs -> E1
+template <int M, bool SC>
+__device__ __forceinline__ void qkv_publish(Ctx& c, int pos0) {
   if (c.tid < 3 * M * REP) {  // RoPE pair j of row m: rows n, n+1 = 6w + 2j, +1 -> replica rr
     const int pr = c.tid / REP, rr = c.tid % REP, m = pr / 3, j = pr % 3, n = 6 * c.w + 2 * j;
     float a = c.L.wsum[2 * j][m], b = c.L.wsum[2 * j + 1][m];
@@ -557,8 +650,9 @@ __device__ __forceinline__ void gather_qkv(Ctx& c, const u64* buf, int pos0, con
 #ifndef DF_PV
 #define DF_PV 2
 #endif
-template <int M>
+template <int M, bool Q4 = false>
 __device__ __forceinline__ void phase_attn(Ctx& c, int pos0, int layer) {
+  static_assert(!Q4 || DF_PV == 2, "the int4 kernel stages the attention output from the DF_PV 2 loop");
   const int h = c.wave, g = h / (HQ / HKV);
   const float scale = 0.08838834764831845f;  // 1 / sqrt(128)
   const int kj = c.lane & 31, hh = c.lane >> 5;
@@ -641,7 +735,18 @@ __device__ __forceinline__ void phase_attn(Ctx& c, int pos0, int layer) {
     t.y = __shfl_xor(o.y, 32, 64);
     t.z = __shfl_xor(o.z, 32, 64);
     t.w = __shfl_xor(o.w, 32, 64);
-    if (kv == 0) {
+    if constexpr (Q4) {
+      // int4 o_proj input: the padded layout (q4p) and its half-group sums -- lanes dq = 8j .. 8j + 7 of
+      // the kv == 0 half hold half group 4h + j
+      const float inv = 1.f / l_run;
+      const float4 ov = make_float4((o.x + t.x) * inv, (o.y + t.y) * inv, (o.z + t.z) * inv, (o.w + t.w) * inv);
+      if (kv == 0) *reinterpret_cast<float4*>(&c.L.aq[m][0][0] + q4p(h * HD + 4 * dq)) = ov;
+      float hs = (ov.x + ov.y) + (ov.z + ov.w);
+      hs += __shfl_xor(hs, 1, 64);
+      hs += __shfl_xor(hs, 2, 64);
+      hs += __shfl_xor(hs, 4, 64);
+      if (kv == 0 && (dq & 7) == 0) c.L.ah[m][4 * h + (dq >> 3)] = hs;
+    } else if (kv == 0) {
       const float inv = 1.f / l_run;
       *reinterpret_cast<float4*>(&c.L.att[m][h * HD + 4 * dq]) =
           make_float4((o.x + t.x) * inv, (o.y + t.y) * inv, (o.z + t.z) * inv, (o.w + t.w) * inv);
@@ -809,6 +914,103 @@ __device__ __forceinline__ void phase_reduce(Ctx& c) {
   }
 }
 
+// ---- int4 phases
+// o_proj: waves 0-1, rows 4w + 2v + h (+ residual) -> E3
+template <int M>
+__device__ __forceinline__ void phase_o4(Ctx& c, const WO4& W) {
+  if (c.wave < 2) {
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const float2 h = half_sums(q4dot32(W.a, c.L.aq[m][hgi(c)], W.s, c.L.ah[m][hgi(c)]));
+      if (c.lane == 0) { c.L.wsum[2 * c.wave][m] = h.x; c.L.wsum[2 * c.wave + 1][m] = h.y; }
+    }
+  }
+  __syncthreads();
+  if (c.tid < 4 * M * REP) {
+    const int q = c.tid / REP, m = q / 4, r = q % 4, n = 4 * c.w + r;
+    c.put(G_X, MAXM * D, (size_t)m * D + n, c.L.x[m][n] + c.L.wsum[r][m], c.tid % REP);
+  }
+}
+// gate/up (load i of wave v: the SiLU*up column 4v + i from its two lane halves) and the down partials
+// of rows 2t, 2t + 1 over the WG's 32 columns -> E4 (two granules per 16-B sc1 store, as DF_E4_16)
+template <int M, bool SC>
+__device__ __forceinline__ void phase_mlp4(Ctx& c, const WGu4& G, const WDn4& Wd) {
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const float rs = SC ? row_rs(c, m) : 1.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float2 h = half_sums(q4dot32(G.a[i], c.L.xq[m][hgi(c)], G.s[i], c.L.xh[m][hgi(c)]));
+      if (c.lane == i) c.L.hb[m][4 * c.wave + i] = silu_f(rs * h.x) * (rs * h.y);
+    }
+  }
+  if (c.tid < MAXM) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this layer's K/V cache stores
+  __syncthreads();
+  u64* g = c.buf(G_PART, (size_t)NWG * MAXM * D) + (size_t)c.w * MAXM * D;
+  const unsigned tg = c.tag();
+  const __amdgpu_buffer_rsrc_t rsc = __builtin_amdgcn_make_buffer_rsrc(g, 0, 0x7fffffff, 0x00020000);
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    float hs = 0.f;
+#pragma unroll
+    for (int j = 0; j < 32; j += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(&c.L.hb[m][j]);
+      hs += (v.x + v.y) + (v.z + v.w);
+    }
+    const float a0 = q4dot32(Wd.a[0], c.L.hb[m], Wd.s[0], hs), a1 = q4dot32(Wd.a[1], c.L.hb[m], Wd.s[1], hs);
+    const u32x4_t v = {__float_as_uint(a0), tg, __float_as_uint(a1), tg};
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rsc, (m * D + 2 * c.tid) * 8, 0, 16);  // sc1
+  }
+}
+// an x hand-off (E3 / E5) -> x, xq = x * nw (padded), xh, per-wave sums of squares (folded RMSNorm)
+template <int M, int DELAY>
+__device__ __forceinline__ void gather_x4(Ctx& c, const u64* buf, float2 nw) {
+  int poff[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) poff[m] = m * D + 2 * c.tid;
+  float sq[MAXM], pr[MAXM];
+  poll_pairs<M, DELAY, DF_REPOLL>(buf, 0x7fffffff, poff, c.tag(), [&](unsigned spin) { return spin_fail(c, spin); },
+                                  [&](const u32x4_t (&g)[M]) {
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const float v0 = __uint_as_float(g[m].x), v1 = __uint_as_float(g[m].z);
+      const float a = v0 * nw.x, b = v1 * nw.y;
+      *reinterpret_cast<float2*>(&c.L.x[m][2 * c.tid]) = make_float2(v0, v1);
+      *reinterpret_cast<float2*>(&c.L.xq[m][0][0] + q4p(2 * c.tid)) = make_float2(a, b);
+      sq[m] = fmaf(v1, v1, v0 * v0);
+      pr[m] = a + b;
+    }
+  });
+  c.stamp();
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    half_group_sum16(c, pr[m], c.L.xh[m]);
+    const float t = wave_sum(sq[m]);
+    if (c.lane == 0) c.L.sq[c.wave][m] = t;
+  }
+  __syncthreads();
+}
+// RMSNorm of rows m < M from L.x (step 1's layer 0: x * rsqrt(mean(x^2) + eps) * nw, as rms_rows) -> xq, xh
+template <int M>
+__device__ __forceinline__ void rms_rows4(Ctx& c, float2 nw) {
+  if (c.wave < M) {
+    const float* x = c.L.x[c.wave];
+    float s = 0.f;
+    for (int k = c.lane; k < D; k += 64) s = fmaf(x[k], x[k], s);
+    s = wave_sum(s);
+    if (c.lane == 0) c.L.wsum[0][c.wave] = s;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const float r = rsqrtf(c.L.wsum[0][m] / (float)D + c.p.eps);
+    const float a = c.L.x[m][2 * c.tid] * r * nw.x, b = c.L.x[m][2 * c.tid + 1] * r * nw.y;
+    *reinterpret_cast<float2*>(&c.L.xq[m][0][0] + q4p(2 * c.tid)) = make_float2(a, b);
+    half_group_sum16(c, a + b, c.L.xh[m]);
+  }
+  __syncthreads();
+}
+
 // Temperature sampling without a top-k threshold (the reference generate()'s default, generation.py:
 // 51-54, :102): handled by per-workgroup Gumbel-max keys (phase_head / gumbel_code), not by handing
 // every logit to every workgroup.
@@ -822,24 +1024,40 @@ __device__ __forceinline__ unsigned long long dkey(double d) {
 }
 
 // Head rows of this WG on row xn[0] (K = 1024 or 2048) -> arg-max key -> E6 granules (hi, lo words)
-template <int KH>
+__device__ __forceinline__ void head_publish(Ctx& c, float s, float t, int n_valid, float* logits, int cb);
+// PAD: the input row is the int4 kernel's padded xq[xm] (element k at q4p(k): an 8-element chunk stays
+// contiguous), else L.xn[xm]
+template <int KH, bool PAD = false>
 __device__ __forceinline__ void phase_head(Ctx& c, const bf16_t* W, int n_valid, const u32x4_t (&wa)[KH / 512],
                                            const u32x4_t (&wx)[KH / 512], float* logits, int cb, int xm = 0, float rs = 1.f) {
   constexpr int CPL = KH / 512;  // chunks per lane
-  const int row = 8 * c.w + c.wave;
-  const float* xin = c.L.xn[xm];  // input row (folded RMSNorm: un-normalised, scaled by rs after the dot)
+  static_assert(!PAD || KH == D, "the padded input holds one decoder row");
+  // input row (folded RMSNorm: un-normalised, scaled by rs after the dot)
+  auto xin = [&](int i) -> const float* {
+    if constexpr (PAD) return &c.L.xq[xm][0][0] + q4p(8 * (c.lane + 64 * i));
+    else return c.L.xn[xm] + 8 * (c.lane + 64 * i);
+  };
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < CPL; ++i) s += dot8(wa[i], xin + 8 * (c.lane + 64 * i));
+  for (int i = 0; i < CPL; ++i) s += dot8(wa[i], xin(i));
   s = wave_sum(s) * rs;
-  unsigned long long best = row < n_valid ? pack_argmax(s, row) : 0ull;
-  if (c.lane == 0 && row < n_valid) logits[row] = s;
-  const int xr = 2048 + c.w;
   float t = 0.f;
   if (c.wave == 0 && c.w < 3) {
 #pragma unroll
-    for (int i = 0; i < CPL; ++i) t += dot8(wx[i], xin + 8 * (c.lane + 64 * i));
+    for (int i = 0; i < CPL; ++i) t += dot8(wx[i], xin(i));
     t = wave_sum(t) * rs;
+  }
+  head_publish(c, s, t, n_valid, logits, cb);
+  (void)W;
+}
+// A head's rows of this WG -- s: row 8w + wave, t: row 2048 + w (wave 0 of WGs 0-2) -- -> logits taps
+// and the hand-off: arg-max keys (E6), Gumbel-max keys, or every logit (sampling with a top-k)
+__device__ __forceinline__ void head_publish(Ctx& c, float s, float t, int n_valid, float* logits, int cb) {
+  const int row = 8 * c.w + c.wave;
+  unsigned long long best = row < n_valid ? pack_argmax(s, row) : 0ull;
+  if (c.lane == 0 && row < n_valid) logits[row] = s;
+  const int xr = 2048 + c.w;
+  if (c.wave == 0 && c.w < 3) {
     const unsigned long long k2 = xr < n_valid ? pack_argmax(t, xr) : 0ull;
     best = k2 > best ? k2 : best;
     if (c.lane == 0 && xr < n_valid) logits[xr] = t;
@@ -1092,13 +1310,44 @@ struct Pre {
   WHd wh;
   float2 nw1;
 };
+struct Pre4 {  // the int4 kernel's (the ci heads stay bf16: audio_head is not quantized)
+  WQkv4 wq;
+  WO4 wo;
+  WGu4 wg;
+  WDn4 wd;
+  WHd wh;
+  float2 nw1;
+};
+template <bool Q4> using PreT = std::conditional_t<Q4, Pre4, Pre>;
+#ifndef DF_GU4_EARLY
+#define DF_GU4_EARLY 2  // int4: gate/up loads per wave fetched before the attention (of 4; the rest after o_proj)
+#endif
+static_assert(DF_FOLD && DF_PAIR16 && DF_E4_16 && DF_KVDIRECT && DF_TAB16 && DF_GU_E45 == 0 && !DF_DN_EARLY &&
+              !DF_DN_AFTER_E1, "the int4 kernel implements the default variants only");
+// weight-format dispatch of the loaders / phases the layer calls
+template <bool Q4, typename P> __device__ __forceinline__ void ld_dn(Ctx& c, int l, P& r) {
+  if constexpr (Q4) load_dn4(c, l, r.wd); else load_dn(c, l, r.wd);
+}
+template <bool Q4, typename P> __device__ __forceinline__ void ld_qkv(Ctx& c, int l, P& r) {
+  if constexpr (Q4) load_qkv4(c, l, r.wq); else load_qkv(c, l, r.wq);
+}
+template <bool Q4, typename P> __device__ __forceinline__ void ld_o(Ctx& c, int l, P& r) {
+  if constexpr (Q4) load_o4(c, l, r.wo); else load_o(c, l, r.wo);
+}
+template <bool Q4, bool EARLY, typename P> __device__ __forceinline__ void ld_gu(Ctx& c, int l, P& r) {
+  if constexpr (Q4) {
+    if constexpr (EARLY) load_gu4<0, DF_GU4_EARLY>(c, l, r.wg); else load_gu4<DF_GU4_EARLY, 4>(c, l, r.wg);
+  } else {
+    if constexpr (EARLY) load_gu<0, GU_EARLY>(c, l, r.wg); else load_gu<GU_EARLY, 8>(c, l, r.wg);
+  }
+}
 
 // One decoder layer of step `step` (M rows at positions pos0..).  FIRST: layer 0, which at steps
 // >= 2 takes q | k | v (RoPE'd) from the folded qkv0 table and its input row from proj_tab (no QKV
 // hand-off).  LAST: the final layer, which also fetches this step's head rows and the next step's
 // layer-0 o / layer-1 QKV slices.
-template <int M, bool FIRST, bool LAST>
-__device__ __forceinline__ void decoder_layer(Ctx& c, int l, int step, int pos0, Pre& r) {
+template <int M, bool FIRST, bool LAST, bool Q4>
+__device__ __forceinline__ void decoder_layer(Ctx& c, int l, int step, int pos0, PreT<Q4>& r) {
   const DecFrameArgs& p = c.p;
   Lds& L = c.L;
   c.refresh();
@@ -1121,7 +1370,7 @@ __device__ __forceinline__ void decoder_layer(Ctx& c, int l, int step, int pos0,
     const int i0 = c.tid, i1 = NT + c.tid;
     const float4 va = i0 < NQ4 ? t4[i0] : x4[i0 - NQ4];
     const float4 vb = i1 < NQ4 + NX4 ? x4[min(i1, NQ4 + NX4 - 1) - NQ4] : make_float4(0.f, 0.f, 0.f, 0.f);
-    load_dn(c, l, r.wd);
+    ld_dn<Q4>(c, l, r);
     auto put4 = [&](int i, const float4 v) {
       if (i < NQ4) {
         qkv_place(c, 0, 4 * i, pos0, v.x);
@@ -1160,12 +1409,17 @@ __device__ __forceinline__ void decoder_layer(Ctx& c, int l, int step, int pos0,
     KvRegs kv;
     if (FIRST && c.tid < M * (HD / 2)) L.rope[c.tid / (HD / 2)][c.tid % (HD / 2)] = rp;
     // layers >= 1 (folded): the previous layer's E5 gather already wrote xn = x * n1
-    if (FIRST || !DF_FOLD) rms_rows<M>(c, r.nw1);  // (its barriers also publish the RoPE rows)
-    phase_qkv<M, DF_FOLD && !FIRST>(c, pos0, r.wq);   // -> E1
+    if constexpr (Q4) {
+      if (FIRST) rms_rows4<M>(c, r.nw1);               // (its barriers also publish the RoPE rows)
+      phase_qkv4<M, !FIRST>(c, pos0, r.wq);            // -> E1
+    } else {
+      if (FIRST || !DF_FOLD) rms_rows<M>(c, r.nw1);  // (its barriers also publish the RoPE rows)
+      phase_qkv<M, DF_FOLD && !FIRST>(c, pos0, r.wq);   // -> E1
+    }
     // prefetches issued after the publish (its RoPE operand load would otherwise retire behind
     // them in vmcnt order), still ahead of the hand-off wait they hide under
     kv_issue(c, l, pos0, kv);
-    if ((FIRST || !DF_DN_EARLY) && !DF_DN_AFTER_E1) load_dn(c, l, r.wd);
+    if ((FIRST || !DF_DN_EARLY) && !DF_DN_AFTER_E1) ld_dn<Q4>(c, l, r);
 #if DF_KVDIRECT
     gather_qkv<M>(c, c.rbuf(G_QKV, MAXM * QKV), pos0, kv);  // (its barrier publishes the history too)
     ++c.e;
@@ -1181,41 +1435,51 @@ __device__ __forceinline__ void decoder_layer(Ctx& c, int l, int step, int pos0,
   c.mark();
   const float2 nw2 = nw_fetch(c, p.n2[l]);
   // DF_DN_AFTER_E1: the down slices issued after the q|k|v wait (not ahead of it) on layers that wait
-  if (DF_DN_AFTER_E1 && !(FIRST && step > 1)) load_dn(c, l, r.wd);
-  if (FIRST || DF_GU_E45 == 0) load_gu<0, GU_EARLY>(c, l, r.wg);  // (layers >= 1: rows < DF_GU_E45 came at E4 / E5)
-  else if (DF_GU_E45 < GU_EARLY) load_gu<DF_GU_E45, GU_EARLY>(c, l, r.wg);
-  phase_attn<M>(c, pos0, l);
+  if constexpr (!Q4) {
+    if (DF_DN_AFTER_E1 && !(FIRST && step > 1)) load_dn(c, l, r.wd);
+    if (FIRST || DF_GU_E45 == 0) load_gu<0, GU_EARLY>(c, l, r.wg);  // (layers >= 1: rows < DF_GU_E45 came at E4 / E5)
+    else if (DF_GU_E45 < GU_EARLY) load_gu<DF_GU_E45, GU_EARLY>(c, l, r.wg);
+  } else {
+    ld_gu<Q4, true>(c, l, r);
+  }
+  phase_attn<M, Q4>(c, pos0, l);
   c.mark();
-  phase_o<M>(c, r.wo);                                // -> E3
+  if constexpr (Q4) phase_o4<M>(c, r.wo);             // -> E3
+  else phase_o<M>(c, r.wo);
   c.mark();
-  load_gu<GU_EARLY, 8>(c, l, r.wg);
-  if (!LAST) { load_qkv(c, l + 1, r.wq); load_o(c, l + 1, r.wo); }
+  ld_gu<Q4, false>(c, l, r);
+  if (!LAST) { ld_qkv<Q4>(c, l + 1, r); ld_o<Q4>(c, l + 1, r); }
 #if DF_FOLD
-  gather_x<M, DF_DELAY_E3>(c, c.rbuf(G_X, MAXM * D), nw2);  // E3 -> x, xn = x * n2
+  if constexpr (Q4) gather_x4<M, DF_DELAY_E3>(c, c.rbuf(G_X, MAXM * D), nw2);  // E3 -> x, xq = x * n2
+  else gather_x<M, DF_DELAY_E3>(c, c.rbuf(G_X, MAXM * D), nw2);  // E3 -> x, xn = x * n2
 #else
   gather<M * D / NT>(c, c.rbuf(G_X, MAXM * D), M * D, &L.x[0][0]);
 #endif
   ++c.e;
   c.refresh();
   if (!DF_FOLD) rms_rows<M>(c, nw2);
-  phase_mlp<M, DF_FOLD>(c, r.wg, r.wd);                // -> E4
+  if constexpr (Q4) phase_mlp4<M, true>(c, r.wg, r.wd);  // -> E4
+  else phase_mlp<M, DF_FOLD>(c, r.wg, r.wd);                // -> E4
   // DF_DN_EARLY: the next layer's down slices stream during this layer's E4 / E5 (its registers
   // were just consumed) instead of during the next E1 wait
-  if (DF_DN_EARLY && !LAST) load_dn(c, l + 1, r.wd);
-  if (DF_GU_E45 > 0 && !LAST) load_gu<0, DF_GU_E45>(c, l + 1, r.wg);
+  if constexpr (!Q4) {
+    if (DF_DN_EARLY && !LAST) load_dn(c, l + 1, r.wd);
+    if (DF_GU_E45 > 0 && !LAST) load_gu<0, DF_GU_E45>(c, l + 1, r.wg);
+  }
   r.nw1 = nw_fetch(c, LAST ? p.norm : p.n1[l + 1]);  // next layer's norm, or the final one
   c.mark();
   if (LAST) {
     load_head(c, p.audio_head + (size_t)(step - 1) * p.VP * D, D, r.wh);
     if (step + 1 < p.K) {
-      load_o(c, 0, r.wo);
-      load_qkv(c, 1, r.wq);
+      ld_o<Q4>(c, 0, r);
+      ld_qkv<Q4>(c, 1, r);
     }
   }
   c.refresh();
   phase_reduce<M>(c);                                 // waits E4, -> E5
 #if DF_FOLD
-  gather_x<M, DF_DELAY_E5>(c, c.rbuf(G_X, MAXM * D), r.nw1);  // E5 -> x, xn = x * (next n1 | final norm)
+  if constexpr (Q4) gather_x4<M, DF_DELAY_E5>(c, c.rbuf(G_X, MAXM * D), r.nw1);  // E5 -> x, xq
+  else gather_x<M, DF_DELAY_E5>(c, c.rbuf(G_X, MAXM * D), r.nw1);  // E5 -> x, xn = x * (next n1 | final norm)
 #else
   gather<M * D / NT>(c, c.rbuf(G_X, MAXM * D), M * D, &L.x[0][0]);
 #endif
@@ -1223,18 +1487,18 @@ __device__ __forceinline__ void decoder_layer(Ctx& c, int l, int step, int pos0,
 }
 
 // One decoder step (generation.py:72-90): 4 layers over the step's M rows, the ci head, the arg-max.
-template <int M>
-__device__ __forceinline__ void run_step(Ctx& c, int step, Pre& r) {
+template <int M, bool Q4>
+__device__ __forceinline__ void run_step(Ctx& c, int step, PreT<Q4>& r) {
   const DecFrameArgs& p = c.p;
   const int pos0 = M == 2 ? 0 : step;  // step 1: positions 0, 1
-  decoder_layer<M, true, false>(c, 0, step, pos0, r);
-  for (int l = 1; l < NL - 1; ++l) decoder_layer<M, false, false>(c, l, step, pos0, r);
-  decoder_layer<M, false, true>(c, NL - 1, step, pos0, r);
+  decoder_layer<M, true, false, Q4>(c, 0, step, pos0, r);
+  for (int l = 1; l < NL - 1; ++l) decoder_layer<M, false, false, Q4>(c, l, step, pos0, r);
+  decoder_layer<M, false, true, Q4>(c, NL - 1, step, pos0, r);
   // ci head on the last row: final norm, audio_head[step - 1] (generation.py:79)
   c.refresh();
 #if DF_FOLD
-  phase_head<D>(c, p.audio_head + (size_t)(step - 1) * p.VP * D, p.V, r.wh.a, r.wh.x, p.ci_logits + (size_t)(step - 1) * p.VP,
-                step, M - 1, row_rs(c, M - 1));  // -> E6
+  phase_head<D, Q4>(c, p.audio_head + (size_t)(step - 1) * p.VP * D, p.V, r.wh.a, r.wh.x, p.ci_logits + (size_t)(step - 1) * p.VP,
+                    step, M - 1, row_rs(c, M - 1));  // -> E6
 #else
   rms_rows<1>(c, r.nw1, M - 1);
   phase_head<D>(c, p.audio_head + (size_t)(step - 1) * p.VP * D, p.V, r.wh.a, r.wh.x, p.ci_logits + (size_t)(step - 1) * p.VP, step);  // -> E6
@@ -1246,13 +1510,67 @@ __device__ __forceinline__ void run_step(Ctx& c, int step, Pre& r) {
   if (c.w == 0 && c.tid == 0) p.codes[step] = ci;
   if (step + 1 < p.K) kv_store(c, step + 1, kv0);  // and in LDS before the loop back-edge
 }
+
+// Frame start of the int4 kernel: codebook0_head (one 2048-wide row per wave: a chunk per lane) and the
+// projection of h_last (waves 0-3, rows 4w + v) against h_last staged in the padded layout -> the same
+// two hand-offs as the bf16 kernel's frame start
+__device__ __forceinline__ void frame_start4(Ctx& c) {
+  const DecFrameArgs& p = c.p;
+  Lds& L = c.L;
+  const char* H = reinterpret_cast<const char*>(p.c0_head);
+  const char* P = reinterpret_cast<const char*>(p.proj);
+  const int sbh = p.VP * RBH;  // codebook0_head's affine words follow its VP rows of nibbles
+  const u32x4_t ha = bload(H, c.wave * RBH + c.lane * 16, 8 * c.w * RBH);
+  const unsigned hs = bload4(H, c.wave * SBRH + (c.lane >> 1) * 4, sbh + 8 * c.w * SBRH);
+  u32x4_t hx = {0u, 0u, 0u, 0u};
+  unsigned hxs = 0u;
+  if (c.wave == 0 && c.w < 3) {
+    hx = bload(H, c.lane * 16, (2048 + c.w) * RBH);
+    hxs = bload4(H, (c.lane >> 1) * 4, sbh + (2048 + c.w) * SBRH);
+  }
+  const int pw = min(c.wave, 3);  // waves 4-7 re-read row 4w + 3 (no branch around a load; unused)
+  const u32x4_t pa = bload(P, pw * RBH + c.lane * 16, 4 * c.w * RBH);
+  const unsigned ps = bload4(P, pw * SBRH + (c.lane >> 1) * 4, SB_PROJ + 4 * c.w * SBRH);
+  // h_last -> hq (padded), hh: thread t stages elements 2t, 2t + 1 and 1024 + 2t, + 1
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int k = h * (DB / 2) + 2 * c.tid;
+    const float2 v = *reinterpret_cast<const float2*>(p.h_last + k);
+    *reinterpret_cast<float2*>(&L.h0.hq[0][0] + q4p(k)) = v;
+    float sum = v.x + v.y;
+    sum += __shfl_xor(sum, 1, 64);
+    sum += __shfl_xor(sum, 2, 64);
+    sum += __shfl_xor(sum, 4, 64);
+    sum += __shfl_xor(sum, 8, 64);
+    if ((c.tid & 15) == 0) L.h0.hh[k >> 5] = sum;
+  }
+  __syncthreads();
+  const float s = wave_sum(q4dot32(ha, L.h0.hq[c.lane], hs, L.h0.hh[c.lane]));
+  float t = 0.f;
+  if (c.wave == 0 && c.w < 3) t = wave_sum(q4dot32(hx, L.h0.hq[c.lane], hxs, L.h0.hh[c.lane]));
+  head_publish(c, s, t, p.V, p.c0_logits, 0);  // -> G_ARG (hand-off 0)
+  const float pv = wave_sum(q4dot32(pa, L.h0.hq[c.lane], ps, L.h0.hh[c.lane]));
+  if (c.lane == 0 && c.wave < 4) L.wsum[c.wave][0] = pv;
+  __syncthreads();
+  if (c.tid < 4 * REP) {
+    const int q = c.tid / REP;
+    c.put(G_X, MAXM * D, 4 * c.w + q, L.wsum[q][0], c.tid % REP);
+  }
+}
 }  // namespace
 
+template <bool Q4>
 __global__ __launch_bounds__(NT, 1) void dec_frame_kernel(DecFrameArgs p) {
   __shared__ __attribute__((aligned(16))) Lds L;
   Ctx c{p, L, (int)blockIdx.x, (int)threadIdx.x, (int)(threadIdx.x & 63), (int)(threadIdx.x >> 6), 0u, 0};
   c.tag0 = __hip_atomic_load(p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
   if (p.stamps && c.tid == 0) p.stamps[(size_t)c.w * DEC_FRAME_STAMPS + DEC_FRAME_STAMPS - 2] = __builtin_amdgcn_s_memrealtime();
+  PreT<Q4> r;
+  if constexpr (Q4) {
+    ld_qkv<Q4>(c, 0, r);
+    ld_o<Q4>(c, 0, r);
+    frame_start4(c);
+  } else {
   // ---- frame start: codebook0_head (K = 2048, 8 rows per WG + 1 for WGs 0-2) and the projection of
   // h_last (rows 4w..4w+3) for decoder step 1, both published in one hand-off
   u32x4_t c0a[4], c0x[4], pa[2];
@@ -1270,7 +1588,6 @@ __global__ __launch_bounds__(NT, 1) void dec_frame_kernel(DecFrameArgs p) {
     pa[0] = bload(pr, pv, 0);
     pa[1] = bload(pr, pv, 1024);
   }
-  Pre r;
   load_qkv(c, 0, r.wq);
   load_o(c, 0, r.wo);
   for (int k = c.tid; k < DB; k += NT) L.xn[0][k] = p.h_last[k];
@@ -1285,6 +1602,7 @@ __global__ __launch_bounds__(NT, 1) void dec_frame_kernel(DecFrameArgs p) {
       const int q = c.tid / REP;
       c.put(G_X, MAXM * D, 4 * c.w + q, L.wsum[2 * q][0] + L.wsum[2 * q + 1][0], c.tid % REP);
     }
+  }
   }
   const int c0 = head_code(c, p.V, 0);
   gather<2>(c, c.rbuf(G_X, MAXM * D), D, L.x[0]);  // x row 0 = projection(h_last)
@@ -1306,16 +1624,19 @@ __global__ __launch_bounds__(NT, 1) void dec_frame_kernel(DecFrameArgs p) {
   r.nw1 = nw_fetch(c, p.n1[0]);  // RMSNorm weights, fetched a phase ahead of use
   // step 1 carries two rows ([h_last, E_a[c0]]), steps >= 2 one: each its own instantiation, so the
   // one-row steps compute and read nothing for a second row
-  run_step<2>(c, 1, r);
-  for (int step = 2; step < p.K; ++step) run_step<1>(c, step, r);
+  run_step<2, Q4>(c, 1, r);
+  for (int step = 2; step < p.K; ++step) run_step<1, Q4>(c, step, r);
   if (p.stamps && c.tid == 0) p.stamps[(size_t)c.w * DEC_FRAME_STAMPS + DEC_FRAME_STAMPS - 1] = __builtin_amdgcn_s_memrealtime();
   if (c.w == 0 && c.tid == 0) __hip_atomic_store(p.epoch, c.tag0 - 1u + (unsigned)c.e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 size_t dec_frame_gbuf_bytes() { return G_TOTAL * sizeof(u64); }
 
-void launch_dec_frame(const DecFrameArgs& p, hipStream_t st) {
-  hipLaunchKernelGGL(dec_frame_kernel, dim3(NWG), dim3(NT), 0, st, p);
+void launch_dec_frame(const DecFrameArgs& p, hipStream_t st, bool q4) {
+  if (q4) hipLaunchKernelGGL(dec_frame_kernel<true>, dim3(NWG), dim3(NT), 0, st, p);
+  else hipLaunchKernelGGL(dec_frame_kernel<false>, dim3(NWG), dim3(NT), 0, st, p);
 }
 
-const void* dec_frame_kernel_ptr() { return reinterpret_cast<const void*>(&dec_frame_kernel); }
+const void* dec_frame_kernel_ptr(bool q4) {
+  return q4 ? reinterpret_cast<const void*>(&dec_frame_kernel<true>) : reinterpret_cast<const void*>(&dec_frame_kernel<false>);
+}

@@ -28,14 +28,18 @@ def _run(model, prompt, frames):
     return hist[: n[0], 0], logs
 
 
-def test_dec_frame_matches_launch_path_and_oracle():
+@pytest.mark.parametrize("dtype", ["bf16", "q4"])
+def test_dec_frame_matches_launch_path_and_oracle(dtype):
+    """q4: dec_frame_kernel<true> (an nn.quantize'd engine: int4 nibbles + group affine words for every
+    decoder projection, codebook0_head and the projection; audio_head bf16) against the int4 GEMV launch
+    path and the oracle on the dequantized weights."""
     from csm_mlx import _lib
     from csm_mlx.generation import generate_codes_batch
     from csm_mlx.models import CSM
     from csm_mlx.sampling import Sampler
     from csm_mlx.tokenizers import tokenize_text_segment
     args, w = csm_weights("1b")
-    model = CSM(args, dtype="bf16")
+    model = CSM(args, dtype=dtype)
     model.load_weights(w)
     L = _lib.lib()
     prompt = tokenize_text_segment(prompt_ids(31), 0, 32)
@@ -57,13 +61,13 @@ def test_dec_frame_matches_launch_path_and_oracle():
     h2, n2, _ = generate_codes_batch(model, [prompt], 40, sampler=Sampler(0.0, 0))
     assert np.array_equal(h1, h2) and np.array_equal(n1, n2)
     assert first_divergence(h1[:12, 0], got) is None
-    orc = oracle_for(args, w, bf16=True).generate_codes(*prompt, 12)
+    orc = oracle_for(args, w, bf16=(dtype == "bf16"), q4=(dtype == "q4")).generate_codes(*prompt, 12)
     assert first_divergence(got, orc) is None
     del model
 
 
-@pytest.mark.parametrize("top_k", [0, 50])
-def test_dec_frame_sampled_matches_launch_path_and_oracle(top_k):
+@pytest.mark.parametrize("top_k,dtype", [(0, "bf16"), (50, "bf16"), (0, "q4"), (50, "q4")])
+def test_dec_frame_sampled_matches_launch_path_and_oracle(top_k, dtype):
     """The reference's default sampler (temperature 0.8, generation.py:102, :51-54; top_k 0) and
     config 3's top-k 50 at batch 1 on the persistent frame decoder: every head hands all its logits
     to every workgroup, which runs sample_kernel's top-k radix select + Gumbel-max.  12 frames: codes
@@ -75,7 +79,7 @@ def test_dec_frame_sampled_matches_launch_path_and_oracle(top_k):
     from csm_mlx.sampling import Sampler
     from csm_mlx.tokenizers import tokenize_text_segment
     args, w = csm_weights("1b")
-    model = CSM(args, dtype="bf16")
+    model = CSM(args, dtype=dtype)
     model.load_weights(w)
     L = _lib.lib()
     prompt = tokenize_text_segment(prompt_ids(33), 0, 32)
@@ -96,7 +100,8 @@ def test_dec_frame_sampled_matches_launch_path_and_oracle(top_k):
     assert len(got) == frames and first_divergence(got, ref) is None, \
         f"sampled dec_frame codes differ from the launch path at {first_divergence(got, ref)}"
     assert np.array_equal(run(), got)                                     # deterministic per seed
-    orc = oracle_for(args, w, bf16=True).generate_codes(*prompt, frames, temperature=0.8, top_k=top_k, seed=seed)
+    orc = oracle_for(args, w, bf16=(dtype == "bf16"), q4=(dtype == "q4")).generate_codes(
+        *prompt, frames, temperature=0.8, top_k=top_k, seed=seed)
     assert first_divergence(got, orc) is None
     del model
 
