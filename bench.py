@@ -208,6 +208,8 @@ CONFIGS = {
             workload="int4 g64 (nn.quantize) csm_1b stream_generate, B=1, greedy, 10 s (per-frame Mimi decode_step)"),
     9: dict(batch=1, dtype="float32", temperature=0.0, top_k=0, stream=False, context=False,
             workload="configs[1] with fp32 weights (MLX's random-init arithmetic class), B=1 greedy, 10 s + Mimi decode"),
+    10: dict(batch=1, dtype="q4", temperature=0.0, top_k=0, stream=False, context=False,
+             workload="configs[1] on int4 g64 weights (nn.quantize): csm_1b greedy generate(), B=1, 10 s + Mimi decode"),
 }
 
 
@@ -312,7 +314,7 @@ def _traffic(key: str):
 
 def rooflines(model, batch: int, iters: int = 400):
     """Live HIP-event rooflines on the engine stream.  ``dominant``: the persistent frame decoder
-    (dec_frame_kernel, one launch per frame) when it runs the frame's head -- batch 1 bf16 --
+    (dec_frame_kernel, one launch per frame) when it runs the frame's head -- batch 1 bf16 or int4 --
     else the decoder gate/up projection at this batch; ``backbone_gate_up`` beside it: the persistent
     backbone step (bb_step_kernel) when it runs the batch-1 backbone, else the backbone gate/up
     projection at this batch."""
@@ -337,14 +339,16 @@ def rooflines(model, batch: int, iters: int = 400):
 
     us, nb = ctypes.c_float(0), ctypes.c_double(0)
     if batch == 1 and iters > 0 and L.csm_bench_bb_step(model.engine, 20, ctypes.byref(us), ctypes.byref(nb)) == 0:
-        out = {"backbone_gate_up": entry(us.value, nb.value, "bb_step_kernel = persistent backbone step: the 16 "
+        bbk = "bb_step_q4_kernel" if model.dtype == "q4" else "bb_step_kernel"
+        out = {"backbone_gate_up": entry(us.value, nb.value, f"{bbk} = persistent backbone step: the 16 "
                                          "backbone blocks + final norm of one decode row, one launch",
                                          f"bb_step/{model.dtype}/B1")}
     else:
         out = {"backbone_gate_up": gemv(0, "backbone")}
     us, nb = ctypes.c_float(0), ctypes.c_double(0)
     if batch == 1 and iters > 0 and L.csm_bench_dec_frame(model.engine, 20, ctypes.byref(us), ctypes.byref(nb)) == 0:
-        out["dominant"] = entry(us.value, nb.value, "dec_frame_kernel = persistent frame decoder: codebook0_head + "
+        dfk = f"dec_frame_kernel<{'true' if model.dtype == 'q4' else 'false'}>"
+        out["dominant"] = entry(us.value, nb.value, f"{dfk} = persistent frame decoder: codebook0_head + "
                                 "31 decoder steps (4 layers + audio_head slice each) of one frame, one launch",
                                 f"dec_frame/{model.dtype}/B1")
     else:
@@ -366,7 +370,7 @@ def main():
     ap.add_argument("--no-decode", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=96, help="oracle frames timed for cpu_baseline (~10 s on 16 cores)")
-    ap.add_argument("--config", type=int, default=0, choices=[0, 2, 3, 4, 5, 6, 7, 8, 9],
+    ap.add_argument("--config", type=int, default=0, choices=[0, 2, 3, 4, 5, 6, 7, 8, 9, 10],
                     help="run BASELINE.json configs[N-1] (batch, dtype, sampling, streaming, context) instead of "
                          "the default configs[1] line; the metric stays audio frames/s")
     ap.add_argument("--roofline-iters", type=int, default=400,
