@@ -182,6 +182,15 @@ struct csm_engine {
   int bb_hw = -1, bb_hw_q4 = -1;
   int df_hw_q4 = -1;
   unsigned long long* bb_stamps = nullptr;  // csm_set_option "bb_step_stamps": per-hand-off clock stamps
+  // persistent batched depth-decoder step (dec_step_xs.hip): codebook steps >= 2 of 1..32 bf16 rows in one
+  // launch instead of run_dec_xs's ~20; csm_set_option "dec_xsd" / CSM_DEC_XSD=0 turn it off
+  bool xsd_on = [] { const char* v = getenv("CSM_DEC_XSD"); return !(v && v[0] == '0'); }();
+  int xsd_hw = -1;
+  DecStepXsArgs xsd{};    // scratch pointers (ensure_batch) + control words
+  unsigned* xsd_ctrl = nullptr;
+  unsigned* xsd_epoch = nullptr;
+  int* xsd_err = nullptr;
+  unsigned long long* xsd_stamps = nullptr;  // csm_set_option "dec_xsd_stamps": per-role clock marks of the last launch
 
   void* balloc(size_t bytes) {
     void* p = nullptr;
@@ -574,17 +583,65 @@ void enqueue_dec_frame(csm_engine* e, hipStream_t st) {
   launch_advance(ap, st);
 }
 
+// The persistent batched decoder step (dec_step_xs.hip) runs a codebook step >= 2 of the streaming
+// matrix-core path (xs_dec) when the decoder has csm_1b's shapes in bf16, the rows fit one 32-row tile and
+// the device holds one 512-thread workgroup on each of its 256 CUs (every workgroup must be resident).
+bool xsd_eligible(csm_engine* e, int M) {
+  if (!e->xsd_on || !e->xsd_ctrl || M < 1 || M > DEC_XSD_MAX_M || e->wdt != WDT_BF16 || e->head_wdt != WDT_BF16 || e->tiled_dirty)
+    return false;
+  const csm_llama_dims& d = e->dec.d;
+  if (d.hidden != 1024 || d.intermediate != 8192 || d.n_heads != 8 || d.n_kv_heads != 2 || d.head_dim != 128 ||
+      d.n_layers != DEC_FRAME_LAYERS || e->dec.S_cap > 32)
+    return false;
+  if (e->xsd_hw < 0) {
+    hipDeviceProp_t prop;
+    int per_cu = 0;
+    e->xsd_hw = hipGetDeviceProperties(&prop, e->dev) == hipSuccess && prop.multiProcessorCount == DEC_XSD_WGS &&
+                        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dec_step_xs_kernel_ptr(), DEC_XSD_THREADS, 0) ==
+                            hipSuccess && per_cu >= 1
+                    ? 1 : 0;
+  }
+  return e->xsd_hw == 1;
+}
+
+// step i >= 2 of the batched decoder: M rows (utterances 0..M-1) at position i; the codes of codebook
+// i - 1 come from the head partials part_prev (part_n per row)
+void launch_xsd(csm_engine* e, int M, int i, const unsigned long long* part_prev, int part_n, hipStream_t st) {
+  DecStepXsArgs a = e->xsd;
+  const Stack& s = e->dec;
+  for (int l = 0; l < DEC_FRAME_LAYERS; ++l) {
+    const LayerW& w = s.L[l];
+    a.wqkv[l] = (const uint8_t*)e->ws.tiled.at(w.wqkv); a.wo[l] = (const uint8_t*)e->ws.tiled.at(w.wo);
+    a.wgu[l] = (const uint8_t*)e->ws.tiled.at(w.wgu); a.wd[l] = (const uint8_t*)e->ws.tiled.at(w.wd);
+    a.n1[l] = w.n1; a.n2[l] = w.n2; a.kc[l] = w.kc; a.vc[l] = w.vc;
+  }
+  a.norm = s.norm; a.rope = s.rope; a.S_cap = s.S_cap; a.eps = s.d.eps;
+  a.M = M; a.step = i;
+  a.part = part_prev; a.part_stride = e->part_stride; a.part_n = part_n; a.V = e->V;
+  a.qkv0_tab = e->qkv0_tab + (size_t)(i - 1) * e->V * s.qkv_rows();
+  a.proj_tab = e->proj_tab + (size_t)(i - 1) * e->V * e->Dd;
+  a.codes = e->codes; a.codes_K = e->K;
+  a.xs_out = e->xs_D; a.ss_out = e->xs_ss; a.ss_stride = GEMM_XS_MAX_M;
+  a.ctrl = e->xsd_ctrl; a.epoch = e->xsd_epoch; a.err = e->xsd_err; a.stamps = e->xsd_stamps;
+  launch_dec_step_xs(a, st);
+}
+
 // A hand-off wait of a persistent kernel that timed out leaves its flag raised: report it.
 // Every raised flag is cleared and named in the one error.
 void check_dec_frame(csm_engine* e) {
   std::string who;
-  for (int* f : {e->df_err, e->bb_err}) {
+  for (int* f : {e->df_err, e->bb_err, e->xsd_err}) {
     if (!f) continue;
     int v = 0;
     HIPCHK(hipMemcpy(&v, f, 4, hipMemcpyDeviceToHost));
     if (v) {
       HIPCHK(hipMemset(f, 0, 4));
-      who += std::string(who.empty() ? "" : " and ") + (f == e->df_err ? "persistent frame decoder" : "persistent backbone step");
+      if (f == e->xsd_err) {  // counters and flags are out of step with the epoch: start both afresh
+        HIPCHK(hipMemset(e->xsd_ctrl, 0, dec_step_xs_ctrl_bytes()));
+        HIPCHK(hipMemset(e->xsd_epoch, 0, 4));
+      }
+      who += std::string(who.empty() ? "" : " and ") +
+             (f == e->df_err ? "persistent frame decoder" : (f == e->bb_err ? "persistent backbone step" : "persistent batched decoder step"));
     }
   }
   if (!who.empty()) throw CsmError(CSM_ERR_HIP, who + ": a hand-off wait timed out (results of this batch are invalid)");
@@ -644,6 +701,7 @@ void enqueue_head_phase(csm_engine* e, hipStream_t st, int phase, int piece = 0)
     RowMap rm = (i == 1) ? RowMap{2, 0, nullptr, 0} : RowMap{1, 0, nullptr, i};
     const bool use_tab = folded && e->use_qkv0_tab && e->qkv0_built && !e->no_tab_batched;
     const bool xs_dec = use_tab && dec_xs_eligible(e, M);  // streaming matrix-core decoder + head
+    bool xsd_used = false;  // the persistent step ran (its combines wrote 32 sum-of-squares tiles)
     // step 1 (two rows per utterance) on the streaming GEMM too: the projected rows split once, layer 0's
     // QKV projected from them; the head stays on the dense path (it reads one row of each pair)
     const bool xs_s1 = i == 1 && !folded && e->xs_step1 && dec_xs_eligible(e, M) && Dd % 512 == 0;
@@ -676,8 +734,14 @@ void enqueue_head_phase(csm_engine* e, hipStream_t st, int phase, int piece = 0)
       a0.g_part = g.xpart; a0.g_part_stride = g.xpart_stride; a0.g_part_n = g.xpart_n; a0.g_V = V;
       a0.g_codes = e->codes; a0.g_codes_K = K; a0.g_cb = i - 1;
       a0.g_xtab = e->proj_tab + (size_t)(i - 1) * V * Dd; a0.g_xout = e->dx; a0.g_D = Dd;
-      if (xs_dec) run_dec_xs(e, M, rm, st, a0);
-      else run_stack(e, e->dec, e->dx, M, e->dq, e->datt, e->dmlp, rm, st, nullptr, &a0);
+      if (xs_dec && xsd_eligible(e, M)) {
+        launch_xsd(e, M, i, g.xpart, g.xpart_n, st);
+        xsd_used = true;
+      } else if (xs_dec) {
+        run_dec_xs(e, M, rm, st, a0);
+      } else {
+        run_stack(e, e->dec, e->dx, M, e->dq, e->datt, e->dmlp, rm, st, nullptr, &a0);
+      }
     } else {
       if (!folded) launch_gemv(g, e->wdt, EPI_STORE, 0, st);
       run_stack(e, e->dec, e->dx, M, e->dq, e->datt, e->dmlp, rm, st, folded ? &g0 : nullptr);
@@ -689,7 +753,7 @@ void enqueue_head_phase(csm_engine* e, hipStream_t st, int phase, int piece = 0)
     g.eps = e->dec.d.eps; g.out = e->ci_logits + (size_t)(i - 1) * B * Vp; g.os = Vp;
     g.part = part(i); g.part_stride = e->part_stride; g.n_valid = V;
     if (xs_dec) {  // the head reads the split rows (x * final norm) the last down wrote
-      g.xs_in = e->xs_D; g.ss_in = e->xs_ss; g.ss_n = gemm_xs_tiles(Dd, e->dec.d.intermediate, M);
+      g.xs_in = e->xs_D; g.ss_in = e->xs_ss; g.ss_n = xsd_used ? 32 : gemm_xs_tiles(Dd, e->dec.d.intermediate, M);
       g.ss_stride = GEMM_XS_MAX_M;
       launch_gemm_xs(g, greedy ? EPI_ARGMAX : EPI_STORE, st, gemv_nt(2), e->head_wdt);
     } else if (!(ablate() & 64)) {
@@ -793,6 +857,28 @@ void ensure_batch(csm_engine* e, int B) {
     e->xs_F = e->balloc(bF);
     e->xs_ss = (float*)e->balloc((size_t)64 * xm * 4);
     for (float** h : {&e->hs_D, &e->hs_A, &e->hs_F}) *h = (float*)e->balloc(bF / xs::XS_EB / xm / 32 * xs::HS_ROWS * 4 + 4096);
+  }
+  // the persistent batched decoder step's scratch (csm_1b decoder shapes only; control words once per engine)
+  {
+    const csm_llama_dims& d = e->dec.d;
+    if (d.hidden == 1024 && d.intermediate == 8192 && d.head_dim == 128 && d.n_heads == 8 && d.n_kv_heads == 2) {
+      const size_t R = DEC_XSD_MAX_M;
+      DecStepXsArgs& x = e->xsd;
+      x.qkv = (float*)e->balloc(R * e->dec.qkv_rows() * 4);
+      x.xs_att = e->balloc(xs::bytes(R, 1024));
+      x.xs_x = e->balloc(xs::bytes(R, 1024));
+      x.xs_h = e->balloc(xs::bytes(R, 8192));
+      x.x_o = (float*)e->balloc(R * 1024 * 4);
+      x.x_d = (float*)e->balloc(R * 1024 * 4);
+      x.ss_o = (float*)e->balloc(32 * R * 4);
+      x.dpart = (float*)e->balloc(8 * R * 1024 * 4);
+      x.code_buf = (int*)e->balloc(R * 4);
+      if (!e->xsd_ctrl) {
+        e->xsd_ctrl = (unsigned*)e->alloc(dec_step_xs_ctrl_bytes());
+        e->xsd_epoch = (unsigned*)e->alloc(16);
+        e->xsd_err = (int*)e->alloc(16);
+      }
+    }
   }
 }
 
@@ -1775,6 +1861,8 @@ int csm_debug_read(csm_engine* e, const char* what, void* host, int64_t nbytes, 
     else if (w == "codes") { src = e->codes; n = B * e->K * 4; }
     else if (w == "pos") { src = e->pos; n = B * 4; }
     else if (w == "dec_frame_epoch") { src = e->df_epoch; n = 4; }
+    else if (w == "dec_xsd_epoch") { src = e->xsd_epoch; n = 4; }
+    else if (w == "dec_xsd_stamps" && e->xsd_stamps) { src = e->xsd_stamps; n = (size_t)DEC_XSD_WGS * DEC_XSD_STAMPS * 8; }
     else if (w == "bb_step_epoch" && e->bb_epoch) { src = e->bb_epoch; n = 4; }  // advances by 80 per row it ran
     else if (w == "bb_step_stamps" && e->bb_stamps) { src = e->bb_stamps; n = (size_t)BB_STEP_WGS * BB_STEP_STAMPS * 8; }  // advances by the hand-offs of every frame it ran
     else if (w == "dec_frame_stamps" && e->df_stamps) { src = e->df_stamps; n = (size_t)DEC_FRAME_WGS * DEC_FRAME_STAMPS * 8; }
@@ -2059,6 +2147,17 @@ int csm_set_option(csm_engine* e, const char* key, int value) {
       if (!e) throw CsmError(CSM_ERR_ARG, "bb_step_stamps needs an engine");
       if (value && !e->bb_stamps) e->bb_stamps = (unsigned long long*)e->alloc((size_t)BB_STEP_WGS * BB_STEP_STAMPS * 8);
       if (!value && e->bb_stamps) { e->release(e->bb_stamps); e->bb_stamps = nullptr; }
+    }
+    else if (k == "dec_xsd_stamps") {
+      if (!e) throw CsmError(CSM_ERR_ARG, "dec_xsd_stamps needs an engine");
+      if (value && !e->xsd_stamps) e->xsd_stamps = (unsigned long long*)e->alloc((size_t)DEC_XSD_WGS * DEC_XSD_STAMPS * 8);
+      if (!value && e->xsd_stamps) { e->release(e->xsd_stamps); e->xsd_stamps = nullptr; }
+      e->g_B = -1;
+    }
+    else if (k == "dec_xsd") {
+      if (!e) throw CsmError(CSM_ERR_ARG, "dec_xsd needs an engine");
+      e->xsd_on = value != 0;
+      e->g_B = -1;  // captured frame graphs hold the previous path
     }
     else if (k == "bb_step") {
       if (!e) throw CsmError(CSM_ERR_ARG, "bb_step needs an engine");

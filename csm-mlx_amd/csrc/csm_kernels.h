@@ -423,3 +423,49 @@ constexpr int DEC_FRAME_WGS = 256, DEC_FRAME_THREADS = 512;
 // audio_head bf16)
 void launch_dec_frame(const DecFrameArgs& p, hipStream_t st, bool q4 = false);
 const void* dec_frame_kernel_ptr(bool q4 = false);  // for the occupancy query
+
+// Persistent batched depth-decoder step (dec_step_xs.hip): the 4 decoder layers of codebook step
+// `step` >= 2 for rows (utterances) 0..M-1, M <= 32, bf16 weights, one launch.
+constexpr int DEC_XSD_WGS = 256, DEC_XSD_THREADS = 512, DEC_XSD_MAX_M = 32;
+struct DecStepXsArgs {
+  const uint8_t* wqkv[DEC_FRAME_LAYERS];  // fragment-tiled bf16 copies (gemm_retile)
+  const uint8_t* wo[DEC_FRAME_LAYERS];
+  const uint8_t* wgu[DEC_FRAME_LAYERS];
+  const uint8_t* wd[DEC_FRAME_LAYERS];
+  const float* n1[DEC_FRAME_LAYERS];
+  const float* n2[DEC_FRAME_LAYERS];
+  const float* norm;                      // decoder final norm
+  const float* rope;                      // [S_cap][HD/2][2]
+  float* kc[DEC_FRAME_LAYERS];            // [B][Hkv][S_cap][HD]
+  float* vc[DEC_FRAME_LAYERS];
+  int S_cap;
+  float eps;
+  int M, step;                            // rows; codebook step (= the rows' position)
+  const unsigned long long* part;         // the previous head's arg-max partials [B][part_stride]
+  int part_stride, part_n, V;
+  const float* qkv0_tab;                  // this step's folded tables: [V][1536] RoPE'd layer-0 q | k | v
+  const float* proj_tab;                  // [V][1024] projection(E_a[c])
+  int* codes;                             // [B][codes_K]: codes[m][step - 1] written
+  int codes_K;
+  // scratch (dec_step_xs_scratch_bytes) and outputs
+  float* qkv;                             // [32][1536]
+  void* xs_att;                           // split rows (xs.h), K = 1024
+  void* xs_x;                             // K = 1024
+  void* xs_h;                             // K = 8192
+  void* xs_out;                           // K = 1024: x * (next n1 | final norm) -- the head's xs_in
+  float* ss_out;                          // [32 tiles][ss_stride] sums of squares -- the head's ss_in
+  int ss_stride;
+  float* x_o;                             // [32][1024]
+  float* x_d;                             // [32][1024]
+  float* ss_o;                            // [32 tiles][32]
+  float* dpart;                           // [8][32][1024]
+  int* code_buf;                          // [32]
+  unsigned* ctrl;                         // hand-off flags / counters (dec_step_xs_ctrl_bytes, zeroed once)
+  unsigned* epoch;                        // advanced by every launch
+  int* err;                               // raised when a hand-off wait times out
+  unsigned long long* stamps;             // optional [NWG][DEC_XSD_STAMPS] s_memrealtime marks (profiling)
+};
+constexpr int DEC_XSD_STAMPS = 64;
+size_t dec_step_xs_ctrl_bytes();
+void launch_dec_step_xs(const DecStepXsArgs& p, hipStream_t st);
+const void* dec_step_xs_kernel_ptr();
