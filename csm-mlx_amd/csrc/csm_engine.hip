@@ -191,6 +191,7 @@ struct csm_engine {
   unsigned* xsd_epoch = nullptr;
   int* xsd_err = nullptr;
   unsigned long long* xsd_stamps = nullptr;  // csm_set_option "dec_xsd_stamps": per-role clock marks of the last launch
+  bool xsd_head = [] { const char* v = getenv("CSM_DEC_XSD_HEAD"); return !(v && v[0] == '0'); }();  // "dec_xsd_head": the head in the same launch
 
   void* balloc(size_t bytes) {
     void* p = nullptr;
@@ -606,7 +607,9 @@ bool xsd_eligible(csm_engine* e, int M) {
 
 // step i >= 2 of the batched decoder: M rows (utterances 0..M-1) at position i; the codes of codebook
 // i - 1 come from the head partials part_prev (part_n per row)
-void launch_xsd(csm_engine* e, int M, int i, const unsigned long long* part_prev, int part_n, hipStream_t st) {
+// returns true when the step's head ran in the same launch (its logits and arg-max partials are written)
+bool launch_xsd(csm_engine* e, int M, int i, const unsigned long long* part_prev, int part_n, unsigned long long* part_out,
+                hipStream_t st) {
   DecStepXsArgs a = e->xsd;
   const Stack& s = e->dec;
   for (int l = 0; l < DEC_FRAME_LAYERS; ++l) {
@@ -623,7 +626,16 @@ void launch_xsd(csm_engine* e, int M, int i, const unsigned long long* part_prev
   a.codes = e->codes; a.codes_K = e->K;
   a.xs_out = e->xs_D; a.ss_out = e->xs_ss; a.ss_stride = GEMM_XS_MAX_M;
   a.ctrl = e->xsd_ctrl; a.epoch = e->xsd_epoch; a.err = e->xsd_err; a.stamps = e->xsd_stamps;
+  // the head in the same launch: 64-row tiles, one arg-max partial each -- the launch path's partial count
+  const int Vp = e->Vpad, ht = (Vp + 63) / 64;
+  const void* hw = (const char*)e->audio_head + (size_t)(i - 1) * Vp * e->Dd * 2;
+  auto it = e->ws.tiled.find(hw);
+  if (e->xsd_head && it != e->ws.tiled.end() && ht == head_blocks(Vp, e->Dd, M, e->head_wdt) && ht <= 64) {
+    a.head_w = (const uint8_t*)it->second; a.head_nt32 = (Vp + 31) / 32; a.head_tiles = ht; a.Vp = Vp; a.n_valid = e->V;
+    a.head_out = e->ci_logits + (size_t)(i - 1) * e->B * Vp; a.head_part = part_out;
+  }
   launch_dec_step_xs(a, st);
+  return a.head_w != nullptr;
 }
 
 // A hand-off wait of a persistent kernel that timed out leaves its flag raised: report it.
@@ -702,6 +714,7 @@ void enqueue_head_phase(csm_engine* e, hipStream_t st, int phase, int piece = 0)
     const bool use_tab = folded && e->use_qkv0_tab && e->qkv0_built && !e->no_tab_batched;
     const bool xs_dec = use_tab && dec_xs_eligible(e, M);  // streaming matrix-core decoder + head
     bool xsd_used = false;  // the persistent step ran (its combines wrote 32 sum-of-squares tiles)
+    bool xsd_head_done = false;  // ... and the head in the same launch
     // step 1 (two rows per utterance) on the streaming GEMM too: the projected rows split once, layer 0's
     // QKV projected from them; the head stays on the dense path (it reads one row of each pair)
     const bool xs_s1 = i == 1 && !folded && e->xs_step1 && dec_xs_eligible(e, M) && Dd % 512 == 0;
@@ -735,7 +748,7 @@ void enqueue_head_phase(csm_engine* e, hipStream_t st, int phase, int piece = 0)
       a0.g_codes = e->codes; a0.g_codes_K = K; a0.g_cb = i - 1;
       a0.g_xtab = e->proj_tab + (size_t)(i - 1) * V * Dd; a0.g_xout = e->dx; a0.g_D = Dd;
       if (xs_dec && xsd_eligible(e, M)) {
-        launch_xsd(e, M, i, g.xpart, g.xpart_n, st);
+        xsd_head_done = launch_xsd(e, M, i, g.xpart, g.xpart_n, part(i), st);
         xsd_used = true;
       } else if (xs_dec) {
         run_dec_xs(e, M, rm, st, a0);
@@ -752,7 +765,9 @@ void enqueue_head_phase(csm_engine* e, hipStream_t st, int phase, int piece = 0)
     g.x = e->dx + (i == 1 ? Dd : 0); g.xs = (i == 1 ? 2 * Dd : Dd); g.M = B; g.nw = e->dec.norm;
     g.eps = e->dec.d.eps; g.out = e->ci_logits + (size_t)(i - 1) * B * Vp; g.os = Vp;
     g.part = part(i); g.part_stride = e->part_stride; g.n_valid = V;
-    if (xs_dec) {  // the head reads the split rows (x * final norm) the last down wrote
+    if (xsd_head_done) {
+      // (logits and arg-max partials written by the persistent step)
+    } else if (xs_dec) {  // the head reads the split rows (x * final norm) the last down wrote
       g.xs_in = e->xs_D; g.ss_in = e->xs_ss; g.ss_n = xsd_used ? 32 : gemm_xs_tiles(Dd, e->dec.d.intermediate, M);
       g.ss_stride = GEMM_XS_MAX_M;
       launch_gemm_xs(g, greedy ? EPI_ARGMAX : EPI_STORE, st, gemv_nt(2), e->head_wdt);
@@ -2152,6 +2167,11 @@ int csm_set_option(csm_engine* e, const char* key, int value) {
       if (!e) throw CsmError(CSM_ERR_ARG, "dec_xsd_stamps needs an engine");
       if (value && !e->xsd_stamps) e->xsd_stamps = (unsigned long long*)e->alloc((size_t)DEC_XSD_WGS * DEC_XSD_STAMPS * 8);
       if (!value && e->xsd_stamps) { e->release(e->xsd_stamps); e->xsd_stamps = nullptr; }
+      e->g_B = -1;
+    }
+    else if (k == "dec_xsd_head") {
+      if (!e) throw CsmError(CSM_ERR_ARG, "dec_xsd_head needs an engine");
+      e->xsd_head = value != 0;
       e->g_B = -1;
     }
     else if (k == "dec_xsd") {

@@ -464,6 +464,13 @@ struct DecStepXsArgs {
   unsigned* epoch;                        // advanced by every launch
   int* err;                               // raised when a hand-off wait times out
   unsigned long long* stamps;             // optional [NWG][DEC_XSD_STAMPS] s_memrealtime marks (profiling)
+  // the step's head in the same launch (head_w null: a launch of its own after this one):
+  // audio_head[step - 1]'s fragment-tiled copy (head_nt32 32-row tiles of the Vp padded rows), logits ->
+  // head_out [M][Vp], one arg-max partial per 64-row tile (head_tiles of them) -> head_part[m][part_stride]
+  const uint8_t* head_w;
+  int head_nt32, head_tiles, Vp, n_valid;
+  float* head_out;
+  unsigned long long* head_part;
 };
 constexpr int DEC_XSD_STAMPS = 64;
 size_t dec_step_xs_ctrl_bytes();

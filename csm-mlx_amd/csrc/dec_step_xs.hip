@@ -12,8 +12,9 @@
 // Roles (NWG = 256 workgroups x 8 waves, w = blockIdx.x), per layer:
 //   Q  w < 48        QKV tile w (32 of the 1536 rows), full K: x * n1 (split rows) -> RoPE, q | k | v
 //                    rows + the K/V cache row at pos                              -> flag F1[w]
-//   A  every w       attention of row m = w / 8, query head h = w % 8 over keys 0..pos (wave 0; layer 0
-//                    takes q | k | v of the row's code from the folded table)    -> counter C2 (XCD shard)
+//   A  80 <= w < 112 attention of row m = w - 80, query head h = wave, keys 0..pos (the cached rows staged in
+//                    LDS at the layer start; layer 0 takes q | k | v of the row's code from the folded
+//                    table)                                                      -> counter C2
 //   O  48 <= w < 80  o_proj tile j = w - 48 (32 columns), full K: + residual -> x_o, x_o * n2 (split),
 //                    row sums of squares                                         -> flag F3[j]
 //   G  every w       gate/up tiles 2b, 2b + 1, b = 32 (w % 8) + w / 8 (the SiLU*up columns 32b..32b+31)
@@ -57,7 +58,9 @@ constexpr int D = 1024, F = 8192, HQ = 8, HKV = 2, HD = 128, NL = DEC_FRAME_LAYE
 constexpr int KS_D = D / 64, KS_F = F / 64;  // K stages of 64
 constexpr int NQT = QKV / 32, NDT = D / 32;   // 48 QKV tiles; 32 o_proj / down / combine tiles
 constexpr int NGRP = 8;                       // down K groups (1024 h columns each)
-constexpr int O_WG0 = NQT;
+constexpr int O_WG0 = NQT;       // o_proj workgroups 48 .. 79
+constexpr int A_WG0 = O_WG0 + 32; // attention workgroups 80 .. 111 (row m = w - 80, wave = query head)
+constexpr int H_WG0 = A_WG0 + 32; // head workgroups 112 .. (64 padded-vocabulary rows each)
 constexpr unsigned SPIN_LIMIT = 1u << 22;
 constexpr int SC1 = 16;  // buffer cache policy: sc1 (agent-coherent)
 static_assert(NWG == 256 && NWV == 8, "roles assume 256 workgroups of 8 waves");
@@ -72,9 +75,13 @@ struct Lds {
   float red[NWV][16][64];  // one tile's per-wave accumulators
   float ct[2][32][33];     // reduced tiles [batch row][column]
   float rs[32];            // row scales
-  float qsh[HD];           // attention: the scaled query
-  float Ks[32][HD + 4];    // attention: keys 0..pos (rows padded: conflict-free row-parallel reads)
-  float Vs[32][HD];        //            values
+  // attention workgroups (wave = query head): cached keys / values 0..pos-1 of both kv heads (rows padded:
+  // conflict-free row-parallel reads), each wave's scaled query and the new key / value row at pos
+  float Ks[HKV][32][HD + 4];
+  float Vs[HKV][32][HD];
+  float qsh[HQ][HD];
+  float kn[HQ][HD];
+  float vn[HQ][HD];
   int flag;
 };
 
@@ -267,133 +274,155 @@ __device__ __forceinline__ void role_q(Ctx& c, int l, const WT& W) {
   c.mark(2);
 }
 
-// The cached K / V rows 0..pos-1 of the attention's (row, kv head) -> LDS (written by earlier launches:
-// plain loads), at the start of the layer, before any hand-off wait of the workgroup
+// The cached K / V rows 0..pos-1 of the attention workgroup's row, both kv heads -> LDS (written by earlier
+// launches: plain loads), at the start of the layer, before any hand-off wait of the workgroup
 __device__ __forceinline__ void stage_kv(Ctx& c, int l) {
   const DecStepXsArgs& p = c.p;
-  const int m = c.w >> 3, g = (c.w & 7) / (HQ / HKV), pos = p.step;
-  if (m >= p.M) return;
+  const int m = c.w - A_WG0, pos = p.step;
+  if (m < 0 || m >= p.M) return;
   typedef float f4 __attribute__((ext_vector_type(4)));
-  const float* K = p.kc[l] + ((size_t)m * HKV + g) * p.S_cap * HD;
-  const float* V = p.vc[l] + ((size_t)m * HKV + g) * p.S_cap * HD;
-  for (int e = c.tid; e < pos * (HD / 4); e += NT) {
-    const int jj = e / (HD / 4), d4 = e % (HD / 4);
-    *reinterpret_cast<f4*>(&c.L.Ks[jj][4 * d4]) = *reinterpret_cast<const f4*>(K + (size_t)jj * HD + 4 * d4);
-    *reinterpret_cast<f4*>(&c.L.Vs[jj][4 * d4]) = *reinterpret_cast<const f4*>(V + (size_t)jj * HD + 4 * d4);
+  // 2 kv heads x pos rows x 32 float4 of K, then of V: <= 4 float4 per thread per round, a round's loads in
+  // flight together (two round trips, under the Q hand-off the attention waits for anyway)
+  constexpr int PER = HKV * 32 * (HD / 4) / NT;
+  const int n4 = pos * (HD / 4);
+#pragma unroll
+  for (int kv = 0; kv < 2; ++kv) {
+    const float* src = kv ? p.vc[l] : p.kc[l];
+    f4 t[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int e = c.tid + u * NT, g = e / (32 * (HD / 4)), r = e % (32 * (HD / 4));
+      if (r < n4) t[u] = *reinterpret_cast<const f4*>(src + (((size_t)m * HKV + g) * p.S_cap) * HD + 4 * (size_t)r);
+    }
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int e = c.tid + u * NT, g = e / (32 * (HD / 4)), r = e % (32 * (HD / 4));
+      if (r < n4) {
+        float* dst = kv ? &c.L.Vs[g][r / (HD / 4)][4 * (r % (HD / 4))] : &c.L.Ks[g][r / (HD / 4)][4 * (r % (HD / 4))];
+        *reinterpret_cast<f4*>(dst) = t[u];
+      }
+    }
   }
 }
 
-// A: attention of row m, head h, keys 0..pos -> xs_att (split rows of the o_proj).  The cached K / V rows
-// are in LDS (stage_kv); wave 0 fetches the row at pos and the query (layer 0: of the row's code, from
-// the folded table; else from the QKV tiles, after their flags) and computes.
+// A (workgroups A_WG0 .. A_WG0 + 31): attention of row m = w - A_WG0, query head h = wave, keys 0..pos ->
+// xs_att (split rows of the o_proj).  The cached K / V rows are in LDS (stage_kv); each wave fetches its
+// query and the new key / value row at pos (layer 0: of the row's code, from the folded table; else from
+// the QKV tiles, after their flags) and computes.
 __device__ __forceinline__ void role_a(Ctx& c, int l) {
   const DecStepXsArgs& p = c.p;
-  const int m = c.w >> 3, h = c.w & 7, g = h / (HQ / HKV), pos = p.step, n = pos + 1;
+  const int m = c.w - A_WG0, h = c.wave, g = h / (HQ / HKV), pos = p.step, n = pos + 1;
   const unsigned tag = c.ep * NL + l + 1;
   typedef float f4 __attribute__((ext_vector_type(4)));
+  const int lane = c.lane;
+  c.sub(7);
   if (m < p.M) {
-    if (c.wave == 0) {
-      const int lane = c.lane;
-      const float scale = 0.08838834764831845f;  // 1 / sqrt(128)
-      float2 qv, kv2, vv2;
-      if (l == 0) {
-        // the row's code: arg-max of the previous head's partials (or the sampler's single partial)
-        const unsigned long long best = wave_argmax_partials(p.part + (size_t)m * p.part_stride, p.part_n, lane);
-        const int code = min(max(unpack_argmax(best), 0), p.V - 1);
-        const float* trow = p.qkv0_tab + (size_t)code * QKV;  // RoPE'd q | k | v of layer 0 (static table)
-        qv = reinterpret_cast<const float2*>(trow + h * HD)[lane];
-        kv2 = reinterpret_cast<const float2*>(trow + HQ * HD + g * HD)[lane];
-        vv2 = reinterpret_cast<const float2*>(trow + (HQ + HKV) * HD + g * HD)[lane];
-        if (h % (HQ / HKV) == 0) {  // this kv head's row at pos -> cache (later codebook steps)
-          const size_t o = (((size_t)m * HKV + g) * p.S_cap + pos) * HD + 2 * lane;
-          *reinterpret_cast<float2*>(p.kc[0] + o) = kv2;
-          *reinterpret_cast<float2*>(p.vc[0] + o) = vv2;
-        }
-        if (h == 0 && lane == 0) {
-          p.codes[(size_t)m * p.codes_K + pos - 1] = code;
-          __hip_atomic_store(p.code_buf + m, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      } else {
-        // q tiles 4h..4h+3, k tiles 32 + 4g.., v tiles 40 + 4g..
-        if (lane < 12) {
-          const int t = lane < 4 ? 4 * h + lane : (lane < 8 ? HQ * 4 + 4 * g + lane - 4 : (HQ + HKV) * 4 + 4 * g + lane - 8);
-          const unsigned* a = c.cw(CW_F1 + t);
-          __builtin_amdgcn_s_sleep(8);
-          for (unsigned spin = 0; (int)(ld_cw(a) - tag) < 0; ++spin) {
-            if (spin_fail(c, spin)) break;
-            __builtin_amdgcn_s_sleep(2);
-          }
-        }
-        // (the wave leaves the poll loop once every polling lane has matched)
-        const float* row = p.qkv + (size_t)m * QKV;
-        qv = ld8(row + h * HD + 2 * lane);
-        kv2 = ld8(row + HQ * HD + g * HD + 2 * lane);
-        vv2 = ld8(row + (HQ + HKV) * HD + g * HD + 2 * lane);
+    const float scale = 0.08838834764831845f;  // 1 / sqrt(128)
+    float2 qv, kv2, vv2;
+    if (l == 0) {
+      // the row's code: arg-max of the previous head's partials (or the sampler's single partial)
+      const unsigned long long best = wave_argmax_partials(p.part + (size_t)m * p.part_stride, p.part_n, lane);
+      const int code = min(max(unpack_argmax(best), 0), p.V - 1);
+      const float* trow = p.qkv0_tab + (size_t)code * QKV;  // RoPE'd q | k | v of layer 0 (static table)
+      qv = reinterpret_cast<const float2*>(trow + h * HD)[lane];
+      kv2 = reinterpret_cast<const float2*>(trow + HQ * HD + g * HD)[lane];
+      vv2 = reinterpret_cast<const float2*>(trow + (HQ + HKV) * HD + g * HD)[lane];
+      if (h % (HQ / HKV) == 0) {  // this kv head's row at pos -> cache (later codebook steps)
+        const size_t o = (((size_t)m * HKV + g) * p.S_cap + pos) * HD + 2 * lane;
+        *reinterpret_cast<float2*>(p.kc[0] + o) = kv2;
+        *reinterpret_cast<float2*>(p.vc[0] + o) = vv2;
       }
-      *reinterpret_cast<float2*>(&c.L.qsh[2 * lane]) = make_float2(qv.x * scale, qv.y * scale);
-      *reinterpret_cast<float2*>(&c.L.Ks[pos][2 * lane]) = kv2;
-      *reinterpret_cast<float2*>(&c.L.Vs[pos][2 * lane]) = vv2;
+      if (h == 0 && lane == 0) {
+        p.codes[(size_t)m * p.codes_K + pos - 1] = code;
+        __hip_atomic_store(p.code_buf + m, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    } else {
+      // q tiles 4h..4h+3, k tiles 32 + 4g.., v tiles 40 + 4g..
+      if (lane < 12) {
+        const int t = lane < 4 ? 4 * h + lane : (lane < 8 ? HQ * 4 + 4 * g + lane - 4 : (HQ + HKV) * 4 + 4 * g + lane - 8);
+        const unsigned* a = c.cw(CW_F1 + t);
+        __builtin_amdgcn_s_sleep(8);
+        for (unsigned spin = 0; (int)(ld_cw(a) - tag) < 0; ++spin) {
+          if (spin_fail(c, spin)) break;
+          __builtin_amdgcn_s_sleep(2);
+        }
+      }
+      // (the wave leaves the poll loop once every polling lane has matched)
+      c.sub(8);
+      const float* row = p.qkv + (size_t)m * QKV;
+      qv = ld8(row + h * HD + 2 * lane);
+      kv2 = ld8(row + HQ * HD + g * HD + 2 * lane);
+      vv2 = ld8(row + (HQ + HKV) * HD + g * HD + 2 * lane);
     }
-    __syncthreads();
-    c.mark(3);
-    if (c.wave == 0) {
-      // lane = (key kj = lane & 31, half hh of the head dims): scores from two half dots added by one
-      // shuffle, max-subtracted softmax, P.V in key order (lane = key half kv, dims 4 dq .. + 3)
-      const int lane = c.lane, kj = lane & 31, hh = lane >> 5, kv = lane >> 5, dq = lane & 31;
-      float s;
-      {
-        const f4* kr = reinterpret_cast<const f4*>(&c.L.Ks[min(kj, pos)][hh * (HD / 2)]);
-        const f4* qr = reinterpret_cast<const f4*>(c.L.qsh + hh * (HD / 2));
-        float d0 = 0.f, d1 = 0.f, d2 = 0.f, d3 = 0.f;
-#pragma unroll
-        for (int d4 = 0; d4 < HD / 8; ++d4) {
-          const f4 a = kr[d4], q4 = qr[d4];
-          d0 = fmaf(q4.x, a.x, d0);
-          d1 = fmaf(q4.y, a.y, d1);
-          d2 = fmaf(q4.z, a.z, d2);
-          d3 = fmaf(q4.w, a.w, d3);
-        }
-        const float part = (d0 + d1) + (d2 + d3);
-        const float other = __shfl_xor(part, 32, 64);
-        s = hh == 0 ? part + other : other + part;
-        if (kj >= n) s = -INFINITY;
-      }
-      const float mx = wave_max(s);
-      const float pj = kj < n ? expf(s - mx) : 0.f;
-      const float l_run = wave_sum(hh == 0 ? pj : 0.f);
-      const int pji = __float_as_int(pj);
-      f4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int u0 = 0; u0 < 16; u0 += 8) {
-        if (u0 < n) {
-          f4 vv[8];
-#pragma unroll
-          for (int u = 0; u < 8; ++u) vv[u] = *reinterpret_cast<const f4*>(&c.L.Vs[16 * kv + u0 + u][4 * dq]);
-#pragma unroll
-          for (int u = 0; u < 8; ++u) {
-            const float pa = __int_as_float(__builtin_amdgcn_readlane(pji, u0 + u));
-            const float pb = __int_as_float(__builtin_amdgcn_readlane(pji, 16 + u0 + u));
-            const float pw = kv ? pb : pa;
-            if (16 * kv + u0 + u < n) {
-              acc.x = fmaf(pw, vv[u].x, acc.x);
-              acc.y = fmaf(pw, vv[u].y, acc.y);
-              acc.z = fmaf(pw, vv[u].z, acc.z);
-              acc.w = fmaf(pw, vv[u].w, acc.w);
-            }
-          }
-        }
-      }
-      const float inv = 1.f / l_run;
-      const float t0 = __shfl_xor(acc.x, 32, 64), t1 = __shfl_xor(acc.y, 32, 64), t2 = __shfl_xor(acc.z, 32, 64),
-                  t3 = __shfl_xor(acc.w, 32, 64);
-      if (lane < 32)
-        st16(p.xs_att, xs::off(D, m, h * HD + 4 * dq),
-             f32x4_t{(acc.x + t0) * inv, (acc.y + t1) * inv, (acc.z + t2) * inv, (acc.w + t3) * inv});
-      drain();
-    }
+    *reinterpret_cast<float2*>(&c.L.qsh[h][2 * lane]) = make_float2(qv.x * scale, qv.y * scale);
+    *reinterpret_cast<float2*>(&c.L.kn[h][2 * lane]) = kv2;
+    *reinterpret_cast<float2*>(&c.L.vn[h][2 * lane]) = vv2;
+    c.sub(9);
   }
-  // one arrival per workgroup (rows past M arrive without work): wave 0 stored and drained
-  if (c.tid == 0) add_ctr(c.cw(CW_C2 + (c.w & 7)));
+  __syncthreads();  // stage_kv's rows (every wave) and this wave's own rows
+  c.mark(3);
+  if (m < p.M) {
+    // lane = (key kj = lane & 31, half hh of the head dims): scores from two half dots added by one
+    // shuffle, max-subtracted softmax, P.V in key order (lane = key half kv, dims 4 dq .. + 3)
+    const int kj = lane & 31, hh = lane >> 5, kv = lane >> 5, dq = lane & 31;
+    float s;
+    {
+      const float* krow = kj < pos ? &c.L.Ks[g][kj][0] : &c.L.kn[h][0];
+      const f4* kr = reinterpret_cast<const f4*>(krow + hh * (HD / 2));
+      const f4* qr = reinterpret_cast<const f4*>(&c.L.qsh[h][hh * (HD / 2)]);
+      float d0 = 0.f, d1 = 0.f, d2 = 0.f, d3 = 0.f;
+#pragma unroll
+      for (int d4 = 0; d4 < HD / 8; ++d4) {
+        const f4 a = kr[d4], q4 = qr[d4];
+        d0 = fmaf(q4.x, a.x, d0);
+        d1 = fmaf(q4.y, a.y, d1);
+        d2 = fmaf(q4.z, a.z, d2);
+        d3 = fmaf(q4.w, a.w, d3);
+      }
+      const float part = (d0 + d1) + (d2 + d3);
+      const float other = __shfl_xor(part, 32, 64);
+      s = hh == 0 ? part + other : other + part;
+      if (kj >= n) s = -INFINITY;
+    }
+    const float mx = wave_max(s);
+    const float pj = kj < n ? expf(s - mx) : 0.f;
+    const float l_run = wave_sum(hh == 0 ? pj : 0.f);
+    const int pji = __float_as_int(pj);
+    f4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u0 = 0; u0 < 16; u0 += 8) {
+      if (u0 < n) {
+        f4 vv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int jj = 16 * kv + u0 + u;
+          vv[u] = *reinterpret_cast<const f4*>(jj < pos ? &c.L.Vs[g][jj][4 * dq] : &c.L.vn[h][4 * dq]);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const float pa = __int_as_float(__builtin_amdgcn_readlane(pji, u0 + u));
+          const float pb = __int_as_float(__builtin_amdgcn_readlane(pji, 16 + u0 + u));
+          const float pw = kv ? pb : pa;
+          if (16 * kv + u0 + u < n) {
+            acc.x = fmaf(pw, vv[u].x, acc.x);
+            acc.y = fmaf(pw, vv[u].y, acc.y);
+            acc.z = fmaf(pw, vv[u].z, acc.z);
+            acc.w = fmaf(pw, vv[u].w, acc.w);
+          }
+        }
+      }
+    }
+    const float inv = 1.f / l_run;
+    const float t0 = __shfl_xor(acc.x, 32, 64), t1 = __shfl_xor(acc.y, 32, 64), t2 = __shfl_xor(acc.z, 32, 64),
+                t3 = __shfl_xor(acc.w, 32, 64);
+    if (lane < 32)
+      st16(p.xs_att, xs::off(D, m, h * HD + 4 * dq),
+           f32x4_t{(acc.x + t0) * inv, (acc.y + t1) * inv, (acc.z + t2) * inv, (acc.w + t3) * inv});
+  }
+  drain();
+  __syncthreads();
+  // one arrival per attention workgroup (rows past M arrive without work)
+  if (c.tid == 0) add_ctr(c.cw(CW_C2));
   c.mark(4);
 }
 
@@ -402,7 +431,7 @@ __device__ __forceinline__ void role_o(Ctx& c, int l, const WT& W) {
   const DecStepXsArgs& p = c.p;
   const int j = c.w - O_WG0;
   const unsigned tag = c.ep * NL + l + 1;
-  wait_words(c, 8, [](int i) { return CW_C2 + i; }, tag * (NWG / 8));
+  wait_words(c, 1, [](int) { return CW_C2; }, tag * 32);
   c.mark(5);
   AF A;
   load_af(p.xs_att, 2 * c.wave, c.lane, A);
@@ -517,37 +546,114 @@ __device__ __forceinline__ void role_d(Ctx& c, int l, const WT& W) {
   c.mark(11);
 }
 
+// H: audio_head[step - 1] rows 64 t .. 64 t + 63 (two 32-row tiles) of the final-normed rows (the last
+// combines' split x * norm + sums of squares) -> logits [row][Vp] and the tile's arg-max partial per row
+// (pack_argmax: the largest logit, the first index on ties), exactly the partial layout of the launch
+// path's head (gemm_xs EPI_ARGMAX, 64-row tiles), which the next step / advance_kernel reduce
+__device__ __forceinline__ void role_h(Ctx& c, const WT (&W)[2]) {
+  const DecStepXsArgs& p = c.p;
+  const int t = c.w - H_WG0;
+  const unsigned tag = c.ep * NL + NL;  // the last layer's combine flags
+  wait_words(c, NDT, [](int i) { return CW_F5 + i; }, tag);
+  AF A;
+  load_af(p.xs_out, 2 * c.wave, c.lane, A);
+  row_scales(c, p.ss_out, p.ss_stride);
+  f32x16_t acc[2];
+  mma<2>(A, W, acc);
+  reduce_tiles<2>(c, acc);
+  // row m = tid / 16, columns 4 (tid % 16) .. + 3 of the 64
+  const int m = c.tid >> 4, c4 = 4 * (c.tid & 15), n = 64 * t + c4;
+  const float r = c.L.rs[m];
+  unsigned long long best = 0;
+  if (m < p.M && n < p.Vp) {
+    const float4 v = make_float4(c.L.ct[c4 >> 5][m][c4 & 31] * r, c.L.ct[c4 >> 5][m][(c4 & 31) + 1] * r,
+                                 c.L.ct[c4 >> 5][m][(c4 & 31) + 2] * r, c.L.ct[c4 >> 5][m][(c4 & 31) + 3] * r);
+    *reinterpret_cast<float4*>(p.head_out + (size_t)m * p.Vp + n) = v;
+    const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (n + i < p.n_valid) {
+        const unsigned long long k = pack_argmax(vv[i], n + i);
+        best = k > best ? k : best;
+      }
+  }
+#pragma unroll
+  for (int o = 1; o < 16; o <<= 1) {
+    const unsigned long long v = __shfl_xor(best, o, 64);
+    best = v > best ? v : best;
+  }
+  if (m < p.M && (c.tid & 15) == 0) p.head_part[(size_t)m * p.part_stride + t] = best;
+}
+
+// The layer loop of one workgroup class (each its own straight-line code: exact register liveness per
+// class, no merged paths holding another class's prefetch registers).  CLS: 0 QKV, 1 o_proj,
+// 2 attention, 3 head (+ plain), 4 plain (gate/up + down only).
+enum { C_Q = 0, C_O = 1, C_A = 2, C_H = 3, C_P = 4 };
+template <int CLS>
+__device__ __forceinline__ void run_layers(Ctx& c) {
+  static_assert(CLS >= C_Q && CLS <= C_P, "workgroup class");
+  const DecStepXsArgs& p = c.p;
+  const int b = 32 * (c.w & 7) + (c.w >> 3), g = c.w & 7, j = c.w >> 3;
+  WT wq, wgu[2], wd;
+  auto ld_gu = [&](int l) {
+    load_wt(p.wgu[l], 2 * b, KS_D, 2 * c.wave, c.lane, wgu[0]);
+    load_wt(p.wgu[l], 2 * b + 1, KS_D, 2 * c.wave, c.lane, wgu[1]);
+  };
+  // layer 0's o_proj (O) and gate/up tiles: in flight through the attention
+  if constexpr (CLS == C_O) load_wt(p.wo[0], c.w - O_WG0, KS_D, 2 * c.wave, c.lane, wq);
+  if constexpr (CLS != C_A) ld_gu(0);
+  for (int l = 0; l < NL; ++l) {
+    c.l = l;
+    c.mark(0);
+    // gate/up tiles: vmcnt retires in issue order and every publish drains it, so a workgroup whose next
+    // steps are latency-critical loads + a publish (Q, A) issues them after that publish
+    if constexpr (CLS == C_O || CLS == C_H || CLS == C_P) {
+      if (l > 0) ld_gu(l);
+    }
+    if constexpr (CLS == C_O) {
+      if (l > 0) load_wt(p.wo[l], c.w - O_WG0, KS_D, 2 * c.wave, c.lane, wq);
+    }
+    if constexpr (CLS == C_Q) {
+      if (l > 0) {
+        role_q(c, l, wq);
+        ld_gu(l);
+      }
+    }
+    if constexpr (CLS == C_A) {
+      stage_kv(c, l);  // (role_a's barrier publishes the LDS rows)
+      role_a(c, l);
+      ld_gu(l);
+    }
+    if constexpr (CLS == C_O) role_o(c, l, wq);
+    role_g(c, l, wgu);
+    // the down tile and the next layer's QKV tile (the last layer: the head tiles) stream during the h
+    // hand-off
+    load_wt(p.wd[l], j, KS_F, 16 * g + 2 * c.wave, c.lane, wd);
+    if constexpr (CLS == C_Q) {
+      if (l + 1 < NL) load_wt(p.wqkv[l + 1], c.w, KS_D, 2 * c.wave, c.lane, wq);
+    }
+    if constexpr (CLS == C_H) {
+      if (l + 1 == NL) {  // (a 32-row tile past the last is clamped: its columns are never stored)
+        load_wt(p.head_w, 2 * (c.w - H_WG0), KS_D, 2 * c.wave, c.lane, wgu[0]);
+        load_wt(p.head_w, min(2 * (c.w - H_WG0) + 1, p.head_nt32 - 1), KS_D, 2 * c.wave, c.lane, wgu[1]);
+      }
+    }
+    role_d(c, l, wd);
+  }
+  if constexpr (CLS == C_H) role_h(c, wgu);
+}
+
 }  // namespace
 
 __global__ __launch_bounds__(NT, 1) void dec_step_xs_kernel(DecStepXsArgs p) {
   __shared__ __attribute__((aligned(16))) Lds L;
   Ctx c{p, L, (int)blockIdx.x, (int)threadIdx.x, (int)(threadIdx.x & 63), __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), 0u};
   c.ep = __hip_atomic_load(p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const bool isq = c.w < NQT, iso = c.w >= O_WG0 && c.w < O_WG0 + NDT;
-  const int b = 32 * (c.w & 7) + (c.w >> 3), g = c.w & 7, j = c.w >> 3;
-  WT wq, wgu[2], wd;
-  // layer 0's o_proj (O) and gate/up tiles: in flight through the attention
-  if (iso) load_wt(p.wo[0], c.w - O_WG0, KS_D, 2 * c.wave, c.lane, wq);
-  load_wt(p.wgu[0], 2 * b, KS_D, 2 * c.wave, c.lane, wgu[0]);
-  load_wt(p.wgu[0], 2 * b + 1, KS_D, 2 * c.wave, c.lane, wgu[1]);
-  for (int l = 0; l < NL; ++l) {
-    c.l = l;
-    c.mark(0);
-    stage_kv(c, l);  // (role_q's barriers and role_a's publish the LDS rows)
-    if (l > 0 && isq) role_q(c, l, wq);
-    if (l > 0 && iso) load_wt(p.wo[l], c.w - O_WG0, KS_D, 2 * c.wave, c.lane, wq);  // Q and O workgroups are disjoint
-    role_a(c, l);
-    if (iso) role_o(c, l, wq);
-    role_g(c, l, wgu);
-    // the down tile and the next layer's QKV tile stream during the h hand-off
-    load_wt(p.wd[l], j, KS_F, 16 * g + 2 * c.wave, c.lane, wd);
-    if (l + 1 < NL && isq) load_wt(p.wqkv[l + 1], c.w, KS_D, 2 * c.wave, c.lane, wq);
-    role_d(c, l, wd);
-    if (l + 1 < NL) {
-      load_wt(p.wgu[l + 1], 2 * b, KS_D, 2 * c.wave, c.lane, wgu[0]);
-      load_wt(p.wgu[l + 1], 2 * b + 1, KS_D, 2 * c.wave, c.lane, wgu[1]);
-    }
-  }
+  if (c.w < NQT) run_layers<C_Q>(c);
+  else if (c.w < O_WG0 + NDT) run_layers<C_O>(c);
+  else if (c.w < A_WG0 + 32) run_layers<C_A>(c);
+  else if (p.head_w && c.w < H_WG0 + p.head_tiles) run_layers<C_H>(c);
+  else run_layers<C_P>(c);
   if (p.stamps && c.tid == 0) p.stamps[(size_t)c.w * DEC_XSD_STAMPS + DEC_XSD_STAMPS - 1] = __builtin_amdgcn_s_memrealtime();
   if (c.w == 0 && c.tid == 0) __hip_atomic_store(p.epoch, c.ep + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

@@ -51,11 +51,12 @@ for l in range(4):
 print("(median/max over the role's workgroups, us since the first workgroup started)")
 # layer 1 sub-phases, relative to the role's own wait end (median over its workgroups)
 sub = {0: ("Q mma+reduce", isq, 13), 1: ("Q stores issued", isq, 13), 2: ("G mma issued", None, 19),
-       3: ("G reduce", None, 19), 4: ("G stores issued", None, 19), 5: ("D mma+reduce", None, 21), 6: ("O mma+reduce", iso, 17)}
+       3: ("G reduce", None, 19), 4: ("G stores issued", None, 19), 5: ("D mma+reduce", None, 21), 6: ("O mma+reduce", iso, 17),
+       7: ("A entered (after stage_kv)", None, 12), 8: ("A polled (wave 0)", None, 12), 9: ("A rows loaded (wave 0)", None, 12)}
 for k, (nm, sel, base) in sub.items():
     col = rel[:, 48 + k] - rel[:, base]
     col = col if sel is None else col[sel]
-    print(f"  L1 {nm}: {np.nanmedian(col):.2f} us after its wait (max {np.nanmax(col):.2f})")
+    print(f"  L1 {nm}: {np.nanmedian(col):.2f} us after {'the layer start' if base == 12 else 'its wait'} (max {np.nanmax(col):.2f})")
 for nm, a, b_, sel in (("Q publish (drain+barrier)", 49, 14, isq), ("G publish (drain+barrier)", 52, 20, None)):
     col = rel[:, b_] - rel[:, a]
     col = col if sel is None else col[sel]
