@@ -142,8 +142,10 @@ __device__ __forceinline__ f32x4_t ld16(const void* base, size_t off) {
 __device__ __forceinline__ float ld4(const float* p) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc(p), 0, 0, SC1));
 }
-__device__ __forceinline__ float2 ld8(const float* p) {
-  return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rsrc(p), 0, 0, SC1));
+// (base wave-uniform -- it rides in the buffer descriptor; a per-lane base would make the compiler
+// loop over the lanes' distinct descriptors -- and the lane's byte offset in the vector offset)
+__device__ __forceinline__ float2 ld8(const float* base, int off) {
+  return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rsrc(base), off, 0, SC1));
 }
 __device__ __forceinline__ void st4(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
@@ -281,28 +283,27 @@ __device__ __forceinline__ void stage_kv(Ctx& c, int l) {
   const int m = c.w - A_WG0, pos = p.step;
   if (m < 0 || m >= p.M) return;
   typedef float f4 __attribute__((ext_vector_type(4)));
-  // 2 kv heads x pos rows x 32 float4 of K, then of V: <= 4 float4 per thread per round, a round's loads in
-  // flight together (two round trips, under the Q hand-off the attention waits for anyway)
+  // 2 kv heads x pos rows x 32 float4 of K and of V: <= 8 float4 per thread, all in flight together
   constexpr int PER = HKV * 32 * (HD / 4) / NT;
   const int n4 = pos * (HD / 4);
+  f4 t[2][PER];
 #pragma unroll
-  for (int kv = 0; kv < 2; ++kv) {
-    const float* src = kv ? p.vc[l] : p.kc[l];
-    f4 t[PER];
+  for (int kv = 0; kv < 2; ++kv)
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int e = c.tid + u * NT, g = e / (32 * (HD / 4)), r = e % (32 * (HD / 4));
-      if (r < n4) t[u] = *reinterpret_cast<const f4*>(src + (((size_t)m * HKV + g) * p.S_cap) * HD + 4 * (size_t)r);
+      if (r < n4) t[kv][u] = *reinterpret_cast<const f4*>((kv ? p.vc[l] : p.kc[l]) + (((size_t)m * HKV + g) * p.S_cap) * HD + 4 * (size_t)r);
     }
+#pragma unroll
+  for (int kv = 0; kv < 2; ++kv)
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
       const int e = c.tid + u * NT, g = e / (32 * (HD / 4)), r = e % (32 * (HD / 4));
       if (r < n4) {
         float* dst = kv ? &c.L.Vs[g][r / (HD / 4)][4 * (r % (HD / 4))] : &c.L.Ks[g][r / (HD / 4)][4 * (r % (HD / 4))];
-        *reinterpret_cast<f4*>(dst) = t[u];
+        *reinterpret_cast<f4*>(dst) = t[kv][u];
       }
     }
-  }
 }
 
 // A (workgroups A_WG0 .. A_WG0 + 31): attention of row m = w - A_WG0, query head h = wave, keys 0..pos ->
@@ -350,9 +351,9 @@ __device__ __forceinline__ void role_a(Ctx& c, int l) {
       // (the wave leaves the poll loop once every polling lane has matched)
       c.sub(8);
       const float* row = p.qkv + (size_t)m * QKV;
-      qv = ld8(row + h * HD + 2 * lane);
-      kv2 = ld8(row + HQ * HD + g * HD + 2 * lane);
-      vv2 = ld8(row + (HQ + HKV) * HD + g * HD + 2 * lane);
+      qv = ld8(row, (h * HD + 2 * lane) * 4);
+      kv2 = ld8(row, (HQ * HD + g * HD + 2 * lane) * 4);
+      vv2 = ld8(row, ((HQ + HKV) * HD + g * HD + 2 * lane) * 4);
     }
     *reinterpret_cast<float2*>(&c.L.qsh[h][2 * lane]) = make_float2(qv.x * scale, qv.y * scale);
     *reinterpret_cast<float2*>(&c.L.kn[h][2 * lane]) = kv2;
