@@ -14,11 +14,11 @@
 //                    rows + the K/V cache row at pos                              -> flag F1[w]
 //   A  80 <= w < 112 attention of row m = w - 80, query head h = wave, keys 0..pos (the cached rows staged in
 //                    LDS at the layer start; layer 0 takes q | k | v of the row's code from the folded
-//                    table)                                                      -> counter C2
+//                    table)                                                      -> flag F2[m]
 //   O  48 <= w < 80  o_proj tile j = w - 48 (32 columns), full K: + residual -> x_o, x_o * n2 (split),
 //                    row sums of squares                                         -> flag F3[j]
 //   G  every w       gate/up tiles 2b, 2b + 1, b = 32 (w % 8) + w / 8 (the SiLU*up columns 32b..32b+31)
-//                                                                                -> counter CH[w % 8]
+//                                                                                -> flag FH[w]
 //   D  every w       down, output tile j = w / 8 over h columns 1024 g .. + 1023, g = w % 8 (the G
 //                    workgroups of group g: the same XCD under round-robin placement, speed only)
 //                    -> partial tile; arrival ticket C4[j]; the eighth arrival sums the 8 partials in group
@@ -67,12 +67,12 @@ static_assert(NWG == 256 && NWV == 8, "roles assume 256 workgroups of 8 waves");
 static_assert(KS_D == 2 * NWV && KS_F / NGRP == 2 * NWV, "every wave takes two K stages of its tile");
 
 // control words (u32), one per 128-B line
-enum { CW_F1 = 0, CW_C2 = CW_F1 + NQT, CW_F3 = CW_C2 + 8, CW_CH = CW_F3 + NDT, CW_C4 = CW_CH + NGRP, CW_F5 = CW_C4 + NDT,
+enum { CW_F1 = 0, CW_F2 = CW_F1 + NQT, CW_F3 = CW_F2 + 32, CW_FH = CW_F3 + NDT, CW_C4 = CW_FH + NWG, CW_F5 = CW_C4 + NDT,
        CW_N = CW_F5 + NDT };
 constexpr int CW_STRIDE = 32;
 
 struct Lds {
-  float red[NWV][16][64];  // one tile's per-wave accumulators
+  float red[NWV][2][16][64];  // the per-wave accumulators of up to two tiles
   float ct[2][32][33];     // reduced tiles [batch row][column]
   float rs[32];            // row scales
   // attention workgroups (wave = query head): cached keys / values 0..pos-1 of both kv heads (rows padded:
@@ -194,20 +194,18 @@ __device__ __forceinline__ void mma(const AF& A, const WT (&W)[NTL], f32x16_t (&
 template <int NTL>
 __device__ __forceinline__ void reduce_tiles(Ctx& c, const f32x16_t (&acc)[NTL]) {
 #pragma unroll
-  for (int t = 0; t < NTL; ++t) {
-    if (t > 0) __syncthreads();
+  for (int t = 0; t < NTL; ++t)
 #pragma unroll
-    for (int j = 0; j < 16; ++j) c.L.red[c.wave][j][c.lane] = acc[t][j];
-    __syncthreads();
+    for (int j = 0; j < 16; ++j) c.L.red[c.wave][t][j][c.lane] = acc[t][j];
+  __syncthreads();
 #pragma unroll
-    for (int e0 = 0; e0 < 1024; e0 += NT) {
-      const int e = e0 + c.tid, m = e >> 5, col = e & 31;
-      const int j = (m & 3) + 4 * (m >> 3), ln = col + 32 * ((m >> 2) & 1);
-      float v = c.L.red[0][j][ln];
+  for (int e0 = 0; e0 < NTL * 1024; e0 += NT) {
+    const int e = e0 + c.tid, t = e >> 10, m = (e >> 5) & 31, col = e & 31;
+    const int j = (m & 3) + 4 * (m >> 3), ln = col + 32 * ((m >> 2) & 1);
+    float v = c.L.red[0][t][j][ln];
 #pragma unroll
-      for (int wv = 1; wv < NWV; ++wv) v += c.L.red[wv][j][ln];
-      c.L.ct[t][m][col] = v;
-    }
+    for (int wv = 1; wv < NWV; ++wv) v += c.L.red[wv][t][j][ln];
+    c.L.ct[t][m][col] = v;
   }
   __syncthreads();
 }
@@ -422,8 +420,8 @@ __device__ __forceinline__ void role_a(Ctx& c, int l) {
   }
   drain();
   __syncthreads();
-  // one arrival per attention workgroup (rows past M arrive without work)
-  if (c.tid == 0) add_ctr(c.cw(CW_C2));
+  // one flag per attention workgroup (rows past M publish without work)
+  if (c.tid == 0) set_flag(c.cw(CW_F2 + m), tag);
   c.mark(4);
 }
 
@@ -432,7 +430,7 @@ __device__ __forceinline__ void role_o(Ctx& c, int l, const WT& W) {
   const DecStepXsArgs& p = c.p;
   const int j = c.w - O_WG0;
   const unsigned tag = c.ep * NL + l + 1;
-  wait_words(c, 1, [](int) { return CW_C2; }, tag * 32);
+  wait_words(c, 32, [](int i) { return CW_F2 + i; }, tag);
   c.mark(5);
   AF A;
   load_af(p.xs_att, 2 * c.wave, c.lane, A);
@@ -496,7 +494,7 @@ __device__ __forceinline__ void role_g(Ctx& c, int l, const WT (&W)[2]) {
   c.sub(4);
   drain();
   __syncthreads();
-  if (c.tid == 0) add_ctr(c.cw(CW_CH + (c.w & 7)));
+  if (c.tid == 0) set_flag(c.cw(CW_FH + c.w), tag);
   c.mark(8);
 }
 
@@ -505,7 +503,7 @@ __device__ __forceinline__ void role_d(Ctx& c, int l, const WT& W) {
   const DecStepXsArgs& p = c.p;
   const int g = c.w & 7, j = c.w >> 3;
   const unsigned tag = c.ep * NL + l + 1;
-  wait_words(c, 1, [g](int) { return CW_CH + g; }, tag * 32);
+  wait_words(c, 32, [g](int i) { return CW_FH + g + 8 * i; }, tag);  // the G workgroups of group g
   c.mark(9);
   AF A;
   load_af(p.xs_h, 16 * g + 2 * c.wave, c.lane, A);
@@ -596,23 +594,24 @@ __device__ __forceinline__ void run_layers(Ctx& c) {
   const DecStepXsArgs& p = c.p;
   const int b = 32 * (c.w & 7) + (c.w >> 3), g = c.w & 7, j = c.w >> 3;
   WT wq, wgu[2], wd;
+  // vmcnt retires in issue order and every publish drains it: a prefetch issued just before a hand-off
+  // poll or a latency-critical operand load holds that back, so each class issues its next tiles after
+  // its own latency-critical steps (Q, A: after their publish)
   auto ld_gu = [&](int l) {
     load_wt(p.wgu[l], 2 * b, KS_D, 2 * c.wave, c.lane, wgu[0]);
     load_wt(p.wgu[l], 2 * b + 1, KS_D, 2 * c.wave, c.lane, wgu[1]);
   };
-  // layer 0's o_proj (O) and gate/up tiles: in flight through the attention
+  if constexpr (CLS == C_Q) load_wt(p.wqkv[1], c.w, KS_D, 2 * c.wave, c.lane, wq);
   if constexpr (CLS == C_O) load_wt(p.wo[0], c.w - O_WG0, KS_D, 2 * c.wave, c.lane, wq);
   if constexpr (CLS != C_A) ld_gu(0);
   for (int l = 0; l < NL; ++l) {
     c.l = l;
     c.mark(0);
-    // gate/up tiles: vmcnt retires in issue order and every publish drains it, so a workgroup whose next
-    // steps are latency-critical loads + a publish (Q, A) issues them after that publish
     if constexpr (CLS == C_O || CLS == C_H || CLS == C_P) {
-      if (l > 0) ld_gu(l);
-    }
-    if constexpr (CLS == C_O) {
-      if (l > 0) load_wt(p.wo[l], c.w - O_WG0, KS_D, 2 * c.wave, c.lane, wq);
+      if (l > 0) {
+        if constexpr (CLS == C_O) load_wt(p.wo[l], c.w - O_WG0, KS_D, 2 * c.wave, c.lane, wq);
+        ld_gu(l);
+      }
     }
     if constexpr (CLS == C_Q) {
       if (l > 0) {
@@ -627,21 +626,18 @@ __device__ __forceinline__ void run_layers(Ctx& c) {
     }
     if constexpr (CLS == C_O) role_o(c, l, wq);
     role_g(c, l, wgu);
-    // the down tile and the next layer's QKV tile (the last layer: the head tiles) stream during the h
-    // hand-off
-    load_wt(p.wd[l], j, KS_F, 16 * g + 2 * c.wave, c.lane, wd);
-    if constexpr (CLS == C_Q) {
-      if (l + 1 < NL) load_wt(p.wqkv[l + 1], c.w, KS_D, 2 * c.wave, c.lane, wq);
-    }
-    if constexpr (CLS == C_H) {
-      if (l + 1 == NL) {  // (a 32-row tile past the last is clamped: its columns are never stored)
-        load_wt(p.head_w, 2 * (c.w - H_WG0), KS_D, 2 * c.wave, c.lane, wgu[0]);
-        load_wt(p.head_w, min(2 * (c.w - H_WG0) + 1, p.head_nt32 - 1), KS_D, 2 * c.wave, c.lane, wgu[1]);
-      }
-    }
+    load_wt(p.wd[l], j, KS_F, 16 * g + 2 * c.wave, c.lane, wd);  // during the h hand-off
     role_d(c, l, wd);
+    // the next layer's QKV tile: during the combine the Q hand-off waits for
+    if constexpr (CLS == C_Q) {
+      if (l > 0 && l + 1 < NL) load_wt(p.wqkv[l + 1], c.w, KS_D, 2 * c.wave, c.lane, wq);
+    }
   }
-  if constexpr (CLS == C_H) role_h(c, wgu);
+  if constexpr (CLS == C_H) {  // (a 32-row tile past the last is clamped: its columns are never stored)
+    load_wt(p.head_w, 2 * (c.w - H_WG0), KS_D, 2 * c.wave, c.lane, wgu[0]);
+    load_wt(p.head_w, min(2 * (c.w - H_WG0) + 1, p.head_nt32 - 1), KS_D, 2 * c.wave, c.lane, wgu[1]);
+    role_h(c, wgu);
+  }
 }
 
 }  // namespace
