@@ -74,7 +74,7 @@ constexpr int CW_STRIDE = 32;
 struct Lds {
   float red[NWV][2][16][64];  // the per-wave accumulators of up to two tiles
   float ct[2][32][33];     // reduced tiles [batch row][column]
-  float rs[32];            // row scales
+  float rsp[8][32];        // row scales: partial sums of squares (row_scales)
   // attention workgroups (wave = query head): cached keys / values 0..pos-1 of both kv heads (rows padded:
   // conflict-free row-parallel reads), each wave's scaled query and the new key / value row at pos
   float Ks[HKV][32][HD + 4];
@@ -210,20 +210,25 @@ __device__ __forceinline__ void reduce_tiles(Ctx& c, const f32x16_t (&acc)[NTL])
   __syncthreads();
 }
 
-// row scales rsqrt(sum_t ss[t][m] / D + eps) from 32 tiles' partial sums of squares (sc1), threads < 32
-// (all 32 loads in flight together, then summed in tile order)
+// Row scales rsqrt(sum_t ss[t][m] / D + eps) from 32 tiles' partial sums of squares (sc1): threads < 256
+// each add 4 tiles of one row (loads in flight together) into L.rsp[part][row]; row_scale() adds the 8
+// parts in order once a barrier (reduce_tiles') has published them
 __device__ __forceinline__ void row_scales(Ctx& c, const float* ss, int stride) {
-  if (c.tid < 32) {
+  if (c.tid < 256) {
+    const int m = c.tid & 31, q = c.tid >> 5;
     const __amdgpu_buffer_rsrc_t rs = rsrc(ss);
-    float v[32];
+    float v[4];
 #pragma unroll
-    for (int t = 0; t < 32; ++t)
-      v[t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, c.tid * 4, __builtin_amdgcn_readfirstlane(t * stride * 4), SC1));
-    float s = 0.f;
-#pragma unroll
-    for (int t = 0; t < 32; ++t) s += v[t];
-    c.L.rs[c.tid] = rsqrtf(s / (float)D + c.p.eps);
+    for (int t = 0; t < 4; ++t)
+      v[t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, (m + 4 * q * stride) * 4, t * stride * 4, SC1));
+    c.L.rsp[q][m] = ((v[0] + v[1]) + v[2]) + v[3];
   }
+}
+__device__ __forceinline__ float row_scale(const Ctx& c, int m) {
+  float s = c.L.rsp[0][m];
+#pragma unroll
+  for (int q = 1; q < 8; ++q) s += c.L.rsp[q][m];
+  return rsqrtf(s / (float)D + c.p.eps);
 }
 
 // sum over the 8 lanes of a row group (lanes 8r .. 8r + 7), fixed butterfly order
@@ -251,7 +256,7 @@ __device__ __forceinline__ void role_q(Ctx& c, int l, const WT& W) {
   c.sub(0);
   // rows m = tid / 16, columns 2 (tid % 16) + {0, 1} (RoPE pairs)
   const int m = c.tid >> 4, cc = 2 * (c.tid & 15), n = 32 * T + cc;
-  const float r = c.L.rs[m];
+  const float r = row_scale(c, m);
   float a = c.L.ct[0][m][cc] * r, b = c.L.ct[0][m][cc + 1] * r;
   if (n < (HQ + HKV) * HD) {
     const float2 cs = reinterpret_cast<const float2*>(p.rope)[(size_t)p.step * (HD / 2) + (n % HD) / 2];
@@ -481,7 +486,7 @@ __device__ __forceinline__ void role_g(Ctx& c, int l, const WT (&W)[2]) {
   c.sub(3);
   if (c.tid < 256) {
     const int m = c.tid >> 3, q = c.tid & 7;
-    const float r = c.L.rs[m];
+    const float r = row_scale(c, m);
     float hv[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -562,7 +567,7 @@ __device__ __forceinline__ void role_h(Ctx& c, const WT (&W)[2]) {
   reduce_tiles<2>(c, acc);
   // row m = tid / 16, columns 4 (tid % 16) .. + 3 of the 64
   const int m = c.tid >> 4, c4 = 4 * (c.tid & 15), n = 64 * t + c4;
-  const float r = c.L.rs[m];
+  const float r = row_scale(c, m);
   unsigned long long best = 0;
   if (m < p.M && n < p.Vp) {
     const float4 v = make_float4(c.L.ct[c4 >> 5][m][c4 & 31] * r, c.L.ct[c4 >> 5][m][(c4 & 31) + 1] * r,
@@ -597,9 +602,13 @@ __device__ __forceinline__ void run_layers(Ctx& c) {
   // vmcnt retires in issue order and every publish drains it: a prefetch issued just before a hand-off
   // poll or a latency-critical operand load holds that back, so each class issues its next tiles after
   // its own latency-critical steps (Q, A: after their publish)
+  // the plain and head classes (the most registers to spare) fetch their down tile with gate/up: a load
+  // issued just before the h hand-off's poll would hold the poll back (vmcnt order)
+  constexpr bool WD_EARLY = CLS == C_P || CLS == C_H;
   auto ld_gu = [&](int l) {
     load_wt(p.wgu[l], 2 * b, KS_D, 2 * c.wave, c.lane, wgu[0]);
     load_wt(p.wgu[l], 2 * b + 1, KS_D, 2 * c.wave, c.lane, wgu[1]);
+    if constexpr (WD_EARLY) load_wt(p.wd[l], j, KS_F, 16 * g + 2 * c.wave, c.lane, wd);
   };
   if constexpr (CLS == C_Q) load_wt(p.wqkv[1], c.w, KS_D, 2 * c.wave, c.lane, wq);
   if constexpr (CLS == C_O) load_wt(p.wo[0], c.w - O_WG0, KS_D, 2 * c.wave, c.lane, wq);
@@ -626,7 +635,7 @@ __device__ __forceinline__ void run_layers(Ctx& c) {
     }
     if constexpr (CLS == C_O) role_o(c, l, wq);
     role_g(c, l, wgu);
-    load_wt(p.wd[l], j, KS_F, 16 * g + 2 * c.wave, c.lane, wd);  // during the h hand-off
+    if constexpr (!WD_EARLY) load_wt(p.wd[l], j, KS_F, 16 * g + 2 * c.wave, c.lane, wd);  // during the h hand-off
     role_d(c, l, wd);
     // the next layer's QKV tile: during the combine the Q hand-off waits for
     if constexpr (CLS == C_Q) {
