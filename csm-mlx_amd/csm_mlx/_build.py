@@ -23,7 +23,8 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wno-unused-re
 # waits at 256 VGPRs; the AMDGPU scheduler's own register-pressure trackers keep it from spilling
 # them (55 -> 5 spilled VGPRs; a spill store waits for its load, draining the prefetch).
 SRC_FLAGS = {"dec_frame.hip": ["-mllvm", "-amdgpu-use-amdgpu-trackers=1"],
-             "bb_step.hip": ["-mllvm", "-amdgpu-use-amdgpu-trackers=1"]}
+             "bb_step.hip": ["-mllvm", "-amdgpu-use-amdgpu-trackers=1"],
+             "dec_step_xs.hip": ["-mllvm", "-amdgpu-use-amdgpu-trackers=1"]}
 
 
 def _sources():

@@ -185,7 +185,7 @@ struct csm_engine {
   // persistent batched depth-decoder step (dec_step_xs.hip): codebook steps >= 2 of 1..32 bf16 rows in one
   // launch instead of run_dec_xs's ~20; csm_set_option "dec_xsd" / CSM_DEC_XSD=0 turn it off
   bool xsd_on = [] { const char* v = getenv("CSM_DEC_XSD"); return !(v && v[0] == '0'); }();
-  int xsd_hw = -1;
+  int xsd_hw = -1, xsd_hw_q4 = -1;
   DecStepXsArgs xsd{};    // scratch pointers (ensure_batch) + control words
   unsigned* xsd_ctrl = nullptr;
   unsigned* xsd_epoch = nullptr;
@@ -588,21 +588,24 @@ void enqueue_dec_frame(csm_engine* e, hipStream_t st) {
 // matrix-core path (xs_dec) when the decoder has csm_1b's shapes in bf16, the rows fit one 32-row tile and
 // the device holds one 512-thread workgroup on each of its 256 CUs (every workgroup must be resident).
 bool xsd_eligible(csm_engine* e, int M) {
-  if (!e->xsd_on || !e->xsd_ctrl || M < 1 || M > DEC_XSD_MAX_M || e->wdt != WDT_BF16 || e->head_wdt != WDT_BF16 || e->tiled_dirty)
+  const bool q4 = e->wdt == WDT_Q4;
+  if (!e->xsd_on || !e->xsd_ctrl || M < 1 || M > (q4 ? DEC_XSD_MAX_M_Q4 : DEC_XSD_MAX_M) || (e->wdt != WDT_BF16 && !q4) ||
+      e->head_wdt != WDT_BF16 || e->tiled_dirty || GEMM_XS_MAX_M != 64)
     return false;
   const csm_llama_dims& d = e->dec.d;
   if (d.hidden != 1024 || d.intermediate != 8192 || d.n_heads != 8 || d.n_kv_heads != 2 || d.head_dim != 128 ||
       d.n_layers != DEC_FRAME_LAYERS || e->dec.S_cap > 32)
     return false;
-  if (e->xsd_hw < 0) {
+  int& hw = q4 ? e->xsd_hw_q4 : e->xsd_hw;
+  if (hw < 0) {
     hipDeviceProp_t prop;
     int per_cu = 0;
-    e->xsd_hw = hipGetDeviceProperties(&prop, e->dev) == hipSuccess && prop.multiProcessorCount == DEC_XSD_WGS &&
-                        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dec_step_xs_kernel_ptr(), DEC_XSD_THREADS, 0) ==
-                            hipSuccess && per_cu >= 1
-                    ? 1 : 0;
+    hw = hipGetDeviceProperties(&prop, e->dev) == hipSuccess && prop.multiProcessorCount == DEC_XSD_WGS &&
+                 hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, dec_step_xs_kernel_ptr(q4), DEC_XSD_THREADS, 0) ==
+                     hipSuccess && per_cu >= 1
+             ? 1 : 0;
   }
-  return e->xsd_hw == 1;
+  return hw == 1;
 }
 
 // step i >= 2 of the batched decoder: M rows (utterances 0..M-1) at position i; the codes of codebook
@@ -625,6 +628,7 @@ bool launch_xsd(csm_engine* e, int M, int i, const unsigned long long* part_prev
   a.proj_tab = e->proj_tab + (size_t)(i - 1) * e->V * e->Dd;
   a.codes = e->codes; a.codes_K = e->K;
   a.xs_out = e->xs_D; a.ss_out = e->xs_ss; a.ss_stride = GEMM_XS_MAX_M;
+  a.hs_out = e->hs_D;  // (int4: the half-group sums of xs_out)
   a.ctrl = e->xsd_ctrl; a.epoch = e->xsd_epoch; a.err = e->xsd_err; a.stamps = e->xsd_stamps;
   // the head in the same launch: 64-row tiles, one arg-max partial each -- the launch path's partial count
   const int Vp = e->Vpad, ht = (Vp + 63) / 64;
@@ -634,7 +638,7 @@ bool launch_xsd(csm_engine* e, int M, int i, const unsigned long long* part_prev
     a.head_w = (const uint8_t*)it->second; a.head_nt32 = (Vp + 31) / 32; a.head_tiles = ht; a.Vp = Vp; a.n_valid = e->V;
     a.head_out = e->ci_logits + (size_t)(i - 1) * e->B * Vp; a.head_part = part_out;
   }
-  launch_dec_step_xs(a, st);
+  launch_dec_step_xs(a, st, e->wdt == WDT_Q4);
   return a.head_w != nullptr;
 }
 
@@ -877,7 +881,7 @@ void ensure_batch(csm_engine* e, int B) {
   {
     const csm_llama_dims& d = e->dec.d;
     if (d.hidden == 1024 && d.intermediate == 8192 && d.head_dim == 128 && d.n_heads == 8 && d.n_kv_heads == 2) {
-      const size_t R = DEC_XSD_MAX_M;
+      const size_t R = DEC_XSD_MAX_M_Q4;
       DecStepXsArgs& x = e->xsd;
       x.qkv = (float*)e->balloc(R * e->dec.qkv_rows() * 4);
       x.xs_att = e->balloc(xs::bytes(R, 1024));
@@ -888,6 +892,9 @@ void ensure_batch(csm_engine* e, int B) {
       x.ss_o = (float*)e->balloc(32 * R * 4);
       x.dpart = (float*)e->balloc(8 * R * 1024 * 4);
       x.code_buf = (int*)e->balloc(R * 4);
+      x.hs_att = (float*)e->balloc(1024 / 32 * R * 4);
+      x.hs_x = (float*)e->balloc(1024 / 32 * R * 4);
+      x.hs_h = (float*)e->balloc(8192 / 32 * R * 4);
       if (!e->xsd_ctrl) {
         e->xsd_ctrl = (unsigned*)e->alloc(dec_step_xs_ctrl_bytes());
         e->xsd_epoch = (unsigned*)e->alloc(16);

@@ -424,9 +424,9 @@ constexpr int DEC_FRAME_WGS = 256, DEC_FRAME_THREADS = 512;
 void launch_dec_frame(const DecFrameArgs& p, hipStream_t st, bool q4 = false);
 const void* dec_frame_kernel_ptr(bool q4 = false);  // for the occupancy query
 
-// Persistent batched depth-decoder step (dec_step_xs.hip): the 4 decoder layers of codebook step
-// `step` >= 2 for rows (utterances) 0..M-1, M <= 32, bf16 weights, one launch.
-constexpr int DEC_XSD_WGS = 256, DEC_XSD_THREADS = 512, DEC_XSD_MAX_M = 32;
+// Persistent batched depth-decoder step (dec_step_xs.hip): the 4 decoder layers (+ the head) of codebook
+// step `step` >= 2 for rows (utterances) 0..M-1 in one launch: M <= 32 with bf16 weights, M <= 64 int4.
+constexpr int DEC_XSD_WGS = 256, DEC_XSD_THREADS = 512, DEC_XSD_MAX_M = 32, DEC_XSD_MAX_M_Q4 = 64;
 struct DecStepXsArgs {
   const uint8_t* wqkv[DEC_FRAME_LAYERS];  // fragment-tiled bf16 copies (gemm_retile)
   const uint8_t* wo[DEC_FRAME_LAYERS];
@@ -448,18 +448,24 @@ struct DecStepXsArgs {
   int* codes;                             // [B][codes_K]: codes[m][step - 1] written
   int codes_K;
   // scratch (dec_step_xs_scratch_bytes) and outputs
-  float* qkv;                             // [32][1536]
+  float* qkv;                             // [64][1536]
   void* xs_att;                           // split rows (xs.h), K = 1024
   void* xs_x;                             // K = 1024
   void* xs_h;                             // K = 8192
   void* xs_out;                           // K = 1024: x * (next n1 | final norm) -- the head's xs_in
   float* ss_out;                          // [32 tiles][ss_stride] sums of squares -- the head's ss_in
   int ss_stride;
-  float* x_o;                             // [32][1024]
-  float* x_d;                             // [32][1024]
-  float* ss_o;                            // [32 tiles][32]
-  float* dpart;                           // [8][32][1024]
-  int* code_buf;                          // [32]
+  float* x_o;                             // [64][1024]
+  float* x_d;                             // [64][1024]
+  float* ss_o;                            // [32 tiles][64]
+  float* dpart;                           // [8][64][1024]
+  int* code_buf;                          // [64]
+  // int4 consumers: half-group sums [k / 32][64] of the split rows (xs.h) -- attention out, x_o * n2, h,
+  // and of xs_out (the engine's hs_D)
+  float* hs_att;
+  float* hs_x;
+  float* hs_h;
+  float* hs_out;
   unsigned* ctrl;                         // hand-off flags / counters (dec_step_xs_ctrl_bytes, zeroed once)
   unsigned* epoch;                        // advanced by every launch
   int* err;                               // raised when a hand-off wait times out
@@ -474,5 +480,5 @@ struct DecStepXsArgs {
 };
 constexpr int DEC_XSD_STAMPS = 64;
 size_t dec_step_xs_ctrl_bytes();
-void launch_dec_step_xs(const DecStepXsArgs& p, hipStream_t st);
-const void* dec_step_xs_kernel_ptr();
+void launch_dec_step_xs(const DecStepXsArgs& p, hipStream_t st, bool q4);
+const void* dec_step_xs_kernel_ptr(bool q4);

@@ -1,45 +1,48 @@
-// Persistent batched depth-decoder step: the 4 decoder layers of one codebook step i >= 2 for up to 32
-// utterance rows (/root/reference/csm_mlx/generation.py:72-89 at batch B: decoder(projection(E_a[c]))
-// over the step's rows) in ONE launch, bf16 weights, matrix cores for every projection.
+// Persistent batched depth-decoder step: the 4 decoder layers + the head of one codebook step i >= 2 for
+// up to 32 (bf16 weights) or 64 (int4 g64 weights, MLX affine: nn.quantize) utterance rows
+// (/root/reference/csm_mlx/generation.py:72-89 at batch B: decoder(projection(E_a[c])), then
+// audio_head[i - 1]) in ONE launch, matrix cores for every projection.
 //
-// Why: on the launch path (run_dec_xs) a step is ~20 dependent launches (QKV, attention, o_proj, gate/up,
-// down per layer); at 32 rows each is latency-bound -- ramp, first weight loads, split-K combine, drain:
-// ~44 us per layer for ~53 MB of MALL-resident weights (profiles/r05_prof_config4_per_frame_roles.txt).
-// Here every CU keeps one workgroup for the step, owns fixed weight tiles of every projection and
-// loads them into registers AHEAD of the hand-off that releases their activations, so the weight
-// stream and the first-load latency sit under the dependency waits.
+// Why: on the launch path (run_dec_xs + the head launch) a step is ~21 dependent launches (QKV,
+// attention, o_proj, gate/up, down per layer; the head); at 32-64 rows each is latency-bound -- ramp,
+// first weight loads, split-K combine, drain: ~44 us per layer for ~53 MB of MALL-resident bf16 weights
+// (profiles/r05_prof_config4_per_frame_roles.txt).  Here every CU keeps one workgroup for the step, owns
+// fixed weight tiles of every projection and loads them into registers AHEAD of the hand-off that
+// releases their activations, so the weight stream and the first-load latency sit under the waits.
 //
-// Roles (NWG = 256 workgroups x 8 waves, w = blockIdx.x), per layer:
-//   Q  w < 48        QKV tile w (32 of the 1536 rows), full K: x * n1 (split rows) -> RoPE, q | k | v
-//                    rows + the K/V cache row at pos                              -> flag F1[w]
-//   A  80 <= w < 112 attention of row m = w - 80, query head h = wave, keys 0..pos (the cached rows staged in
-//                    LDS at the layer start; layer 0 takes q | k | v of the row's code from the folded
-//                    table)                                                      -> flag F2[m]
-//   O  48 <= w < 80  o_proj tile j = w - 48 (32 columns), full K: + residual -> x_o, x_o * n2 (split),
-//                    row sums of squares                                         -> flag F3[j]
-//   G  every w       gate/up tiles 2b, 2b + 1, b = 32 (w % 8) + w / 8 (the SiLU*up columns 32b..32b+31)
-//                                                                                -> flag FH[w]
-//   D  every w       down, output tile j = w / 8 over h columns 1024 g .. + 1023, g = w % 8 (the G
-//                    workgroups of group g: the same XCD under round-robin placement, speed only)
-//                    -> partial tile; arrival ticket C4[j]; the eighth arrival sums the 8 partials in group
-//                    order + residual -> x_d, x_d * (next n1 | final norm) split, row sums of squares
-//                                                                                -> flag F5[j]
-// The head (audio_head[i - 1], its arg-max or sampler) stays a launch of its own after this one: it reads
-// the split rows + sums of squares the last layer's combines wrote (engine's xs_D / xs_ss, 32 tiles).
+// Roles (NWG = 256 workgroups x 8 waves, w = blockIdx.x; MR = 32 MT rows, MT row tiles of 32), per layer:
+//   Q  w < 48         QKV tile w (32 of the 1536 rows), full K: x * n1 (split rows) -> RoPE, q | k | v
+//                     rows + the K/V cache row at pos                               -> flag F1[w]
+//   O  48 <= w < 80   o_proj tile j = w - 48 (32 columns), full K: + residual -> x_o, x_o * n2 (split),
+//                     row sums of squares (int4: + half-group sums)               -> flag F3[j]
+//   A  80 <= w < 80 + MR  attention of row m = w - 80, query head h = wave, keys 0..pos (the cached rows
+//                     staged in LDS at the layer start; layer 0 takes q | k | v of the row's code from the
+//                     folded table)                                               -> flag F2[m]
+//   G  every w        gate/up tiles 2b, 2b + 1, b = 32 (w % 8) + w / 8 (the SiLU*up columns 32b..32b+31)
+//                                                                                 -> flag FH[w]
+//   D  every w        down, output tile j = w / 8 over h columns 1024 g .. + 1023, g = w % 8 (the G
+//                     workgroups of group g: the same XCD under round-robin placement, speed only)
+//                     -> partial tile; arrival ticket C4[j]; the eighth arrival sums the 8 partials in group
+//                     order + residual -> x_d, x_d * (next n1 | final norm) split, row sums of squares
+//                                                                                 -> flag F5[j]
+//   H  80 + MR <= w   after the last layer: audio_head[i - 1] rows 64 t .. 64 t + 63 (bf16 tiles): logits
+//                     and one arg-max partial per row -- the launch path's head partial layout
 //
 // Hand-offs (MI355X_MICROARCH.md, inter-workgroup visibility, valid form "ONE lane of each storing
 // workgroup ... sc1 flag store or agent-scope atomic add"): every payload byte is stored sc1 and loaded
 // sc1; each storing wave drains (s_waitcnt vmcnt(0)) before the workgroup barrier behind which one lane
-// stores the flag / adds to the counter; consumers poll with sc1 loads (one lane per flag), then a
-// barrier.  Flags carry tag = epoch * 4 + layer + 1 and counters count monotonically from the epoch the
-// launch read at its start (advanced by workgroup 0 at its end), so nothing is reset.  Every spin is
+// stores the flag / adds to the ticket; consumers poll with sc1 loads (one lane per flag), then a
+// barrier.  Flags carry tag = epoch * 4 + layer + 1 and the tickets count monotonically from the epoch
+// the launch read at its start (advanced by workgroup 0 at its end), so nothing is reset.  Every spin is
 // bounded: on timeout a workgroup raises the error word and stops waiting (results garbage, the host
 // raises) -- the grid always drains.  Single scratch buffers suffice: every rewrite of a buffer is
 // ordered (through the hand-off chain) after every read of its previous contents.
 //
 // Arithmetic: the activations are fp32, split into three bf16 parts in registers (xs.h split_frag), so
 // the matrix-core products are exact in fp32 and accumulate in fp32 (gemm_xs's arithmetic; summation
-// order differs); RMSNorm folded as the streaming path's (x * norm weight split, row scale
+// order differs); int4: the nibbles enter the matrix cores as exact bf16 integers, per 64-column group
+// acc += scale * sum_k q a + bias * sum_k a (the producers publish the half-group sums of the split
+// rows, xs.h); RMSNorm folded as the streaming path's (x * norm weight split, row scale
 // rsqrt(sum x^2 / D + eps) after the dot product); softmax with max subtraction in fp32.
 #include "csm_kernels.h"
 #include "handoff.h"
@@ -58,30 +61,41 @@ constexpr int D = 1024, F = 8192, HQ = 8, HKV = 2, HD = 128, NL = DEC_FRAME_LAYE
 constexpr int KS_D = D / 64, KS_F = F / 64;  // K stages of 64
 constexpr int NQT = QKV / 32, NDT = D / 32;   // 48 QKV tiles; 32 o_proj / down / combine tiles
 constexpr int NGRP = 8;                       // down K groups (1024 h columns each)
-constexpr int O_WG0 = NQT;       // o_proj workgroups 48 .. 79
-constexpr int A_WG0 = O_WG0 + 32; // attention workgroups 80 .. 111 (row m = w - 80, wave = query head)
-constexpr int H_WG0 = A_WG0 + 32; // head workgroups 112 .. (64 padded-vocabulary rows each)
+constexpr int O_WG0 = NQT;                    // o_proj workgroups 48 .. 79
+constexpr int A_WG0 = O_WG0 + 32;             // attention workgroups 80 .. 80 + MR - 1
+constexpr int RMAX = 64;                      // rows of the scratch buffers (row stride of sums)
 constexpr unsigned SPIN_LIMIT = 1u << 22;
 constexpr int SC1 = 16;  // buffer cache policy: sc1 (agent-coherent)
 static_assert(NWG == 256 && NWV == 8, "roles assume 256 workgroups of 8 waves");
 static_assert(KS_D == 2 * NWV && KS_F / NGRP == 2 * NWV, "every wave takes two K stages of its tile");
+static_assert(RMAX == xs::HS_ROWS, "half-group sums use the xs.h row stride");
 
 // control words (u32), one per 128-B line
-enum { CW_F1 = 0, CW_F2 = CW_F1 + NQT, CW_F3 = CW_F2 + 32, CW_FH = CW_F3 + NDT, CW_C4 = CW_FH + NWG, CW_F5 = CW_C4 + NDT,
+enum { CW_F1 = 0, CW_F2 = CW_F1 + NQT, CW_F3 = CW_F2 + RMAX, CW_FH = CW_F3 + NDT, CW_C4 = CW_FH + NWG, CW_F5 = CW_C4 + NDT,
        CW_N = CW_F5 + NDT };
 constexpr int CW_STRIDE = 32;
 
+#ifndef XSD_UNION
+#define XSD_UNION 1  // lab: 0 keeps the attention buffers apart from the MFMA reduction slots
+#endif
 struct Lds {
-  float red[NWV][2][16][64];  // the per-wave accumulators of up to two tiles
-  float ct[2][32][33];     // reduced tiles [batch row][column]
-  float rsp[8][32];        // row scales: partial sums of squares (row_scales)
-  // attention workgroups (wave = query head): cached keys / values 0..pos-1 of both kv heads (rows padded:
-  // conflict-free row-parallel reads), each wave's scaled query and the new key / value row at pos
-  float Ks[HKV][32][HD + 4];
-  float Vs[HKV][32][HD];
-  float qsh[HQ][HD];
-  float kn[HQ][HD];
-  float vn[HQ][HD];
+#if XSD_UNION
+  union {
+#else
+  struct {
+#endif
+    float red[NWV][2][16][64];  // MFMA roles: the per-wave accumulators of up to two tiles
+    struct {                    // attention workgroups (wave = query head): cached keys / values 0..pos-1 of
+      float Ks[HKV][32][HD + 4];//   both kv heads (rows padded: conflict-free row-parallel reads), each
+      float Vs[HKV][32][HD];    //   wave's scaled query and the new key / value row at pos
+      float qsh[HQ][HD];
+      float kn[HQ][HD];
+      float vn[HQ][HD];
+    } at;
+  };
+  float ct[2][2][32][33];  // reduced tiles [row tile][tile][batch row][column]
+  float rsp[8][RMAX];      // row scales: partial sums of squares (row_scales)
+  float xg[NWV][2][RMAX];  // int4: X_g = sum over the stage's 64 columns of the split rows, per wave stage
   int flag;
 };
 
@@ -110,7 +124,7 @@ __device__ __forceinline__ bool spin_fail(const Ctx& c, unsigned spin) {
   return false;
 }
 __device__ __forceinline__ unsigned ld_cw(const unsigned* a) { return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-// lanes < n of wave 0 wait until word idx(lane) has reached `target` (flags hold tags, counters counts:
+// lanes < n of wave 0 wait until word idx(lane) has reached `target` (flags hold tags, tickets counts:
 // both only grow), then the workgroup barrier
 template <typename Idx>
 __device__ __forceinline__ void wait_words(const Ctx& c, int n, Idx&& idx, unsigned target) {
@@ -132,104 +146,18 @@ __device__ __forceinline__ unsigned add_ctr(unsigned* a) { return __hip_atomic_f
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0x7fffffff, 0x00020000);
 }
+// (base wave-uniform -- it rides in the buffer descriptor; a per-lane base would make the compiler loop
+// over the lanes' distinct descriptors -- and the lane's byte offset in the vector offset)
 __device__ __forceinline__ void st16(void* base, size_t off, f32x4_t v) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), rsrc(base), (int)off, 0, SC1);
 }
 __device__ __forceinline__ f32x4_t ld16(const void* base, size_t off) {
   return __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rsrc(base), (int)off, 0, SC1));
 }
-// 4-B sc1 load as a plain buffer load (not an atomic: independent loads issue back to back)
-__device__ __forceinline__ float ld4(const float* p) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc(p), 0, 0, SC1));
-}
-// (base wave-uniform -- it rides in the buffer descriptor; a per-lane base would make the compiler
-// loop over the lanes' distinct descriptors -- and the lane's byte offset in the vector offset)
 __device__ __forceinline__ float2 ld8(const float* base, int off) {
   return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rsrc(base), off, 0, SC1));
 }
 __device__ __forceinline__ void st4(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-
-// ---- matrix-core tiles.  Weight tile registers: the wave's two K stages (st0, st0 + 1) of one 32-row
-// tile of a fragment-tiled copy (gemm_retile: [tile][stage][s][lane] x 16 B); activation registers: the
-// same stages of the 32 split rows (xs.h XS_F32 layout, row tile 0).
-struct WT { u32x4_t a[2][4]; };
-struct AF { u32x4_t a[2][4][2]; };
-
-__device__ __forceinline__ void load_wt(const uint8_t* T, int tile, int nks, int st0, int lane, WT& r) {
-#pragma unroll
-  for (int q = 0; q < 2; ++q)
-#pragma unroll
-    for (int s = 0; s < 4; ++s) r.a[q][s] = bload<0>(T, lane * 16, __builtin_amdgcn_readfirstlane(((tile * nks + st0 + q) * 4 + s) * 1024));
-}
-__device__ __forceinline__ void load_af(const void* X, int st0, int lane, AF& r) {
-  const __amdgpu_buffer_rsrc_t rs = rsrc(X);
-#pragma unroll
-  for (int q = 0; q < 2; ++q)
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-      for (int hf = 0; hf < 2; ++hf)
-        r.a[q][s][hf] = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, __builtin_amdgcn_readfirstlane((((st0 + q) * 4 + s) * 2 + hf) * 1024), SC1);
-}
-template <int NTL>
-__device__ __forceinline__ void mma(const AF& A, const WT (&W)[NTL], f32x16_t (&acc)[NTL]) {
-#pragma unroll
-  for (int t = 0; t < NTL; ++t) acc[t] = f32x16_t{};
-#pragma unroll
-  for (int q = 0; q < 2; ++q)
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      u32x4_t pt[3];
-      xs::split_frag(A.a[q][s][0], A.a[q][s][1], pt);
-#pragma unroll
-      for (int pp = 0; pp < 3; ++pp)
-#pragma unroll
-        for (int t = 0; t < NTL; ++t)
-          acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, pt[pp]),
-                                                          __builtin_bit_cast(bf16x8_t, W[t].a[q][s]), acc[t], 0, 0, 0);
-    }
-}
-// the 8 waves' partial tiles -> L.ct[t][batch row][column], added in wave order.  Accumulator register
-// j of lane (r, h): batch row (j & 3) + 8 (j >> 2) + 4 h, column r.
-template <int NTL>
-__device__ __forceinline__ void reduce_tiles(Ctx& c, const f32x16_t (&acc)[NTL]) {
-#pragma unroll
-  for (int t = 0; t < NTL; ++t)
-#pragma unroll
-    for (int j = 0; j < 16; ++j) c.L.red[c.wave][t][j][c.lane] = acc[t][j];
-  __syncthreads();
-#pragma unroll
-  for (int e0 = 0; e0 < NTL * 1024; e0 += NT) {
-    const int e = e0 + c.tid, t = e >> 10, m = (e >> 5) & 31, col = e & 31;
-    const int j = (m & 3) + 4 * (m >> 3), ln = col + 32 * ((m >> 2) & 1);
-    float v = c.L.red[0][t][j][ln];
-#pragma unroll
-    for (int wv = 1; wv < NWV; ++wv) v += c.L.red[wv][t][j][ln];
-    c.L.ct[t][m][col] = v;
-  }
-  __syncthreads();
-}
-
-// Row scales rsqrt(sum_t ss[t][m] / D + eps) from 32 tiles' partial sums of squares (sc1): threads < 256
-// each add 4 tiles of one row (loads in flight together) into L.rsp[part][row]; row_scale() adds the 8
-// parts in order once a barrier (reduce_tiles') has published them
-__device__ __forceinline__ void row_scales(Ctx& c, const float* ss, int stride) {
-  if (c.tid < 256) {
-    const int m = c.tid & 31, q = c.tid >> 5;
-    const __amdgpu_buffer_rsrc_t rs = rsrc(ss);
-    float v[4];
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-      v[t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, (m + 4 * q * stride) * 4, t * stride * 4, SC1));
-    c.L.rsp[q][m] = ((v[0] + v[1]) + v[2]) + v[3];
-  }
-}
-__device__ __forceinline__ float row_scale(const Ctx& c, int m) {
-  float s = c.L.rsp[0][m];
-#pragma unroll
-  for (int q = 1; q < 8; ++q) s += c.L.rsp[q][m];
-  return rsqrtf(s / (float)D + c.p.eps);
-}
 
 // sum over the 8 lanes of a row group (lanes 8r .. 8r + 7), fixed butterfly order
 __device__ __forceinline__ float sum8(float v) {
@@ -239,37 +167,204 @@ __device__ __forceinline__ float sum8(float v) {
   return v;
 }
 
+// ---- matrix-core tiles.  Weight tile registers: the wave's two K stages (st0, st0 + 1) of one 32-row
+// tile of a fragment-tiled copy (gemm_retile) -- bf16: [tile][stage][s][lane] x 16 B; int4: [tile][stage]
+// [lane] x 16 B of nibbles (word s = sub-step s) + the rows' {scale, bias} words after all nibbles.
+// Activation registers: the same stages of one 32-row tile of the split rows (xs.h XS_F32 layout).
+template <bool Q4> struct WTile;
+template <> struct WTile<false> { u32x4_t a[2][4]; };
+template <> struct WTile<true> { u32x4_t a[2]; unsigned sb[2]; };
+struct AF { u32x4_t a[2][4][2]; };
+
+// nt32: the matrix's 32-row tile count (int4: where the {scale, bias} words start)
+template <bool Q4>
+__device__ __forceinline__ void load_wt(const uint8_t* T, int tile, int nks, int nt32, int st0, int lane, WTile<Q4>& r) {
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int ts = tile * nks + st0 + q;
+    if constexpr (Q4) {
+      r.a[q] = bload<0>(T, lane * 16, __builtin_amdgcn_readfirstlane(ts * 1024));
+      r.sb[q] = bload4<0>(T, (lane & 31) * 4, __builtin_amdgcn_readfirstlane(nt32 * nks * 1024 + ts * 128));
+    } else {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) r.a[q][s] = bload<0>(T, lane * 16, __builtin_amdgcn_readfirstlane((ts * 4 + s) * 1024));
+    }
+  }
+}
+// row tile t of split rows with nks K stages
+__device__ __forceinline__ void load_af(const void* X, int nks, int t, int st0, int lane, AF& r) {
+  const __amdgpu_buffer_rsrc_t rs = rsrc(X);
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int hf = 0; hf < 2; ++hf)
+        r.a[q][s][hf] = __builtin_amdgcn_raw_buffer_load_b128(
+            rs, lane * 16, __builtin_amdgcn_readfirstlane((((t * nks + st0 + q) * 4 + s) * 2 + hf) * 1024), SC1);
+}
+// int4: X_g of the wave's two stages for every row -> L.xg[wave] (from the producer's half-group sums
+// hs[k / 32][RMAX]); a barrier follows before use
+__device__ __forceinline__ void stage_xg(Ctx& c, const float* hs, int st0) {
+  const __amdgpu_buffer_rsrc_t rs = rsrc(hs);
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int st = st0 + q;
+    const float a = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, c.lane * 4, __builtin_amdgcn_readfirstlane(2 * st * RMAX * 4), SC1));
+    const float b = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, c.lane * 4, __builtin_amdgcn_readfirstlane((2 * st + 1) * RMAX * 4), SC1));
+    c.L.xg[c.wave][q][c.lane] = a + b;
+  }
+}
+// the wave's partial tiles of row tile t.  Accumulator register j of lane (r, h): batch row (j & 3) +
+// 8 (j >> 2) + 4 h of the row tile, column r.
+template <bool Q4, int NTL>
+__device__ __forceinline__ void mma(const Ctx& c, const AF& A, const WTile<Q4> (&W)[NTL], int t, f32x16_t (&acc)[NTL]) {
+#pragma unroll
+  for (int i = 0; i < NTL; ++i) acc[i] = f32x16_t{};
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    if constexpr (Q4) {
+      f32x16_t gq[NTL];
+#pragma unroll
+      for (int i = 0; i < NTL; ++i) gq[i] = f32x16_t{};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        bf16x8_t bq[NTL];
+#pragma unroll
+        for (int i = 0; i < NTL; ++i) bq[i] = __builtin_bit_cast(bf16x8_t, xs::q4_word_bf16(W[i].a[q][s]));
+        u32x4_t pt[3];
+        xs::split_frag(A.a[q][s][0], A.a[q][s][1], pt);
+#pragma unroll
+        for (int pp = 0; pp < 3; ++pp)
+#pragma unroll
+          for (int i = 0; i < NTL; ++i)
+            gq[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, pt[pp]), bq[i], gq[i], 0, 0, 0);
+      }
+      // per-group fold: acc += scale * S_g + bias * X_g (the row's stage sum)
+      const int hrow = 32 * t + 4 * (c.lane >> 5);
+      float xr[16];
+#pragma unroll
+      for (int j4 = 0; j4 < 4; ++j4) {
+        const f32x4_t x4 = *reinterpret_cast<const f32x4_t*>(&c.L.xg[c.wave][q][hrow + 8 * j4]);
+        xr[4 * j4] = x4.x; xr[4 * j4 + 1] = x4.y; xr[4 * j4 + 2] = x4.z; xr[4 * j4 + 3] = x4.w;
+      }
+#pragma unroll
+      for (int i = 0; i < NTL; ++i) {
+        const float sc = bf16_lo(W[i].sb[q]), bi = bf16_hi(W[i].sb[q]);
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) {
+          acc[i][jj] = fmaf(sc, gq[i][jj], acc[i][jj]);
+          acc[i][jj] = fmaf(bi, xr[jj], acc[i][jj]);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);  // one stage's temporaries live at a time
+    } else {
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        u32x4_t pt[3];
+        xs::split_frag(A.a[q][s][0], A.a[q][s][1], pt);
+#pragma unroll
+        for (int pp = 0; pp < 3; ++pp)
+#pragma unroll
+          for (int i = 0; i < NTL; ++i)
+            acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, pt[pp]),
+                                                            __builtin_bit_cast(bf16x8_t, W[i].a[q][s]), acc[i], 0, 0, 0);
+      }
+    }
+  }
+}
+// the 8 waves' partial tiles -> L.ct[t][i][batch row][column], added in wave order
+template <int NTL>
+__device__ __forceinline__ void reduce_tiles(Ctx& c, const f32x16_t (&acc)[NTL], int t) {
+#pragma unroll
+  for (int i = 0; i < NTL; ++i)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) c.L.red[c.wave][i][j][c.lane] = acc[i][j];
+  __syncthreads();
+#pragma unroll
+  for (int e0 = 0; e0 < NTL * 1024; e0 += NT) {
+    const int e = e0 + c.tid, i = e >> 10, m = (e >> 5) & 31, col = e & 31;
+    const int j = (m & 3) + 4 * (m >> 3), ln = col + 32 * ((m >> 2) & 1);
+    float v = c.L.red[0][i][j][ln];
+#pragma unroll
+    for (int wv = 1; wv < NWV; ++wv) v += c.L.red[wv][i][j][ln];
+    c.L.ct[t][i][m][col] = v;
+  }
+  __syncthreads();
+}
+// one projection role's tiles for every row tile: split rows X (nks stages; int4: half-group sums hs)
+// against the weight tiles W over the wave's stages st0, st0 + 1 -> L.ct.  The second row tile's operand
+// loads are issued once the first tile's products are (its registers are then free).
+// pre(): the role's other loads (row scales, residual), issued after the first operand loads (vmcnt
+// retires in issue order: a load whose value is consumed first must be issued first).
+template <bool Q4, int MT, int NTL, typename Pre>
+__device__ __forceinline__ void gemm_tiles(Ctx& c, const void* X, const float* hs, int nks, int st0, const WTile<Q4> (&W)[NTL], Pre&& pre) {
+  AF A;
+  load_af(X, nks, 0, st0, c.lane, A);
+  pre();
+  if constexpr (Q4) {
+    stage_xg(c, hs, st0);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int t = 0; t < MT; ++t) {
+    f32x16_t acc[NTL];
+    mma<Q4, NTL>(c, A, W, t, acc);
+    if (t + 1 < MT) load_af(X, nks, t + 1, st0, c.lane, A);
+    reduce_tiles<NTL>(c, acc, t);
+  }
+}
+
+// Row scales rsqrt(sum_t ss[t][m] / D + eps) from 32 tiles' partial sums of squares (sc1, row stride
+// RMAX): every thread adds 4 tiles of one row (loads in flight together) into L.rsp[part][row];
+// row_scale() adds the 8 parts in order once a barrier (reduce_tiles') has published them
+__device__ __forceinline__ void row_scales(Ctx& c, const float* ss) {
+  const int m = c.tid & (RMAX - 1), q = c.tid / RMAX;  // (q wave-uniform)
+  const __amdgpu_buffer_rsrc_t rs = rsrc(ss);
+  float v[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+    v[t] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, m * 4, __builtin_amdgcn_readfirstlane((4 * q + t) * RMAX * 4), SC1));
+  c.L.rsp[q][m] = ((v[0] + v[1]) + v[2]) + v[3];
+}
+__device__ __forceinline__ float row_scale(const Ctx& c, int m) {
+  float s = c.L.rsp[0][m];
+#pragma unroll
+  for (int q = 1; q < 8; ++q) s += c.L.rsp[q][m];
+  return rsqrtf(s / (float)D + c.p.eps);
+}
+
 // ---------------------------------------------------------------------------------------------------
 // Q: QKV tile T of layer l (l >= 1)
-__device__ __forceinline__ void role_q(Ctx& c, int l, const WT& W) {
+template <bool Q4, int MT>
+__device__ __forceinline__ void role_q(Ctx& c, int l, const WTile<Q4>& W) {
   const DecStepXsArgs& p = c.p;
   const int T = c.w;
   const unsigned tag = c.ep * NL + l;  // the previous layer's combine flags
   wait_words(c, NDT, [](int i) { return CW_F5 + i; }, tag);
   c.mark(1);
-  AF A;
-  load_af(p.xs_out, 2 * c.wave, c.lane, A);
-  row_scales(c, p.ss_out, p.ss_stride);
-  f32x16_t acc[1];
-  mma<1>(A, reinterpret_cast<const WT(&)[1]>(W), acc);
-  reduce_tiles<1>(c, acc);
+  gemm_tiles<Q4, MT, 1>(c, p.xs_out, p.hs_out, KS_D, 2 * c.wave, reinterpret_cast<const WTile<Q4>(&)[1]>(W),
+                        [&] { row_scales(c, p.ss_out); });
   c.sub(0);
-  // rows m = tid / 16, columns 2 (tid % 16) + {0, 1} (RoPE pairs)
-  const int m = c.tid >> 4, cc = 2 * (c.tid & 15), n = 32 * T + cc;
-  const float r = row_scale(c, m);
-  float a = c.L.ct[0][m][cc] * r, b = c.L.ct[0][m][cc + 1] * r;
-  if (n < (HQ + HKV) * HD) {
-    const float2 cs = reinterpret_cast<const float2*>(p.rope)[(size_t)p.step * (HD / 2) + (n % HD) / 2];
-    const float y0 = a * cs.x - b * cs.y, y1 = b * cs.x + a * cs.y;
-    a = y0;
-    b = y1;
-  }
-  if (m < p.M) {
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, make_float2(a, b)), rsrc(p.qkv), (int)(((size_t)m * QKV + n) * 4), 0, SC1);
-    if (n >= HQ * HD) {  // KVCache.update_and_fetch: the row at pos for the later codebook steps
-      const int nn = n < (HQ + HKV) * HD ? n - HQ * HD : n - (HQ + HKV) * HD;
-      float* cache = n < (HQ + HKV) * HD ? p.kc[l] : p.vc[l];
-      *reinterpret_cast<float2*>(cache + (((size_t)m * HKV + nn / HD) * p.S_cap + p.step) * HD + nn % HD) = make_float2(a, b);
+  // rows m = tid / 16 (+ 32 per pass), columns 2 (tid % 16) + {0, 1} (RoPE pairs)
+#pragma unroll
+  for (int t = 0; t < MT; ++t) {
+    const int ml = c.tid >> 4, m = 32 * t + ml, cc = 2 * (c.tid & 15), n = 32 * T + cc;
+    const float r = row_scale(c, m);
+    float a = c.L.ct[t][0][ml][cc] * r, b = c.L.ct[t][0][ml][cc + 1] * r;
+    if (n < (HQ + HKV) * HD) {
+      const float2 cs = reinterpret_cast<const float2*>(p.rope)[(size_t)p.step * (HD / 2) + (n % HD) / 2];
+      const float y0 = a * cs.x - b * cs.y, y1 = b * cs.x + a * cs.y;
+      a = y0;
+      b = y1;
+    }
+    if (m < p.M) {
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, make_float2(a, b)), rsrc(p.qkv), (int)(((size_t)m * QKV + n) * 4), 0, SC1);
+      if (n >= HQ * HD) {  // KVCache.update_and_fetch: the row at pos for the later codebook steps
+        const int nn = n < (HQ + HKV) * HD ? n - HQ * HD : n - (HQ + HKV) * HD;
+        float* cache = n < (HQ + HKV) * HD ? p.kc[l] : p.vc[l];
+        *reinterpret_cast<float2*>(cache + (((size_t)m * HKV + nn / HD) * p.S_cap + p.step) * HD + nn % HD) = make_float2(a, b);
+      }
     }
   }
   c.sub(1);
@@ -303,16 +398,17 @@ __device__ __forceinline__ void stage_kv(Ctx& c, int l) {
     for (int u = 0; u < PER; ++u) {
       const int e = c.tid + u * NT, g = e / (32 * (HD / 4)), r = e % (32 * (HD / 4));
       if (r < n4) {
-        float* dst = kv ? &c.L.Vs[g][r / (HD / 4)][4 * (r % (HD / 4))] : &c.L.Ks[g][r / (HD / 4)][4 * (r % (HD / 4))];
+        float* dst = kv ? &c.L.at.Vs[g][r / (HD / 4)][4 * (r % (HD / 4))] : &c.L.at.Ks[g][r / (HD / 4)][4 * (r % (HD / 4))];
         *reinterpret_cast<f4*>(dst) = t[kv][u];
       }
     }
 }
 
-// A (workgroups A_WG0 .. A_WG0 + 31): attention of row m = w - A_WG0, query head h = wave, keys 0..pos ->
-// xs_att (split rows of the o_proj).  The cached K / V rows are in LDS (stage_kv); each wave fetches its
-// query and the new key / value row at pos (layer 0: of the row's code, from the folded table; else from
-// the QKV tiles, after their flags) and computes.
+// A (workgroups A_WG0 .. A_WG0 + MR - 1): attention of row m = w - A_WG0, query head h = wave, keys
+// 0..pos -> xs_att (split rows of the o_proj; int4: + half-group sums).  The cached K / V rows are in LDS
+// (stage_kv); each wave fetches its query and the new key / value row at pos (layer 0: of the row's code,
+// from the folded table; else from the QKV tiles, after their flags) and computes.
+template <bool Q4>
 __device__ __forceinline__ void role_a(Ctx& c, int l) {
   const DecStepXsArgs& p = c.p;
   const int m = c.w - A_WG0, h = c.wave, g = h / (HQ / HKV), pos = p.step, n = pos + 1;
@@ -358,9 +454,9 @@ __device__ __forceinline__ void role_a(Ctx& c, int l) {
       kv2 = ld8(row, (HQ * HD + g * HD + 2 * lane) * 4);
       vv2 = ld8(row, ((HQ + HKV) * HD + g * HD + 2 * lane) * 4);
     }
-    *reinterpret_cast<float2*>(&c.L.qsh[h][2 * lane]) = make_float2(qv.x * scale, qv.y * scale);
-    *reinterpret_cast<float2*>(&c.L.kn[h][2 * lane]) = kv2;
-    *reinterpret_cast<float2*>(&c.L.vn[h][2 * lane]) = vv2;
+    *reinterpret_cast<float2*>(&c.L.at.qsh[h][2 * lane]) = make_float2(qv.x * scale, qv.y * scale);
+    *reinterpret_cast<float2*>(&c.L.at.kn[h][2 * lane]) = kv2;
+    *reinterpret_cast<float2*>(&c.L.at.vn[h][2 * lane]) = vv2;
     c.sub(9);
   }
   __syncthreads();  // stage_kv's rows (every wave) and this wave's own rows
@@ -371,9 +467,9 @@ __device__ __forceinline__ void role_a(Ctx& c, int l) {
     const int kj = lane & 31, hh = lane >> 5, kv = lane >> 5, dq = lane & 31;
     float s;
     {
-      const float* krow = kj < pos ? &c.L.Ks[g][kj][0] : &c.L.kn[h][0];
+      const float* krow = kj < pos ? &c.L.at.Ks[g][kj][0] : &c.L.at.kn[h][0];
       const f4* kr = reinterpret_cast<const f4*>(krow + hh * (HD / 2));
-      const f4* qr = reinterpret_cast<const f4*>(&c.L.qsh[h][hh * (HD / 2)]);
+      const f4* qr = reinterpret_cast<const f4*>(&c.L.at.qsh[h][hh * (HD / 2)]);
       float d0 = 0.f, d1 = 0.f, d2 = 0.f, d3 = 0.f;
 #pragma unroll
       for (int d4 = 0; d4 < HD / 8; ++d4) {
@@ -400,7 +496,7 @@ __device__ __forceinline__ void role_a(Ctx& c, int l) {
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           const int jj = 16 * kv + u0 + u;
-          vv[u] = *reinterpret_cast<const f4*>(jj < pos ? &c.L.Vs[g][jj][4 * dq] : &c.L.vn[h][4 * dq]);
+          vv[u] = *reinterpret_cast<const f4*>(jj < pos ? &c.L.at.Vs[g][jj][4 * dq] : &c.L.at.vn[h][4 * dq]);
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
@@ -419,9 +515,12 @@ __device__ __forceinline__ void role_a(Ctx& c, int l) {
     const float inv = 1.f / l_run;
     const float t0 = __shfl_xor(acc.x, 32, 64), t1 = __shfl_xor(acc.y, 32, 64), t2 = __shfl_xor(acc.z, 32, 64),
                 t3 = __shfl_xor(acc.w, 32, 64);
-    if (lane < 32)
-      st16(p.xs_att, xs::off(D, m, h * HD + 4 * dq),
-           f32x4_t{(acc.x + t0) * inv, (acc.y + t1) * inv, (acc.z + t2) * inv, (acc.w + t3) * inv});
+    const f32x4_t o = {(acc.x + t0) * inv, (acc.y + t1) * inv, (acc.z + t2) * inv, (acc.w + t3) * inv};
+    if (lane < 32) st16(p.xs_att, xs::off(D, m, h * HD + 4 * dq), o);
+    if constexpr (Q4) {  // half group (h * 128 + 4 dq) / 32: lanes dq = 8j .. 8j + 7, columns in order
+      const float hs = sum8((o.x + o.y) + (o.z + o.w));
+      if (lane < 32 && (dq & 7) == 0) st4(p.hs_att + (size_t)((h * HD + 4 * dq) / 32) * RMAX + m, hs);
+    }
   }
   drain();
   __syncthreads();
@@ -430,38 +529,43 @@ __device__ __forceinline__ void role_a(Ctx& c, int l) {
   c.mark(4);
 }
 
-// O: o_proj tile j (+ residual) -> x_o, split x_o * n2, row sums of squares
-__device__ __forceinline__ void role_o(Ctx& c, int l, const WT& W) {
+// O: o_proj tile j (+ residual) -> x_o, split x_o * n2, row sums of squares (int4: half-group sums)
+template <bool Q4, int MT>
+__device__ __forceinline__ void role_o(Ctx& c, int l, const WTile<Q4>& W) {
   const DecStepXsArgs& p = c.p;
   const int j = c.w - O_WG0;
   const unsigned tag = c.ep * NL + l + 1;
-  wait_words(c, 32, [](int i) { return CW_F2 + i; }, tag);
+  wait_words(c, 32 * MT, [](int i) { return CW_F2 + i; }, tag);
   c.mark(5);
-  AF A;
-  load_af(p.xs_att, 2 * c.wave, c.lane, A);
   // residual: layer 0 the projected input row proj_tab[code], else the previous layer's x_d
   const int m = c.tid >> 3, q = c.tid & 7, n = 32 * j + 4 * q;
-  f32x4_t res = {0.f, 0.f, 0.f, 0.f};
-  if (c.tid < 256 && m < p.M) {
-    if (l == 0) {
-      const int code = __hip_atomic_load(p.code_buf + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      res = *reinterpret_cast<const f32x4_t*>(p.proj_tab + (size_t)code * D + n);
-    } else {
-      res = ld16(p.x_d, ((size_t)m * D + n) * 4);
+  f32x4_t res = {0.f, 0.f, 0.f, 0.f}, nw;
+  gemm_tiles<Q4, MT, 1>(c, p.xs_att, p.hs_att, KS_D, 2 * c.wave, reinterpret_cast<const WTile<Q4>(&)[1]>(W), [&] {
+    // residual: layer 0 the projected input row proj_tab[code], else the previous layer's x_d
+    if (m < p.M) {
+      if (l == 0) {
+        const int code = __hip_atomic_load(p.code_buf + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        res = *reinterpret_cast<const f32x4_t*>(p.proj_tab + (size_t)code * D + n);
+      } else {
+        res = ld16(p.x_d, ((size_t)m * D + n) * 4);
+      }
     }
-  }
-  const f32x4_t nw = *reinterpret_cast<const f32x4_t*>(p.n2[l] + n);
-  f32x16_t acc[1];
-  mma<1>(A, reinterpret_cast<const WT(&)[1]>(W), acc);
-  reduce_tiles<1>(c, acc);
+    nw = *reinterpret_cast<const f32x4_t*>(p.n2[l] + n);
+  });
   c.sub(6);
-  if (c.tid < 256) {
+  if (m < 32 * MT) {
     f32x4_t x = {0.f, 0.f, 0.f, 0.f};
-    if (m < p.M) x = res + f32x4_t{c.L.ct[0][m][4 * q], c.L.ct[0][m][4 * q + 1], c.L.ct[0][m][4 * q + 2], c.L.ct[0][m][4 * q + 3]};
+    const int t = m >> 5, ml = m & 31;
+    if (m < p.M) x = res + f32x4_t{c.L.ct[t][0][ml][4 * q], c.L.ct[t][0][ml][4 * q + 1], c.L.ct[t][0][ml][4 * q + 2], c.L.ct[t][0][ml][4 * q + 3]};
+    const f32x4_t xn = x * nw;
     st16(p.x_o, ((size_t)m * D + n) * 4, x);
-    st16(p.xs_x, xs::off(D, m, n), x * nw);
+    st16(p.xs_x, xs::off(D, m, n), xn);
     const float sq = sum8(fmaf(x.w, x.w, fmaf(x.z, x.z, fmaf(x.y, x.y, x.x * x.x))));
-    if (q == 0) st4(p.ss_o + (size_t)j * 32 + m, sq);
+    if (q == 0) st4(p.ss_o + (size_t)j * RMAX + m, sq);
+    if constexpr (Q4) {
+      const float hs = sum8((xn.x + xn.y) + (xn.z + xn.w));
+      if (q == 0) st4(p.hs_x + (size_t)j * RMAX + m, hs);
+    }
   }
   drain();
   __syncthreads();
@@ -469,32 +573,32 @@ __device__ __forceinline__ void role_o(Ctx& c, int l, const WT& W) {
   c.mark(6);
 }
 
-// G: gate/up tiles 2b, 2b + 1 -> SiLU*up columns 32b .. 32b + 31 (split, K = F)
-__device__ __forceinline__ void role_g(Ctx& c, int l, const WT (&W)[2]) {
+// G: gate/up tiles 2b, 2b + 1 -> SiLU*up columns 32b .. 32b + 31 (split, K = F; int4: + half-group sums)
+template <bool Q4, int MT>
+__device__ __forceinline__ void role_g(Ctx& c, int l, const WTile<Q4> (&W)[2]) {
   const DecStepXsArgs& p = c.p;
   const int b = 32 * (c.w & 7) + (c.w >> 3);
   const unsigned tag = c.ep * NL + l + 1;
   wait_words(c, NDT, [](int i) { return CW_F3 + i; }, tag);
   c.mark(7);
-  AF A;
-  load_af(p.xs_x, 2 * c.wave, c.lane, A);
-  row_scales(c, p.ss_o, 32);
-  f32x16_t acc[2];
-  mma<2>(A, W, acc);
-  c.sub(2);
-  reduce_tiles<2>(c, acc);
+  gemm_tiles<Q4, MT, 2>(c, p.xs_x, p.hs_x, KS_D, 2 * c.wave, W, [&] { row_scales(c, p.ss_o); });
   c.sub(3);
-  if (c.tid < 256) {
-    const int m = c.tid >> 3, q = c.tid & 7;
+  const int m = c.tid >> 3, q = c.tid & 7;
+  if (m < 32 * MT) {
+    const int t = m >> 5, ml = m & 31;
     const float r = row_scale(c, m);
     float hv[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int pc = 4 * q + i, t = pc >> 4, cc = 2 * (pc & 15);  // wgu rows interleave gate_j, up_j
-      const float gt = c.L.ct[t][m][cc] * r, up = c.L.ct[t][m][cc + 1] * r;
+      const int pc = 4 * q + i, ti = pc >> 4, cc = 2 * (pc & 15);  // wgu rows interleave gate_j, up_j
+      const float gt = c.L.ct[t][ti][ml][cc] * r, up = c.L.ct[t][ti][ml][cc + 1] * r;
       hv[i] = silu_f(gt) * up;
     }
     st16(p.xs_h, xs::off(F, m, 32 * b + 4 * q), f32x4_t{hv[0], hv[1], hv[2], hv[3]});
+    if constexpr (Q4) {
+      const float hs = sum8((hv[0] + hv[1]) + (hv[2] + hv[3]));
+      if (q == 0) st4(p.hs_h + (size_t)b * RMAX + m, hs);
+    }
   }
   c.sub(4);
   drain();
@@ -504,22 +608,21 @@ __device__ __forceinline__ void role_g(Ctx& c, int l, const WT (&W)[2]) {
 }
 
 // D: down tile j over K group g -> partial; the eighth arrival combines
-__device__ __forceinline__ void role_d(Ctx& c, int l, const WT& W) {
+template <bool Q4, int MT>
+__device__ __forceinline__ void role_d(Ctx& c, int l, const WTile<Q4>& W) {
   const DecStepXsArgs& p = c.p;
   const int g = c.w & 7, j = c.w >> 3;
   const unsigned tag = c.ep * NL + l + 1;
   wait_words(c, 32, [g](int i) { return CW_FH + g + 8 * i; }, tag);  // the G workgroups of group g
   c.mark(9);
-  AF A;
-  load_af(p.xs_h, 16 * g + 2 * c.wave, c.lane, A);
-  f32x16_t acc[1];
-  mma<1>(A, reinterpret_cast<const WT(&)[1]>(W), acc);
-  reduce_tiles<1>(c, acc);
+  gemm_tiles<Q4, MT, 1>(c, p.xs_h, p.hs_h, KS_F, 16 * g + 2 * c.wave, reinterpret_cast<const WTile<Q4>(&)[1]>(W), [] {});
   c.sub(5);
   const int m = c.tid >> 3, q = c.tid & 7, n = 32 * j + 4 * q;
-  if (c.tid < 256)
-    st16(p.dpart, (((size_t)g * 32 + m) * D + n) * 4,
-         f32x4_t{c.L.ct[0][m][4 * q], c.L.ct[0][m][4 * q + 1], c.L.ct[0][m][4 * q + 2], c.L.ct[0][m][4 * q + 3]});
+  if (m < 32 * MT) {
+    const int t = m >> 5, ml = m & 31;
+    st16(p.dpart, (((size_t)g * RMAX + m) * D + n) * 4,
+         f32x4_t{c.L.ct[t][0][ml][4 * q], c.L.ct[t][0][ml][4 * q + 1], c.L.ct[t][0][ml][4 * q + 2], c.L.ct[t][0][ml][4 * q + 3]});
+  }
   drain();
   __syncthreads();
   if (c.tid == 0) c.L.flag = add_ctr(c.cw(CW_C4 + j)) + 1u == tag * NGRP;
@@ -528,10 +631,10 @@ __device__ __forceinline__ void role_d(Ctx& c, int l, const WT& W) {
   if (!c.L.flag) return;
   // combine (the last of the tile's 8 groups): x_d = x_o + sum_g partial_g, split with the next norm
   const float* nwp = l + 1 < NL ? p.n1[l + 1] : p.norm;
-  if (c.tid < 256) {
+  if (m < 32 * MT) {
     f32x4_t pp[NGRP];
 #pragma unroll
-    for (int gg = 0; gg < NGRP; ++gg) pp[gg] = ld16(p.dpart, (((size_t)gg * 32 + m) * D + n) * 4);
+    for (int gg = 0; gg < NGRP; ++gg) pp[gg] = ld16(p.dpart, (((size_t)gg * RMAX + m) * D + n) * 4);
     const f32x4_t xo = ld16(p.x_o, ((size_t)m * D + n) * 4);
     const f32x4_t nw = *reinterpret_cast<const f32x4_t*>(nwp + n);
     f32x4_t s = pp[0];
@@ -539,10 +642,15 @@ __device__ __forceinline__ void role_d(Ctx& c, int l, const WT& W) {
     for (int gg = 1; gg < NGRP; ++gg) s += pp[gg];
     f32x4_t x = {0.f, 0.f, 0.f, 0.f};
     if (m < p.M) x = xo + s;
+    const f32x4_t xn = x * nw;
     st16(p.x_d, ((size_t)m * D + n) * 4, x);
-    st16(p.xs_out, xs::off(D, m, n), x * nw);
+    st16(p.xs_out, xs::off(D, m, n), xn);
     const float sq = sum8(fmaf(x.w, x.w, fmaf(x.z, x.z, fmaf(x.y, x.y, x.x * x.x))));
-    if (q == 0) st4(p.ss_out + (size_t)j * p.ss_stride + m, sq);
+    if (q == 0) st4(p.ss_out + (size_t)j * RMAX + m, sq);
+    if constexpr (Q4) {
+      const float hs = sum8((xn.x + xn.y) + (xn.z + xn.w));
+      if (q == 0) st4(p.hs_out + (size_t)j * RMAX + m, hs);
+    }
   }
   drain();
   __syncthreads();
@@ -550,124 +658,133 @@ __device__ __forceinline__ void role_d(Ctx& c, int l, const WT& W) {
   c.mark(11);
 }
 
-// H: audio_head[step - 1] rows 64 t .. 64 t + 63 (two 32-row tiles) of the final-normed rows (the last
-// combines' split x * norm + sums of squares) -> logits [row][Vp] and the tile's arg-max partial per row
-// (pack_argmax: the largest logit, the first index on ties), exactly the partial layout of the launch
-// path's head (gemm_xs EPI_ARGMAX, 64-row tiles), which the next step / advance_kernel reduce
-__device__ __forceinline__ void role_h(Ctx& c, const WT (&W)[2]) {
+// H: audio_head[step - 1] rows 64 t .. 64 t + 63 (two bf16 32-row tiles) of the final-normed rows (the
+// last combines' split x * norm + sums of squares) -> logits [row][Vp] and the tile's arg-max partial
+// per row (pack_argmax: the largest logit, the first index on ties), exactly the partial layout of the
+// launch path's head (gemm_xs EPI_ARGMAX, 64-row tiles), which the next step / advance_kernel reduce
+template <int MT>
+__device__ __forceinline__ void role_h(Ctx& c, int t0, const WTile<false> (&W)[2]) {
   const DecStepXsArgs& p = c.p;
-  const int t = c.w - H_WG0;
+  const int t = c.w - t0;
   const unsigned tag = c.ep * NL + NL;  // the last layer's combine flags
   wait_words(c, NDT, [](int i) { return CW_F5 + i; }, tag);
-  AF A;
-  load_af(p.xs_out, 2 * c.wave, c.lane, A);
-  row_scales(c, p.ss_out, p.ss_stride);
-  f32x16_t acc[2];
-  mma<2>(A, W, acc);
-  reduce_tiles<2>(c, acc);
-  // row m = tid / 16, columns 4 (tid % 16) .. + 3 of the 64
-  const int m = c.tid >> 4, c4 = 4 * (c.tid & 15), n = 64 * t + c4;
-  const float r = row_scale(c, m);
-  unsigned long long best = 0;
-  if (m < p.M && n < p.Vp) {
-    const float4 v = make_float4(c.L.ct[c4 >> 5][m][c4 & 31] * r, c.L.ct[c4 >> 5][m][(c4 & 31) + 1] * r,
-                                 c.L.ct[c4 >> 5][m][(c4 & 31) + 2] * r, c.L.ct[c4 >> 5][m][(c4 & 31) + 3] * r);
-    *reinterpret_cast<float4*>(p.head_out + (size_t)m * p.Vp + n) = v;
-    const float vv[4] = {v.x, v.y, v.z, v.w};
+  gemm_tiles<false, MT, 2>(c, p.xs_out, nullptr, KS_D, 2 * c.wave, W, [&] { row_scales(c, p.ss_out); });
+  // row m = tid / 16 (+ 32 per row tile), columns 4 (tid % 16) .. + 3 of the 64
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-      if (n + i < p.n_valid) {
-        const unsigned long long k = pack_argmax(vv[i], n + i);
-        best = k > best ? k : best;
-      }
-  }
+  for (int rt = 0; rt < MT; ++rt) {
+    const int ml = c.tid >> 4, m = 32 * rt + ml, c4 = 4 * (c.tid & 15), n = 64 * t + c4;
+    const float r = row_scale(c, m);
+    unsigned long long best = 0;
+    if (m < p.M && n < p.Vp) {
+      const float* ct = &c.L.ct[rt][c4 >> 5][ml][c4 & 31];
+      const float4 v = make_float4(ct[0] * r, ct[1] * r, ct[2] * r, ct[3] * r);
+      *reinterpret_cast<float4*>(p.head_out + (size_t)m * p.Vp + n) = v;
+      const float vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-  for (int o = 1; o < 16; o <<= 1) {
-    const unsigned long long v = __shfl_xor(best, o, 64);
-    best = v > best ? v : best;
+      for (int i = 0; i < 4; ++i)
+        if (n + i < p.n_valid) {
+          const unsigned long long k = pack_argmax(vv[i], n + i);
+          best = k > best ? k : best;
+        }
+    }
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      const unsigned long long v = __shfl_xor(best, o, 64);
+      best = v > best ? v : best;
+    }
+    if (m < p.M && (c.tid & 15) == 0) p.head_part[(size_t)m * p.part_stride + t] = best;
   }
-  if (m < p.M && (c.tid & 15) == 0) p.head_part[(size_t)m * p.part_stride + t] = best;
 }
 
 // The layer loop of one workgroup class (each its own straight-line code: exact register liveness per
 // class, no merged paths holding another class's prefetch registers).  CLS: 0 QKV, 1 o_proj,
 // 2 attention, 3 head (+ plain), 4 plain (gate/up + down only).
 enum { C_Q = 0, C_O = 1, C_A = 2, C_H = 3, C_P = 4 };
-template <int CLS>
+template <bool Q4, int CLS>
 __device__ __forceinline__ void run_layers(Ctx& c) {
   static_assert(CLS >= C_Q && CLS <= C_P, "workgroup class");
+  constexpr int MT = Q4 ? 2 : 1;
   const DecStepXsArgs& p = c.p;
   const int b = 32 * (c.w & 7) + (c.w >> 3), g = c.w & 7, j = c.w >> 3;
-  WT wq, wgu[2], wd;
+  WTile<Q4> wq, wgu[2], wd;
   // vmcnt retires in issue order and every publish drains it: a prefetch issued just before a hand-off
   // poll or a latency-critical operand load holds that back, so each class issues its next tiles after
-  // its own latency-critical steps (Q, A: after their publish)
-  // the plain and head classes (the most registers to spare) fetch their down tile with gate/up: a load
-  // issued just before the h hand-off's poll would hold the poll back (vmcnt order)
+  // its own latency-critical steps (Q, A: after their publish).  The plain and head classes (the most
+  // registers to spare) fetch their down tile with gate/up; the others during the h hand-off.
   constexpr bool WD_EARLY = CLS == C_P || CLS == C_H;
   auto ld_gu = [&](int l) {
-    load_wt(p.wgu[l], 2 * b, KS_D, 2 * c.wave, c.lane, wgu[0]);
-    load_wt(p.wgu[l], 2 * b + 1, KS_D, 2 * c.wave, c.lane, wgu[1]);
-    if constexpr (WD_EARLY) load_wt(p.wd[l], j, KS_F, 16 * g + 2 * c.wave, c.lane, wd);
+    load_wt<Q4>(p.wgu[l], 2 * b, KS_D, 2 * F / 32, 2 * c.wave, c.lane, wgu[0]);
+    load_wt<Q4>(p.wgu[l], 2 * b + 1, KS_D, 2 * F / 32, 2 * c.wave, c.lane, wgu[1]);
+    if constexpr (WD_EARLY) load_wt<Q4>(p.wd[l], j, KS_F, D / 32, 16 * g + 2 * c.wave, c.lane, wd);
   };
-  if constexpr (CLS == C_Q) load_wt(p.wqkv[1], c.w, KS_D, 2 * c.wave, c.lane, wq);
-  if constexpr (CLS == C_O) load_wt(p.wo[0], c.w - O_WG0, KS_D, 2 * c.wave, c.lane, wq);
+  if constexpr (CLS == C_Q) load_wt<Q4>(p.wqkv[1], c.w, KS_D, NQT, 2 * c.wave, c.lane, wq);
+  if constexpr (CLS == C_O) load_wt<Q4>(p.wo[0], c.w - O_WG0, KS_D, NDT, 2 * c.wave, c.lane, wq);
   if constexpr (CLS != C_A) ld_gu(0);
   for (int l = 0; l < NL; ++l) {
     c.l = l;
     c.mark(0);
     if constexpr (CLS == C_O || CLS == C_H || CLS == C_P) {
       if (l > 0) {
-        if constexpr (CLS == C_O) load_wt(p.wo[l], c.w - O_WG0, KS_D, 2 * c.wave, c.lane, wq);
+        if constexpr (CLS == C_O) load_wt<Q4>(p.wo[l], c.w - O_WG0, KS_D, NDT, 2 * c.wave, c.lane, wq);
         ld_gu(l);
       }
     }
     if constexpr (CLS == C_Q) {
       if (l > 0) {
-        role_q(c, l, wq);
+        role_q<Q4, MT>(c, l, wq);
         ld_gu(l);
       }
     }
     if constexpr (CLS == C_A) {
       stage_kv(c, l);  // (role_a's barrier publishes the LDS rows)
-      role_a(c, l);
+      role_a<Q4>(c, l);
       ld_gu(l);
     }
-    if constexpr (CLS == C_O) role_o(c, l, wq);
-    role_g(c, l, wgu);
-    if constexpr (!WD_EARLY) load_wt(p.wd[l], j, KS_F, 16 * g + 2 * c.wave, c.lane, wd);  // during the h hand-off
-    role_d(c, l, wd);
+    if constexpr (CLS == C_O) role_o<Q4, MT>(c, l, wq);
+    role_g<Q4, MT>(c, l, wgu);
+    if constexpr (!WD_EARLY) load_wt<Q4>(p.wd[l], j, KS_F, D / 32, 16 * g + 2 * c.wave, c.lane, wd);  // during the h hand-off
+    role_d<Q4, MT>(c, l, wd);
     // the next layer's QKV tile: during the combine the Q hand-off waits for
     if constexpr (CLS == C_Q) {
-      if (l > 0 && l + 1 < NL) load_wt(p.wqkv[l + 1], c.w, KS_D, 2 * c.wave, c.lane, wq);
+      if (l > 0 && l + 1 < NL) load_wt<Q4>(p.wqkv[l + 1], c.w, KS_D, NQT, 2 * c.wave, c.lane, wq);
     }
   }
-  if constexpr (CLS == C_H) {  // (a 32-row tile past the last is clamped: its columns are never stored)
-    load_wt(p.head_w, 2 * (c.w - H_WG0), KS_D, 2 * c.wave, c.lane, wgu[0]);
-    load_wt(p.head_w, min(2 * (c.w - H_WG0) + 1, p.head_nt32 - 1), KS_D, 2 * c.wave, c.lane, wgu[1]);
-    role_h(c, wgu);
+  if constexpr (CLS == C_H) {  // bf16 head tiles (a 32-row tile past the last is clamped: its columns are never stored)
+    constexpr int H_WG0 = A_WG0 + 32 * MT;
+    WTile<false> wh[2];
+    load_wt<false>(p.head_w, 2 * (c.w - H_WG0), KS_D, 0, 2 * c.wave, c.lane, wh[0]);
+    load_wt<false>(p.head_w, min(2 * (c.w - H_WG0) + 1, p.head_nt32 - 1), KS_D, 0, 2 * c.wave, c.lane, wh[1]);
+    role_h<MT>(c, H_WG0, wh);
   }
 }
 
-}  // namespace
-
-__global__ __launch_bounds__(NT, 1) void dec_step_xs_kernel(DecStepXsArgs p) {
+template <bool Q4>
+__device__ __forceinline__ void step_kernel(const DecStepXsArgs& p) {
+  constexpr int MT = Q4 ? 2 : 1, H_WG0 = A_WG0 + 32 * MT;
   __shared__ __attribute__((aligned(16))) Lds L;
   Ctx c{p, L, (int)blockIdx.x, (int)threadIdx.x, (int)(threadIdx.x & 63), __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), 0u};
   c.ep = __hip_atomic_load(p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (c.w < NQT) run_layers<C_Q>(c);
-  else if (c.w < O_WG0 + NDT) run_layers<C_O>(c);
-  else if (c.w < A_WG0 + 32) run_layers<C_A>(c);
-  else if (p.head_w && c.w < H_WG0 + p.head_tiles) run_layers<C_H>(c);
-  else run_layers<C_P>(c);
+  if (c.w < NQT) run_layers<Q4, C_Q>(c);
+  else if (c.w < O_WG0 + NDT) run_layers<Q4, C_O>(c);
+  else if (c.w < A_WG0 + 32 * MT) run_layers<Q4, C_A>(c);
+  else if (p.head_w && c.w < H_WG0 + p.head_tiles) run_layers<Q4, C_H>(c);
+  else run_layers<Q4, C_P>(c);
   if (p.stamps && c.tid == 0) p.stamps[(size_t)c.w * DEC_XSD_STAMPS + DEC_XSD_STAMPS - 1] = __builtin_amdgcn_s_memrealtime();
   if (c.w == 0 && c.tid == 0) __hip_atomic_store(p.epoch, c.ep + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+}  // namespace
+
+__global__ __launch_bounds__(NT, 1) void dec_step_xs_kernel(DecStepXsArgs p) { step_kernel<false>(p); }
+__global__ __launch_bounds__(NT, 1) void dec_step_xs_q4_kernel(DecStepXsArgs p) { step_kernel<true>(p); }
+
 size_t dec_step_xs_ctrl_bytes() { return (size_t)CW_N * CW_STRIDE * 4; }
 
-void launch_dec_step_xs(const DecStepXsArgs& p, hipStream_t st) {
-  hipLaunchKernelGGL(dec_step_xs_kernel, dim3(NWG), dim3(NT), 0, st, p);
+void launch_dec_step_xs(const DecStepXsArgs& p, hipStream_t st, bool q4) {
+  if (q4) hipLaunchKernelGGL(dec_step_xs_q4_kernel, dim3(NWG), dim3(NT), 0, st, p);
+  else hipLaunchKernelGGL(dec_step_xs_kernel, dim3(NWG), dim3(NT), 0, st, p);
 }
 
-const void* dec_step_xs_kernel_ptr() { return reinterpret_cast<const void*>(&dec_step_xs_kernel); }
+const void* dec_step_xs_kernel_ptr(bool q4) {
+  return q4 ? reinterpret_cast<const void*>(&dec_step_xs_q4_kernel) : reinterpret_cast<const void*>(&dec_step_xs_kernel);
+}

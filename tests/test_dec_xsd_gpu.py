@@ -114,3 +114,38 @@ def test_dec_xsd_sampled_matches_launch_path(model_1b):
     for b in range(B):
         d = first_divergence(gh[: gn[b], b], rh[: rn[b], b])
         assert d is None, f"utterance {b}: sampled codes differ from the launch path at frame {d}"
+
+
+@pytest.fixture(scope="module")
+def model_1b_q4():
+    from csm_mlx.models import CSM
+    args, w = csm_weights("1b")
+    model = CSM(args, dtype="q4", max_batch=64)
+    model.load_weights(w)
+    yield args, w, model
+    del model
+
+
+@pytest.mark.parametrize("B", [8, 40, 64])
+def test_dec_xsd_q4_matches_launch_path_and_oracle(model_1b_q4, B):
+    """The int4 kernel (nn.quantize'd decoder, two 32-row tiles: configs[4]'s B = 64): nibbles as exact
+    bf16 operands, the per-group scale / bias fold over the producers' half-group sums.  4 frames greedy:
+    codes identical to the launch path and to the oracle on the dequantized weights, ci logits within
+    1e-3 x max of the launch path."""
+    from csm_mlx.sampling import Sampler
+    from csm_mlx.tokenizers import tokenize_text_segment
+    args, w, model = model_1b_q4
+    prompts = [tokenize_text_segment(prompt_ids(800 + b, 10 + b % 3), 0, args.n_audio_codebooks) for b in range(B)]
+    (rh, rn, rl), (gh, gn, gl) = _ab(model, prompts, 4, Sampler(0.0, 0))
+    assert np.array_equal(rn, gn)
+    for b in range(B):
+        d = first_divergence(gh[: gn[b], b], rh[: rn[b], b])
+        assert d is None, f"utterance {b}: codes differ from the launch path at frame {d}"
+    for f, (a, r) in enumerate(zip(gl, rl)):
+        err = np.abs(a - r).max(axis=-1)
+        assert (err <= 1e-3 * np.abs(r).max(axis=-1)).all(), f"frame {f}: ci logits differ (max {err.max():.3e})"
+    if B == 64:
+        ref = oracle_batch(oracle_for(args, w, q4=True), prompts, 4)
+        for b in range(B):
+            d = first_divergence(gh[: gn[b], b], ref[b][0])
+            assert d is None and gn[b] == len(ref[b][0]), f"utterance {b}: first divergence {d} vs the oracle"

@@ -2,7 +2,7 @@
 """Per-role timing of the persistent batched decoder step (dec_step_xs.hip) from its s_memrealtime marks
 (100 MHz): csm_1b bf16, B utterances (default 32), a few frames; the marks hold the last launch (the last
 codebook step of the last frame).
-usage: python tools/xsd_stamps.py [B] [frames]  -> per layer: when each role's wait ended / it published
+usage: python tools/xsd_stamps.py [B] [frames] [bf16|q4]  -> per layer: when each role's wait ended / it published
 (max over the workgroups of that role, us since the first workgroup started), and the kernel span."""
 import os
 import sys
@@ -19,7 +19,8 @@ from csm_mlx.tokenizers import tokenize_text_segment  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 32
 frames = int(sys.argv[2]) if len(sys.argv) > 2 else 3
-model = bench.build_model("bf16", B)
+dtype = sys.argv[3] if len(sys.argv) > 3 else "bf16"
+model = bench.build_model(dtype, B)
 L = _lib.lib()
 _lib.check(L.csm_set_option(model.engine, b"dec_xsd_stamps", 1))
 cache = FrameCache(model, B, Sampler(0.0, 0), list(range(B)))
@@ -35,7 +36,8 @@ t0 = s[:, 0][s[:, 0] > 0].min()
 rel = np.where(s > 0, (s - t0) / 100.0, np.nan)
 w = np.arange(256)
 isq, iso = w < 48, (w >= 48) & (w < 80)
-print(f"B={B}: kernel span {np.nanmax(rel[:, NS - 1]):.1f} us (start skew {np.nanmax(rel[:, 0]):.2f} us)")
+MR = 64 if dtype == "q4" else 32
+print(f"B={B} {dtype}: kernel span {np.nanmax(rel[:, NS - 1]):.1f} us (start skew {np.nanmax(rel[:, 0]):.2f} us)")
 names = {1: ("Q waited", isq), 2: ("Q published", isq), 3: ("A K/V staged", None), 4: ("A arrived", None),
          5: ("O waited", iso), 6: ("O published", iso), 7: ("G waited", None), 8: ("G published", None),
          9: ("D waited", None), 10: ("D ticket", None), 11: ("combine published", None)}
