@@ -314,8 +314,9 @@ def _traffic(key: str):
 
 def rooflines(model, batch: int, iters: int = 400):
     """Live HIP-event rooflines on the engine stream.  ``dominant``: the persistent frame decoder
-    (dec_frame_kernel, one launch per frame) when it runs the frame's head -- batch 1 bf16 or int4 --
-    else the decoder gate/up projection at this batch; ``backbone_gate_up`` beside it: the persistent
+    (dec_frame_kernel, one launch per frame) when it runs the frame's head -- batch 1 bf16 or int4 --,
+    the persistent batched decoder step (dec_step_xs_kernel, one launch per codebook step >= 2) when it
+    runs the batch's steps, else the decoder gate/up projection at this batch; ``backbone_gate_up`` beside it: the persistent
     backbone step (bb_step_kernel) when it runs the batch-1 backbone, else the backbone gate/up
     projection at this batch."""
     from csm_mlx import _lib
@@ -351,6 +352,11 @@ def rooflines(model, batch: int, iters: int = 400):
         out["dominant"] = entry(us.value, nb.value, f"{dfk} = persistent frame decoder: codebook0_head + "
                                 "31 decoder steps (4 layers + audio_head slice each) of one frame, one launch",
                                 f"dec_frame/{model.dtype}/B1")
+    elif batch > 1 and iters > 0 and L.csm_bench_dec_xsd(model.engine, 20, ctypes.byref(us), ctypes.byref(nb)) == 0:
+        xk = "dec_step_xs_q4_kernel" if model.dtype == "q4" else "dec_step_xs_kernel"
+        out["dominant"] = entry(us.value, nb.value, f"{xk} = persistent batched decoder step: the 4 decoder layers + "
+                                f"audio_head slice of one codebook step for {batch} rows, one launch (30 per frame)",
+                                f"dec_xsd/{model.dtype}/B{batch}")
     else:
         out["dominant"] = gemv(4, "decoder")
     return out

@@ -101,6 +101,7 @@ def lib():
             "csm_bench_gemv": ([P, I, I, I, ctypes.POINTER(F), ctypes.POINTER(ctypes.c_double)], I),
             "csm_bench_dec_frame": ([P, I, ctypes.POINTER(F), ctypes.POINTER(ctypes.c_double)], I),
             "csm_bench_bb_step": ([P, I, ctypes.POINTER(F), ctypes.POINTER(ctypes.c_double)], I),
+            "csm_bench_dec_xsd": ([P, I, ctypes.POINTER(F), ctypes.POINTER(ctypes.c_double)], I),
             "csm_weight_buffers": ([P, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint64), I,
                                     ctypes.POINTER(I)], I),
             "csm_weights_received": ([P], I),

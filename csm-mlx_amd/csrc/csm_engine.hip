@@ -2103,6 +2103,46 @@ int csm_bench_dec_frame(csm_engine* e, int iters, float* avg_us, double* bytes) 
   CSM_CATCH
 }
 
+int csm_bench_dec_xsd(csm_engine* e, int iters, float* avg_us, double* bytes) {
+  CSM_TRY {
+    if (!e || iters <= 0) throw CsmError(CSM_ERR_ARG, "bad bench arguments");
+    const int M = e->B, K = e->K;
+    if (e->frames_run < 1 || !xsd_eligible(e, M)) throw CsmError(CSM_ERR_STATE, "the persistent batched decoder step is not active on this engine");
+    HIPCHK(hipSetDevice(e->dev));
+    // The replay recomputes the last frame's last codebook step (i = K - 1) from the same partials of
+    // step K - 2: the same K/V rows, codes, logits and partials are written again.
+    const int Vp = e->Vpad, i = K - 1;
+    const bool greedy = e->temperature <= 0.f;
+    auto part = [&](int cb) { return e->part + (size_t)cb * e->B_max * e->part_stride; };
+    const int pn = greedy ? head_blocks(Vp, e->Dd, M, e->head_wdt) : 1;
+    const size_t D = e->Dd, F = e->dec.d.intermediate, QKV = e->dec.qkv_rows(), HKV = e->dec.d.n_kv_heads, HD = e->dec.d.head_dim;
+    auto wb = [&](size_t n, size_t k) { return (double)e->wbytes(n, k); };
+    double nb = (double)M * (QKV + D) * 4;                                  // layer 0: folded table rows
+    for (int l = 0; l < DEC_FRAME_LAYERS; ++l) {
+      if (l > 0) nb += wb(QKV, D);
+      nb += wb(D, D) + wb(2 * F, D) + wb(D, F);                             // weights in their storage format
+      nb += 2.0 * M * HKV * (i + 1) * HD * 4;                               // K/V history read + append
+    }
+    nb += (double)Vp * D * 2;                                               // audio_head[i - 1] (bf16)
+    for (int r = 0; r < 2; ++r) launch_xsd(e, M, i, part(i - 1), pn, part(i), e->st);
+    hipEvent_t a, b;
+    HIPCHK(hipEventCreate(&a));
+    HIPCHK(hipEventCreate(&b));
+    HIPCHK(hipEventRecord(a, e->st));
+    for (int r = 0; r < iters; ++r) launch_xsd(e, M, i, part(i - 1), pn, part(i), e->st);
+    HIPCHK(hipEventRecord(b, e->st));
+    HIPCHK(hipEventSynchronize(b));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, a, b));
+    (void)hipEventDestroy(a);
+    (void)hipEventDestroy(b);
+    check_dec_frame(e);
+    if (avg_us) *avg_us = ms * 1000.f / (float)iters;
+    if (bytes) *bytes = nb;
+  }
+  CSM_CATCH
+}
+
 int csm_bench_bb_step(csm_engine* e, int iters, float* avg_us, double* bytes) {
   CSM_TRY {
     if (!e || iters <= 0) throw CsmError(CSM_ERR_ARG, "bad bench arguments");
@@ -2213,7 +2253,7 @@ int csm_set_option(csm_engine* e, const char* key, int value) {
     else if (k == "inject_handoff_error") {  // test hook: raise the persistent kernels' timeout flags
       if (!e) throw CsmError(CSM_ERR_ARG, "inject_handoff_error needs an engine");
       const int one = 1;
-      for (int* f : {e->df_err, e->bb_err})
+      for (int* f : {e->df_err, e->bb_err, e->xsd_err})
         if (f && value) HIPCHK(hipMemcpy(f, &one, 4, hipMemcpyHostToDevice));
     }
     else throw CsmError(CSM_ERR_ARG, "unknown option " + k);

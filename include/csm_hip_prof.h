@@ -33,6 +33,12 @@ int csm_bench_dec_frame(csm_engine* e, int iters, float* avg_us, double* bytes);
  * bytes one launch moves (every backbone weight in bf16 + the K/V rows).  CSM_ERR_STATE when the
  * engine does not run it (not batch-1 bf16 csm_1b shapes, or no frame run yet). */
 int csm_bench_bb_step(csm_engine* e, int iters, float* avg_us, double* bytes);
+/* The persistent batched decoder step (dec_step_xs.hip; batch 1..32 bf16 / 1..64 int4 on the streaming
+ * path) replayed `iters` times for the last codebook step of the last frame (same partials, same
+ * position; idempotent): average launch time and the algorithmic bytes one launch reads (decoder weights
+ * in their storage format + the bf16 audio_head slice + folded table rows + K/V history).  CSM_ERR_STATE
+ * when the step kernel is not active on this engine. */
+int csm_bench_dec_xsd(csm_engine* e, int iters, float* avg_us, double* bytes);
 
 /* Tuning / debug switches (re-capture the frame graphs), per engine: "fold_proj" (decoder steps >= 2
  * gather projection(E_a[c]) from a table built at csm_begin, default 1), "qkv0_tab" (decoder layer 0's
@@ -46,8 +52,11 @@ int csm_bench_bb_step(csm_engine* e, int iters, float* avg_us, double* bytes);
  * tests), "gemm_xs" (the batched depth decoder on the streaming matrix-core GEMM, gemm_xs.hip,
  * default 1), "bb_xs" (the batched backbone on it too, default 1), "prefill_rows" (row cap of one
  * csm_prefill_batch group, 0 = the engine's capacity), "attn_prefill" (prompt attention on the fp32 matrix
- * cores, a block per 64-row prompt run and kv head, default 1; 0 = one block per row, tests), "inject_handoff_error"
- * (test hook).
+ * cores, a block per 64-row prompt run and kv head, default 1; 0 = one block per row, tests), "dec_xsd"
+ * (codebook steps >= 2 of the streaming path on the persistent batched decoder step, dec_step_xs.hip:
+ * <= 32 bf16 / <= 64 int4 rows, default 1), "dec_xsd_head" (its head in the same launch, default 1),
+ * "dec_xsd_stamps" (its per-role clock marks, csm_debug_read "dec_xsd_stamps", default 0),
+ * "inject_handoff_error" (test hook).
  * Process-wide lab knobs are environment variables read once (CSM_NT_MASK, CSM_GEMV_XL, CSM_XS_*). */
 int csm_set_option(csm_engine* e, const char* key, int value);
 

@@ -149,3 +149,25 @@ def test_dec_xsd_q4_matches_launch_path_and_oracle(model_1b_q4, B):
         for b in range(B):
             d = first_divergence(gh[: gn[b], b], ref[b][0])
             assert d is None and gn[b] == len(ref[b][0]), f"utterance {b}: first divergence {d} vs the oracle"
+
+
+def test_dec_xsd_timeout_reported_and_recovered(model_1b):
+    """A raised hand-off timeout flag: every wait of the step kernel gives up (bounded spins, the grid
+    drains), the frame raises, and the flags / tickets / epoch are reset so the next frames are exact
+    again (codes identical to the launch path)."""
+    from csm_mlx import _lib
+    from csm_mlx.sampling import Sampler
+    from csm_mlx.tokenizers import tokenize_text_segment
+    args, w, model = model_1b
+    L = _lib.lib()
+    B = 16
+    prompts = [tokenize_text_segment(prompt_ids(900 + b, 10 + b % 3), 0, args.n_audio_codebooks) for b in range(B)]
+    _lib.check(L.csm_set_option(model.engine, b"dec_xsd", 1))
+    _lib.check(L.csm_set_option(model.engine, b"inject_handoff_error", 1))
+    with pytest.raises(_lib.CsmHipError, match="hand-off wait timed out"):
+        _run(model, prompts, 2, Sampler(0.0, 0))
+    _lib.check(L.csm_synchronize(model.engine))
+    (rh, rn, _), (gh, gn, _) = _ab(model, prompts, 3, Sampler(0.0, 0))
+    assert np.array_equal(rn, gn)
+    for b in range(B):
+        assert first_divergence(gh[: gn[b], b], rh[: rn[b], b]) is None, f"utterance {b} after the reset"
