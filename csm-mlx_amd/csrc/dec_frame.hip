@@ -650,6 +650,9 @@ __device__ __forceinline__ void gather_qkv(Ctx& c, const u64* buf, int pos0, con
 #ifndef DF_PV
 #define DF_PV 2
 #endif
+#ifndef DF_ATTN_SUB
+#define DF_ATTN_SUB 0  // lab: 1 / 2 move the attention-end mark after the softmax / after P.V (tools/df_stamps.py)
+#endif
 template <int M, bool Q4 = false>
 __device__ __forceinline__ void phase_attn(Ctx& c, int pos0, int layer) {
   static_assert(!Q4 || DF_PV == 2, "the int4 kernel stages the attention output from the DF_PV 2 loop");
@@ -684,6 +687,7 @@ __device__ __forceinline__ void phase_attn(Ctx& c, int pos0, int layer) {
     const float pj = kj < n ? expf(s - mx) : 0.f;
     const float l_run = wave_sum(hh == 0 ? pj : 0.f);
     const int pji = __float_as_int(pj);
+    if (DF_ATTN_SUB == 1 && m == M - 1) c.mark();  // lab: the attention mark after the softmax
 #if DF_PV == 1
     // lane = dims 2 lane, 2 lane + 1 (one 8-B V read per key), keys in order
     float o0 = 0.f, o1 = 0.f;
@@ -777,6 +781,7 @@ __device__ __forceinline__ void phase_attn(Ctx& c, int pos0, int layer) {
     c.L.att[m][h * HD + c.lane + 64] = o1 * inv;
 #endif
   }
+  if (DF_ATTN_SUB == 2) c.mark();  // lab: the attention mark after P.V (before the K/V store + barrier)
   // the new K / V rows -> cache, spread over the workgroups (WG w stores element w of each row:
   // 2 heads x 128 = 256 elements), write-through; the storing threads drain them (vmcnt(0)) before
   // this WG's next publish (phase_mlp), so a reader that saw that hand-off reads them coherently
@@ -1443,7 +1448,7 @@ __device__ __forceinline__ void decoder_layer(Ctx& c, int l, int step, int pos0,
     ld_gu<Q4, true>(c, l, r);
   }
   phase_attn<M, Q4>(c, pos0, l);
-  c.mark();
+  if (DF_ATTN_SUB == 0) c.mark();
   if constexpr (Q4) phase_o4<M>(c, r.wo);             // -> E3
   else phase_o<M>(c, r.wo);
   c.mark();
