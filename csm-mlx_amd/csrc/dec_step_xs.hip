@@ -75,9 +75,6 @@ enum { CW_F1 = 0, CW_F2 = CW_F1 + NQT, CW_F3 = CW_F2 + RMAX, CW_FH = CW_F3 + NDT
        CW_N = CW_F5 + NDT };
 constexpr int CW_STRIDE = 32;
 
-#ifndef XSD_LAB
-#define XSD_LAB 0  // lab (timing only, wrong results): 1 = no activation split, 2 = a third operand load per stage
-#endif
 #ifndef XSD_UNION
 #define XSD_UNION 1  // lab: 0 keeps the attention buffers apart from the MFMA reduction slots
 #endif
@@ -205,14 +202,6 @@ __device__ __forceinline__ void load_af(const void* X, int nks, int t, int st0, 
       for (int hf = 0; hf < 2; ++hf)
         r.a[q][s][hf] = __builtin_amdgcn_raw_buffer_load_b128(
             rs, lane * 16, __builtin_amdgcn_readfirstlane((((t * nks + st0 + q) * 4 + s) * 2 + hf) * 1024), SC1);
-  if constexpr ((XSD_LAB & 2) != 0) {
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-#pragma unroll
-      for (int s = 0; s < 4; ++s)
-        r.a[q][s][0] ^= __builtin_amdgcn_raw_buffer_load_b128(
-            rs, lane * 16, __builtin_amdgcn_readfirstlane((((t * nks + st0 + q) * 4 + s) * 2 + (s & 1)) * 1024 + 512), SC1);
-  }
 }
 // int4: X_g of the wave's two stages for every row -> L.xg[wave] (from the producer's half-group sums
 // hs[k / 32][RMAX]); a barrier follows before use
@@ -244,11 +233,7 @@ __device__ __forceinline__ void mma(const Ctx& c, const AF& A, const WTile<Q4> (
 #pragma unroll
         for (int i = 0; i < NTL; ++i) bq[i] = __builtin_bit_cast(bf16x8_t, xs::q4_word_bf16(W[i].a[q][s]));
         u32x4_t pt[3];
-        if constexpr ((XSD_LAB & 1) != 0) {
-          pt[0] = A.a[q][s][0]; pt[1] = A.a[q][s][1]; pt[2] = A.a[q][s][0];
-        } else {
-          xs::split_frag(A.a[q][s][0], A.a[q][s][1], pt);
-        }
+        xs::split_frag(A.a[q][s][0], A.a[q][s][1], pt);
 #pragma unroll
         for (int pp = 0; pp < 3; ++pp)
 #pragma unroll
@@ -277,11 +262,7 @@ __device__ __forceinline__ void mma(const Ctx& c, const AF& A, const WTile<Q4> (
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         u32x4_t pt[3];
-        if constexpr ((XSD_LAB & 1) != 0) {
-          pt[0] = A.a[q][s][0]; pt[1] = A.a[q][s][1]; pt[2] = A.a[q][s][0];
-        } else {
-          xs::split_frag(A.a[q][s][0], A.a[q][s][1], pt);
-        }
+        xs::split_frag(A.a[q][s][0], A.a[q][s][1], pt);
 #pragma unroll
         for (int pp = 0; pp < 3; ++pp)
 #pragma unroll
