@@ -831,12 +831,28 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(AttnParams p) {
   __shared__ __attribute__((aligned(16))) float Vs[64 * HD];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, c32 = lane & 31, hh = lane >> 5;
   const int kvh = blockIdx.x % p.Hkv, tile = blockIdx.x / p.Hkv;
-  const int2 tl = p.rm.tiles[tile];
-  const int m0 = tl.x, n = tl.y;
+  int m0, n;
+  if (p.rm.tiles) {
+    const int2 tl = p.rm.tiles[tile];
+    m0 = tl.x;
+    n = tl.y;
+  } else {  // uniform calls (the codec transformer): rm.T rows per utterance, ceil(T / 64) tiles each
+    const int tpu = (p.rm.T + 63) / 64, r0 = 64 * (tile % tpu);
+    m0 = (tile / tpu) * p.rm.T + r0;
+    n = min(64, p.rm.T - r0);
+  }
   const int G = p.Hq / p.Hkv;
   const bool head_ok = wave < G;
   const int h = kvh * G + min(wave, G - 1);
-  const int b = p.rm.b(m0), pos0 = p.rm.pos(m0), kmax = pos0 + n - 1;
+  const int b = p.rm.b(m0), pos0 = p.rm.pos(m0);
+  // keys kbeg .. kmax: causal -- 0 .. the tile's last position, each row masked past its own; ATTN_BLOCK
+  // (moshi_mlx, as attn_block) -- every row of the call sees the call's keys and `window` past ones
+  int kbeg = 0, kmax = pos0 + n - 1;
+  if (p.mode == ATTN_BLOCK) {
+    const int off = pos0 - (m0 % p.rm.T);
+    kbeg = max(0, off - p.window);
+    kmax = off + p.rm.T - 1;
+  }
   const float* K = p.kc + ((size_t)b * p.Hkv + kvh) * p.S_cap * HD;
   const float* V = p.vc + ((size_t)b * p.Hkv + kvh) * p.S_cap * HD;
   typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -850,7 +866,7 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(AttnParams p) {
       vv[u] = *reinterpret_cast<const f32x4*>(V + (size_t)j * HD + d4 * 4);
     }
   };
-  fetch(0);
+  fetch(kbeg);
   // this lane's query rows (clamped: rows past the tile repeat its last row, never stored), scaled,
   // dims 32 hh .. 32 hh + 31 (the score steps' B operand)
   float qv[2][HD / 2];
@@ -858,7 +874,7 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(AttnParams p) {
 #pragma unroll
   for (int rt = 0; rt < 2; ++rt) {
     const int r = min(32 * rt + c32, n - 1);
-    rpos[rt] = pos0 + r;
+    rpos[rt] = p.mode == ATTN_BLOCK ? kmax : pos0 + r;
     const f32x4* qp = reinterpret_cast<const f32x4*>(p.q + (size_t)(m0 + r) * p.qs + h * HD + 32 * hh);
 #pragma unroll
     for (int s4 = 0; s4 < HD / 8; ++s4) {
@@ -875,7 +891,7 @@ __global__ __launch_bounds__(256) void attn_prefill_kernel(AttnParams p) {
   for (int rt = 0; rt < 2; ++rt)
 #pragma unroll
     for (int dt = 0; dt < 2; ++dt) o[rt][dt] = f32x16{};
-  for (int c = 0; c <= kmax; c += 64) {
+  for (int c = kbeg; c <= kmax; c += 64) {
     __syncthreads();  // the previous chunk consumed
 #pragma unroll
     for (int u = 0; u < PER; ++u) {
@@ -1527,6 +1543,16 @@ void launch_attn(const AttnParams& p, int hd, hipStream_t st) {
   if (p.rm.tiles && p.rm.ntiles > 0 && p.M >= 16 * p.rm.ntiles && hd == 64 && p.mode == ATTN_CAUSAL && !p.g_tab &&
       !p.xs_out && p.Hq / p.Hkv <= 4) {
     hipLaunchKernelGGL(attn_prefill_kernel<64>, dim3(p.rm.ntiles * p.Hkv), dim3(256), 0, st, p);
+    return;
+  }
+  // the codec transformer's whole-call rows (Mimi encode / decode: rm.T rows per utterance, every key of
+  // the call visible): the same matrix-core tiles, tiles derived from rm.T (CSM_MIMI_ATTN_TILES=0: per row)
+  static const bool mimi_tiles = [] { const char* e = getenv("CSM_MIMI_ATTN_TILES"); return !(e && e[0] == '0'); }();
+  if (mimi_tiles && !p.rm.tiles && !p.rm.row_b && !p.rm.row_pos && p.mode == ATTN_BLOCK && hd == 64 && !p.g_tab &&
+      !p.xs_out && p.rm.T >= 16 && p.M % p.rm.T == 0 && p.Hq / p.Hkv <= 4) {
+    AttnParams q = p;
+    q.rm.ntiles = p.M / p.rm.T * ((p.rm.T + 63) / 64);
+    hipLaunchKernelGGL(attn_prefill_kernel<64>, dim3(q.rm.ntiles * q.Hkv), dim3(256), 0, st, q);
     return;
   }
   const int blocks = p.M * p.Hkv;

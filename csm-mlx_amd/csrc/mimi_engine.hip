@@ -82,7 +82,7 @@ struct mimi_codec {
   std::vector<void*> allocs;
   // workspace (grown on demand)
   size_t ws_big = 0, ws_rows = 0;
-  float *W0 = nullptr, *W1 = nullptr, *H = nullptr;
+  float *W0 = nullptr, *W1 = nullptr, *H = nullptr, *E = nullptr;  // E: ELU of the encoder's current buffer
   float* ks_ws = nullptr;  // split-K scratch of the codec GEMMs (MIMI_KS_WS_FLOATS, mimi_kernels.h)
   float *R = nullptr, *Rh = nullptr, *Rqkv = nullptr, *Rq = nullptr, *Ratt = nullptr, *Rf = nullptr;
   int* dcodes = nullptr;
@@ -107,7 +107,7 @@ struct mimi_codec {
   }
   ~mimi_codec() {
     for (void* p : allocs) (void)hipFree(p);
-    for (float* p : {W0, W1, H, R, Rh, Rqkv, Rq, Ratt, Rf, dpcm}) if (p) (void)hipFree(p);
+    for (float* p : {W0, W1, H, E, R, Rh, Rqkv, Rq, Ratt, Rf, dpcm}) if (p) (void)hipFree(p);
     if (dcodes) (void)hipFree(dcodes);
     if (rvq_r) (void)hipFree(rvq_r);
     if (rvq_p) (void)hipFree(rvq_p);
@@ -283,9 +283,9 @@ void grow(T*& p, size_t& cap, size_t n) {
 
 void ensure_ws(mimi_codec* m, size_t big, size_t rows_M) {
   if (big > m->ws_big) {
-    for (float** p : {&m->W0, &m->W1, &m->H})
+    for (float** p : {&m->W0, &m->W1, &m->H, &m->E})
       if (*p) (void)hipFree(*p);
-    for (float** p : {&m->W0, &m->W1, &m->H})
+    for (float** p : {&m->W0, &m->W1, &m->H, &m->E})
       if (hipMalloc((void**)p, big * 4) != hipSuccess) throw CsmError(CSM_ERR_HIP, "workspace allocation failed");
     m->ws_big = big;
   }
@@ -576,10 +576,23 @@ int mimi_encode(mimi_codec* m, int B, int N, const float* pcm, int32_t* codes, i
     float* bufs[2] = {m->W0, m->W1};
     int cur = 0;
     int64_t Tin = N;
+    // ELU once per element (CSM_MIMI_ELU_PRE=0: in every consumer's staging loads, A/B): an op whose
+    // next op is an ELU-input conv stores ELU(y) in place of y; one whose next op is a residual block
+    // (ELU for its first conv, y itself for the skip) also writes ELU(y) to m->E.  in_elu: bufs[cur]
+    // holds ELU(x); have_e: m->E holds ELU(bufs[cur]).
+    static const bool elu_pre = [] { const char* e = getenv("CSM_MIMI_ELU_PRE"); return !(e && e[0] == '0'); }();
+    bool in_elu = false, have_e = false;
+    auto out_elu = [&](size_t i, ConvParams& p) {
+      const MOp* nx = i + 1 < m->enc_ops.size() ? &m->enc_ops[i + 1] : nullptr;
+      if (!elu_pre || !nx) return;
+      if (nx->kind == 0 && m->convs[nx->idx].elu) p.elu_out = 1;
+      else if (nx->kind != 0) p.y2 = m->E;
+    };
     for (size_t i = 0; i < m->enc_ops.size(); ++i) {
       const MOp& o = m->enc_ops[i];
       float* in = bufs[cur];
       float* out = bufs[cur ^ 1];
+      bool nx_in_elu = false, nx_have_e = false;
       if (o.kind == 0) {
         const MConv& c = m->convs[o.idx];
         const int k_eff = (c.k - 1) * c.dil + 1;
@@ -590,6 +603,11 @@ int mimi_encode(mimi_codec* m, int B, int N, const float* pcm, int32_t* codes, i
         p.w = c.w; p.bias = c.b; p.Cout = c.cout; p.k = c.k; p.stride = c.stride; p.dil = c.dil;
         p.pad_l = k_eff - c.stride; p.elu_in = c.elu; p.y = out; p.Tout = (int)Tout;
         p.y_bstride = c.cout * (int)Tout; p.y_cstride = (int)Tout; p.B = B;
+        if (in_elu && !c.elu) throw CsmError(CSM_ERR_HIP, "mimi encoder: ELU bookkeeping");
+        if (in_elu) p.elu_in = 0;
+        out_elu(i, p);
+        nx_in_elu = p.elu_out != 0;
+        nx_have_e = p.y2 != nullptr;
         launch_conv1d(p, st);
         Tin = Tout;
       } else {  // resblock on the full sequence (causal, zero left pad)
@@ -600,15 +618,23 @@ int mimi_encode(mimi_codec* m, int B, int N, const float* pcm, int32_t* codes, i
         p.w = r.c1.w; p.bias = r.c1.b; p.Cout = r.hid; p.k = r.k; p.stride = 1; p.dil = r.dil;
         p.pad_l = (r.k - 1) * r.dil; p.elu_in = 1; p.y = m->H; p.Tout = (int)Tin; p.y_bstride = r.hid * (int)Tin;
         p.y_cstride = (int)Tin; p.B = B;
+        if (in_elu) throw CsmError(CSM_ERR_HIP, "mimi encoder: ELU bookkeeping");
+        if (have_e) { p.x = m->E; p.elu_in = 0; }
+        p.elu_out = elu_pre;  // H feeds only the block's second (ELU-input) conv
         launch_conv1d(p, st);
         ConvParams q{};
         q.ks_ws = m->ks_ws;
         q.x = m->H; q.Cin = r.hid; q.Tin = (int)Tin; q.x_bstride = r.hid * (int)Tin; q.x_cstride = (int)Tin;
-        q.w = r.c2.w; q.bias = r.c2.b; q.Cout = r.ch; q.k = 1; q.stride = 1; q.dil = 1; q.elu_in = 1; q.y = out;
+        q.w = r.c2.w; q.bias = r.c2.b; q.Cout = r.ch; q.k = 1; q.stride = 1; q.dil = 1; q.elu_in = elu_pre ? 0 : 1; q.y = out;
         q.Tout = (int)Tin; q.y_bstride = r.ch * (int)Tin; q.y_cstride = (int)Tin; q.resid = in;
         q.r_bstride = r.ch * (int)Tin; q.r_cstride = (int)Tin; q.B = B;
+        out_elu(i, q);
+        nx_in_elu = q.elu_out != 0;
+        nx_have_e = q.y2 != nullptr;
         launch_conv1d(q, st);
       }
+      in_elu = nx_in_elu;
+      have_e = nx_have_e;
       cur ^= 1;
     }
     // transformer on [B][dim][T25]

@@ -23,6 +23,11 @@ struct ConvParams {
   int r_bstride, r_cstride, r_off;
   int B;
   float* ks_ws;                    // split-K scratch (MIMI_KS_WS_FLOATS) or null
+  // ELU of the output for a consumer that would apply it on every load (the encoder's ELU-input convs:
+  // each input read k x ceil(Cout / tile) times): elu_out stores ELU(y) in place of y, y2 (same layout
+  // as y) receives ELU(y) beside it.  ELU(v) of the stored v is what the consumer computed: bit-identical.
+  int elu_out;
+  float* y2;
 };
 
 // ConvTranspose1d with k = 2*s (every Mimi transposed conv): per output phase r = t % s,

@@ -510,7 +510,9 @@ struct ConvProblem {
     }
     if (c.bias) v += e.x;
     if (c.resid) v += e.y;
-    c.y[(size_t)z * c.y_bstride + (size_t)co * c.y_cstride + c.y_off + t] = v;
+    const size_t o = (size_t)z * c.y_bstride + (size_t)co * c.y_cstride + c.y_off + t;
+    if (c.y2) c.y2[o] = elu_f(v);
+    c.y[o] = c.elu_out ? elu_f(v) : v;
   }
   __device__ void store(int z, int co, int t, float v) const { post(z, co, t, v, pre(z, co, t)); }
 };

@@ -156,3 +156,18 @@ def test_decode_step_batch_folding_bit_identical(tmp_path):
         o.reset_state()
         ref = np.concatenate([o.decode_step(codes[b: b + 1, :, f: f + 1]) for f in range(5)], axis=2)
         assert _rms(outs["1"][b: b + 1], ref) <= 1e-4, (b, _rms(outs["1"][b: b + 1], ref))
+
+
+def test_transformer_tile_attention_two_tiles():
+    """The codec transformer's attention on the matrix-core tiles (attn_prefill_kernel in ATTN_BLOCK mode:
+    rm.T rows per utterance, every key of the call visible): 5 s segments put 125 rows in each call, two
+    tiles per utterance, the second ragged (61 rows).  Encode codes bit-exact against the oracle; the decode
+    of 63 frames (126 rows a call) within the waveform bar."""
+    m, codec, o = _pair("mimi_202407", "mlx")
+    pcm = np.stack([_pcm(24000 * 5, 61), _pcm(24000 * 5, 62)])
+    codes = codec.encode(pcm[:, None, :])
+    ref = o.encode(pcm[:, None, :])
+    assert codes.shape == ref.shape and codes.shape[2] >= 60
+    assert np.array_equal(codes, ref), f"first diff at {np.argwhere(codes != ref)[:3].tolist()}"
+    y = codec.decode(ref)
+    assert _rms(y, o.decode(ref)) <= 1e-4
