@@ -111,6 +111,7 @@ def lib():
             "mimi_set_rope_table": ([P, P, I, I], I),
             "mimi_weights_ready": ([P], I),
             "mimi_encode": ([P, I, I, P, P, ctypes.POINTER(I)], I),
+            "mimi_encode_rows": ([P, I, I, P, P, P, ctypes.POINTER(I)], I),
             "mimi_decode": ([P, I, I, P, I, I, P, I], I),
             "mimi_reset_state": ([P, I], I),
             "mimi_decode_step": ([P, I, P, P], I),

@@ -106,6 +106,25 @@ class MimiCodec:
             out.append(codes.reshape(-1)[: nb * self.m.n_q * got.value].reshape(nb, self.m.n_q, got.value))
         return np.concatenate(out, 0)
 
+    def encode_rows(self, rows) -> np.ndarray:
+        """Same-length 1-D float32 clips -> (B, n_q, Tf) int32, as ``encode(np.stack(rows))`` without the
+        stacking copy (each clip is uploaded into its slot: mimi_encode_rows)."""
+        xs = [np.ascontiguousarray(r, np.float32).reshape(-1) for r in rows]
+        if not xs or len({x.shape[0] for x in xs}) != 1:
+            raise ValueError("encode_rows: same-length clips only")
+        N = xs[0].shape[0]
+        out = []
+        for b0 in range(0, len(xs), self.max_batch):
+            part = xs[b0: b0 + self.max_batch]
+            nb = len(part)
+            ptrs = (ctypes.c_void_p * nb)(*[x.ctypes.data for x in part])
+            Tf = int(np.ceil(N / self.m.frame_size)) + 2
+            codes = np.zeros((nb, self.m.n_q, Tf), np.int32)
+            got = ctypes.c_int(0)
+            _lib.check(_lib.lib().mimi_encode_rows(self._h, nb, N, None, ptrs, _lib.ptr(codes), ctypes.byref(got)))
+            out.append(codes.reshape(-1)[: nb * self.m.n_q * got.value].reshape(nb, self.m.n_q, got.value))
+        return np.concatenate(out, 0)
+
     def decode(self, codes: np.ndarray) -> np.ndarray:
         """(B, n_q, F) int32 -> (B, 1, F*frame_size) float32.  Resets streaming state (moshi_mlx)."""
         c = np.asarray(codes, np.int32)

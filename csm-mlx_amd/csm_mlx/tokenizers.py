@@ -131,7 +131,8 @@ def tokenize_segments_batch(segments: List[Segment], *, n_audio_codebooks: int =
     codec = get_audio_tokenizer(n_audio_codebooks)
     audios = [np.asarray(s.audio, np.float32) for s in segments]
     if len({len(a) for a in audios}) == 1 and audios:
-        codes = codec.encode(np.stack(audios)[:, None, :])
+        rows = getattr(codec, "encode_rows", None)  # (a registered stand-in codec may only have encode)
+        codes = rows(audios) if rows else codec.encode(np.stack(audios)[:, None, :])
     else:
         codes = [codec.encode(a[None, None])[0] for a in audios]
     out = []

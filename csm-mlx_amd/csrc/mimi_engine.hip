@@ -354,10 +354,18 @@ int64_t conv_out_len(int64_t T, int k_eff, int stride) {  // causal conv with ri
   return (T + pad + extra - k_eff) / stride + 1;
 }
 
+// CSM_MIMI_ELU_PRE=0: ELU in every consumer's staging loads (A/B); else once, by the producer
+bool mimi_elu_pre() {
+  static const bool v = [] { const char* e = getenv("CSM_MIMI_ELU_PRE"); return !(e && e[0] == '0'); }();
+  return v;
+}
+
 // One decoder-SEANet op on a window buffer: input window [B][cin][P + n] in `in` (channel stride
 // cs_in), output [B][cout][P' + n'] written at offset P' (the next op's history length) of `out`.
+// in_elu: the window holds ELU(x) (its producer stored it so); out_elu: store ELU(y) for an ELU-input
+// next op (histories copy whichever the window holds, so the two stay consistent from call to call)
 void run_window_op(mimi_codec* m, const MOp& o, const float* in, int cs_in, int P, int n, float* out, int cs_out,
-                   int P_next, int B) {
+                   int P_next, int B, bool in_elu = false, bool out_elu = false) {
   hipStream_t st = m->st;
   if (o.kind == 0) {
     const MConv& c = m->convs[o.idx];
@@ -365,15 +373,15 @@ void run_window_op(mimi_codec* m, const MOp& o, const float* in, int cs_in, int 
     p.ks_ws = m->ks_ws;
     p.x = in; p.Cin = c.cin; p.Tin = P + n; p.x_bstride = c.cin * cs_in; p.x_cstride = cs_in; p.x_off = 0;
     p.w = c.w; p.bias = c.b; p.Cout = c.cout; p.k = c.k; p.stride = 1; p.dil = c.dil; p.pad_l = 0;
-    p.replicate = 0; p.elu_in = c.elu; p.y = out; p.Tout = n; p.y_bstride = c.cout * cs_out; p.y_cstride = cs_out;
-    p.y_off = P_next; p.B = B;
+    p.replicate = 0; p.elu_in = c.elu && !in_elu; p.y = out; p.Tout = n; p.y_bstride = c.cout * cs_out; p.y_cstride = cs_out;
+    p.y_off = P_next; p.B = B; p.elu_out = out_elu;
     launch_conv1d(p, st);
   } else if (o.kind == 1) {
     const MConvTr& t = m->convtrs[o.idx];
     ConvTrParams p{};
     p.ks_ws = m->ks_ws;
     p.x = in; p.Cin = t.cin; p.Tin = P + n; p.x_bstride = t.cin * cs_in; p.x_cstride = cs_in; p.x_off = 0;
-    p.wt = t.wt; p.bias = t.b; p.Cout = t.cout; p.s = t.s; p.elu_in = t.elu; p.t_in0 = P; p.n_in = n; p.y = out;
+    p.wt = t.wt; p.bias = t.b; p.Cout = t.cout; p.s = t.s; p.elu_in = t.elu && !in_elu; p.t_in0 = P; p.n_in = n; p.y = out;
     p.y_bstride = t.cout * cs_out; p.y_cstride = cs_out; p.y_off = P_next; p.B = B;
     launch_convtr(p, st);
   } else {
@@ -383,13 +391,15 @@ void run_window_op(mimi_codec* m, const MOp& o, const float* in, int cs_in, int 
     p.x = in; p.Cin = r.ch; p.Tin = P + n; p.x_bstride = r.ch * cs_in; p.x_cstride = cs_in; p.x_off = 0;
     p.w = r.c1.w; p.bias = r.c1.b; p.Cout = r.hid; p.k = r.k; p.stride = 1; p.dil = r.dil; p.pad_l = 0;
     p.elu_in = 1; p.y = m->H; p.Tout = n; p.y_bstride = r.hid * n; p.y_cstride = n; p.y_off = 0; p.B = B;
+    p.elu_out = mimi_elu_pre();  // H feeds only block.3's ELU
     launch_conv1d(p, st);
     ConvParams q{};
     q.ks_ws = m->ks_ws;  // block.3: ELU -> conv(1, hid -> ch) + identity skip (true_skip)
     q.x = m->H; q.Cin = r.hid; q.Tin = n; q.x_bstride = r.hid * n; q.x_cstride = n; q.x_off = 0;
-    q.w = r.c2.w; q.bias = r.c2.b; q.Cout = r.ch; q.k = 1; q.stride = 1; q.dil = 1; q.pad_l = 0; q.elu_in = 1;
+    q.w = r.c2.w; q.bias = r.c2.b; q.Cout = r.ch; q.k = 1; q.stride = 1; q.dil = 1; q.pad_l = 0;
+    q.elu_in = !mimi_elu_pre();
     q.y = out; q.Tout = n; q.y_bstride = r.ch * cs_out; q.y_cstride = cs_out; q.y_off = P_next;
-    q.resid = in; q.r_bstride = r.ch * cs_in; q.r_cstride = cs_in; q.r_off = P; q.B = B;
+    q.resid = in; q.r_bstride = r.ch * cs_in; q.r_cstride = cs_in; q.r_off = P; q.B = B; q.elu_out = out_elu;
     launch_conv1d(q, st);
   }
 }
@@ -401,6 +411,10 @@ const float* run_decoder_seanet(mimi_codec* m, int B, int n_lat, bool use_hist) 
   float* bufs[2] = {m->W0, m->W1};
   int n = n_lat;
   int cur = 0;
+  bool in_elu = false;
+  auto elu_input = [&](const MOp& o) {
+    return (o.kind == 0 && m->convs[o.idx].elu) || (o.kind == 1 && m->convtrs[o.idx].elu);
+  };
   for (size_t i = 0; i < ops.size(); ++i) {
     const MOp& o = ops[i];
     const int P = m->op_pad(o);
@@ -412,15 +426,19 @@ const float* run_decoder_seanet(mimi_codec* m, int B, int n_lat, bool use_hist) 
       if (use_hist) {
         launch_copy_window(m->hist[i], B, cin, cin * P, P, 0, in, cin * cs_in, cs_in, 0, P, m->st);
       } else {
-        for (int b = 0; b < B; ++b)
-          HIPCHK(hipMemset2DAsync(in + (size_t)b * cin * cs_in, (size_t)cs_in * 4, 0, (size_t)P * 4, cin, m->st));
+        // the B utterances' cin rows are B * cin rows of pitch cs_in: one 2-D fill for all (not one per utterance)
+        HIPCHK(hipMemset2DAsync(in, (size_t)cs_in * 4, 0, (size_t)P * 4, (size_t)cin * B, m->st));
       }
     }
     const int n_out = o.kind == 1 ? n * m->convtrs[o.idx].s : n;
     const bool last = i + 1 == ops.size();
     const int P_next = last ? 0 : m->op_pad(ops[i + 1]);
     const int cs_out = P_next + n_out;
-    run_window_op(m, o, in, cs_in, P, n, bufs[cur ^ 1], cs_out, P_next, B);
+    // an output that only an ELU-input op reads is stored as ELU(y) (a transposed conv's output feeds a
+    // residual block, whose skip needs y itself)
+    const bool out_elu = mimi_elu_pre() && !last && o.kind != 1 && elu_input(ops[i + 1]);
+    run_window_op(m, o, in, cs_in, P, n, bufs[cur ^ 1], cs_out, P_next, B, in_elu, out_elu);
+    in_elu = out_elu;
     // window tail -> history for the next call
     if (use_hist && P > 0) launch_copy_window(in, B, cin, cin * cs_in, cs_in, n, m->hist[i], cin * P, P, 0, P, m->st);
     n = n_out;
@@ -549,8 +567,14 @@ int mimi_weights_ready(mimi_codec* m) {
 }
 
 int mimi_encode(mimi_codec* m, int B, int N, const float* pcm, int32_t* codes, int* n_frames_out) {
+  return mimi_encode_rows(m, B, N, pcm, nullptr, codes, n_frames_out);
+}
+
+int mimi_encode_rows(mimi_codec* m, int B, int N, const float* pcm, const float* const* rows, int32_t* codes,
+                     int* n_frames_out) {
   CSM_TRY {
     if (B <= 0 || B > m->B_max || N <= 0) throw CsmError(CSM_ERR_ARG, "bad encode shape");
+    if (!pcm && !rows) throw CsmError(CSM_ERR_ARG, "encode: no audio");
     HIPCHK(hipSetDevice(m->dev));
     const mimi_dims& d = m->d;
     hipStream_t st = m->st;
@@ -572,7 +596,12 @@ int mimi_encode(mimi_codec* m, int B, int N, const float* pcm, int32_t* codes, i
     const int64_t Tf = conv_out_len(T25, 2 * s, s);
     big = std::max(big, (size_t)d.dimension * (T25 + 8));
     ensure_ws(m, big * B, (size_t)B * std::max<int64_t>(T25, Tf) + 8);
-    HIPCHK(hipMemcpyAsync(m->W0, pcm, (size_t)B * N * 4, hipMemcpyHostToDevice, st));
+    if (pcm) {
+      HIPCHK(hipMemcpyAsync(m->W0, pcm, (size_t)B * N * 4, hipMemcpyHostToDevice, st));
+    } else {  // one host row per utterance, straight into its slot (no host-side stacking copy)
+      for (int b = 0; b < B; ++b)
+        HIPCHK(hipMemcpyAsync(m->W0 + (size_t)b * N, rows[b], (size_t)N * 4, hipMemcpyHostToDevice, st));
+    }
     float* bufs[2] = {m->W0, m->W1};
     int cur = 0;
     int64_t Tin = N;
@@ -580,7 +609,7 @@ int mimi_encode(mimi_codec* m, int B, int N, const float* pcm, int32_t* codes, i
     // next op is an ELU-input conv stores ELU(y) in place of y; one whose next op is a residual block
     // (ELU for its first conv, y itself for the skip) also writes ELU(y) to m->E.  in_elu: bufs[cur]
     // holds ELU(x); have_e: m->E holds ELU(bufs[cur]).
-    static const bool elu_pre = [] { const char* e = getenv("CSM_MIMI_ELU_PRE"); return !(e && e[0] == '0'); }();
+    const bool elu_pre = mimi_elu_pre();
     bool in_elu = false, have_e = false;
     auto out_elu = [&](size_t i, ConvParams& p) {
       const MOp* nx = i + 1 < m->enc_ops.size() ? &m->enc_ops[i + 1] : nullptr;
@@ -708,7 +737,7 @@ static void decode_frames(mimi_codec* m, int B, int F, const int32_t* dcodes, in
   if (stream) {
     launch_copy_window(m->up_hist, B, D, D, 1, 0, m->H, D * cs, cs, 0, 1, st);
   } else {
-    for (int b = 0; b < B; ++b) HIPCHK(hipMemset2DAsync(m->H + (size_t)b * D * cs, (size_t)cs * 4, 0, 4, D, st));
+    HIPCHK(hipMemset2DAsync(m->H, (size_t)cs * 4, 0, 4, (size_t)D * B, st));  // B * D rows of pitch cs
   }
   launch_copy_window(m->W1, B, D, D * F, F, 0, m->H, D * cs, cs, 1, F, st);
   if (stream) launch_copy_window(m->H, B, D, D * cs, cs, F, m->up_hist, D, 1, 0, 1, st);

@@ -176,6 +176,10 @@ int mimi_set_rope_table(mimi_codec* m, const float* table, int n_pos, int head_d
 int mimi_weights_ready(mimi_codec* m);
 /* pcm [B][N] float32 host -> codes [B][n_q][Tf] int32 host; *n_frames_out = Tf */
 int mimi_encode(mimi_codec* m, int B, int N, const float* pcm, int32_t* codes, int* n_frames_out);
+/* as mimi_encode with utterance b's N samples at rows[b] (pcm NULL): the batched context encode of
+   tokenize_segments_batch (reference tokenizers.py:61-85 per segment) without a host-side stacking copy */
+int mimi_encode_rows(mimi_codec* m, int B, int N, const float* pcm, const float* const* rows, int32_t* codes,
+                     int* n_frames_out);
 /* codes [B][n_q][F] -> pcm [B][F*frame_size].  codes_on_device / pcm_on_device select device pointers;
  * codes_layout 0 = [B][n_q][F], 1 = engine history [F][B][n_q] */
 int mimi_decode(mimi_codec* m, int B, int F, const int32_t* codes, int codes_on_device, int codes_layout,

@@ -171,3 +171,50 @@ def test_transformer_tile_attention_two_tiles():
     assert np.array_equal(codes, ref), f"first diff at {np.argwhere(codes != ref)[:3].tolist()}"
     y = codec.decode(ref)
     assert _rms(y, o.decode(ref)) <= 1e-4
+
+
+def test_encode_rows_equals_stacked_encode():
+    """mimi_encode_rows (one host clip per utterance, uploaded into its slot: the batched context
+    encode's path) gives the codes of mimi_encode on the stacked array, across a max_batch split."""
+    m, codec, _ = _pair("mimi_202407", "mlx", max_batch=2)
+    clips = [_pcm(24000 + 960, 70 + b) for b in range(3)]
+    assert np.array_equal(codec.encode_rows(clips), codec.encode(np.stack(clips)[:, None, :]))
+
+
+_ELU_SCRIPT = r"""
+import dataclasses, sys
+import numpy as np
+sys.path[:0] = [sys.argv[2] + "/csm-mlx_amd", sys.argv[2]]
+from csm_mlx.config import MIMI_CONFIGURATION
+from csm_mlx.mimi import MimiCodec
+from csm_mlx.weights import synthetic_mimi_weights
+m = dataclasses.replace(MIMI_CONFIGURATION["mimi_202407"], attn_mode="mlx")
+codec = MimiCodec(m, max_batch=3, max_frames=200)
+codec.load_weights(synthetic_mimi_weights(m))
+rng = np.random.default_rng(12)
+pcm = (0.1 * rng.standard_normal((3, 1, 24000 + 480))).astype(np.float32)
+codes = codec.encode(pcm)
+y = codec.decode(codes)
+codec.reset_state(3)
+ys = np.concatenate([codec.decode_step(codes[:, :, f: f + 1]) for f in range(4)], axis=2)
+np.savez(sys.argv[1], codes=codes, y=y, ys=ys)
+"""
+
+
+def test_elu_once_bit_identical(tmp_path):
+    """ELU once per element (CSM_MIMI_ELU_PRE=1: the producer stores ELU(y) for an ELU-input consumer, or
+    beside y for a residual block) against ELU in every consumer's loads: encode codes, one-shot decode
+    and streaming decode_step (whose window histories then hold ELU(y)) bit-identical."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    outs = {}
+    for v in ("0", "1"):
+        out = str(tmp_path / f"elu_{v}.npz")
+        r = subprocess.run([sys.executable, "-c", _ELU_SCRIPT, out, root], env=dict(os.environ, CSM_MIMI_ELU_PRE=v),
+                           capture_output=True, text=True, timeout=180)
+        assert r.returncode == 0, r.stderr[-2000:]
+        outs[v] = np.load(out)
+    for k in ("codes", "y", "ys"):
+        assert np.array_equal(outs["0"][k], outs["1"][k]), k
