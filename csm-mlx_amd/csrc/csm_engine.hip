@@ -1151,7 +1151,13 @@ int csm_engine_create(const csm_dims* dims, int device, int weight_dtype, int ma
     const int S = dims->max_seq_len;
     e->M_cap = std::max(S, 2 * max_batch);
     if (const char* v = getenv("CSM_ATTN_PREFILL")) e->attn_tiles_on = atoi(v) != 0;  // lab: 0 = per-row prompt attention (A/B)
-    HIPCHK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
+    if (const char* v = getenv("CSM_STREAM_PRIO"); !v || atoi(v) != 0) {  // the engine's stream first (mimi_create)
+      int least = 0, greatest = 0;
+      HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+      HIPCHK(hipStreamCreateWithPriority(&e->st, hipStreamNonBlocking, greatest));
+    } else {
+      HIPCHK(hipStreamCreateWithFlags(&e->st, hipStreamNonBlocking));
+    }
     alloc_stack(e.get(), e->bb, b, S, "backbone");
     alloc_stack(e.get(), e->dec, d, e->K, "decoder");
     const size_t D = e->D, Dd = e->Dd, K = e->K, Vp = e->Vpad, B = max_batch;

@@ -484,7 +484,16 @@ int mimi_create(const mimi_dims* dims, int device, int max_batch, int max_frames
     (void)hop;
     m->S_cap = 2 * max_frames * dims->downsample_stride / 2 + 16;  // latent (25 Hz) positions
     m->S_cap = std::max(m->S_cap, 2 * max_frames + 16);
-    HIPCHK(hipStreamCreateWithFlags(&m->st, hipStreamNonBlocking));
+    // the codec's stream at the lowest priority (the engine's at the highest), so a streaming decode_step
+    // overlapping the frame engine yields the CUs to the engine's dependent launches: config 3 +0.4-0.5 %
+    // in two alternating pairs (profiles/r06_ab_stream_prio.txt).  CSM_STREAM_PRIO=0: default priorities
+    if (const char* v = getenv("CSM_STREAM_PRIO"); !v || atoi(v) != 0) {
+      int least = 0, greatest = 0;
+      HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+      HIPCHK(hipStreamCreateWithPriority(&m->st, hipStreamNonBlocking, least));
+    } else {
+      HIPCHK(hipStreamCreateWithFlags(&m->st, hipStreamNonBlocking));
+    }
     build_layout(m.get());
     m->rope = (float*)m->alloc((size_t)m->S_cap * hd * 4);
     const size_t kv = (size_t)max_batch * dims->num_heads * m->S_cap * hd * 4;
