@@ -71,8 +71,12 @@ static_assert(KS_D == 2 * NWV && KS_F / NGRP == 2 * NWV, "every wave takes two K
 static_assert(RMAX == xs::HS_ROWS, "half-group sums use the xs.h row stride");
 
 // control words (u32), one per 128-B line
-enum { CW_F1 = 0, CW_F2 = CW_F1 + NQT, CW_F3 = CW_F2 + RMAX, CW_FH = CW_F3 + NDT, CW_C4 = CW_FH + NWG, CW_F5 = CW_C4 + NDT,
-       CW_N = CW_F5 + NDT };
+// (F1 / F3: one flag per (tile, row tile) -- the int4 kernel's QKV and o_proj row tiles run on separate
+// workgroups)
+enum { CW_F1 = 0, CW_F2 = CW_F1 + 2 * NQT, CW_F3 = CW_F2 + RMAX, CW_FH = CW_F3 + 2 * NDT, CW_C4 = CW_FH + NWG,
+       CW_F5 = CW_C4 + NDT, CW_N = CW_F5 + NDT };
+// int4 (two row tiles): the second row tile's QKV and o_proj workgroups
+constexpr int Q1_WG0 = A_WG0 + 64, O1_WG0 = Q1_WG0 + NQT;
 constexpr int CW_STRIDE = 32;
 
 #ifndef XSD_UNION
@@ -297,17 +301,17 @@ __device__ __forceinline__ void reduce_tiles(Ctx& c, const f32x16_t (&acc)[NTL],
 // loads are issued once the first tile's products are (its registers are then free).
 // pre(): the role's other loads (row scales, residual), issued after the first operand loads (vmcnt
 // retires in issue order: a load whose value is consumed first must be issued first).
-template <bool Q4, int MT, int NTL, typename Pre>
+template <bool Q4, int MT, int NTL, int T0 = 0, typename Pre>
 __device__ __forceinline__ void gemm_tiles(Ctx& c, const void* X, const float* hs, int nks, int st0, const WTile<Q4> (&W)[NTL], Pre&& pre) {
   AF A;
-  load_af(X, nks, 0, st0, c.lane, A);
+  load_af(X, nks, T0, st0, c.lane, A);
   pre();
   if constexpr (Q4) {
     stage_xg(c, hs, st0);
     __syncthreads();
   }
 #pragma unroll
-  for (int t = 0; t < MT; ++t) {
+  for (int t = T0; t < MT; ++t) {
     f32x16_t acc[NTL];
     mma<Q4, NTL>(c, A, W, t, acc);
     if (t + 1 < MT) load_af(X, nks, t + 1, st0, c.lane, A);
@@ -336,19 +340,19 @@ __device__ __forceinline__ float row_scale(const Ctx& c, int m) {
 
 // ---------------------------------------------------------------------------------------------------
 // Q: QKV tile T of layer l (l >= 1)
-template <bool Q4, int MT>
-__device__ __forceinline__ void role_q(Ctx& c, int l, const WTile<Q4>& W) {
+// (row tiles RT0 .. RT1 - 1)
+template <bool Q4, int RT0, int RT1>
+__device__ __forceinline__ void role_q(Ctx& c, int l, int T, const WTile<Q4>& W) {
   const DecStepXsArgs& p = c.p;
-  const int T = c.w;
   const unsigned tag = c.ep * NL + l;  // the previous layer's combine flags
   wait_words(c, NDT, [](int i) { return CW_F5 + i; }, tag);
   c.mark(1);
-  gemm_tiles<Q4, MT, 1>(c, p.xs_out, p.hs_out, KS_D, 2 * c.wave, reinterpret_cast<const WTile<Q4>(&)[1]>(W),
-                        [&] { row_scales(c, p.ss_out); });
+  gemm_tiles<Q4, RT1, 1, RT0>(c, p.xs_out, p.hs_out, KS_D, 2 * c.wave, reinterpret_cast<const WTile<Q4>(&)[1]>(W),
+                              [&] { row_scales(c, p.ss_out); });
   c.sub(0);
   // rows m = tid / 16 (+ 32 per pass), columns 2 (tid % 16) + {0, 1} (RoPE pairs)
 #pragma unroll
-  for (int t = 0; t < MT; ++t) {
+  for (int t = RT0; t < RT1; ++t) {
     const int ml = c.tid >> 4, m = 32 * t + ml, cc = 2 * (c.tid & 15), n = 32 * T + cc;
     const float r = row_scale(c, m);
     float a = c.L.ct[t][0][ml][cc] * r, b = c.L.ct[t][0][ml][cc + 1] * r;
@@ -370,7 +374,7 @@ __device__ __forceinline__ void role_q(Ctx& c, int l, const WTile<Q4>& W) {
   c.sub(1);
   drain();
   __syncthreads();
-  if (c.tid == 0) set_flag(c.cw(CW_F1 + T), tag + 1);
+  if (c.tid == 0) set_flag(c.cw(CW_F1 + T + NQT * RT0), tag + 1);
   c.mark(2);
 }
 
@@ -440,7 +444,7 @@ __device__ __forceinline__ void role_a(Ctx& c, int l) {
       // q tiles 4h..4h+3, k tiles 32 + 4g.., v tiles 40 + 4g..
       if (lane < 12) {
         const int t = lane < 4 ? 4 * h + lane : (lane < 8 ? HQ * 4 + 4 * g + lane - 4 : (HQ + HKV) * 4 + 4 * g + lane - 8);
-        const unsigned* a = c.cw(CW_F1 + t);
+        const unsigned* a = c.cw(CW_F1 + t + NQT * (m >> 5));  // the row's row tile
         __builtin_amdgcn_s_sleep(8);
         for (unsigned spin = 0; (int)(ld_cw(a) - tag) < 0; ++spin) {
           if (spin_fail(c, spin)) break;
@@ -530,19 +534,18 @@ __device__ __forceinline__ void role_a(Ctx& c, int l) {
 }
 
 // O: o_proj tile j (+ residual) -> x_o, split x_o * n2, row sums of squares (int4: half-group sums)
-template <bool Q4, int MT>
-__device__ __forceinline__ void role_o(Ctx& c, int l, const WTile<Q4>& W) {
+// (row tiles RT0 .. RT1 - 1: the attention rows 32 RT0 .. 32 RT1 - 1)
+template <bool Q4, int RT0, int RT1>
+__device__ __forceinline__ void role_o(Ctx& c, int l, int j, const WTile<Q4>& W) {
   const DecStepXsArgs& p = c.p;
-  const int j = c.w - O_WG0;
   const unsigned tag = c.ep * NL + l + 1;
-  wait_words(c, 32 * MT, [](int i) { return CW_F2 + i; }, tag);
+  wait_words(c, 32 * (RT1 - RT0), [](int i) { return CW_F2 + 32 * RT0 + i; }, tag);
   c.mark(5);
   // residual: layer 0 the projected input row proj_tab[code], else the previous layer's x_d
-  const int m = c.tid >> 3, q = c.tid & 7, n = 32 * j + 4 * q;
+  const int mm = c.tid >> 3, m = 32 * RT0 + mm, q = c.tid & 7, n = 32 * j + 4 * q;
   f32x4_t res = {0.f, 0.f, 0.f, 0.f}, nw;
-  gemm_tiles<Q4, MT, 1>(c, p.xs_att, p.hs_att, KS_D, 2 * c.wave, reinterpret_cast<const WTile<Q4>(&)[1]>(W), [&] {
-    // residual: layer 0 the projected input row proj_tab[code], else the previous layer's x_d
-    if (m < p.M) {
+  gemm_tiles<Q4, RT1, 1, RT0>(c, p.xs_att, p.hs_att, KS_D, 2 * c.wave, reinterpret_cast<const WTile<Q4>(&)[1]>(W), [&] {
+    if (mm < 32 * (RT1 - RT0) && m < p.M) {
       if (l == 0) {
         const int code = __hip_atomic_load(p.code_buf + m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         res = *reinterpret_cast<const f32x4_t*>(p.proj_tab + (size_t)code * D + n);
@@ -553,7 +556,7 @@ __device__ __forceinline__ void role_o(Ctx& c, int l, const WTile<Q4>& W) {
     nw = *reinterpret_cast<const f32x4_t*>(p.n2[l] + n);
   });
   c.sub(6);
-  if (m < 32 * MT) {
+  if (mm < 32 * (RT1 - RT0)) {
     f32x4_t x = {0.f, 0.f, 0.f, 0.f};
     const int t = m >> 5, ml = m & 31;
     if (m < p.M) x = res + f32x4_t{c.L.ct[t][0][ml][4 * q], c.L.ct[t][0][ml][4 * q + 1], c.L.ct[t][0][ml][4 * q + 2], c.L.ct[t][0][ml][4 * q + 3]};
@@ -569,7 +572,7 @@ __device__ __forceinline__ void role_o(Ctx& c, int l, const WTile<Q4>& W) {
   }
   drain();
   __syncthreads();
-  if (c.tid == 0) set_flag(c.cw(CW_F3 + j), tag);
+  if (c.tid == 0) set_flag(c.cw(CW_F3 + j + NDT * RT0), tag);
   c.mark(6);
 }
 
@@ -579,7 +582,7 @@ __device__ __forceinline__ void role_g(Ctx& c, int l, const WTile<Q4> (&W)[2]) {
   const DecStepXsArgs& p = c.p;
   const int b = 32 * (c.w & 7) + (c.w >> 3);
   const unsigned tag = c.ep * NL + l + 1;
-  wait_words(c, NDT, [](int i) { return CW_F3 + i; }, tag);
+  wait_words(c, NDT * MT, [](int i) { return CW_F3 + i; }, tag);  // every (o_proj tile, row tile)
   c.mark(7);
   gemm_tiles<Q4, MT, 2>(c, p.xs_x, p.hs_x, KS_D, 2 * c.wave, W, [&] { row_scales(c, p.ss_o); });
   c.sub(3);
@@ -698,12 +701,17 @@ __device__ __forceinline__ void role_h(Ctx& c, int t0, const WTile<false> (&W)[2
 
 // The layer loop of one workgroup class (each its own straight-line code: exact register liveness per
 // class, no merged paths holding another class's prefetch registers).  CLS: 0 QKV, 1 o_proj,
-// 2 attention, 3 head (+ plain), 4 plain (gate/up + down only).
-enum { C_Q = 0, C_O = 1, C_A = 2, C_H = 3, C_P = 4 };
+// 2 attention, 3 head (+ plain), 4 plain (gate/up + down only), 5 / 6 QKV / o_proj of the second row
+// tile (int4).  int4: the head runs on the attention workgroups (their registers are free after the last
+// layer), the head class does not exist.
+enum { C_Q = 0, C_O = 1, C_A = 2, C_H = 3, C_P = 4, C_Q1 = 5, C_O1 = 6 };
 template <bool Q4, int CLS>
 __device__ __forceinline__ void run_layers(Ctx& c) {
-  static_assert(CLS >= C_Q && CLS <= C_P, "workgroup class");
+  static_assert(CLS >= C_Q && CLS <= C_O1, "workgroup class");
   constexpr int MT = Q4 ? 2 : 1;
+  constexpr bool IS_Q = CLS == C_Q || CLS == C_Q1, IS_O = CLS == C_O || CLS == C_O1;
+  constexpr int RT0 = (CLS == C_Q1 || CLS == C_O1) ? 1 : 0, RT1 = Q4 ? RT0 + 1 : MT;
+  const int qt = c.w - (CLS == C_Q1 ? Q1_WG0 : 0), ot = c.w - (CLS == C_O1 ? O1_WG0 : O_WG0);
   const DecStepXsArgs& p = c.p;
   const int b = 32 * (c.w & 7) + (c.w >> 3), g = c.w & 7, j = c.w >> 3;
   WTile<Q4> wq, wgu[2], wd;
@@ -717,21 +725,21 @@ __device__ __forceinline__ void run_layers(Ctx& c) {
     load_wt<Q4>(p.wgu[l], 2 * b + 1, KS_D, 2 * F / 32, 2 * c.wave, c.lane, wgu[1]);
     if constexpr (WD_EARLY) load_wt<Q4>(p.wd[l], j, KS_F, D / 32, 16 * g + 2 * c.wave, c.lane, wd);
   };
-  if constexpr (CLS == C_Q) load_wt<Q4>(p.wqkv[1], c.w, KS_D, NQT, 2 * c.wave, c.lane, wq);
-  if constexpr (CLS == C_O) load_wt<Q4>(p.wo[0], c.w - O_WG0, KS_D, NDT, 2 * c.wave, c.lane, wq);
+  if constexpr (IS_Q) load_wt<Q4>(p.wqkv[1], qt, KS_D, NQT, 2 * c.wave, c.lane, wq);
+  if constexpr (IS_O) load_wt<Q4>(p.wo[0], ot, KS_D, NDT, 2 * c.wave, c.lane, wq);
   if constexpr (CLS != C_A) ld_gu(0);
   for (int l = 0; l < NL; ++l) {
     c.l = l;
     c.mark(0);
-    if constexpr (CLS == C_O || CLS == C_H || CLS == C_P) {
+    if constexpr (IS_O || CLS == C_H || CLS == C_P) {
       if (l > 0) {
-        if constexpr (CLS == C_O) load_wt<Q4>(p.wo[l], c.w - O_WG0, KS_D, NDT, 2 * c.wave, c.lane, wq);
+        if constexpr (IS_O) load_wt<Q4>(p.wo[l], ot, KS_D, NDT, 2 * c.wave, c.lane, wq);
         ld_gu(l);
       }
     }
-    if constexpr (CLS == C_Q) {
+    if constexpr (IS_Q) {
       if (l > 0) {
-        role_q<Q4, MT>(c, l, wq);
+        role_q<Q4, RT0, RT1>(c, l, qt, wq);
         ld_gu(l);
       }
     }
@@ -740,17 +748,18 @@ __device__ __forceinline__ void run_layers(Ctx& c) {
       role_a<Q4>(c, l);
       ld_gu(l);
     }
-    if constexpr (CLS == C_O) role_o<Q4, MT>(c, l, wq);
+    if constexpr (IS_O) role_o<Q4, RT0, RT1>(c, l, ot, wq);
     role_g<Q4, MT>(c, l, wgu);
     if constexpr (!WD_EARLY) load_wt<Q4>(p.wd[l], j, KS_F, D / 32, 16 * g + 2 * c.wave, c.lane, wd);  // during the h hand-off
     role_d<Q4, MT>(c, l, wd);
     // the next layer's QKV tile: during the combine the Q hand-off waits for
-    if constexpr (CLS == C_Q) {
-      if (l > 0 && l + 1 < NL) load_wt<Q4>(p.wqkv[l + 1], c.w, KS_D, NQT, 2 * c.wave, c.lane, wq);
+    if constexpr (IS_Q) {
+      if (l > 0 && l + 1 < NL) load_wt<Q4>(p.wqkv[l + 1], qt, KS_D, NQT, 2 * c.wave, c.lane, wq);
     }
   }
-  if constexpr (CLS == C_H) {  // bf16 head tiles (a 32-row tile past the last is clamped: its columns are never stored)
-    constexpr int H_WG0 = A_WG0 + 32 * MT;
+  constexpr int H_WG0 = Q4 ? A_WG0 : A_WG0 + 32 * MT;
+  if (CLS == C_H || (Q4 && CLS == C_A && p.head_w && c.w < H_WG0 + p.head_tiles)) {
+    // bf16 head tiles (a 32-row tile past the last is clamped: its columns are never stored)
     WTile<false> wh[2];
     load_wt<false>(p.head_w, 2 * (c.w - H_WG0), KS_D, 0, 2 * c.wave, c.lane, wh[0]);
     load_wt<false>(p.head_w, min(2 * (c.w - H_WG0) + 1, p.head_nt32 - 1), KS_D, 0, 2 * c.wave, c.lane, wh[1]);
@@ -761,13 +770,18 @@ __device__ __forceinline__ void run_layers(Ctx& c) {
 template <bool Q4>
 __device__ __forceinline__ void step_kernel(const DecStepXsArgs& p) {
   constexpr int MT = Q4 ? 2 : 1, H_WG0 = A_WG0 + 32 * MT;
+  static_assert(!Q4 || O1_WG0 + NDT <= NWG, "int4 roles fit the grid");
   __shared__ __attribute__((aligned(16))) Lds L;
   Ctx c{p, L, (int)blockIdx.x, (int)threadIdx.x, (int)(threadIdx.x & 63), __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), 0u};
   c.ep = __hip_atomic_load(p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (c.w < NQT) run_layers<Q4, C_Q>(c);
   else if (c.w < O_WG0 + NDT) run_layers<Q4, C_O>(c);
   else if (c.w < A_WG0 + 32 * MT) run_layers<Q4, C_A>(c);
-  else if (p.head_w && c.w < H_WG0 + p.head_tiles) run_layers<Q4, C_H>(c);
+  else if constexpr (Q4) {
+    if (c.w < Q1_WG0 + NQT) run_layers<Q4, C_Q1>(c);
+    else if (c.w < O1_WG0 + NDT) run_layers<Q4, C_O1>(c);
+    else run_layers<Q4, C_P>(c);
+  } else if (p.head_w && c.w < H_WG0 + p.head_tiles) run_layers<Q4, C_H>(c);
   else run_layers<Q4, C_P>(c);
   if (p.stamps && c.tid == 0) p.stamps[(size_t)c.w * DEC_XSD_STAMPS + DEC_XSD_STAMPS - 1] = __builtin_amdgcn_s_memrealtime();
   if (c.w == 0 && c.tid == 0) __hip_atomic_store(p.epoch, c.ep + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
