@@ -192,6 +192,8 @@ struct csm_engine {
   int* xsd_err = nullptr;
   unsigned long long* xsd_stamps = nullptr;  // csm_set_option "dec_xsd_stamps": per-role clock marks of the last launch
   bool xsd_head = [] { const char* v = getenv("CSM_DEC_XSD_HEAD"); return !(v && v[0] == '0'); }();  // "dec_xsd_head": the head in the same launch
+  bool xsd_sample = [] { const char* v = getenv("CSM_DEC_XSD_SAMPLE"); return !(v && v[0] == '0'); }();  // "dec_xsd_sample": + the sampler
+  bool xsd_sampled = false;  // the last launch_xsd sampled in the launch
 
   void* balloc(size_t bytes) {
     void* p = nullptr;
@@ -612,7 +614,7 @@ bool xsd_eligible(csm_engine* e, int M) {
 // i - 1 come from the head partials part_prev (part_n per row)
 // returns true when the step's head ran in the same launch (its logits and arg-max partials are written)
 bool launch_xsd(csm_engine* e, int M, int i, const unsigned long long* part_prev, int part_n, unsigned long long* part_out,
-                hipStream_t st) {
+                hipStream_t st, bool sample = false) {
   DecStepXsArgs a = e->xsd;
   const Stack& s = e->dec;
   for (int l = 0; l < DEC_FRAME_LAYERS; ++l) {
@@ -637,8 +639,14 @@ bool launch_xsd(csm_engine* e, int M, int i, const unsigned long long* part_prev
   if (e->xsd_head && it != e->ws.tiled.end() && ht == head_blocks(Vp, e->Dd, M, e->head_wdt) && ht <= 64) {
     a.head_w = (const uint8_t*)it->second; a.head_nt32 = (Vp + 31) / 32; a.head_tiles = ht; a.Vp = Vp; a.n_valid = e->V;
     a.head_out = e->ci_logits + (size_t)(i - 1) * e->B * Vp; a.head_part = part_out;
+    // the sampled step's sampler in the same launch (option dec_xsd_sample; V within the sampler's reach)
+    if (sample && e->xsd_sample && e->V <= DEC_XSD_THREADS * DEC_XSD_SAMPLE_NPT) {
+      a.sample = 1; a.s_top_k = e->top_k; a.s_K = e->K; a.s_cb = i; a.s_temperature = e->temperature;
+      a.s_seeds = e->seeds; a.s_frame_ctr = e->frame_ctr;
+    }
   }
   launch_dec_step_xs(a, st, e->wdt == WDT_Q4);
+  e->xsd_sampled = a.sample != 0;
   return a.head_w != nullptr;
 }
 
@@ -719,6 +727,7 @@ void enqueue_head_phase(csm_engine* e, hipStream_t st, int phase, int piece = 0)
     const bool xs_dec = use_tab && dec_xs_eligible(e, M);  // streaming matrix-core decoder + head
     bool xsd_used = false;  // the persistent step ran (its combines wrote 32 sum-of-squares tiles)
     bool xsd_head_done = false;  // ... and the head in the same launch
+    bool xsd_sampled = false;    // ... and the sampler
     // step 1 (two rows per utterance) on the streaming GEMM too: the projected rows split once, layer 0's
     // QKV projected from them; the head stays on the dense path (it reads one row of each pair)
     const bool xs_s1 = i == 1 && !folded && e->xs_step1 && dec_xs_eligible(e, M) && Dd % 512 == 0;
@@ -752,7 +761,10 @@ void enqueue_head_phase(csm_engine* e, hipStream_t st, int phase, int piece = 0)
       a0.g_codes = e->codes; a0.g_codes_K = K; a0.g_cb = i - 1;
       a0.g_xtab = e->proj_tab + (size_t)(i - 1) * V * Dd; a0.g_xout = e->dx; a0.g_D = Dd;
       if (xs_dec && xsd_eligible(e, M)) {
-        xsd_head_done = launch_xsd(e, M, i, g.xpart, g.xpart_n, part(i), st);
+        // sampled frames (phases 0 / 2; top-k only): the sampler runs in the step's launch too
+        const bool fuse_sample = !greedy && (phase == 0 || phase == 2) && !e->use_top_p && !e->use_min_p;
+        xsd_head_done = launch_xsd(e, M, i, g.xpart, g.xpart_n, part(i), st, fuse_sample);
+        xsd_sampled = xsd_head_done && e->xsd_sampled;
         xsd_used = true;
       } else if (xs_dec) {
         run_dec_xs(e, M, rm, st, a0);
@@ -778,7 +790,7 @@ void enqueue_head_phase(csm_engine* e, hipStream_t st, int phase, int piece = 0)
     } else if (!(ablate() & 64)) {
       launch_gemv(g, e->head_wdt, greedy ? EPI_ARGMAX : EPI_STORE, 1, st);
     }
-    if (!greedy && phase != 4) {
+    if (!greedy && phase != 4 && !xsd_sampled) {
       sp.logits = e->ci_logits + (size_t)(i - 1) * B * Vp; sp.cb = i; sp.part = part(i);
       launch_sample(sp, e->wdt, B, st);
     }
@@ -2225,6 +2237,11 @@ int csm_set_option(csm_engine* e, const char* key, int value) {
     else if (k == "dec_xsd_head") {
       if (!e) throw CsmError(CSM_ERR_ARG, "dec_xsd_head needs an engine");
       e->xsd_head = value != 0;
+      e->g_B = -1;
+    }
+    else if (k == "dec_xsd_sample") {
+      if (!e) throw CsmError(CSM_ERR_ARG, "dec_xsd_sample needs an engine");
+      e->xsd_sample = value != 0;
       e->g_B = -1;
     }
     else if (k == "dec_xsd") {

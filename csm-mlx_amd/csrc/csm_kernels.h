@@ -477,8 +477,16 @@ struct DecStepXsArgs {
   int head_nt32, head_tiles, Vp, n_valid;
   float* head_out;
   unsigned long long* head_part;
+  // sampled steps (temperature > 0, top-k only; needs the head in the launch): workgroup m < M samples
+  // row m from the head's logits as sample_kernel does (radix-select top-k threshold, Gumbel-max with
+  // the counter key(seeds[m], frame_ctr[0] * K + cb)) -> codes[m][cb] and the single partial head_part[m][0]
+  int sample, s_top_k, s_K, s_cb;
+  float s_temperature;
+  const uint64_t* s_seeds;
+  const int* s_frame_ctr;
 };
 constexpr int DEC_XSD_STAMPS = 64;
+constexpr int DEC_XSD_SAMPLE_NPT = 5;  // logits per thread of the in-launch sampler: V <= 512 x 5
 size_t dec_step_xs_ctrl_bytes();
 void launch_dec_step_xs(const DecStepXsArgs& p, hipStream_t st, bool q4);
 const void* dec_step_xs_kernel_ptr(bool q4);

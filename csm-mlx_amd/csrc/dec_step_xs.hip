@@ -74,7 +74,7 @@ static_assert(RMAX == xs::HS_ROWS, "half-group sums use the xs.h row stride");
 // (F1 / F3: one flag per (tile, row tile) -- the int4 kernel's QKV and o_proj row tiles run on separate
 // workgroups)
 enum { CW_F1 = 0, CW_F2 = CW_F1 + 2 * NQT, CW_F3 = CW_F2 + RMAX, CW_FH = CW_F3 + 2 * NDT, CW_C4 = CW_FH + NWG,
-       CW_F5 = CW_C4 + NDT, CW_N = CW_F5 + NDT };
+       CW_F5 = CW_C4 + NDT, CW_FS = CW_F5 + NDT, CW_N = CW_FS + 64 };  // FS: head tiles done (sampled steps)
 // int4 (two row tiles): the second row tile's QKV and o_proj workgroups
 constexpr int Q1_WG0 = A_WG0 + 64, O1_WG0 = Q1_WG0 + NQT;
 constexpr int CW_STRIDE = 32;
@@ -681,7 +681,8 @@ __device__ __forceinline__ void role_h(Ctx& c, int t0, const WTile<false> (&W)[2
     if (m < p.M && n < p.Vp) {
       const float* ct = &c.L.ct[rt][c4 >> 5][ml][c4 & 31];
       const float4 v = make_float4(ct[0] * r, ct[1] * r, ct[2] * r, ct[3] * r);
-      *reinterpret_cast<float4*>(p.head_out + (size_t)m * p.Vp + n) = v;
+      if (p.sample) st16(p.head_out, ((size_t)m * p.Vp + n) * 4, f32x4_t{v.x, v.y, v.z, v.w});  // (role_s reads them)
+      else *reinterpret_cast<float4*>(p.head_out + (size_t)m * p.Vp + n) = v;
       const float vv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -695,7 +696,119 @@ __device__ __forceinline__ void role_h(Ctx& c, int t0, const WTile<false> (&W)[2
       const unsigned long long v = __shfl_xor(best, o, 64);
       best = v > best ? v : best;
     }
-    if (m < p.M && (c.tid & 15) == 0) p.head_part[(size_t)m * p.part_stride + t] = best;
+    // (sampled steps: role_s publishes the row's single partial; slot 0 written here too would race it
+    // across the XCDs' L2s)
+    if (m < p.M && (c.tid & 15) == 0 && !p.sample) p.head_part[(size_t)m * p.part_stride + t] = best;
+  }
+  if (p.sample) {  // this tile's logits -> the sampling workgroups
+    drain();
+    __syncthreads();
+    if (c.tid == 0) set_flag(c.cw(CW_FS + t), c.ep + 1u);
+  }
+}
+
+// S (sampled steps; workgroup m < M, after its layers): row m's code from the head's logits -- the sampler
+// of sample_kernel (csm_kernels.hip) on 512 threads, as dec_frame.hip's sample_code: the top_k-th largest
+// logit by radix select (keys >= it kept, ties included), then the Gumbel-max of logit * (1 / T) + noise
+// over the kept entries, the lowest index on ties (the same winner whatever the visiting order) ->
+// codes[m][cb] and the 1-entry partial the next step reads.
+__device__ __forceinline__ void role_s(Ctx& c) {
+  constexpr int NPT = DEC_XSD_SAMPLE_NPT;
+  const DecStepXsArgs& p = c.p;
+  const int m = c.w, V = p.n_valid;
+  // the Gumbel noise does not depend on the logits: drawn before the wait
+  const uint64_t key = gumbel_key(p.s_seeds[m], p.s_frame_ctr[0] * p.s_K + p.s_cb);
+  double gn[NPT];
+#pragma unroll
+  for (int i = 0; i < NPT; ++i) {
+    const int v = c.tid + NT * i;
+    gn[i] = v < V ? gumbel_noise(key, v) : 0.0;
+  }
+  wait_words(c, p.head_tiles, [](int i) { return CW_FS + i; }, c.ep + 1u);
+  float lg[NPT];
+  const __amdgpu_buffer_rsrc_t rs = rsrc(p.head_out + (size_t)m * p.Vp);
+#pragma unroll
+  for (int i = 0; i < NPT; ++i) {
+    const int v = c.tid + NT * i;
+    lg[i] = v < V ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs, v * 4, 0, SC1)) : 0.f;
+  }
+  float thr = -INFINITY;
+  uint32_t* hist = reinterpret_cast<uint32_t*>(&c.L.red[0][0][0][0]);
+  uint32_t* wsum = hist + 256;
+  uint32_t* sh = hist + 264;  // [prefix, remain]
+  if (p.s_top_k > 0 && p.s_top_k < V) {  // radix select, 8 bits per pass; threads 0..255 hold digit 255 - tid
+    uint32_t prefix = 0, maskbits = 0, rem = (uint32_t)p.s_top_k;
+    for (int shift = 24; shift >= 0; shift -= 8) {
+      if (c.tid < 256) hist[c.tid] = 0;
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < NPT; ++i) {
+        const int v = c.tid + NT * i;
+        if (v < V) {
+          const uint32_t k = f2key(lg[i]);
+          if ((k & maskbits) == prefix) atomicAdd(&hist[(k >> shift) & 255u], 1u);
+        }
+      }
+      __syncthreads();
+      uint32_t h = 0, cnt = 0;
+      if (c.tid < 256) {
+        h = hist[255 - c.tid];
+        cnt = h;  // inclusive prefix over t = count of keys with digit >= 255 - t
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t u = __shfl_up(cnt, o, 64);
+          if (c.lane >= o) cnt += u;
+        }
+        if (c.lane == 63) wsum[c.wave] = cnt;
+      }
+      __syncthreads();
+      if (c.tid < 256) {
+        for (int w = 0; w < c.wave; ++w) cnt += wsum[w];
+        const uint32_t above = cnt - h;
+        if (h > 0 && above < rem && rem <= cnt) {  // exactly one digit
+          sh[0] = prefix | ((uint32_t)(255 - c.tid) << shift);
+          sh[1] = rem - above;
+        }
+      }
+      __syncthreads();
+      prefix = sh[0];
+      rem = sh[1];
+      maskbits |= 255u << shift;
+      __syncthreads();  // hist / sh reused by the next pass
+    }
+    thr = key2f(prefix);
+  }
+  const float inv_t = 1.0f / p.s_temperature;
+  double best = -INFINITY;
+  int bi = 0x7fffffff;
+#pragma unroll
+  for (int i = 0; i < NPT; ++i) {
+    const int v = c.tid + NT * i;
+    if (v >= V || !(lg[i] >= thr)) continue;
+    const double val = (double)(lg[i] * inv_t) + gn[i];  // = gumbel_perturbed(l, inv_t, key, v)
+    if (val > best) {  // increasing v per thread: first max kept
+      best = val;
+      bi = v;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double ov = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+  }
+  double* sv = reinterpret_cast<double*>(hist + 272);
+  int* si = reinterpret_cast<int*>(sv + NWV);
+  if (c.lane == 0) { sv[c.wave] = best; si[c.wave] = bi; }
+  __syncthreads();
+  if (c.tid == 0) {
+    double bv = sv[0];
+    int b = si[0];
+    for (int w2 = 1; w2 < NWV; ++w2)
+      if (sv[w2] > bv || (sv[w2] == bv && si[w2] < b)) { bv = sv[w2]; b = si[w2]; }
+    const int code = min(max(b, 0), V - 1);  // NaN logits leave no winner: clamp (as sample_kernel)
+    p.codes[(size_t)m * p.codes_K + p.s_cb] = code;
+    p.head_part[(size_t)m * p.part_stride] = pack_argmax(0.f, code);  // consumed as a 1-entry partial
   }
 }
 
@@ -783,6 +896,7 @@ __device__ __forceinline__ void step_kernel(const DecStepXsArgs& p) {
     else run_layers<Q4, C_P>(c);
   } else if (p.head_w && c.w < H_WG0 + p.head_tiles) run_layers<Q4, C_H>(c);
   else run_layers<Q4, C_P>(c);
+  if (p.sample && c.w < p.M) role_s(c);
   if (p.stamps && c.tid == 0) p.stamps[(size_t)c.w * DEC_XSD_STAMPS + DEC_XSD_STAMPS - 1] = __builtin_amdgcn_s_memrealtime();
   if (c.w == 0 && c.tid == 0) __hip_atomic_store(p.epoch, c.ep + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

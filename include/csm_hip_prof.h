@@ -55,6 +55,7 @@ int csm_bench_dec_xsd(csm_engine* e, int iters, float* avg_us, double* bytes);
  * cores, a block per 64-row prompt run and kv head, default 1; 0 = one block per row, tests), "dec_xsd"
  * (codebook steps >= 2 of the streaming path on the persistent batched decoder step, dec_step_xs.hip:
  * <= 32 bf16 / <= 64 int4 rows, default 1), "dec_xsd_head" (its head in the same launch, default 1),
+ * "dec_xsd_sample" (sampled top-k steps: sample_kernel's sampler in the same launch too, default 1),
  * "dec_xsd_stamps" (its per-role clock marks, csm_debug_read "dec_xsd_stamps", default 0),
  * "inject_handoff_error" (test hook).
  * Process-wide lab knobs are environment variables read once (CSM_NT_MASK, CSM_GEMV_XL, CSM_XS_*). */

@@ -171,3 +171,26 @@ def test_dec_xsd_timeout_reported_and_recovered(model_1b):
     assert np.array_equal(rn, gn)
     for b in range(B):
         assert first_divergence(gh[: gn[b], b], rh[: rn[b], b]) is None, f"utterance {b} after the reset"
+
+
+@pytest.mark.parametrize("B", [32, 64])
+def test_dec_xsd_in_launch_sampler_matches_sample_kernel(model_1b_q4, B):
+    """Sampled steps (temperature 0.8, top-k 50) with the sampler inside the step's launch (role_s: the
+    radix-select threshold and Gumbel-max of sample_kernel on 512 threads) against the same kernel with
+    sample_kernel launched after it (option dec_xsd_sample 0): 4 frames of int4 rows, codes identical."""
+    from csm_mlx import _lib
+    from csm_mlx.sampling import Sampler
+    from csm_mlx.tokenizers import tokenize_text_segment
+    args, w, model = model_1b_q4
+    L = _lib.lib()
+    prompts = [tokenize_text_segment(prompt_ids(950 + b, 10 + b % 3), 0, args.n_audio_codebooks) for b in range(B)]
+    _lib.check(L.csm_set_option(model.engine, b"dec_xsd", 1))
+    _lib.check(L.csm_set_option(model.engine, b"dec_xsd_sample", 0))
+    ref = _run(model, prompts, 4, Sampler(0.8, 50))
+    _lib.check(L.csm_set_option(model.engine, b"dec_xsd_sample", 1))
+    got = _run(model, prompts, 4, Sampler(0.8, 50))
+    _lib.check(L.csm_synchronize(model.engine))
+    assert np.array_equal(ref[1], got[1])
+    for b in range(B):
+        d = first_divergence(got[0][: got[1][b], b], ref[0][: ref[1][b], b])
+        assert d is None, f"utterance {b}: in-launch sampled codes differ at frame {d}"
