@@ -77,6 +77,14 @@ enum { CW_F1 = 0, CW_F2 = CW_F1 + 2 * NQT, CW_F3 = CW_F2 + RMAX, CW_FH = CW_F3 +
        CW_F5 = CW_C4 + NDT, CW_FS = CW_F5 + NDT, CW_N = CW_FS + 64 };  // FS: head tiles done (sampled steps)
 // int4 (two row tiles): the second row tile's QKV and o_proj workgroups
 constexpr int Q1_WG0 = A_WG0 + 64, O1_WG0 = Q1_WG0 + NQT;
+// XSD_QSPLIT (bf16): each QKV tile's K split over two workgroups (stages 0-7 on w < 48, 8-15 on QB_WG0 +
+// the tile: workgroups idle until gate/up), one K stage per wave; they publish raw partial sums and the
+// attention adds the halves, applies the row scale and RoPE and appends its row's K / V.  0: one
+// workgroup per tile (A/B).
+#ifndef XSD_QSPLIT
+#define XSD_QSPLIT 1
+#endif
+constexpr int QB_WG0 = NWG - NQT;
 constexpr int CW_STRIDE = 32;
 
 #ifndef XSD_UNION
@@ -181,10 +189,10 @@ template <> struct WTile<true> { u32x4_t a[2]; unsigned sb[2]; };
 struct AF { u32x4_t a[2][4][2]; };
 
 // nt32: the matrix's 32-row tile count (int4: where the {scale, bias} words start)
-template <bool Q4>
+template <bool Q4, int NS = 2>
 __device__ __forceinline__ void load_wt(const uint8_t* T, int tile, int nks, int nt32, int st0, int lane, WTile<Q4>& r) {
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
+  for (int q = 0; q < NS; ++q) {
     const int ts = tile * nks + st0 + q;
     if constexpr (Q4) {
       r.a[q] = bload<0>(T, lane * 16, __builtin_amdgcn_readfirstlane(ts * 1024));
@@ -196,10 +204,11 @@ __device__ __forceinline__ void load_wt(const uint8_t* T, int tile, int nks, int
   }
 }
 // row tile t of split rows with nks K stages
+template <int NS = 2>
 __device__ __forceinline__ void load_af(const void* X, int nks, int t, int st0, int lane, AF& r) {
   const __amdgpu_buffer_rsrc_t rs = rsrc(X);
 #pragma unroll
-  for (int q = 0; q < 2; ++q)
+  for (int q = 0; q < NS; ++q)
 #pragma unroll
     for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -221,12 +230,12 @@ __device__ __forceinline__ void stage_xg(Ctx& c, const float* hs, int st0) {
 }
 // the wave's partial tiles of row tile t.  Accumulator register j of lane (r, h): batch row (j & 3) +
 // 8 (j >> 2) + 4 h of the row tile, column r.
-template <bool Q4, int NTL>
+template <bool Q4, int NTL, int NS = 2>
 __device__ __forceinline__ void mma(const Ctx& c, const AF& A, const WTile<Q4> (&W)[NTL], int t, f32x16_t (&acc)[NTL]) {
 #pragma unroll
   for (int i = 0; i < NTL; ++i) acc[i] = f32x16_t{};
 #pragma unroll
-  for (int q = 0; q < 2; ++q) {
+  for (int q = 0; q < NS; ++q) {
     if constexpr (Q4) {
       f32x16_t gq[NTL];
 #pragma unroll
@@ -301,10 +310,11 @@ __device__ __forceinline__ void reduce_tiles(Ctx& c, const f32x16_t (&acc)[NTL],
 // loads are issued once the first tile's products are (its registers are then free).
 // pre(): the role's other loads (row scales, residual), issued after the first operand loads (vmcnt
 // retires in issue order: a load whose value is consumed first must be issued first).
-template <bool Q4, int MT, int NTL, int T0 = 0, typename Pre>
+template <bool Q4, int MT, int NTL, int T0 = 0, int NS = 2, typename Pre>
 __device__ __forceinline__ void gemm_tiles(Ctx& c, const void* X, const float* hs, int nks, int st0, const WTile<Q4> (&W)[NTL], Pre&& pre) {
+  static_assert(!Q4 || NS == 2, "int4: two stages per wave (stage_xg)");
   AF A;
-  load_af(X, nks, T0, st0, c.lane, A);
+  load_af<NS>(X, nks, T0, st0, c.lane, A);
   pre();
   if constexpr (Q4) {
     stage_xg(c, hs, st0);
@@ -313,8 +323,8 @@ __device__ __forceinline__ void gemm_tiles(Ctx& c, const void* X, const float* h
 #pragma unroll
   for (int t = T0; t < MT; ++t) {
     f32x16_t acc[NTL];
-    mma<Q4, NTL>(c, A, W, t, acc);
-    if (t + 1 < MT) load_af(X, nks, t + 1, st0, c.lane, A);
+    mma<Q4, NTL, NS>(c, A, W, t, acc);
+    if (t + 1 < MT) load_af<NS>(X, nks, t + 1, st0, c.lane, A);
     reduce_tiles<NTL>(c, acc, t);
   }
 }
@@ -375,6 +385,29 @@ __device__ __forceinline__ void role_q(Ctx& c, int l, int T, const WTile<Q4>& W)
   drain();
   __syncthreads();
   if (c.tid == 0) set_flag(c.cw(CW_F1 + T + NQT * RT0), tag + 1);
+  c.mark(2);
+}
+
+// bf16 XSD_QSPLIT: QKV tile T over K half HALF (stages 8 HALF .. 8 HALF + 7, one per wave) -> the raw
+// partial sums qkvp[HALF][m][n] (role_a adds the halves, scales, rotates)
+template <int HALF>
+__device__ __forceinline__ void role_qh(Ctx& c, int l, int T, const WTile<false>& W) {
+  const DecStepXsArgs& p = c.p;
+  const unsigned tag = c.ep * NL + l;  // the previous layer's combine flags
+  wait_words(c, NDT, [](int i) { return CW_F5 + i; }, tag);
+  c.mark(1);
+  gemm_tiles<false, 1, 1, 0, 1>(c, p.xs_out, nullptr, KS_D, 8 * HALF + c.wave, reinterpret_cast<const WTile<false>(&)[1]>(W), [] {});
+  c.sub(0);
+  {
+    const int m = c.tid >> 4, cc = 2 * (c.tid & 15), n = 32 * T + cc;
+    if (m < p.M)
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, make_float2(c.L.ct[0][0][m][cc], c.L.ct[0][0][m][cc + 1])),
+                                            rsrc(p.qkvp + (size_t)HALF * RMAX * QKV), (int)(((size_t)m * QKV + n) * 4), 0, SC1);
+  }
+  c.sub(1);
+  drain();
+  __syncthreads();
+  if (c.tid == 0) set_flag(c.cw(CW_F1 + T + NQT * HALF), tag + 1);
   c.mark(2);
 }
 
@@ -441,10 +474,12 @@ __device__ __forceinline__ void role_a(Ctx& c, int l) {
         __hip_atomic_store(p.code_buf + m, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     } else {
-      // q tiles 4h..4h+3, k tiles 32 + 4g.., v tiles 40 + 4g..
-      if (lane < 12) {
-        const int t = lane < 4 ? 4 * h + lane : (lane < 8 ? HQ * 4 + 4 * g + lane - 4 : (HQ + HKV) * 4 + 4 * g + lane - 8);
-        const unsigned* a = c.cw(CW_F1 + t + NQT * (m >> 5));  // the row's row tile
+      // q tiles 4h..4h+3, k tiles 32 + 4g.., v tiles 40 + 4g.. (XSD_QSPLIT: of both K halves)
+      constexpr bool QS = !Q4 && XSD_QSPLIT;
+      if (lane < (QS ? 24 : 12)) {
+        const int lt = lane % 12;
+        const int t = lt < 4 ? 4 * h + lt : (lt < 8 ? HQ * 4 + 4 * g + lt - 4 : (HQ + HKV) * 4 + 4 * g + lt - 8);
+        const unsigned* a = c.cw(CW_F1 + t + NQT * (QS ? lane / 12 : (m >> 5)));  // the K half / the row's row tile
         __builtin_amdgcn_s_sleep(8);
         for (unsigned spin = 0; (int)(ld_cw(a) - tag) < 0; ++spin) {
           if (spin_fail(c, spin)) break;
@@ -453,10 +488,40 @@ __device__ __forceinline__ void role_a(Ctx& c, int l) {
       }
       // (the wave leaves the poll loop once every polling lane has matched)
       c.sub(8);
-      const float* row = p.qkv + (size_t)m * QKV;
-      qv = ld8(row, (h * HD + 2 * lane) * 4);
-      kv2 = ld8(row, (HQ * HD + g * HD + 2 * lane) * 4);
-      vv2 = ld8(row, ((HQ + HKV) * HD + g * HD + 2 * lane) * 4);
+      if constexpr (QS) {
+        // the halves' sums, the row scale (row_scales' order: 4 tiles a part, the 8 parts in turn), RoPE,
+        // the K / V row at pos -> cache (each kv head by its first query head's wave)
+        const float* r0 = p.qkvp + (size_t)m * QKV;
+        const float* r1 = r0 + (size_t)RMAX * QKV;
+        const float2 q0 = ld8(r0, (h * HD + 2 * lane) * 4), q1 = ld8(r1, (h * HD + 2 * lane) * 4);
+        const float2 k0 = ld8(r0, (HQ * HD + g * HD + 2 * lane) * 4), k1 = ld8(r1, (HQ * HD + g * HD + 2 * lane) * 4);
+        const float2 v0 = ld8(r0, ((HQ + HKV) * HD + g * HD + 2 * lane) * 4), v1 = ld8(r1, ((HQ + HKV) * HD + g * HD + 2 * lane) * 4);
+        const float ssv = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc(p.ss_out), (min(lane, 31) * RMAX + m) * 4, 0, SC1));
+        const int si = __float_as_int(ssv);
+        float ss = 0.f;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const float part = ((__int_as_float(__builtin_amdgcn_readlane(si, 4 * q)) + __int_as_float(__builtin_amdgcn_readlane(si, 4 * q + 1))) +
+                              __int_as_float(__builtin_amdgcn_readlane(si, 4 * q + 2))) + __int_as_float(__builtin_amdgcn_readlane(si, 4 * q + 3));
+          ss = q == 0 ? part : ss + part;
+        }
+        const float rs = rsqrtf(ss / (float)D + p.eps);
+        const float2 cs = reinterpret_cast<const float2*>(p.rope)[(size_t)pos * (HD / 2) + lane];
+        auto rot = [&](float a, float b) { return make_float2(a * cs.x - b * cs.y, b * cs.x + a * cs.y); };
+        qv = rot((q0.x + q1.x) * rs, (q0.y + q1.y) * rs);
+        kv2 = rot((k0.x + k1.x) * rs, (k0.y + k1.y) * rs);
+        vv2 = make_float2((v0.x + v1.x) * rs, (v0.y + v1.y) * rs);
+        if (h % (HQ / HKV) == 0) {  // KVCache.update_and_fetch: this kv head's row at pos
+          const size_t o = (((size_t)m * HKV + g) * p.S_cap + pos) * HD + 2 * lane;
+          *reinterpret_cast<float2*>(p.kc[l] + o) = kv2;
+          *reinterpret_cast<float2*>(p.vc[l] + o) = vv2;
+        }
+      } else {
+        const float* row = p.qkv + (size_t)m * QKV;
+        qv = ld8(row, (h * HD + 2 * lane) * 4);
+        kv2 = ld8(row, (HQ * HD + g * HD + 2 * lane) * 4);
+        vv2 = ld8(row, ((HQ + HKV) * HD + g * HD + 2 * lane) * 4);
+      }
     }
     *reinterpret_cast<float2*>(&c.L.at.qsh[h][2 * lane]) = make_float2(qv.x * scale, qv.y * scale);
     *reinterpret_cast<float2*>(&c.L.at.kn[h][2 * lane]) = kv2;
@@ -817,14 +882,17 @@ __device__ __forceinline__ void role_s(Ctx& c) {
 // 2 attention, 3 head (+ plain), 4 plain (gate/up + down only), 5 / 6 QKV / o_proj of the second row
 // tile (int4).  int4: the head runs on the attention workgroups (their registers are free after the last
 // layer), the head class does not exist.
-enum { C_Q = 0, C_O = 1, C_A = 2, C_H = 3, C_P = 4, C_Q1 = 5, C_O1 = 6 };
+enum { C_Q = 0, C_O = 1, C_A = 2, C_H = 3, C_P = 4, C_Q1 = 5, C_O1 = 6, C_QB = 7 };
 template <bool Q4, int CLS>
 __device__ __forceinline__ void run_layers(Ctx& c) {
-  static_assert(CLS >= C_Q && CLS <= C_O1, "workgroup class");
+  static_assert(CLS >= C_Q && CLS <= C_QB, "workgroup class");
   constexpr int MT = Q4 ? 2 : 1;
-  constexpr bool IS_Q = CLS == C_Q || CLS == C_Q1, IS_O = CLS == C_O || CLS == C_O1;
+  constexpr bool IS_Q = CLS == C_Q || CLS == C_Q1 || CLS == C_QB, IS_O = CLS == C_O || CLS == C_O1;
   constexpr int RT0 = (CLS == C_Q1 || CLS == C_O1) ? 1 : 0, RT1 = Q4 ? RT0 + 1 : MT;
-  const int qt = c.w - (CLS == C_Q1 ? Q1_WG0 : 0), ot = c.w - (CLS == C_O1 ? O1_WG0 : O_WG0);
+  constexpr bool QS = !Q4 && XSD_QSPLIT;  // bf16 QKV K halves: stage 8 HALF + wave
+  constexpr int QHALF = CLS == C_QB ? 1 : 0, QNS = QS ? 1 : 2;
+  const int qst = QS ? 8 * QHALF + c.wave : 2 * c.wave;
+  const int qt = c.w - (CLS == C_Q1 ? Q1_WG0 : (CLS == C_QB ? QB_WG0 : 0)), ot = c.w - (CLS == C_O1 ? O1_WG0 : O_WG0);
   const DecStepXsArgs& p = c.p;
   const int b = 32 * (c.w & 7) + (c.w >> 3), g = c.w & 7, j = c.w >> 3;
   WTile<Q4> wq, wgu[2], wd;
@@ -838,7 +906,7 @@ __device__ __forceinline__ void run_layers(Ctx& c) {
     load_wt<Q4>(p.wgu[l], 2 * b + 1, KS_D, 2 * F / 32, 2 * c.wave, c.lane, wgu[1]);
     if constexpr (WD_EARLY) load_wt<Q4>(p.wd[l], j, KS_F, D / 32, 16 * g + 2 * c.wave, c.lane, wd);
   };
-  if constexpr (IS_Q) load_wt<Q4>(p.wqkv[1], qt, KS_D, NQT, 2 * c.wave, c.lane, wq);
+  if constexpr (IS_Q) load_wt<Q4, QNS>(p.wqkv[1], qt, KS_D, NQT, qst, c.lane, wq);
   if constexpr (IS_O) load_wt<Q4>(p.wo[0], ot, KS_D, NDT, 2 * c.wave, c.lane, wq);
   if constexpr (CLS != C_A) ld_gu(0);
   for (int l = 0; l < NL; ++l) {
@@ -852,7 +920,8 @@ __device__ __forceinline__ void run_layers(Ctx& c) {
     }
     if constexpr (IS_Q) {
       if (l > 0) {
-        role_q<Q4, RT0, RT1>(c, l, qt, wq);
+        if constexpr (QS) role_qh<QHALF>(c, l, qt, wq);
+        else role_q<Q4, RT0, RT1>(c, l, qt, wq);
         ld_gu(l);
       }
     }
@@ -867,7 +936,7 @@ __device__ __forceinline__ void run_layers(Ctx& c) {
     role_d<Q4, MT>(c, l, wd);
     // the next layer's QKV tile: during the combine the Q hand-off waits for
     if constexpr (IS_Q) {
-      if (l > 0 && l + 1 < NL) load_wt<Q4>(p.wqkv[l + 1], qt, KS_D, NQT, 2 * c.wave, c.lane, wq);
+      if (l > 0 && l + 1 < NL) load_wt<Q4, QNS>(p.wqkv[l + 1], qt, KS_D, NQT, qst, c.lane, wq);
     }
   }
   constexpr int H_WG0 = Q4 ? A_WG0 : A_WG0 + 32 * MT;
@@ -884,6 +953,7 @@ template <bool Q4>
 __device__ __forceinline__ void step_kernel(const DecStepXsArgs& p) {
   constexpr int MT = Q4 ? 2 : 1, H_WG0 = A_WG0 + 32 * MT;
   static_assert(!Q4 || O1_WG0 + NDT <= NWG, "int4 roles fit the grid");
+  static_assert(H_WG0 + 64 <= QB_WG0 || Q4, "bf16: head tiles and the second QKV K half apart");
   __shared__ __attribute__((aligned(16))) Lds L;
   Ctx c{p, L, (int)blockIdx.x, (int)threadIdx.x, (int)(threadIdx.x & 63), __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), 0u};
   c.ep = __hip_atomic_load(p.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -895,6 +965,7 @@ __device__ __forceinline__ void step_kernel(const DecStepXsArgs& p) {
     else if (c.w < O1_WG0 + NDT) run_layers<Q4, C_O1>(c);
     else run_layers<Q4, C_P>(c);
   } else if (p.head_w && c.w < H_WG0 + p.head_tiles) run_layers<Q4, C_H>(c);
+  else if (XSD_QSPLIT && c.w >= QB_WG0) run_layers<Q4, C_QB>(c);
   else run_layers<Q4, C_P>(c);
   if (p.sample && c.w < p.M) role_s(c);
   if (p.stamps && c.tid == 0) p.stamps[(size_t)c.w * DEC_XSD_STAMPS + DEC_XSD_STAMPS - 1] = __builtin_amdgcn_s_memrealtime();
