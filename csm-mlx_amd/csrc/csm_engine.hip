@@ -896,7 +896,7 @@ void ensure_batch(csm_engine* e, int B) {
       const size_t R = DEC_XSD_MAX_M_Q4;
       DecStepXsArgs& x = e->xsd;
       x.qkv = (float*)e->balloc(R * e->dec.qkv_rows() * 4);
-      x.qkvp = (float*)e->balloc(2 * R * e->dec.qkv_rows() * 4);
+      x.qkvp = (float*)e->balloc((2 * R * e->dec.qkv_rows() + (size_t)e->dec.qkv_rows() / 32 * R) * 4);  // + row scales [48][R]
       x.xs_att = e->balloc(xs::bytes(R, 1024));
       x.xs_x = e->balloc(xs::bytes(R, 1024));
       x.xs_h = e->balloc(xs::bytes(R, 8192));

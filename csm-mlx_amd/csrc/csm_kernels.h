@@ -484,7 +484,7 @@ struct DecStepXsArgs {
   float s_temperature;
   const uint64_t* s_seeds;
   const int* s_frame_ctr;
-  float* qkvp;                            // bf16 XSD_QSPLIT: [2][RMAX][QKV] the QKV K halves' partial sums
+  float* qkvp;                            // bf16 XSD_QSPLIT: [2][RMAX][QKV] the QKV K halves' partial sums, then [48][RMAX] row scales
 };
 constexpr int DEC_XSD_STAMPS = 64;
 constexpr int DEC_XSD_SAMPLE_NPT = 5;  // logits per thread of the in-launch sampler: V <= 512 x 5

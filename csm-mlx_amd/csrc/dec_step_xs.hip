@@ -389,20 +389,27 @@ __device__ __forceinline__ void role_q(Ctx& c, int l, int T, const WTile<Q4>& W)
 }
 
 // bf16 XSD_QSPLIT: QKV tile T over K half HALF (stages 8 HALF .. 8 HALF + 7, one per wave) -> the raw
-// partial sums qkvp[HALF][m][n] (role_a adds the halves, scales, rotates)
+// partial sums qkvp[HALF][m][n] (role_a adds the halves, scales, rotates); the half-0 workgroups also
+// publish the row scales (row_scales / row_scale, their loads under the operand loads) in qkvr[T][m]
 template <int HALF>
 __device__ __forceinline__ void role_qh(Ctx& c, int l, int T, const WTile<false>& W) {
   const DecStepXsArgs& p = c.p;
   const unsigned tag = c.ep * NL + l;  // the previous layer's combine flags
   wait_words(c, NDT, [](int i) { return CW_F5 + i; }, tag);
   c.mark(1);
-  gemm_tiles<false, 1, 1, 0, 1>(c, p.xs_out, nullptr, KS_D, 8 * HALF + c.wave, reinterpret_cast<const WTile<false>(&)[1]>(W), [] {});
+  gemm_tiles<false, 1, 1, 0, 1>(c, p.xs_out, nullptr, KS_D, 8 * HALF + c.wave, reinterpret_cast<const WTile<false>(&)[1]>(W), [&] {
+    if constexpr (HALF == 0) row_scales(c, p.ss_out);
+  });
   c.sub(0);
   {
     const int m = c.tid >> 4, cc = 2 * (c.tid & 15), n = 32 * T + cc;
-    if (m < p.M)
+    if (m < p.M) {
       __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2_t, make_float2(c.L.ct[0][0][m][cc], c.L.ct[0][0][m][cc + 1])),
                                             rsrc(p.qkvp + (size_t)HALF * RMAX * QKV), (int)(((size_t)m * QKV + n) * 4), 0, SC1);
+      if (HALF == 0 && (c.tid & 15) == 0)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(row_scale(c, m)), rsrc(p.qkvp + (size_t)2 * RMAX * QKV),
+                                              (T * RMAX + m) * 4, 0, SC1);
+    }
   }
   c.sub(1);
   drain();
@@ -496,16 +503,9 @@ __device__ __forceinline__ void role_a(Ctx& c, int l) {
         const float2 q0 = ld8(r0, (h * HD + 2 * lane) * 4), q1 = ld8(r1, (h * HD + 2 * lane) * 4);
         const float2 k0 = ld8(r0, (HQ * HD + g * HD + 2 * lane) * 4), k1 = ld8(r1, (HQ * HD + g * HD + 2 * lane) * 4);
         const float2 v0 = ld8(r0, ((HQ + HKV) * HD + g * HD + 2 * lane) * 4), v1 = ld8(r1, ((HQ + HKV) * HD + g * HD + 2 * lane) * 4);
-        const float ssv = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc(p.ss_out), (min(lane, 31) * RMAX + m) * 4, 0, SC1));
-        const int si = __float_as_int(ssv);
-        float ss = 0.f;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const float part = ((__int_as_float(__builtin_amdgcn_readlane(si, 4 * q)) + __int_as_float(__builtin_amdgcn_readlane(si, 4 * q + 1))) +
-                              __int_as_float(__builtin_amdgcn_readlane(si, 4 * q + 2))) + __int_as_float(__builtin_amdgcn_readlane(si, 4 * q + 3));
-          ss = q == 0 ? part : ss + part;
-        }
-        const float rs = rsqrtf(ss / (float)D + p.eps);
+        // the row scale the q tile 4h's half-0 workgroup published (its flag was polled above)
+        const float rs = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc(p.qkvp + (size_t)2 * RMAX * QKV),
+                                                                                       (4 * h * RMAX + m) * 4, 0, SC1));
         const float2 cs = reinterpret_cast<const float2*>(p.rope)[(size_t)pos * (HD / 2) + lane];
         auto rot = [&](float a, float b) { return make_float2(a * cs.x - b * cs.y, b * cs.x + a * cs.y); };
         qv = rot((q0.x + q1.x) * rs, (q0.y + q1.y) * rs);
