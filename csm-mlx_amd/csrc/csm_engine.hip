@@ -636,7 +636,8 @@ bool launch_xsd(csm_engine* e, int M, int i, const unsigned long long* part_prev
   const int Vp = e->Vpad, ht = (Vp + 63) / 64;
   const void* hw = (const char*)e->audio_head + (size_t)(i - 1) * Vp * e->Dd * 2;
   auto it = e->ws.tiled.find(hw);
-  if (e->xsd_head && it != e->ws.tiled.end() && ht == head_blocks(Vp, e->Dd, M, e->head_wdt) && ht <= 64) {
+  // (int4: the head's (tile, row tile) pairs on the 64 attention + 32 plain workgroups: <= 48 tiles)
+  if (e->xsd_head && it != e->ws.tiled.end() && ht == head_blocks(Vp, e->Dd, M, e->head_wdt) && ht <= (e->wdt == WDT_Q4 ? 48 : 64)) {
     a.head_w = (const uint8_t*)it->second; a.head_nt32 = (Vp + 31) / 32; a.head_tiles = ht; a.Vp = Vp; a.n_valid = e->V;
     a.head_out = e->ci_logits + (size_t)(i - 1) * e->B * Vp; a.head_part = part_out;
     // the sampled step's sampler in the same launch (option dec_xsd_sample; V within the sampler's reach)

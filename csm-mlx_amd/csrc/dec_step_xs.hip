@@ -74,7 +74,7 @@ static_assert(RMAX == xs::HS_ROWS, "half-group sums use the xs.h row stride");
 // (F1 / F3: one flag per (tile, row tile) -- the int4 kernel's QKV and o_proj row tiles run on separate
 // workgroups)
 enum { CW_F1 = 0, CW_F2 = CW_F1 + 2 * NQT, CW_F3 = CW_F2 + RMAX, CW_FH = CW_F3 + 2 * NDT, CW_C4 = CW_FH + NWG,
-       CW_F5 = CW_C4 + NDT, CW_FS = CW_F5 + NDT, CW_N = CW_FS + 64 };  // FS: head tiles done (sampled steps)
+       CW_F5 = CW_C4 + NDT, CW_FS = CW_F5 + NDT, CW_N = CW_FS + 128 };  // FS: head (tile, row tile)s done (sampled steps)
 // int4 (two row tiles): the second row tile's QKV and o_proj workgroups
 constexpr int Q1_WG0 = A_WG0 + 64, O1_WG0 = Q1_WG0 + NQT;
 // XSD_QSPLIT (bf16): each QKV tile's K split over two workgroups (stages 0-7 on w < 48, 8-15 on QB_WG0 +
@@ -730,16 +730,16 @@ __device__ __forceinline__ void role_d(Ctx& c, int l, const WTile<Q4>& W) {
 // last combines' split x * norm + sums of squares) -> logits [row][Vp] and the tile's arg-max partial
 // per row (pack_argmax: the largest logit, the first index on ties), exactly the partial layout of the
 // launch path's head (gemm_xs EPI_ARGMAX, 64-row tiles), which the next step / advance_kernel reduce
-template <int MT>
-__device__ __forceinline__ void role_h(Ctx& c, int t0, const WTile<false> (&W)[2]) {
+// (head tile t, row tiles RT0 .. RT1 - 1: the int4 kernel's two row tiles on separate workgroups)
+template <int RT0, int RT1>
+__device__ __forceinline__ void role_h(Ctx& c, int t, const WTile<false> (&W)[2]) {
   const DecStepXsArgs& p = c.p;
-  const int t = c.w - t0;
   const unsigned tag = c.ep * NL + NL;  // the last layer's combine flags
   wait_words(c, NDT, [](int i) { return CW_F5 + i; }, tag);
-  gemm_tiles<false, MT, 2>(c, p.xs_out, nullptr, KS_D, 2 * c.wave, W, [&] { row_scales(c, p.ss_out); });
+  gemm_tiles<false, RT1, 2, RT0>(c, p.xs_out, nullptr, KS_D, 2 * c.wave, W, [&] { row_scales(c, p.ss_out); });
   // row m = tid / 16 (+ 32 per row tile), columns 4 (tid % 16) .. + 3 of the 64
 #pragma unroll
-  for (int rt = 0; rt < MT; ++rt) {
+  for (int rt = RT0; rt < RT1; ++rt) {
     const int ml = c.tid >> 4, m = 32 * rt + ml, c4 = 4 * (c.tid & 15), n = 64 * t + c4;
     const float r = row_scale(c, m);
     unsigned long long best = 0;
@@ -768,7 +768,7 @@ __device__ __forceinline__ void role_h(Ctx& c, int t0, const WTile<false> (&W)[2
   if (p.sample) {  // this tile's logits -> the sampling workgroups
     drain();
     __syncthreads();
-    if (c.tid == 0) set_flag(c.cw(CW_FS + t), c.ep + 1u);
+    if (c.tid == 0) set_flag(c.cw(CW_FS + t + 64 * RT0), c.ep + 1u);
   }
 }
 
@@ -789,7 +789,8 @@ __device__ __forceinline__ void role_s(Ctx& c) {
     const int v = c.tid + NT * i;
     gn[i] = v < V ? gumbel_noise(key, v) : 0.0;
   }
-  wait_words(c, p.head_tiles, [](int i) { return CW_FS + i; }, c.ep + 1u);
+  const int fs0 = CW_FS + 64 * (m >> 5);  // the head tiles of the row's row tile
+  wait_words(c, p.head_tiles, [fs0](int i) { return fs0 + i; }, c.ep + 1u);
   float lg[NPT];
   const __amdgpu_buffer_rsrc_t rs = rsrc(p.head_out + (size_t)m * p.Vp);
 #pragma unroll
@@ -939,13 +940,26 @@ __device__ __forceinline__ void run_layers(Ctx& c) {
       if (l > 0 && l + 1 < NL) load_wt<Q4, QNS>(p.wqkv[l + 1], qt, KS_D, NQT, qst, c.lane, wq);
     }
   }
-  constexpr int H_WG0 = Q4 ? A_WG0 : A_WG0 + 32 * MT;
-  if (CLS == C_H || (Q4 && CLS == C_A && p.head_w && c.w < H_WG0 + p.head_tiles)) {
-    // bf16 head tiles (a 32-row tile past the last is clamped: its columns are never stored)
+  // bf16 head tiles (a 32-row tile past the last is clamped: its columns are never stored).  bf16: head
+  // tile w - H_WG0 on the head class; int4: (tile, row tile) k = (k % tiles, k / tiles) on the attention
+  // workgroups (k = w - A_WG0) and, past their 64, the first plain ones (k = 64 + w - P4_WG0)
+  constexpr int H_WG0 = A_WG0 + 32 * MT, P4_WG0 = O1_WG0 + NDT;
+  if constexpr (!Q4 && CLS == C_H) {
     WTile<false> wh[2];
     load_wt<false>(p.head_w, 2 * (c.w - H_WG0), KS_D, 0, 2 * c.wave, c.lane, wh[0]);
     load_wt<false>(p.head_w, min(2 * (c.w - H_WG0) + 1, p.head_nt32 - 1), KS_D, 0, 2 * c.wave, c.lane, wh[1]);
-    role_h<MT>(c, H_WG0, wh);
+    role_h<0, 1>(c, c.w - H_WG0, wh);
+  }
+  if constexpr (Q4 && (CLS == C_A || CLS == C_P)) {
+    const int k = CLS == C_A ? c.w - A_WG0 : 64 + c.w - P4_WG0;
+    if (p.head_w && k < 2 * p.head_tiles) {
+      const int t = k % p.head_tiles, rt = k / p.head_tiles;
+      WTile<false> wh[2];
+      load_wt<false>(p.head_w, 2 * t, KS_D, 0, 2 * c.wave, c.lane, wh[0]);
+      load_wt<false>(p.head_w, min(2 * t + 1, p.head_nt32 - 1), KS_D, 0, 2 * c.wave, c.lane, wh[1]);
+      if (rt == 0) role_h<0, 1>(c, t, wh);
+      else role_h<1, 2>(c, t, wh);
+    }
   }
 }
 
